@@ -1,0 +1,123 @@
+// pybind11 bindings of the gfx950 kernels. Deliberately torch-ABI-free: Python passes raw
+// device pointers (tensor.data_ptr()), sizes and the current HIP stream handle, so the
+// extension only depends on the HIP runtime that torch itself loaded.
+#include <pybind11/pybind11.h>
+#include <hip/hip_runtime.h>
+#include <string>
+#include "kernels.h"
+
+namespace py = pybind11;
+using uptr = uintptr_t;
+
+#define P(x) reinterpret_cast<void*>(x)
+#define CP(x) reinterpret_cast<const void*>(x)
+#define FP(x) reinterpret_cast<float*>(x)
+#define CFP(x) reinterpret_cast<const float*>(x)
+#define ST(x) reinterpret_cast<hipStream_t>(x)
+
+static void check_last(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "deep_vision_amd native gfx950 kernels";
+  m.attr("STAT_SHARDS") = DV_STAT_SHARDS;
+
+  m.def("conv_fwd", [](uptr x, uptr w, uptr y, uptr bias, uptr stats, int Nb, int H, int W, int Cg, int ldx, int G,
+                       int Kout, int P_, int Q, int R, int S, int sh, int sw, int ph, int pw, int dh, int dw, int tgather,
+                       int OH, int OW, int osh, int osw, int oph, int opw, int ldy, int act, float slope, uptr st) {
+    ConvFwdArgs a{CP(x), CP(w), P(y), CFP(bias), FP(stats), Nb, H, W, Cg, ldx, G, Kout, P_, Q, R, S, sh, sw, ph, pw,
+                  dh, dw, tgather, OH, OW, osh, osw, oph, opw, ldy, act, slope};
+    int r = dv_conv_fwd(a, ST(st));
+    if (r != 0) throw std::runtime_error("conv_fwd: unsupported geometry (channels must be a multiple of 8)");
+    check_last("conv_fwd");
+  });
+  m.def("conv_wgrad", [](uptr x, uptr dy, uptr dw, int Nb, int H, int W, int Cg, int ldx, int G, int Kout, int P_, int Q,
+                         int ldy, int R, int S, int sh, int sw, int ph, int pw, int dh, int dwl, int splits, uptr st) {
+    ConvWgradArgs a{CP(x), CP(dy), FP(dw), Nb, H, W, Cg, ldx, G, Kout, P_, Q, ldy, R, S, sh, sw, ph, pw, dh, dwl, splits};
+    int r = dv_conv_wgrad(a, ST(st));
+    if (r < 0) throw std::runtime_error("conv_wgrad: unsupported geometry (channels must be a multiple of 8)");
+    check_last("conv_wgrad");
+    return r;
+  });
+
+  m.def("bn_stats", [](uptr x, int64_t rows, int C, uptr acc, uptr st) { dv_bn_stats(CP(x), rows, C, FP(acc), ST(st)); check_last("bn_stats"); });
+  m.def("bn_finalize", [](uptr acc, int C, double count, float eps, float mom, uptr gamma, uptr beta, uptr rm, uptr rv,
+                          uptr smean, uptr sinv, uptr scale, uptr shift, uptr st) {
+    dv_bn_finalize(CFP(acc), C, count, eps, mom, CFP(gamma), CFP(beta), FP(rm), FP(rv), FP(smean), FP(sinv), FP(scale), FP(shift), ST(st));
+    check_last("bn_finalize");
+  });
+  m.def("bn_eval_prep", [](int C, float eps, uptr gamma, uptr beta, uptr rm, uptr rv, uptr scale, uptr shift, uptr st) {
+    dv_bn_eval_prep(C, eps, CFP(gamma), CFP(beta), CFP(rm), CFP(rv), FP(scale), FP(shift), ST(st)); check_last("bn_eval_prep");
+  });
+  m.def("bn_apply", [](uptr x, uptr res, uptr out, int64_t n, int C, uptr scale, uptr shift, int act, float slope, uptr st) {
+    dv_bn_apply(CP(x), CP(res), P(out), n, C, CFP(scale), CFP(shift), act, slope, ST(st)); check_last("bn_apply");
+  });
+  m.def("bn_bwd_reduce", [](uptr dout, uptr out, uptr x, int64_t rows, int C, uptr mean, uptr invstd, int act, float slope,
+                            uptr acc, uptr st) {
+    dv_bn_bwd_reduce(CP(dout), CP(out), CP(x), rows, C, CFP(mean), CFP(invstd), act, slope, FP(acc), ST(st)); check_last("bn_bwd_reduce");
+  });
+  m.def("bn_bwd_finalize", [](uptr acc, int C, double count, uptr gamma, uptr invstd, uptr dgamma, uptr dbeta, uptr kmdz,
+                              uptr kmdzx, uptr kscale, uptr st) {
+    dv_bn_bwd_finalize(CFP(acc), C, count, CFP(gamma), CFP(invstd), FP(dgamma), FP(dbeta), FP(kmdz), FP(kmdzx), FP(kscale), ST(st));
+    check_last("bn_bwd_finalize");
+  });
+  m.def("bn_bwd_apply", [](uptr dout, uptr out, uptr x, uptr dx, uptr dres, int64_t n, int C, uptr mean, uptr invstd,
+                           uptr kmdz, uptr kmdzx, uptr kscale, int act, float slope, uptr st) {
+    dv_bn_bwd_apply(CP(dout), CP(out), CP(x), P(dx), P(dres), n, C, CFP(mean), CFP(invstd), CFP(kmdz), CFP(kmdzx), CFP(kscale), act, slope, ST(st));
+    check_last("bn_bwd_apply");
+  });
+  m.def("bn_bwd_eval", [](uptr dout, uptr out, uptr dx, uptr dres, int64_t n, int C, uptr scale, int act, float slope, uptr st) {
+    dv_bn_bwd_eval(CP(dout), CP(out), P(dx), P(dres), n, C, CFP(scale), act, slope, ST(st)); check_last("bn_bwd_eval");
+  });
+
+  m.def("maxpool_fwd", [](uptr x, uptr y, uptr idx, int N, int H, int W, int C, int P_, int Q, int kh, int kw, int sh, int sw,
+                          int ph, int pw, uptr st) {
+    dv_maxpool_fwd(CP(x), P(y), reinterpret_cast<uint8_t*>(idx), N, H, W, C, P_, Q, kh, kw, sh, sw, ph, pw, ST(st)); check_last("maxpool_fwd");
+  });
+  m.def("maxpool_bwd", [](uptr dy, uptr idx, uptr dx, int N, int H, int W, int C, int P_, int Q, int kh, int kw, int sh,
+                          int sw, int ph, int pw, uptr st) {
+    dv_maxpool_bwd(CP(dy), reinterpret_cast<const uint8_t*>(idx), P(dx), N, H, W, C, P_, Q, kh, kw, sh, sw, ph, pw, ST(st)); check_last("maxpool_bwd");
+  });
+  m.def("avgpool_fwd", [](uptr x, uptr y, int N, int H, int W, int C, int P_, int Q, int kh, int kw, int sh, int sw, int ph,
+                          int pw, int cip, int divover, uptr st) {
+    dv_avgpool_fwd(CP(x), P(y), N, H, W, C, P_, Q, kh, kw, sh, sw, ph, pw, cip, divover, ST(st)); check_last("avgpool_fwd");
+  });
+  m.def("avgpool_bwd", [](uptr dy, uptr dx, int N, int H, int W, int C, int P_, int Q, int kh, int kw, int sh, int sw, int ph,
+                          int pw, int cip, int divover, uptr st) {
+    dv_avgpool_bwd(CP(dy), P(dx), N, H, W, C, P_, Q, kh, kw, sh, sw, ph, pw, cip, divover, ST(st)); check_last("avgpool_bwd");
+  });
+  m.def("gap_fwd", [](uptr x, uptr y, int N, int HW, int C, uptr st) { dv_gap_fwd(CP(x), P(y), N, HW, C, ST(st)); check_last("gap_fwd"); });
+  m.def("gap_bwd", [](uptr dy, uptr dx, int N, int HW, int C, uptr st) { dv_gap_bwd(CP(dy), P(dx), N, HW, C, ST(st)); check_last("gap_bwd"); });
+  m.def("upsample_fwd", [](uptr x, uptr y, int N, int H, int W, int C, int f, uptr st) { dv_upsample_fwd(CP(x), P(y), N, H, W, C, f, ST(st)); check_last("upsample_fwd"); });
+  m.def("upsample_bwd", [](uptr dy, uptr dx, int N, int H, int W, int C, int f, uptr st) { dv_upsample_bwd(CP(dy), P(dx), N, H, W, C, f, ST(st)); check_last("upsample_bwd"); });
+
+  m.def("act_fwd", [](uptr x, uptr y, int64_t n, int act, float slope, uptr st) { dv_act_fwd(CP(x), P(y), n, act, slope, ST(st)); check_last("act_fwd"); });
+  m.def("act_bwd", [](uptr dy, uptr y, uptr dx, int64_t n, int act, float slope, uptr st) { dv_act_bwd(CP(dy), CP(y), P(dx), n, act, slope, ST(st)); check_last("act_bwd"); });
+  m.def("add", [](uptr a, uptr b, uptr y, int64_t n, float alpha, float beta, int act, float slope, uptr st) { dv_add(CP(a), CP(b), P(y), n, alpha, beta, act, slope, ST(st)); check_last("add"); });
+  m.def("dropout", [](uptr x, uptr y, int64_t n, float p, uint64_t seed, uptr st) { dv_dropout(CP(x), P(y), n, p, seed, ST(st)); check_last("dropout"); });
+  m.def("wprep", [](uptr w, uptr out, int G, int Og, int Ig, int R, int S, int Ipad, int mode, uptr st) { dv_wprep(CFP(w), P(out), G, Og, Ig, R, S, Ipad, mode, ST(st)); check_last("wprep"); });
+  m.def("wgrad_unprep", [](uptr src, uptr dst, int G, int Og, int Ig, int R, int S, int Ipad, float alpha, int accumulate, uptr st) {
+    dv_wgrad_unprep(CFP(src), FP(dst), G, Og, Ig, R, S, Ipad, alpha, accumulate, ST(st)); check_last("wgrad_unprep");
+  });
+  m.def("to_nhwc", [](uptr x, int is_f32, uptr y, int N, int C, int H, int W, int Cp, uptr st) { dv_to_nhwc(CP(x), is_f32, P(y), N, C, H, W, Cp, ST(st)); check_last("to_nhwc"); });
+  m.def("f32_to_bf16", [](uptr x, uptr y, int64_t n, uptr st) { dv_f32_to_bf16(CFP(x), P(y), n, ST(st)); check_last("f32_to_bf16"); });
+
+  m.def("softmax_xent", [](uptr logits, int is_bf16, uptr labels, int rows, int C, uptr loss_rows, uptr grad, float gscale,
+                           float ls, uptr st) {
+    dv_softmax_xent(CP(logits), is_bf16, reinterpret_cast<const int64_t*>(labels), rows, C, FP(loss_rows), P(grad), gscale, ls, ST(st));
+    check_last("softmax_xent");
+  });
+  m.def("sgd", [](uptr p, uptr g, uptr buf, int64_t n, float lr, float mom, float damp, float wd, int nesterov, int first,
+                  float gscale, uptr st) { dv_sgd(FP(p), CFP(g), FP(buf), n, lr, mom, damp, wd, nesterov, first, gscale, ST(st)); check_last("sgd"); });
+  m.def("adam", [](uptr p, uptr g, uptr mm, uptr v, int64_t n, float lr, float b1, float b2, float eps, float wd, int decoupled,
+                   float bc1, float bc2, float gscale, uptr st) {
+    dv_adam(FP(p), CFP(g), FP(mm), FP(v), n, lr, b1, b2, eps, wd, decoupled, bc1, bc2, gscale, ST(st)); check_last("adam");
+  });
+  m.def("rmsprop", [](uptr p, uptr g, uptr sq, uptr mom, uptr gavg, int64_t n, float lr, float alpha, float eps, float wd,
+                      float momentum, int centered, float gscale, uptr st) {
+    dv_rmsprop(FP(p), CFP(g), FP(sq), FP(mom), FP(gavg), n, lr, alpha, eps, wd, momentum, centered, gscale, ST(st)); check_last("rmsprop");
+  });
+  m.def("sumsq", [](uptr x, int64_t n, uptr out, uptr st) { dv_sumsq(CFP(x), n, FP(out), ST(st)); check_last("sumsq"); });
+}

@@ -1,0 +1,349 @@
+// BatchNorm2d (training + eval) on bf16 NHWC activations, fp32 statistics.
+// per-channel batch statistics, fused BN-apply + ReLU/LeakyReLU
+// (+ residual add) forward, fused activation-backward + BN-backward.
+//
+// Statistics travel through a sharded fp32 accumulator `acc[SHARDS][2][C]`:
+//   * the conv epilogue (igemm.hip) or `bn_stats_kernel` atomically adds per-block partial
+//     (sum, sumsq) into shard blockIdx % SHARDS — spreads same-address atomics 64 ways;
+//   * `bn_finalize_kernel` folds the shards into mean / invstd / scale / shift and updates
+//     the running statistics with PyTorch semantics (unbiased running_var).
+// Backward uses the same shard layout for (sum dz, sum dz*xhat).
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+constexpr int SHARDS = DV_STAT_SHARDS;
+constexpr int NT = 256;
+
+template <int VEC> struct VecIO;
+template <> struct VecIO<8> {
+  DV_DEVICE static void load(const u16* p, float* v) {
+    uint4 r = *reinterpret_cast<const uint4*>(p);
+    uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { v[2 * i] = bf2f(w[i] & 0xffff); v[2 * i + 1] = bf2f(w[i] >> 16); }
+  }
+  DV_DEVICE static void store(u16* p, const float* v) {
+    uint4 r; r.x = pack2bf(v[0], v[1]); r.y = pack2bf(v[2], v[3]); r.z = pack2bf(v[4], v[5]); r.w = pack2bf(v[6], v[7]);
+    *reinterpret_cast<uint4*>(p) = r;
+  }
+};
+template <> struct VecIO<4> {
+  DV_DEVICE static void load(const u16* p, float* v) {
+    uint2 r = *reinterpret_cast<const uint2*>(p);
+    v[0] = bf2f(r.x & 0xffff); v[1] = bf2f(r.x >> 16); v[2] = bf2f(r.y & 0xffff); v[3] = bf2f(r.y >> 16);
+  }
+  DV_DEVICE static void store(u16* p, const float* v) {
+    uint2 r; r.x = pack2bf(v[0], v[1]); r.y = pack2bf(v[2], v[3]);
+    *reinterpret_cast<uint2*>(p) = r;
+  }
+};
+template <> struct VecIO<2> {
+  DV_DEVICE static void load(const u16* p, float* v) {
+    uint32_t r = *reinterpret_cast<const uint32_t*>(p); v[0] = bf2f(r & 0xffff); v[1] = bf2f(r >> 16);
+  }
+  DV_DEVICE static void store(u16* p, const float* v) { *reinterpret_cast<uint32_t*>(p) = pack2bf(v[0], v[1]); }
+};
+template <> struct VecIO<1> {
+  DV_DEVICE static void load(const u16* p, float* v) { v[0] = bf2f(*p); }
+  DV_DEVICE static void store(u16* p, const float* v) { *p = f2bf(v[0]); }
+};
+
+DV_DEVICE float act_fwd(float z, int act, float slope) {
+  if (act == 1) return fmaxf(z, 0.f);
+  if (act == 2) return z > 0.f ? z : z * slope;
+  return z;
+}
+// derivative from the activation OUTPUT (relu: out>0; leaky: out>0 ? 1 : slope)
+DV_DEVICE float act_bwd(float dout, float out, int act, float slope) {
+  if (act == 1) return out > 0.f ? dout : 0.f;
+  if (act == 2) return out > 0.f ? dout : dout * slope;
+  return dout;
+}
+
+// ---- statistics of an NHWC tensor: rows x C -> shard accumulators ----
+// Thread layout: TPR = C/VEC threads per row (capped at NT); each thread owns VEC channels.
+template <int VEC>
+__global__ __launch_bounds__(NT) void bn_stats_kernel(const u16* __restrict__ x, int64_t rows, int C,
+                                                        float* __restrict__ acc) {
+  __shared__ float sh[2][NT * VEC];
+  const int cg = C / VEC;
+  const int tpr = cg < NT ? cg : NT;
+  const int rpi = NT / tpr;
+  const int tid = threadIdx.x;
+  const int lane_c = tid % tpr, lane_r = tid / tpr;
+  const int64_t rows_per_block = (rows + gridDim.x - 1) / gridDim.x;
+  const int64_t r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
+  for (int cb = 0; cb < cg; cb += tpr) {
+    const int g = cb + lane_c;
+    float s[VEC], q[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) { s[i] = 0.f; q[i] = 0.f; }
+    if (lane_r < rpi && g < cg) {
+      for (int64_t r = r0 + lane_r; r < r1; r += rpi) {
+        float v[VEC];
+        VecIO<VEC>::load(x + r * C + g * VEC, v);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) { s[i] += v[i]; q[i] += v[i] * v[i]; }
+      }
+    }
+    // reduce over lane_r through LDS
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) { sh[0][tid * VEC + i] = s[i]; sh[1][tid * VEC + i] = q[i]; }
+    __syncthreads();
+    if (lane_r == 0 && g < cg) {
+      for (int rr = 1; rr < rpi; ++rr) {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) { s[i] += sh[0][(rr * tpr + lane_c) * VEC + i]; q[i] += sh[1][(rr * tpr + lane_c) * VEC + i]; }
+      }
+      float* a = acc + (int64_t)(blockIdx.x % SHARDS) * 2 * C;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) { atomicAdd(a + g * VEC + i, s[i]); atomicAdd(a + C + g * VEC + i, q[i]); }
+    }
+  }
+}
+
+// ---- fold shards -> mean/invstd/scale/shift, update running stats ----
+__global__ void bn_finalize_kernel(const float* __restrict__ acc, int C, double count, float eps,
+                                   float momentum, const float* __restrict__ gamma, const float* __restrict__ beta,
+                                   float* __restrict__ running_mean, float* __restrict__ running_var,
+                                   float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                                   float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int i = 0; i < SHARDS; ++i) { s += acc[(int64_t)i * 2 * C + c]; q += acc[(int64_t)i * 2 * C + C + c]; }
+  const double mean = s / count;
+  double var = q / count - mean * mean;
+  if (var < 0) var = 0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  save_mean[c] = (float)mean; save_invstd[c] = invstd;
+  scale[c] = g * invstd; shift[c] = b - (float)mean * g * invstd;
+  if (running_mean) {
+    const double unb = count > 1 ? var * count / (count - 1) : var;
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
+  }
+}
+
+// eval-mode scale/shift from running statistics
+__global__ void bn_eval_prep_kernel(int C, float eps, const float* gamma, const float* beta, const float* rm,
+                                    const float* rv, float* scale, float* shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float inv = rsqrtf(rv[c] + eps);
+  const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  scale[c] = g * inv; shift[c] = b - rm[c] * g * inv;
+}
+
+// ---- out = act(x*scale + shift (+res)) ----
+template <int VEC>
+__global__ __launch_bounds__(NT) void bn_apply_kernel(const u16* __restrict__ x, const u16* __restrict__ res,
+                                                        u16* __restrict__ out, int64_t nvec, int C,
+                                                        const float* __restrict__ scale, const float* __restrict__ shift,
+                                                        int act, float slope) {
+  const int cg = C / VEC;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * NT) {
+    const int c0 = (int)(i % cg) * VEC;
+    float v[VEC], r[VEC];
+    VecIO<VEC>::load(x + i * VEC, v);
+    if (res) VecIO<VEC>::load(res + i * VEC, r);
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      float z = v[k] * scale[c0 + k] + shift[c0 + k];
+      if (res) z += r[k];
+      v[k] = act_fwd(z, act, slope);
+    }
+    VecIO<VEC>::store(out + i * VEC, v);
+  }
+}
+
+// ---- backward reduce: sum dz, sum dz*xhat (xhat = (x-mean)*invstd) ----
+template <int VEC>
+__global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(const u16* __restrict__ dout, const u16* __restrict__ out,
+                                                             const u16* __restrict__ x, int64_t rows, int C,
+                                                             const float* __restrict__ mean, const float* __restrict__ invstd,
+                                                             int act, float slope, float* __restrict__ acc) {
+  __shared__ float sh[2][NT * VEC];
+  const int cg = C / VEC;
+  const int tpr = cg < NT ? cg : NT;
+  const int rpi = NT / tpr;
+  const int tid = threadIdx.x;
+  const int lane_c = tid % tpr, lane_r = tid / tpr;
+  const int64_t rows_per_block = (rows + gridDim.x - 1) / gridDim.x;
+  const int64_t r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
+  for (int cb = 0; cb < cg; cb += tpr) {
+    const int g = cb + lane_c;
+    float s[VEC], q[VEC], mu[VEC], is[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) { s[i] = 0.f; q[i] = 0.f; }
+    if (lane_r < rpi && g < cg) {
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) { mu[i] = mean[g * VEC + i]; is[i] = invstd[g * VEC + i]; }
+      for (int64_t r = r0 + lane_r; r < r1; r += rpi) {
+        float d[VEC], o[VEC], xv[VEC];
+        VecIO<VEC>::load(dout + r * C + g * VEC, d);
+        if (act) VecIO<VEC>::load(out + r * C + g * VEC, o);
+        VecIO<VEC>::load(x + r * C + g * VEC, xv);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+          const float dz = act ? act_bwd(d[i], o[i], act, slope) : d[i];
+          s[i] += dz; q[i] += dz * (xv[i] - mu[i]) * is[i];
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) { sh[0][tid * VEC + i] = s[i]; sh[1][tid * VEC + i] = q[i]; }
+    __syncthreads();
+    if (lane_r == 0 && g < cg) {
+      for (int rr = 1; rr < rpi; ++rr) {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) { s[i] += sh[0][(rr * tpr + lane_c) * VEC + i]; q[i] += sh[1][(rr * tpr + lane_c) * VEC + i]; }
+      }
+      float* a = acc + (int64_t)(blockIdx.x % SHARDS) * 2 * C;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) { atomicAdd(a + g * VEC + i, s[i]); atomicAdd(a + C + g * VEC + i, q[i]); }
+    }
+  }
+}
+
+// fold backward shards: dbeta = sum dz, dgamma = sum dz*xhat; coef1/coef2 for the apply pass
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ acc, int C, double count, const float* __restrict__ gamma,
+                                       const float* __restrict__ invstd, float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                       float* __restrict__ k_mean_dz, float* __restrict__ k_mean_dzx, float* __restrict__ k_scale) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int i = 0; i < SHARDS; ++i) { s += acc[(int64_t)i * 2 * C + c]; q += acc[(int64_t)i * 2 * C + C + c]; }
+  if (dbeta) dbeta[c] = (float)s;
+  if (dgamma) dgamma[c] = (float)q;
+  k_mean_dz[c] = (float)(s / count);
+  k_mean_dzx[c] = (float)(q / count);
+  k_scale[c] = (gamma ? gamma[c] : 1.f) * invstd[c];
+}
+
+// dx = k_scale * (dz - mean_dz - xhat * mean_dzx); optionally dres = dz
+template <int VEC>
+__global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const u16* __restrict__ dout, const u16* __restrict__ out,
+                                                            const u16* __restrict__ x, u16* __restrict__ dx, u16* __restrict__ dres,
+                                                            int64_t nvec, int C, const float* __restrict__ mean,
+                                                            const float* __restrict__ invstd, const float* __restrict__ k_mean_dz,
+                                                            const float* __restrict__ k_mean_dzx, const float* __restrict__ k_scale,
+                                                            int act, float slope) {
+  const int cg = C / VEC;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * NT) {
+    const int c0 = (int)(i % cg) * VEC;
+    float d[VEC], o[VEC], xv[VEC], r[VEC];
+    VecIO<VEC>::load(dout + i * VEC, d);
+    if (act) VecIO<VEC>::load(out + i * VEC, o);
+    VecIO<VEC>::load(x + i * VEC, xv);
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      const int c = c0 + k;
+      const float dz = act ? act_bwd(d[k], o[k], act, slope) : d[k];
+      const float xh = (xv[k] - mean[c]) * invstd[c];
+      r[k] = dz;
+      d[k] = k_scale[c] * (dz - k_mean_dz[c] - xh * k_mean_dzx[c]);
+    }
+    VecIO<VEC>::store(dx + i * VEC, d);
+    if (dres) VecIO<VEC>::store(dres + i * VEC, r);
+  }
+}
+
+// eval-mode / frozen-stat backward: dx = scale * dz
+template <int VEC>
+__global__ __launch_bounds__(NT) void bn_bwd_eval_kernel(const u16* __restrict__ dout, const u16* __restrict__ out,
+                                                           u16* __restrict__ dx, u16* __restrict__ dres, int64_t nvec, int C,
+                                                           const float* __restrict__ scale, int act, float slope) {
+  const int cg = C / VEC;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * NT) {
+    const int c0 = (int)(i % cg) * VEC;
+    float d[VEC], o[VEC], r[VEC];
+    VecIO<VEC>::load(dout + i * VEC, d);
+    if (act) VecIO<VEC>::load(out + i * VEC, o);
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      const float dz = act ? act_bwd(d[k], o[k], act, slope) : d[k];
+      r[k] = dz; d[k] = dz * scale[c0 + k];
+    }
+    VecIO<VEC>::store(dx + i * VEC, d);
+    if (dres) VecIO<VEC>::store(dres + i * VEC, r);
+  }
+}
+
+inline int vec_for(int C) { return (C % 8 == 0) ? 8 : (C % 4 == 0) ? 4 : (C % 2 == 0) ? 2 : 1; }
+inline int grid_for(int64_t nvec) {
+  int64_t g = (nvec + NT - 1) / NT;
+  return (int)std::min<int64_t>(std::max<int64_t>(g, 1), 256 * 8);
+}
+inline int reduce_grid(int64_t rows) {
+  // >= 4 blocks/CU worth of parallelism but at least ~32 rows per block
+  int64_t g = std::min<int64_t>(1024, std::max<int64_t>(1, rows / 32));
+  return (int)g;
+}
+}  // namespace
+
+#define DISPATCH_VEC(C, KERNEL, ...)                                              \
+  switch (vec_for(C)) {                                                          \
+    case 8: KERNEL<8> __VA_ARGS__; break;                                          \
+    case 4: KERNEL<4> __VA_ARGS__; break;                                          \
+    case 2: KERNEL<2> __VA_ARGS__; break;                                          \
+    default: KERNEL<1> __VA_ARGS__; break;                                         \
+  }
+
+void dv_bn_stats(const void* x, int64_t rows, int C, float* acc, hipStream_t st) {
+  const int g = reduce_grid(rows);
+  DISPATCH_VEC(C, bn_stats_kernel, <<<g, NT, 0, st>>>((const u16*)x, rows, C, acc))
+}
+
+void dv_bn_finalize(const float* acc, int C, double count, float eps, float momentum, const float* gamma,
+                    const float* beta, float* rm, float* rv, float* save_mean, float* save_invstd, float* scale,
+                    float* shift, hipStream_t st) {
+  bn_finalize_kernel<<<(C + 255) / 256, 256, 0, st>>>(acc, C, count, eps, momentum, gamma, beta, rm, rv, save_mean,
+                                                      save_invstd, scale, shift);
+}
+
+void dv_bn_eval_prep(int C, float eps, const float* gamma, const float* beta, const float* rm, const float* rv,
+                     float* scale, float* shift, hipStream_t st) {
+  bn_eval_prep_kernel<<<(C + 255) / 256, 256, 0, st>>>(C, eps, gamma, beta, rm, rv, scale, shift);
+}
+
+void dv_bn_apply(const void* x, const void* res, void* out, int64_t n, int C, const float* scale, const float* shift,
+                 int act, float slope, hipStream_t st) {
+  const int v = vec_for(C);
+  const int64_t nvec = n / v;
+  const int g = grid_for(nvec);
+  DISPATCH_VEC(C, bn_apply_kernel, <<<g, NT, 0, st>>>((const u16*)x, (const u16*)res, (u16*)out, nvec, C, scale, shift, act, slope))
+}
+
+void dv_bn_bwd_reduce(const void* dout, const void* out, const void* x, int64_t rows, int C, const float* mean,
+                      const float* invstd, int act, float slope, float* acc, hipStream_t st) {
+  const int g = reduce_grid(rows);
+  DISPATCH_VEC(C, bn_bwd_reduce_kernel, <<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, rows, C, mean, invstd, act, slope, acc))
+}
+
+void dv_bn_bwd_finalize(const float* acc, int C, double count, const float* gamma, const float* invstd, float* dgamma,
+                        float* dbeta, float* k_mean_dz, float* k_mean_dzx, float* k_scale, hipStream_t st) {
+  bn_bwd_finalize_kernel<<<(C + 255) / 256, 256, 0, st>>>(acc, C, count, gamma, invstd, dgamma, dbeta, k_mean_dz,
+                                                          k_mean_dzx, k_scale);
+}
+
+void dv_bn_bwd_apply(const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t n, int C,
+                     const float* mean, const float* invstd, const float* k_mean_dz, const float* k_mean_dzx,
+                     const float* k_scale, int act, float slope, hipStream_t st) {
+  const int v = vec_for(C);
+  const int64_t nvec = n / v;
+  const int g = grid_for(nvec);
+  DISPATCH_VEC(C, bn_bwd_apply_kernel, <<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, (u16*)dx, (u16*)dres, nvec, C, mean, invstd, k_mean_dz, k_mean_dzx, k_scale, act, slope))
+}
+
+void dv_bn_bwd_eval(const void* dout, const void* out, void* dx, void* dres, int64_t n, int C, const float* scale,
+                    int act, float slope, hipStream_t st) {
+  const int v = vec_for(C);
+  const int64_t nvec = n / v;
+  const int g = grid_for(nvec);
+  DISPATCH_VEC(C, bn_bwd_eval_kernel, <<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (u16*)dx, (u16*)dres, nvec, C, scale, act, slope))
+}

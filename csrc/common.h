@@ -1,0 +1,82 @@
+// Shared device helpers for the deep_vision_amd gfx950 (CDNA4) kernels.
+//
+// Conventions used by every kernel in csrc/:
+//   * Activations are bf16, physically NHWC ("channels_last"), logically NCHW in PyTorch.
+//   * Weights handed to MFMA kernels are bf16 [Cout][R][S][Cin] (K-contiguous rows).
+//   * Statistics / optimizer state / master weights are fp32.
+//   * Wave size is 64 (hard-coded, never warpSize arithmetic on 32).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DV_DEVICE __device__ __forceinline__
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef short i16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16;
+
+#define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
+#define GLB_PTR(p) ((const __attribute__((address_space(1))) void*)(p))
+
+// ---- bf16 <-> fp32 (round-to-nearest-even; NaN preserved by the hardware cvt path) ----
+DV_DEVICE float bf2f(u16 v) { return __uint_as_float(((uint32_t)v) << 16); }
+DV_DEVICE u16 f2bf(float f) {
+  __bf16 b = (__bf16)f;  // hipcc emits v_cvt_pk_bf16_f32 at -O3 (RNE, NaN-safe)
+  return __builtin_bit_cast(u16, b);
+}
+DV_DEVICE uint32_t pack2bf(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+// ---- wave / block reductions (wave64) ----
+DV_DEVICE float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+DV_DEVICE float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// Sum within each 16-lane row via DPP (all 16 lanes receive the row sum).
+DV_DEVICE float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));  // quad_perm [2,3,0,1]
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x124, 0xF, 0xF, false)); // row_ror:4
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false)); // row_ror:8
+  return v;
+}
+
+// Block-wide sum for blockDim.x == NT (multiple of 64). `sh` needs NT/64 floats.
+template <int NT>
+DV_DEVICE float block_sum(float v, float* sh) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) sh[w] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) t += sh[i];
+  return t;
+}
+
+// ---- XCD-aware bijective block remap (MI355X: 8 XCDs, blocks dealt round-robin) ----
+// Consecutive *logical* tiles land on the same XCD so that tiles sharing an operand
+// panel hit the same L2. Bijective for any nwg (see cdna_hip_programming.md §5).
+DV_DEVICE int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, loc = bid >> 3;
+  const int q = nwg >> 3, r = nwg & 7;
+  const int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + loc;
+}
+
+// 16-byte aligned zero page used as the source address of padded / out-of-range
+// LDS-DMA lanes (global_load_lds cannot predicate a lane to "write zeros").
+extern __device__ __attribute__((aligned(16))) char dv_zero_page[256];
+
+#define DV_CHECK_LAUNCH() (void)hipGetLastError()

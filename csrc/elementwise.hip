@@ -1,0 +1,203 @@
+// Vectorized elementwise kernels and layout/cast preparation.
+//   * activations fwd/bwd (relu / leaky / tanh / sigmoid) on bf16, 16-B vectors
+//   * residual add, scale
+//   * dropout with a counter-based hash RNG: the mask is regenerated in backward from
+//     (seed, element index), so nothing but the seed is saved
+//   * weight preparation: fp32 OIHW master weights -> bf16 MFMA operand layouts
+//       mode 0: [G][Og][R][S][Ig_pad]   (forward: K-contiguous rows)
+//       mode 1: [G][Ig][R][S][Og_pad]   (dgrad / ConvTranspose forward)
+//   * fp32 / bf16 NCHW -> bf16 NHWC with channel padding (network input)
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+constexpr int NT = 256;
+
+DV_DEVICE void ld8(const u16* p, float* v) {
+  uint4 r = *reinterpret_cast<const uint4*>(p); uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { v[2 * i] = bf2f(w[i] & 0xffff); v[2 * i + 1] = bf2f(w[i] >> 16); }
+}
+DV_DEVICE void st8(u16* p, const float* v) {
+  uint4 r; r.x = pack2bf(v[0], v[1]); r.y = pack2bf(v[2], v[3]); r.z = pack2bf(v[4], v[5]); r.w = pack2bf(v[6], v[7]);
+  *reinterpret_cast<uint4*>(p) = r;
+}
+
+enum { A_RELU = 1, A_LEAKY = 2, A_TANH = 3, A_SIGMOID = 4 };
+
+DV_DEVICE float actf(float x, int a, float s) {
+  switch (a) {
+    case A_RELU: return fmaxf(x, 0.f);
+    case A_LEAKY: return x > 0.f ? x : x * s;
+    case A_TANH: return tanhf(x);
+    case A_SIGMOID: return 1.f / (1.f + __expf(-x));
+    default: return x;
+  }
+}
+// gradient from the OUTPUT y
+DV_DEVICE float actb(float dy, float y, int a, float s) {
+  switch (a) {
+    case A_RELU: return y > 0.f ? dy : 0.f;
+    case A_LEAKY: return y > 0.f ? dy : dy * s;
+    case A_TANH: return dy * (1.f - y * y);
+    case A_SIGMOID: return dy * y * (1.f - y);
+    default: return dy;
+  }
+}
+
+// n8 = number of 8-vectors, tail handled by the scalar kernel
+__global__ __launch_bounds__(NT) void act_fwd_kernel(const u16* __restrict__ x, u16* __restrict__ y, int64_t n, int a, float s) {
+  const int64_t n8 = n / 8;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n8; i += (int64_t)gridDim.x * NT) {
+    float v[8]; ld8(x + i * 8, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = actf(v[k], a, s);
+    st8(y + i * 8, v);
+  }
+  const int64_t t = n8 * 8 + blockIdx.x * (int64_t)NT + threadIdx.x;
+  if (t < n && blockIdx.x * (int64_t)NT + threadIdx.x < 8) y[t] = f2bf(actf(bf2f(x[t]), a, s));
+}
+
+__global__ __launch_bounds__(NT) void act_bwd_kernel(const u16* __restrict__ dy, const u16* __restrict__ y,
+                                                       u16* __restrict__ dx, int64_t n, int a, float s) {
+  const int64_t n8 = n / 8;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n8; i += (int64_t)gridDim.x * NT) {
+    float d[8], v[8]; ld8(dy + i * 8, d); ld8(y + i * 8, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] = actb(d[k], v[k], a, s);
+    st8(dx + i * 8, d);
+  }
+  const int64_t t = n8 * 8 + blockIdx.x * (int64_t)NT + threadIdx.x;
+  if (t < n && blockIdx.x * (int64_t)NT + threadIdx.x < 8) dx[t] = f2bf(actb(bf2f(dy[t]), bf2f(y[t]), a, s));
+}
+
+// y = alpha*a + beta*b, optional activation
+__global__ __launch_bounds__(NT) void add_kernel(const u16* __restrict__ a, const u16* __restrict__ b, u16* __restrict__ y,
+                                                   int64_t n, float alpha, float beta, int act, float s) {
+  const int64_t n8 = n / 8;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n8; i += (int64_t)gridDim.x * NT) {
+    float u[8], v[8]; ld8(a + i * 8, u); ld8(b + i * 8, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) u[k] = actf(alpha * u[k] + beta * v[k], act, s);
+    st8(y + i * 8, u);
+  }
+  const int64_t t = n8 * 8 + blockIdx.x * (int64_t)NT + threadIdx.x;
+  if (t < n && blockIdx.x * (int64_t)NT + threadIdx.x < 8) y[t] = f2bf(actf(alpha * bf2f(a[t]) + beta * bf2f(b[t]), act, s));
+}
+
+DV_DEVICE uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
+  // murmur3-style finalizer over a 96-bit key (counter-based, stateless)
+  uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u ^ c * 0xC2B2AE3Du;
+  h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+  return h;
+}
+
+// y = x * mask / (1-p);   mask_i = hash(seed, i) >= p*2^32
+__global__ __launch_bounds__(NT) void dropout_kernel(const u16* __restrict__ x, u16* __restrict__ y, int64_t n, uint32_t thr,
+                                                       float scale, uint32_t seed_lo, uint32_t seed_hi) {
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+    const uint32_t h = hash3(seed_lo, seed_hi, (uint32_t)i ^ (uint32_t)(i >> 32) * 0x27D4EB2Fu);
+    y[i] = (h >= thr) ? f2bf(bf2f(x[i]) * scale) : (u16)0;
+  }
+}
+
+__global__ void wprep_kernel(const float* __restrict__ w, u16* __restrict__ out, int G, int Og, int Ig, int R, int S,
+                             int pad, int mode) {
+  // mode 0: out[g][o][r][s][i], i padded to `pad` (>= Ig)
+  // mode 1: out[g][i][r][s][o], o padded to `pad` (>= Og)
+  const int64_t total = mode == 0 ? (int64_t)G * Og * pad * R * S : (int64_t)G * Ig * pad * R * S;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    int64_t u = t;
+    int g, o, i, r, s;
+    bool ok;
+    if (mode == 0) {
+      i = (int)(u % pad); u /= pad;
+      s = (int)(u % S); u /= S;
+      r = (int)(u % R); u /= R;
+      o = (int)(u % Og); g = (int)(u / Og);
+      ok = i < Ig;
+    } else {
+      o = (int)(u % pad); u /= pad;
+      s = (int)(u % S); u /= S;
+      r = (int)(u % R); u /= R;
+      i = (int)(u % Ig); g = (int)(u / Ig);
+      ok = o < Og;
+    }
+    out[t] = ok ? f2bf(w[((((int64_t)(g * Og + o)) * Ig + i) * R + r) * S + s]) : (u16)0;
+  }
+}
+
+// fp32 [G][O][R][S][Ipad] gradient (kernel layout) -> fp32 OIHW param-grad layout (drop padding)
+__global__ void wgrad_unprep_kernel(const float* __restrict__ src, float* __restrict__ dst, int G, int Og, int Ig,
+                                    int R, int S, int Ipad, float alpha, int accumulate) {
+  const int64_t total = (int64_t)G * Og * Ig * R * S;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    int64_t u = t;  // dst index: [o][i][r][s]
+    const int s = (int)(u % S); u /= S;
+    const int r = (int)(u % R); u /= R;
+    const int i = (int)(u % Ig); const int64_t o = u / Ig;  // o includes group
+    const float v = alpha * src[((o * R + r) * S + s) * Ipad + i];
+    dst[t] = accumulate ? dst[t] + v : v;
+  }
+}
+
+// NCHW (fp32 or bf16) -> NHWC bf16 with channel padding
+template <typename T>
+__global__ void to_nhwc_kernel(const T* __restrict__ x, u16* __restrict__ y, int N, int C, int H, int W, int Cp) {
+  const int64_t total = (int64_t)N * H * W * Cp;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    int64_t u = t;
+    const int c = (int)(u % Cp); u /= Cp;
+    const int w = (int)(u % W); u /= W;
+    const int h = (int)(u % H); const int n = (int)(u / H);
+    float v = 0.f;
+    if (c < C) {
+      const int64_t src = (((int64_t)n * C + c) * H + h) * W + w;
+      if constexpr (sizeof(T) == 4) v = x[src]; else v = bf2f(x[src]);
+    }
+    y[t] = f2bf(v);
+  }
+}
+
+__global__ void f32_to_bf16_kernel(const float* __restrict__ x, u16* __restrict__ y, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) y[i] = f2bf(x[i]);
+}
+
+inline int grid_for(int64_t total, int per = 1) {
+  int64_t g = (total / per + NT - 1) / NT;
+  return (int)std::min<int64_t>(std::max<int64_t>(g, 1), 256 * 16);
+}
+}  // namespace
+
+void dv_act_fwd(const void* x, void* y, int64_t n, int act, float slope, hipStream_t st) {
+  act_fwd_kernel<<<grid_for(n, 8), NT, 0, st>>>((const u16*)x, (u16*)y, n, act, slope);
+}
+void dv_act_bwd(const void* dy, const void* y, void* dx, int64_t n, int act, float slope, hipStream_t st) {
+  act_bwd_kernel<<<grid_for(n, 8), NT, 0, st>>>((const u16*)dy, (const u16*)y, (u16*)dx, n, act, slope);
+}
+void dv_add(const void* a, const void* b, void* y, int64_t n, float alpha, float beta, int act, float slope, hipStream_t st) {
+  add_kernel<<<grid_for(n, 8), NT, 0, st>>>((const u16*)a, (const u16*)b, (u16*)y, n, alpha, beta, act, slope);
+}
+void dv_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, hipStream_t st) {
+  const double thr = (double)p * 4294967296.0;
+  const uint32_t t = thr >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)thr;
+  const float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  dropout_kernel<<<grid_for(n), NT, 0, st>>>((const u16*)x, (u16*)y, n, t, scale, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+void dv_wprep(const float* w, void* out, int G, int Og, int Ig, int R, int S, int pad, int mode, hipStream_t st) {
+  const int64_t total = (int64_t)G * (mode == 0 ? Og : Ig) * pad * R * S;
+  wprep_kernel<<<grid_for(total), NT, 0, st>>>(w, (u16*)out, G, Og, Ig, R, S, pad, mode);
+}
+void dv_wgrad_unprep(const float* src, float* dst, int G, int Og, int Ig, int R, int S, int Ipad, float alpha,
+                     int accumulate, hipStream_t st) {
+  const int64_t total = (int64_t)G * Og * Ig * R * S;
+  wgrad_unprep_kernel<<<grid_for(total), NT, 0, st>>>(src, dst, G, Og, Ig, R, S, Ipad, alpha, accumulate);
+}
+void dv_to_nhwc(const void* x, int x_is_f32, void* y, int N, int C, int H, int W, int Cp, hipStream_t st) {
+  const int64_t total = (int64_t)N * H * W * Cp;
+  if (x_is_f32) to_nhwc_kernel<float><<<grid_for(total), NT, 0, st>>>((const float*)x, (u16*)y, N, C, H, W, Cp);
+  else to_nhwc_kernel<u16><<<grid_for(total), NT, 0, st>>>((const u16*)x, (u16*)y, N, C, H, W, Cp);
+}
+void dv_f32_to_bf16(const float* x, void* y, int64_t n, hipStream_t st) {
+  f32_to_bf16_kernel<<<grid_for(n), NT, 0, st>>>(x, (u16*)y, n);
+}

@@ -1,0 +1,91 @@
+// Host-side entry points of every deep_vision_amd gfx950 kernel (called from bindings.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <algorithm>
+
+#define DV_STAT_SHARDS 64
+
+struct ConvFwdArgs {
+  const void* x;      // bf16 NHWC gathered tensor (input, or dY for dgrad)
+  const void* w;      // bf16 [G][Kout][R][S][Cg]
+  void* y;            // bf16 NHWC output
+  const float* bias;  // [G*Kout] or nullptr
+  float* stats;       // [tiles_m][2][G*Kout] or nullptr
+  int Nb, H, W, Cg, ldx, G;
+  int Kout, P, Q;     // GEMM columns per group, pixel grid enumerated by m
+  int R, S, sh, sw, ph, pw, dh, dw;
+  int tgather;        // transposed-conv gather (dgrad with stride > 1)
+  int OH, OW, osh, osw, oph, opw, ldy;  // output pixel mapping
+  int act; float slope;
+};
+
+struct ConvWgradArgs {
+  const void* x;   // bf16 NHWC forward input (im2col source)
+  const void* dy;  // bf16 NHWC gradient of the output
+  float* dw;       // fp32 [G][Kout][R][S][Cg]
+  int Nb, H, W, Cg, ldx, G;
+  int Kout, P, Q, ldy;
+  int R, S, sh, sw, ph, pw, dh, dw_;
+  int splits;      // 0 = heuristic
+};
+
+int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st);
+int dv_conv_wgrad(const ConvWgradArgs& a, hipStream_t st);
+int dv_conv_wgrad_splits(const ConvWgradArgs& a);
+int dv_conv_stats_tiles(int Nb, int P, int Q);
+
+// ---- batchnorm (bn.hip) ----
+void dv_bn_stats(const void* x, int64_t rows, int C, float* acc, hipStream_t st);
+void dv_bn_finalize(const float* acc, int C, double count, float eps, float momentum, const float* gamma,
+                    const float* beta, float* rm, float* rv, float* save_mean, float* save_invstd, float* scale,
+                    float* shift, hipStream_t st);
+void dv_bn_eval_prep(int C, float eps, const float* gamma, const float* beta, const float* rm, const float* rv,
+                     float* scale, float* shift, hipStream_t st);
+void dv_bn_apply(const void* x, const void* res, void* out, int64_t n, int C, const float* scale, const float* shift,
+                 int act, float slope, hipStream_t st);
+void dv_bn_bwd_reduce(const void* dout, const void* out, const void* x, int64_t rows, int C, const float* mean,
+                      const float* invstd, int act, float slope, float* acc, hipStream_t st);
+void dv_bn_bwd_finalize(const float* acc, int C, double count, const float* gamma, const float* invstd, float* dgamma,
+                        float* dbeta, float* k_mean_dz, float* k_mean_dzx, float* k_scale, hipStream_t st);
+void dv_bn_bwd_apply(const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t n, int C,
+                     const float* mean, const float* invstd, const float* k_mean_dz, const float* k_mean_dzx,
+                     const float* k_scale, int act, float slope, hipStream_t st);
+void dv_bn_bwd_eval(const void* dout, const void* out, void* dx, void* dres, int64_t n, int C, const float* scale,
+                    int act, float slope, hipStream_t st);
+
+// ---- pooling (pool.hip) ----
+void dv_maxpool_fwd(const void* x, void* y, uint8_t* idx, int N, int H, int W, int C, int P, int Q, int kh, int kw,
+                    int sh, int sw, int ph, int pw, hipStream_t st);
+void dv_maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, int N, int H, int W, int C, int P, int Q, int kh,
+                    int kw, int sh, int sw, int ph, int pw, hipStream_t st);
+void dv_avgpool_fwd(const void* x, void* y, int N, int H, int W, int C, int P, int Q, int kh, int kw, int sh, int sw,
+                    int ph, int pw, int cip, int divover, hipStream_t st);
+void dv_avgpool_bwd(const void* dy, void* dx, int N, int H, int W, int C, int P, int Q, int kh, int kw, int sh, int sw,
+                    int ph, int pw, int cip, int divover, hipStream_t st);
+void dv_gap_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st);
+void dv_gap_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st);
+void dv_upsample_fwd(const void* x, void* y, int N, int H, int W, int C, int f, hipStream_t st);
+void dv_upsample_bwd(const void* dy, void* dx, int N, int H, int W, int C, int f, hipStream_t st);
+
+// ---- elementwise / layout (elementwise.hip) ----
+void dv_act_fwd(const void* x, void* y, int64_t n, int act, float slope, hipStream_t st);
+void dv_act_bwd(const void* dy, const void* y, void* dx, int64_t n, int act, float slope, hipStream_t st);
+void dv_add(const void* a, const void* b, void* y, int64_t n, float alpha, float beta, int act, float slope, hipStream_t st);
+void dv_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, hipStream_t st);
+void dv_wprep(const float* w, void* out, int G, int Og, int Ig, int R, int S, int Ipad, int mode, hipStream_t st);
+void dv_wgrad_unprep(const float* src, float* dst, int G, int Og, int Ig, int R, int S, int Ipad, float alpha,
+                     int accumulate, hipStream_t st);
+void dv_to_nhwc(const void* x, int x_is_f32, void* y, int N, int C, int H, int W, int Cp, hipStream_t st);
+void dv_f32_to_bf16(const float* x, void* y, int64_t n, hipStream_t st);
+
+// ---- loss / optimizers (loss_optim.hip) ----
+void dv_softmax_xent(const void* logits, int is_bf16, const int64_t* labels, int rows, int C, float* loss_rows, void* grad,
+                     float grad_scale, float label_smoothing, hipStream_t st);
+void dv_sgd(float* p, const float* g, float* buf, int64_t n, float lr, float momentum, float dampening, float wd,
+            int nesterov, int first, float gscale, hipStream_t st);
+void dv_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps, float wd,
+             int decoupled, float bc1, float bc2, float gscale, hipStream_t st);
+void dv_rmsprop(float* p, const float* g, float* sq, float* mom, float* gavg, int64_t n, float lr, float alpha, float eps,
+                float wd, float momentum, int centered, float gscale, hipStream_t st);
+void dv_sumsq(const float* x, int64_t n, float* out, hipStream_t st);

@@ -1,0 +1,150 @@
+// Softmax cross-entropy and fused optimizers over flat fp32 buffers (K20).
+//
+// softmax_xent: one block per row; single pass over the logits computes the row max and the
+//   log-sum-exp (online), the loss, and writes d(loss)/d(logits) = (softmax - onehot) * scale
+//   in the same launch, so the backward is free (the autograd node only rescales when the
+//   upstream gradient is not 1).
+// optimizers: one grid-stride launch updates every parameter of the model (flat buffer):
+//   SGD      d = g*gs + wd*p ; buf = m*buf + (1-dampening)*d (first step buf = d) ; p -= lr*(nesterov ? d + m*buf : buf)
+//   Adam     PyTorch semantics incl. bias correction, optional decoupled (AdamW) decay
+//   RMSprop  PyTorch semantics (alpha, eps, momentum, centered)
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+constexpr int NT = 256;
+
+template <bool BF16>
+__global__ __launch_bounds__(NT) void softmax_xent_kernel(const void* __restrict__ logits, const int64_t* __restrict__ labels,
+                                                            int C, float* __restrict__ loss_rows, void* __restrict__ grad,
+                                                            float grad_scale, float label_smoothing) {
+  __shared__ float sh[NT / 64];
+  const int row = blockIdx.x;
+  const int64_t base = (int64_t)row * C;
+  auto ld = [&](int c) -> float {
+    if (BF16) return bf2f(reinterpret_cast<const u16*>(logits)[base + c]);
+    return reinterpret_cast<const float*>(logits)[base + c];
+  };
+  float m = -INFINITY, s = 0.f, sumx = 0.f;
+  for (int c = threadIdx.x; c < C; c += NT) {
+    const float v = ld(c);
+    sumx += v;
+    if (v > m) { s = s * __expf(m - v) + 1.f; m = v; } else s += __expf(v - m);
+  }
+  // combine (m, s) across the block
+  float gm = wave_max(m);
+  {
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) sh[w] = gm;
+    __syncthreads();
+    gm = sh[0];
+#pragma unroll
+    for (int i = 1; i < NT / 64; ++i) gm = fmaxf(gm, sh[i]);
+    __syncthreads();
+  }
+  float ss = (m == -INFINITY) ? 0.f : s * __expf(m - gm);
+  ss = block_sum<NT>(ss, sh);
+  const float lse = gm + __logf(ss);
+  const int64_t lab = labels[row];
+  const bool valid = lab >= 0 && lab < C;
+  float sx = (label_smoothing > 0.f) ? block_sum<NT>(sumx, sh) : 0.f;
+  if (threadIdx.x == 0) {
+    float l = valid ? (lse - ld((int)lab)) : 0.f;
+    if (label_smoothing > 0.f) l = (1.f - label_smoothing) * l + label_smoothing * (lse - sx / C);
+    loss_rows[row] = l;
+  }
+  if (grad) {
+    const float off = label_smoothing / C;
+    for (int c = threadIdx.x; c < C; c += NT) {
+      float g = __expf(ld(c) - lse);
+      if (label_smoothing > 0.f) g -= off + (c == lab ? (1.f - label_smoothing) : 0.f);
+      else if (c == lab) g -= 1.f;
+      if (!valid) g = 0.f;
+      g *= grad_scale;
+      if (BF16) reinterpret_cast<u16*>(grad)[base + c] = f2bf(g);
+      else reinterpret_cast<float*>(grad)[base + c] = g;
+    }
+  }
+}
+
+__global__ __launch_bounds__(NT) void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ buf,
+                                                   int64_t n, float lr, float momentum, float dampening, float wd,
+                                                   int nesterov, int first, float gscale) {
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+    const float pv = p[i];
+    float d = g[i] * gscale + wd * pv;
+    if (momentum != 0.f) {
+      float b = first ? d : momentum * buf[i] + (1.f - dampening) * d;
+      buf[i] = b;
+      d = nesterov ? d + momentum * b : b;
+    }
+    p[i] = pv - lr * d;
+  }
+}
+
+__global__ __launch_bounds__(NT) void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                                    float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps,
+                                                    float wd, int decoupled, float bc1, float bc2, float gscale) {
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+    float pv = p[i];
+    float gv = g[i] * gscale;
+    if (decoupled) pv *= (1.f - lr * wd); else gv += wd * pv;
+    const float mv = b1 * m[i] + (1.f - b1) * gv;
+    const float vv = b2 * v[i] + (1.f - b2) * gv * gv;
+    m[i] = mv; v[i] = vv;
+    const float denom = sqrtf(vv / bc2) + eps;
+    p[i] = pv - (lr / bc1) * mv / denom;
+  }
+}
+
+__global__ __launch_bounds__(NT) void rmsprop_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ sq,
+                                                       float* __restrict__ mom, float* __restrict__ gavg, int64_t n, float lr,
+                                                       float alpha, float eps, float wd, float momentum, int centered, float gscale) {
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+    const float pv = p[i];
+    const float gv = g[i] * gscale + wd * pv;
+    const float s = alpha * sq[i] + (1.f - alpha) * gv * gv;
+    sq[i] = s;
+    float avg;
+    if (centered) { const float ga = alpha * gavg[i] + (1.f - alpha) * gv; gavg[i] = ga; avg = sqrtf(s - ga * ga) + eps; }
+    else avg = sqrtf(s) + eps;
+    if (momentum > 0.f) { const float b = momentum * mom[i] + gv / avg; mom[i] = b; p[i] = pv - lr * b; }
+    else p[i] = pv - lr * gv / avg;
+  }
+}
+
+// sum of squares (grad-norm / non-finite detection): block partials -> atomic
+__global__ __launch_bounds__(NT) void sumsq_kernel(const float* __restrict__ x, int64_t n, float* __restrict__ out) {
+  __shared__ float sh[NT / 64];
+  float s = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) { const float v = x[i]; s += v * v; }
+  s = block_sum<NT>(s, sh);
+  if (threadIdx.x == 0) atomicAdd(out, s);
+}
+
+inline int grid_for(int64_t n) {
+  int64_t g = (n + NT - 1) / NT;
+  return (int)std::min<int64_t>(std::max<int64_t>(g, 1), 256 * 8);
+}
+}  // namespace
+
+void dv_softmax_xent(const void* logits, int is_bf16, const int64_t* labels, int rows, int C, float* loss_rows, void* grad,
+                     float grad_scale, float label_smoothing, hipStream_t st) {
+  if (is_bf16) softmax_xent_kernel<true><<<rows, NT, 0, st>>>(logits, labels, C, loss_rows, grad, grad_scale, label_smoothing);
+  else softmax_xent_kernel<false><<<rows, NT, 0, st>>>(logits, labels, C, loss_rows, grad, grad_scale, label_smoothing);
+}
+void dv_sgd(float* p, const float* g, float* buf, int64_t n, float lr, float momentum, float dampening, float wd,
+            int nesterov, int first, float gscale, hipStream_t st) {
+  sgd_kernel<<<grid_for(n), NT, 0, st>>>(p, g, buf, n, lr, momentum, dampening, wd, nesterov, first, gscale);
+}
+void dv_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps, float wd,
+             int decoupled, float bc1, float bc2, float gscale, hipStream_t st) {
+  adam_kernel<<<grid_for(n), NT, 0, st>>>(p, g, m, v, n, lr, b1, b2, eps, wd, decoupled, bc1, bc2, gscale);
+}
+void dv_rmsprop(float* p, const float* g, float* sq, float* mom, float* gavg, int64_t n, float lr, float alpha, float eps,
+                float wd, float momentum, int centered, float gscale, hipStream_t st) {
+  rmsprop_kernel<<<grid_for(n), NT, 0, st>>>(p, g, sq, mom, gavg, n, lr, alpha, eps, wd, momentum, centered, gscale);
+}
+void dv_sumsq(const float* x, int64_t n, float* out, hipStream_t st) {
+  sumsq_kernel<<<std::min(grid_for(n), 1024), NT, 0, st>>>(x, n, out);
+}

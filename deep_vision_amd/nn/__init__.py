@@ -1,0 +1,179 @@
+"""Layer modules: drop-in subclasses of the torch.nn layers used by the reference.
+
+Parameter / buffer names and shapes are exactly torch's, so checkpoints are key-compatible
+with the reference's ``state_dict``s (e.g. ``conv2x.0.projection.1.running_mean``). On GPU
+tensors ``forward`` dispatches to the native gfx950 kernels (deep_vision_amd.ops).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as tnn
+
+from .. import ops as F
+from ..ops.common import native
+
+__all__ = [
+    "Conv2d", "ConvTranspose2d", "Linear", "BatchNorm2d", "ReLU", "LeakyReLU", "Tanh", "Sigmoid", "MaxPool2d",
+    "AvgPool2d", "AdaptiveAvgPool2d", "Dropout", "Upsample", "LocalResponseNorm", "Flatten", "Sequential",
+    "ZeroPad2d", "ReflectionPad2d", "ChannelShuffle", "Identity",
+]
+
+Sequential = tnn.Sequential
+Flatten = tnn.Flatten
+Identity = tnn.Identity
+
+
+def _same_pad(k, s, d=1):
+    """Keras 'same' padding: total = max((ceil(i/s)-1)*s + (k-1)*d + 1 - i, 0) — input dependent."""
+    return k, s, d
+
+
+class Conv2d(tnn.Conv2d):
+    """torch.nn.Conv2d; ``padding='same_keras'`` reproduces TF/Keras asymmetric 'same' padding
+    (extra row/col at the bottom/right at stride 2)."""
+
+    def __init__(self, *args, padding=0, **kw):
+        self.keras_same = padding == "same_keras"
+        super().__init__(*args, padding=0 if self.keras_same else padding, **kw)
+
+    def _keras_pads(self, H, W):
+        out = []
+        for i, k, s, d in ((H, self.kernel_size[0], self.stride[0], self.dilation[0]),
+                           (W, self.kernel_size[1], self.stride[1], self.dilation[1])):
+            o = -(-i // s)
+            tot = max((o - 1) * s + (k - 1) * d + 1 - i, 0)
+            out.append((tot // 2, tot - tot // 2))
+        return out
+
+    def forward(self, x):
+        if self.keras_same:
+            (pt, pb), (pl, pr) = self._keras_pads(x.shape[2], x.shape[3])
+            if pt == pb and pl == pr:
+                return F.conv2d(x, self.weight, self.bias, self.stride, (pt, pl), self.dilation, self.groups)
+            x = pad2d(x, (pl, pr, pt, pb))
+            return F.conv2d(x, self.weight, self.bias, self.stride, 0, self.dilation, self.groups)
+        if self.padding_mode != "zeros":
+            return super().forward(x) if not native(x) else F.conv2d(
+                tnn.functional.pad(x, self._reversed_padding_repeated_twice, mode=self.padding_mode), self.weight,
+                self.bias, self.stride, 0, self.dilation, self.groups)
+        return F.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, self.groups)
+
+
+def pad2d(x, pads, mode="constant"):
+    """(left, right, top, bottom) padding in the native layout."""
+    y = tnn.functional.pad(x, pads, mode=mode)
+    if native(x):
+        y = y.contiguous(memory_format=torch.channels_last)
+    return y
+
+
+class ConvTranspose2d(tnn.ConvTranspose2d):
+    def forward(self, x, output_size=None):
+        if output_size is not None or not native(x):
+            return super().forward(x, output_size)
+        return F.conv_transpose2d(x, self.weight, self.bias, self.stride, self.padding, self.output_padding,
+                                  self.groups, self.dilation)
+
+
+class Linear(tnn.Linear):
+    def forward(self, x):
+        return F.linear(x, self.weight, self.bias)
+
+
+class BatchNorm2d(tnn.BatchNorm2d):
+    def forward(self, x):
+        if not native(x):
+            return super().forward(x)
+        return F.batch_norm_act(x, self)
+
+
+class ReLU(tnn.ReLU):
+    def forward(self, x):
+        return F.relu(x) if native(x) else super().forward(x)
+
+
+class LeakyReLU(tnn.LeakyReLU):
+    def forward(self, x):
+        return F.leaky_relu(x, self.negative_slope) if native(x) else super().forward(x)
+
+
+class Tanh(tnn.Tanh):
+    def forward(self, x):
+        return F.activation(x, "tanh") if native(x) else super().forward(x)
+
+
+class Sigmoid(tnn.Sigmoid):
+    def forward(self, x):
+        return F.activation(x, "sigmoid") if native(x) else super().forward(x)
+
+
+class MaxPool2d(tnn.MaxPool2d):
+    def forward(self, x):
+        if not native(x) or self.dilation not in (1, (1, 1)) or self.return_indices:
+            return super().forward(x)
+        return F.max_pool2d(x, self.kernel_size, self.stride, self.padding, self.ceil_mode)
+
+
+class AvgPool2d(tnn.AvgPool2d):
+    def forward(self, x):
+        if not native(x):
+            return super().forward(x)
+        return F.avg_pool2d(x, self.kernel_size, self.stride, self.padding, self.ceil_mode, self.count_include_pad,
+                            self.divisor_override)
+
+
+class AdaptiveAvgPool2d(tnn.AdaptiveAvgPool2d):
+    def forward(self, x):
+        return F.adaptive_avg_pool2d(x, self.output_size) if native(x) else super().forward(x)
+
+
+class Dropout(tnn.Dropout):
+    def forward(self, x):
+        return F.dropout(x, self.p, self.training) if native(x) else super().forward(x)
+
+
+class Upsample(tnn.Upsample):
+    def forward(self, x):
+        if native(x) and self.mode == "nearest" and self.scale_factor is not None:
+            return F.upsample_nearest(x, self.scale_factor)
+        return super().forward(x)
+
+
+class LocalResponseNorm(tnn.LocalResponseNorm):
+    """torch LRN semantics (window ``size`` across channels; the reference uses size = C,
+    R/AlexNet/pytorch/models/alexnet_v1.py:41). Native kernel: deep_vision_amd.ops.lrn."""
+
+    def forward(self, x):
+        if not native(x):
+            return super().forward(x)
+        from ..ops.lrn import local_response_norm
+
+        return local_response_norm(x, self.size, self.alpha, self.beta, self.k)
+
+
+class ZeroPad2d(tnn.ZeroPad2d):
+    def forward(self, x):
+        return pad2d(x, self.padding) if native(x) else super().forward(x)
+
+
+class ReflectionPad2d(tnn.ReflectionPad2d):
+    def forward(self, x):
+        return pad2d(x, self.padding, mode="reflect") if native(x) else super().forward(x)
+
+
+class ChannelShuffle(tnn.Module):
+    """ShuffleNet channel shuffle: (N, g*c, H, W) -> transpose groups."""
+
+    def __init__(self, groups):
+        super().__init__()
+        self.groups = groups
+
+    def forward(self, x):
+        N, C, H, W = x.shape
+        g = self.groups
+        y = x.reshape(N, g, C // g, H, W).transpose(1, 2).reshape(N, C, H, W)
+        if native(x):
+            y = y.contiguous(memory_format=torch.channels_last)
+        return y

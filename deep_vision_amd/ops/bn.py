@@ -1,0 +1,143 @@
+"""BatchNorm2d (+ fused activation and residual add) on the native kernels (csrc/bn.hip).
+
+Training forward  : statistics come from the producing conv's epilogue when available
+                    (``conv2d(..., want_stats=True)``), otherwise from ``bn_stats``; one
+                    ``bn_finalize`` launch computes mean / invstd / scale / shift and updates
+                    running statistics; one ``bn_apply`` pass writes act(x*scale+shift(+res)).
+Training backward : ``bn_bwd_reduce`` (sum dz, sum dz*xhat with the activation mask fused) ->
+                    ``bn_bwd_finalize`` (dgamma, dbeta) -> ``bn_bwd_apply`` (dx, and dz for the
+                    residual branch).
+Eval              : scale/shift from running statistics, single apply pass.
+
+Reference semantics: torch.nn.BatchNorm2d after every conv of the PT ResNet/MobileNet
+(R/ResNet/pytorch/models/resnet50.py:30,110-134); Keras BatchNormalization for the TF-origin
+models (eps 1e-3, momentum 0.99 -> PyTorch momentum 0.01; Hourglass 0.9 -> 0.1).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as TF
+
+from .common import ACT_IDS, BF16, F32, grad_nhwc, is_nhwc, ld_of, lib, native, ptr, stream_handle
+
+STAT_SHARDS = 64
+
+
+def _nrows(x):
+    N, C, H, W = x.shape
+    return N * H * W
+
+
+class _BNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, stats, weight, bias, running_mean, running_var, residual, training, momentum, eps, act,
+                slope):
+        N, C, H, W = x.shape
+        ld = ld_of(x)
+        if ld != C:
+            raise NotImplementedError("BatchNorm on a padded channel view")
+        dev = x.device
+        st = stream_handle()
+        L = lib()
+        scale = torch.empty(C, dtype=F32, device=dev)
+        shift = torch.empty(C, dtype=F32, device=dev)
+        rows = N * H * W
+        g = weight.detach() if weight is not None else None
+        b = bias.detach() if bias is not None else None
+        if training:
+            if stats is None:
+                stats = torch.zeros((STAT_SHARDS, 2, C), dtype=F32, device=dev)
+                L.bn_stats(ptr(x), rows, C, ptr(stats), st)
+            mean = torch.empty(C, dtype=F32, device=dev)
+            invstd = torch.empty(C, dtype=F32, device=dev)
+            L.bn_finalize(ptr(stats), C, float(rows), float(eps), float(momentum), ptr(g), ptr(b), ptr(running_mean),
+                          ptr(running_var), ptr(mean), ptr(invstd), ptr(scale), ptr(shift), st)
+        else:
+            mean = invstd = None
+            L.bn_eval_prep(C, float(eps), ptr(g), ptr(b), ptr(running_mean), ptr(running_var), ptr(scale), ptr(shift), st)
+        out = torch.empty_like(x)
+        L.bn_apply(ptr(x), ptr(residual), ptr(out), x.numel(), C, ptr(scale), ptr(shift), act, float(slope), st)
+        ctx.save_for_backward(x, out if act else None, weight, mean, invstd, scale)
+        ctx.cfg = (training, act, slope, residual is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, out, weight, mean, invstd, scale = ctx.saved_tensors
+        training, act, slope, has_res = ctx.cfg
+        N, C, H, W = x.shape
+        dout = grad_nhwc(dout)
+        if ld_of(dout) != C:
+            dout = dout.contiguous(memory_format=torch.channels_last)
+        dev = x.device
+        st = stream_handle()
+        L = lib()
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(x) if (has_res and ctx.needs_input_grad[6]) else None
+        dgamma = dbeta = None
+        if training:
+            acc = torch.zeros((STAT_SHARDS, 2, C), dtype=F32, device=dev)
+            rows = N * H * W
+            L.bn_bwd_reduce(ptr(dout), ptr(out), ptr(x), rows, C, ptr(mean), ptr(invstd), act, float(slope), ptr(acc), st)
+            dgamma = torch.empty(C, dtype=F32, device=dev) if weight is not None else None
+            dbeta = torch.empty(C, dtype=F32, device=dev) if weight is not None else None
+            kmdz = torch.empty(C, dtype=F32, device=dev)
+            kmdzx = torch.empty(C, dtype=F32, device=dev)
+            kscale = torch.empty(C, dtype=F32, device=dev)
+            L.bn_bwd_finalize(ptr(acc), C, float(rows), ptr(weight.detach() if weight is not None else None), ptr(invstd),
+                              ptr(dgamma), ptr(dbeta), ptr(kmdz), ptr(kmdzx), ptr(kscale), st)
+            L.bn_bwd_apply(ptr(dout), ptr(out), ptr(x), ptr(dx), ptr(dres), x.numel(), C, ptr(mean), ptr(invstd),
+                           ptr(kmdz), ptr(kmdzx), ptr(kscale), act, float(slope), st)
+        else:
+            L.bn_bwd_eval(ptr(dout), ptr(out), ptr(dx), ptr(dres), x.numel(), C, ptr(scale), act, float(slope), st)
+            # frozen statistics: dgamma = sum(dz * xhat), dbeta = sum(dz) are not needed in eval mode
+        return dx, None, dgamma, dbeta, None, None, dres, None, None, None, None, None
+
+
+def _torch_bn_act(x, bn, act, slope, residual):
+    y = bn(x) if bn is not None else x
+    if residual is not None:
+        y = y + residual
+    if act == "relu":
+        y = TF.relu(y)
+    elif act in ("leaky", "leaky_relu"):
+        y = TF.leaky_relu(y, slope)
+    return y
+
+
+def bn_momentum(bn) -> float:
+    """Exponential-average factor with torch semantics (momentum=None -> cumulative)."""
+    if bn.momentum is None:
+        return 1.0 / float(bn.num_batches_tracked.item())
+    return bn.momentum
+
+
+def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None):
+    """act(BN(x) (+ residual)) with ``bn`` an nn.BatchNorm2d (parameters, buffers, mode)."""
+    if not native(x):
+        return _torch_bn_act(x, bn, act, slope, residual)
+    training = bn.training or not bn.track_running_stats
+    if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+    mom = bn_momentum(bn) if bn.training and bn.track_running_stats else 0.0
+    rm = bn.running_mean if bn.track_running_stats else None
+    rv = bn.running_var if bn.track_running_stats else None
+    if residual is not None and not (is_nhwc(residual) and ld_of(residual) == residual.shape[1]):
+        residual = residual.to(dtype=BF16).contiguous(memory_format=torch.channels_last)
+    return _BNActFn.apply(x, stats, bn.weight, bn.bias, rm, rv, residual, training, mom,
+                          bn.eps, ACT_IDS[act], float(slope))
+
+
+def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None):
+    """Fused conv -> BN (batch stats from the conv epilogue) -> (+residual) -> activation."""
+    from .conv import conv2d
+
+    if not native(x):
+        return _torch_bn_act(conv(x), bn, act, slope, residual)
+    want = bn.training or not bn.track_running_stats
+    r = conv2d(x, conv.weight, conv.bias, conv.stride, conv.padding, conv.dilation, conv.groups, want_stats=want)
+    y, stats = r if want else (r, None)
+    if y.shape[1] % 8 != 0:  # padded view: BN kernels require dense channels
+        y = y.contiguous(memory_format=torch.channels_last)
+        stats = None
+    return batch_norm_act(y, bn, act, slope, residual, stats)

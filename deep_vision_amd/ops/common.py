@@ -1,0 +1,104 @@
+"""Shared helpers for the native op layer.
+
+GPU tensor conventions (all native ops):
+  * 4-D activations are ``torch.bfloat16`` with ``torch.channels_last`` strides, i.e.
+    physically NHWC; the channel stride (``ld``) may exceed the channel count when the
+    channel count is not a multiple of 8 (the tensor is then a view of a padded buffer).
+  * 2-D activations (Linear in/out) are bf16 row-major.
+  * parameters, BN statistics and optimizer state are fp32.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from .._ext import lib, ptr, stream_handle  # noqa: F401
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+CL = torch.channels_last
+
+_FORCE_TORCH = os.environ.get("DV_BACKEND", "native").lower() == "torch"
+
+ACT_IDS = {None: 0, "none": 0, "relu": 1, "leaky": 2, "leaky_relu": 2, "tanh": 3, "sigmoid": 4}
+
+
+def set_backend(name: str) -> None:
+    """'native' (default: HIP kernels on GPU) or 'torch' (PyTorch/MIOpen reference path)."""
+    global _FORCE_TORCH
+    _FORCE_TORCH = name.lower() == "torch"
+
+
+def backend() -> str:
+    return "torch" if _FORCE_TORCH else "native"
+
+
+def native(x: torch.Tensor) -> bool:
+    """True when ``x`` should run through the hand-written HIP kernels."""
+    return x.is_cuda and not _FORCE_TORCH
+
+
+def round8(c: int) -> int:
+    return (c + 7) // 8 * 8
+
+
+def ld_of(x: torch.Tensor) -> int:
+    """Pixel (channel) stride of a channels_last 4-D tensor / row stride of a 2-D tensor."""
+    if x.dim() == 4:
+        return x.stride(3) if x.size(3) > 1 else (x.stride(2) if x.size(2) > 1 else x.stride(0) // max(1, x.size(2) * x.size(3)))
+    return x.stride(0)
+
+
+def is_nhwc(x: torch.Tensor) -> bool:
+    """bf16, channel stride 1, pixel-major packed layout (ld may be padded)."""
+    if x.dtype != BF16 or x.dim() != 4:
+        return False
+    N, C, H, W = x.shape
+    if C > 1 and x.stride(1) != 1:
+        return False
+    ld = ld_of(x)
+    if ld < C or ld % 8 != 0 and ld != C:
+        return False
+    return (W == 1 or x.stride(3) == ld) and (H == 1 or x.stride(2) == W * ld) and (N == 1 or x.stride(0) == H * W * ld)
+
+
+def empty_nhwc(N: int, C: int, H: int, W: int, device, zero: bool = False) -> torch.Tensor:
+    """bf16 NHWC tensor; channel stride padded to a multiple of 8 (returned as a view)."""
+    Cp = round8(C)
+    buf = torch.empty((N, Cp, H, W), dtype=BF16, device=device, memory_format=CL)
+    if zero or Cp != C:  # pad channels must be finite zeros
+        buf.zero_()
+    return buf if Cp == C else buf[:, :C]
+
+
+def alloc_cl(shape, zero=False, device=None, dtype=BF16):
+    """channels_last allocation (torch.zeros does not take memory_format)."""
+    t = torch.empty(shape, dtype=dtype, device=device, memory_format=CL)
+    return t.zero_() if zero else t
+
+
+def as_nhwc(x: torch.Tensor, pad_to8: bool = True) -> torch.Tensor:
+    """Convert any 4-D tensor into the native layout (differentiable when needed)."""
+    if is_nhwc(x) and (not pad_to8 or ld_of(x) % 8 == 0):
+        return x
+    N, C, H, W = x.shape
+    if not x.requires_grad and x.dtype in (F32, BF16) and x.is_contiguous():
+        Cp = round8(C) if pad_to8 else C
+        y = torch.empty((N, Cp, H, W), dtype=BF16, device=x.device, memory_format=CL)
+        lib().to_nhwc(ptr(x), int(x.dtype == F32), ptr(y), N, C, H, W, Cp, stream_handle())
+        return y  # padded channels are written as zeros by the kernel
+    y = x.to(dtype=BF16, memory_format=CL)
+    if pad_to8 and C % 8 != 0:
+        y = torch.nn.functional.pad(y, (0, 0, 0, 0, 0, round8(C) - C)).contiguous(memory_format=CL)
+    return y
+
+
+def grad_nhwc(g: torch.Tensor) -> torch.Tensor:
+    """Incoming gradient -> native layout with a channel stride that is a multiple of 8."""
+    if is_nhwc(g) and ld_of(g) % 8 == 0:
+        return g
+    N, C, H, W = g.shape
+    out = empty_nhwc(N, C, H, W, g.device, zero=(C % 8 != 0))
+    out.copy_(g)
+    return out

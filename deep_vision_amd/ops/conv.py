@@ -1,0 +1,334 @@
+"""Convolution / transposed convolution / linear on the native implicit-GEMM kernels.
+
+Forward   : csrc/igemm.hip MODE_FWD (im2col gather by LDS-DMA, MFMA 16x16x32 bf16)
+dgrad     : MODE_FWD on dY with transposed weights: stride 1 via negative pad/dilation,
+            1x1-strided via a scattered output map, other strides via the divisibility gather
+wgrad     : MODE_WGRAD, split-K over pixels, fp32 accumulate
+Epilogue  : bias, ReLU/LeakyReLU, BatchNorm statistics (consumed by ops.bn)
+
+Reference semantics: torch.nn.Conv2d as used by every PT model of the reference, e.g.
+R/ResNet/pytorch/models/resnet50.py:20-27 (7x7 s2 stem), :101-133 (bottleneck 1x1/3x3/1x1).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as TF
+
+from .common import (ACT_IDS, BF16, CL, F32, alloc_cl, as_nhwc, empty_nhwc, grad_nhwc, ld_of, lib, native, ptr, round8,
+                     stream_handle)
+
+STAT_SHARDS = 64
+
+
+def _pair(v):
+    return (v, v) if isinstance(v, int) else tuple(v)
+
+
+def out_size(H, W, R, S, stride, padding, dilation):
+    sh, sw = stride
+    ph, pw = padding
+    dh, dw = dilation
+    P = (H + 2 * ph - dh * (R - 1) - 1) // sh + 1
+    Q = (W + 2 * pw - dw * (S - 1) - 1) // sw + 1
+    return P, Q
+
+
+def _prep_weight(weight: torch.Tensor, G: int, pad: int, mode: int) -> torch.Tensor:
+    """fp32 OIHW -> bf16 kernel operand.
+
+    mode 0: [G][Og][R][S][pad]  (inner = input channels, zero-padded to ``pad``)
+    mode 1: [G][Ig][R][S][pad]  (inner = output channels per group, zero-padded to ``pad``)
+    """
+    O, Ig, R, S = weight.shape
+    w = weight.detach()
+    if w.dtype != F32 or not w.is_contiguous():
+        w = w.float().contiguous()
+    Og = O // G
+    n = G * (Og if mode == 0 else Ig) * R * S * pad
+    out = torch.empty(n, dtype=BF16, device=w.device)
+    lib().wprep(ptr(w), ptr(out), G, Og, Ig, R, S, pad, mode, stream_handle())
+    return out
+
+
+def _channel_sum(dy: torch.Tensor) -> torch.Tensor:
+    """Per-channel sum of an NHWC bf16 tensor (fp32) via the BN statistics kernel."""
+    N, C, H, W = dy.shape
+    ld = ld_of(dy)
+    acc = torch.zeros((STAT_SHARDS, 2, ld), dtype=F32, device=dy.device)
+    lib().bn_stats(ptr(dy), N * H * W, ld, ptr(acc), stream_handle())
+    return acc[:, 0, :C].sum(0)
+
+
+def conv_fwd_raw(x, wk, y, bias, stats, N, H, W, Cg, ldx, G, Kout, P, Q, R, S, stride, padding, dilation,
+                 act=0, slope=0.0, tgather=0, omap=None, ldy=None):
+    sh, sw = stride
+    ph, pw = padding
+    dh, dw = dilation
+    OH, OW, osh, osw, oph, opw = omap if omap is not None else (P, Q, 1, 1, 0, 0)
+    lib().conv_fwd(ptr(x), ptr(wk), ptr(y), ptr(bias), ptr(stats), N, H, W, Cg, ldx, G, Kout, P, Q, R, S, sh, sw, ph,
+                   pw, dh, dw, tgather, OH, OW, osh, osw, oph, opw, ldy if ldy is not None else ld_of(y), act, float(slope),
+                   stream_handle())
+
+
+def _gather_channels(t: torch.Tensor, per_group: int, G: int) -> int:
+    """Channels per group the gather kernel reads from ``t`` (must be a multiple of 8).
+
+    For G == 1 a channel count that is not a multiple of 8 is served by reading the zeroed
+    padding channels of the buffer (the matching weight rows are zero-padded)."""
+    if per_group % 8 == 0:
+        return per_group
+    if G == 1 and ld_of(t) % 8 == 0:
+        return ld_of(t)
+    raise NotImplementedError(f"grouped conv with {per_group} channels per group (needs % 8 == 0)")
+
+
+def _dgrad(dy, weight, x_shape, Cg_x, G, stride, padding, dilation, device):
+    """dX (N, G*Cg_x, H, W) from dY; Cg_x may include zero-padding channels."""
+    N, _, H, W = x_shape
+    O, Ig, R, S = weight.shape
+    Og = O // G
+    _, _, P, Q = dy.shape
+    sh, sw = stride
+    ph, pw = padding
+    dh, dw = dilation
+    Cg_dy = _gather_channels(dy, Og, G)
+    wd = _prep_weight(weight, G, Cg_dy, mode=1)  # [G][Ig][R][S][Cg_dy]
+    ldy_in = ld_of(dy)
+    scatter = (sh, sw) != (1, 1) and R == 1 and S == 1 and (ph, pw) == (0, 0)
+    dX = alloc_cl((N, G * Cg_x, H, W), zero=(scatter or Cg_x != Ig), device=device)
+    if (sh, sw) == (1, 1):
+        conv_fwd_raw(dy, wd, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, H, W, R, S, (1, 1), (-ph, -pw),
+                     (-dh, -dw), ldy=G * Cg_x)
+    elif scatter:
+        conv_fwd_raw(dy, wd, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, P, Q, 1, 1, (1, 1), (0, 0), (1, 1),
+                     omap=(H, W, sh, sw, 0, 0), ldy=G * Cg_x)
+    else:
+        conv_fwd_raw(dy, wd, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, H, W, R, S, stride, padding, dilation,
+                     tgather=1, ldy=G * Cg_x)
+    return dX
+
+
+def _wgrad(x, dy, weight, Cg_x, G, stride, padding, dilation):
+    N, _, H, W = x.shape
+    O, Ig, R, S = weight.shape
+    Og = O // G
+    _, _, P, Q = dy.shape
+    sh, sw = stride
+    ph, pw = padding
+    dh, dw = dilation
+    buf = torch.empty(G * Og * R * S * Cg_x, dtype=F32, device=x.device)
+    lib().conv_wgrad(ptr(x), ptr(dy), ptr(buf), N, H, W, Cg_x, ld_of(x), G, Og, P, Q, ld_of(dy), R, S, sh, sw, ph, pw,
+                     dh, dw, 0, stream_handle())
+    if R == 1 and S == 1 and Cg_x == Ig:
+        return buf.view(O, Ig, 1, 1)
+    dW = torch.empty((O, Ig, R, S), dtype=F32, device=x.device)
+    lib().wgrad_unprep(ptr(buf), ptr(dW), G, Og, Ig, R, S, Cg_x, 1.0, 0, stream_handle())
+    return dW
+
+
+class _ConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats):
+        N, Cx, H, W = x.shape
+        O, Ig, R, S = weight.shape
+        G = groups
+        Og = O // G
+        ldx = ld_of(x)
+        Cg_x = _gather_channels(x, Cx // G, G)  # padded channels (G == 1) are zeros
+        P, Q = out_size(H, W, R, S, stride, padding, dilation)
+        wk = _prep_weight(weight, G, Cg_x, mode=0)
+        y = empty_nhwc(N, O, P, Q, x.device)
+        stats = torch.zeros((STAT_SHARDS, 2, O), dtype=F32, device=x.device) if want_stats else None
+        b = bias.detach().float().contiguous() if bias is not None else None
+        conv_fwd_raw(x, wk, y, b, stats, N, H, W, Cg_x, ldx, G, Og, P, Q, R, S, stride, padding, dilation,
+                     act=act, slope=slope)
+        ctx.save_for_backward(x, weight, y if act else None)
+        ctx.cfg = (stride, padding, dilation, G, act, slope, Cg_x, bias is not None)
+        if want_stats:
+            ctx.mark_non_differentiable(stats)
+            return y, stats
+        return y
+
+    @staticmethod
+    def backward(ctx, dy, *unused):
+        x, weight, y = ctx.saved_tensors
+        stride, padding, dilation, G, act, slope, Cg_x, has_bias = ctx.cfg
+        dy = grad_nhwc(dy)
+        if act:
+            g = torch.empty_like(dy) if ld_of(dy) == dy.shape[1] else empty_nhwc(*dy.shape, dy.device)
+            n = dy.numel() if ld_of(dy) == dy.shape[1] else dy.shape[0] * dy.shape[2] * dy.shape[3] * ld_of(dy)
+            lib().act_bwd(ptr(dy), ptr(y), ptr(g), n, act, float(slope), stream_handle())
+            dy = g
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = _dgrad(dy, weight, x.shape, Cg_x, G, stride, padding, dilation, x.device)
+            if dx.shape[1] != x.shape[1]:
+                dx = dx[:, : x.shape[1]]
+        if ctx.needs_input_grad[1]:
+            dw = _wgrad(x, dy, weight, Cg_x, G, stride, padding, dilation)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = _channel_sum(dy)
+        return dx, dw, db, None, None, None, None, None, None, None
+
+
+def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=None, slope=0.0,
+           want_stats=False):
+    """Conv2d (+fused bias/activation). Returns y, or (y, stats) when want_stats (GPU only)."""
+    stride, padding, dilation = _pair(stride), _pair(padding), _pair(dilation)
+    if not native(x):
+        y = TF.conv2d(x, weight, bias, stride, padding, dilation, groups)
+        if act in ("relu",):
+            y = TF.relu(y)
+        elif act in ("leaky", "leaky_relu"):
+            y = TF.leaky_relu(y, slope)
+        return (y, None) if want_stats else y
+    if isinstance(padding, str):
+        raise NotImplementedError("string padding: use ops.conv.same_padding")
+    x = as_nhwc(x, pad_to8=(groups == 1))
+    return _ConvFn.apply(x, weight, bias, stride, padding, dilation, groups, ACT_IDS[act], float(slope), want_stats)
+
+
+# ---------------------------------------------------------------------------------------
+# ConvTranspose2d: forward = conv dgrad with the transposed-conv weight [Cin][Cout][R][S]
+# ---------------------------------------------------------------------------------------
+class _ConvTFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, padding, output_padding, dilation, groups):
+        # x (N, Cin, H, W), weight (Cin, Cout/G, R, S). Equivalent conv: W_conv = weight with
+        # O := Cin, I := Cout/G; output = dgrad(x) of that conv with output size (OH, OW).
+        N, Cin, H, W = x.shape
+        Ci, Cog, R, S = weight.shape
+        G = groups
+        sh, sw = stride
+        ph, pw = padding
+        dh, dw = dilation
+        OH = (H - 1) * sh - 2 * ph + dh * (R - 1) + output_padding[0] + 1
+        OW = (W - 1) * sw - 2 * pw + dw * (S - 1) + output_padding[1] + 1
+        Cout = Cog * G
+        if G > 1 and (Cog % 8 != 0):
+            raise NotImplementedError("grouped ConvTranspose requires out-channels-per-group % 8 == 0")
+        # The transposed-conv weight [Cin][Cog][R][S] is a conv weight with O = Cin, I = Cog;
+        # its forward is that conv's dgrad: operand [G][Cog][R][S][Cin/G] (wprep mode 1).
+        Cpad = round8(Cog) if G == 1 else Cog
+        Cg_in = _gather_channels(x, Ci // G, G)
+        wd = _prep_weight(weight, G, Cg_in, mode=1)
+        y_full = alloc_cl((N, G * Cpad, OH, OW), zero=True, device=x.device)
+        ldx = ld_of(x)
+        if (sh, sw) == (1, 1):
+            conv_fwd_raw(x, wd, y_full, None, None, N, H, W, Cg_in, ldx, G, Cog, OH, OW, R, S, (1, 1), (-ph, -pw),
+                         (-dh, -dw), ldy=G * Cpad)
+        else:
+            conv_fwd_raw(x, wd, y_full, None, None, N, H, W, Cg_in, ldx, G, Cog, OH, OW, R, S, stride, padding,
+                         dilation, tgather=1, ldy=G * Cpad)
+        y = y_full if Cpad == Cog else y_full[:, :Cout]
+        if bias is not None:
+            y.add_(bias.detach().to(BF16).view(1, -1, 1, 1))
+        ctx.save_for_backward(x, weight)
+        ctx.cfg = (stride, padding, dilation, G, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        stride, padding, dilation, G, has_bias = ctx.cfg
+        dy = grad_nhwc(dy)
+        Ci, Cog, R, S = weight.shape
+        N, Cin, H, W = x.shape
+        dx = dw = db = None
+        Cg_dy = _gather_channels(dy, Cog, G)
+        if ctx.needs_input_grad[0]:
+            # dX = conv_fwd(dY, W_conv) with W_conv[o = Cin][i = Cog]
+            wk = _prep_weight(weight, G, Cg_dy, mode=0)
+            dx = empty_nhwc(N, Cin, H, W, x.device)
+            conv_fwd_raw(dy, wk, dx, None, None, N, dy.shape[2], dy.shape[3], Cg_dy, ld_of(dy), G, Ci // G, H, W, R, S,
+                         stride, padding, dilation)
+        if ctx.needs_input_grad[1]:
+            # conv relationship: X_conv = dY (large), dY_conv = x (small)
+            dw = _wgrad(dy, x, weight, Cg_dy, G, stride, padding, dilation)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = _channel_sum(dy)
+        return dx, dw, db, None, None, None, None, None
+
+
+def conv_transpose2d(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1, dilation=1):
+    stride, padding, output_padding, dilation = _pair(stride), _pair(padding), _pair(output_padding), _pair(dilation)
+    if not native(x):
+        return TF.conv_transpose2d(x, weight, bias, stride, padding, output_padding, groups, dilation)
+    x = as_nhwc(x, pad_to8=(groups == 1))
+    return _ConvTFn.apply(x, weight, bias, stride, padding, output_padding, dilation, groups)
+
+
+# ---------------------------------------------------------------------------------------
+# Linear: a 1x1 conv over an (N, K) "image" of one pixel
+# ---------------------------------------------------------------------------------------
+class _LinearFn(torch.autograd.Function):
+    """y = x W^T + b as a 1x1 conv over N one-pixel images (rows)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, act, slope):
+        N, K = x.shape
+        O, _ = weight.shape
+        Kp = x.stride(0)  # zero-padded row stride, multiple of 8
+        wk = _prep_weight(weight.view(O, K, 1, 1), 1, Kp, mode=0)
+        Op = round8(O)
+        y_full = (torch.zeros if Op != O else torch.empty)((N, Op), dtype=BF16, device=x.device)
+        b = bias.detach().float().contiguous() if bias is not None else None
+        conv_fwd_raw(x, wk, y_full, b, None, N, 1, 1, Kp, Kp, 1, O, 1, 1, 1, 1, (1, 1), (0, 0), (1, 1), act=act,
+                     slope=slope, ldy=Op)
+        y = y_full if Op == O else y_full[:, :O]
+        ctx.save_for_backward(x, weight, y if act else None)
+        ctx.cfg = (act, slope, bias is not None, Kp, Op)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, y = ctx.saved_tensors
+        act, slope, has_bias, Kp, Op = ctx.cfg
+        N, K = x.shape
+        O, _ = weight.shape
+        if dy.dtype != BF16 or dy.stride(1) != 1 or dy.stride(0) != Op:
+            g = (torch.zeros if Op != O else torch.empty)((N, Op), dtype=BF16, device=dy.device)
+            g[:, :O].copy_(dy)
+            dy = g[:, :O]
+        if act:
+            g = (torch.zeros if Op != O else torch.empty)((N, Op), dtype=BF16, device=dy.device)
+            lib().act_bwd(ptr(dy), ptr(y), ptr(g), N * Op, act, float(slope), stream_handle())
+            dy = g[:, :O]
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            wd = _prep_weight(weight.view(O, K, 1, 1), 1, Op, mode=1)  # [K][Op]
+            dx_full = (torch.zeros if Kp != K else torch.empty)((N, Kp), dtype=BF16, device=dy.device)
+            conv_fwd_raw(dy, wd, dx_full, None, None, N, 1, 1, Op, Op, 1, K, 1, 1, 1, 1, (1, 1), (0, 0), (1, 1),
+                         ldy=Kp)
+            dx = dx_full if Kp == K else dx_full[:, :K]
+        if ctx.needs_input_grad[1]:
+            buf = torch.empty(O * Kp, dtype=F32, device=dy.device)
+            lib().conv_wgrad(ptr(x), ptr(dy), ptr(buf), N, 1, 1, Kp, Kp, 1, O, 1, 1, Op, 1, 1, 1, 1, 0, 0, 1, 1, 0,
+                             stream_handle())
+            dw = buf.view(O, Kp)[:, :K].contiguous() if Kp != K else buf.view(O, K)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = dy.float().sum(0)
+        return dx, dw, db, None, None
+
+
+def linear(x, weight, bias=None, act=None, slope=0.0):
+    if not native(x):
+        y = TF.linear(x, weight, bias)
+        if act == "relu":
+            y = TF.relu(y)
+        elif act in ("leaky", "leaky_relu"):
+            y = TF.leaky_relu(y, slope)
+        return y
+    lead = x.shape[:-1]
+    x2 = x.reshape(-1, x.shape[-1])
+    K = x2.shape[1]
+    if x2.dtype != BF16 or x2.stride(1) != 1 or x2.stride(0) % 8 != 0 or x2.stride(0) < K:
+        Kp = round8(K)
+        xp = (torch.zeros if Kp != K else torch.empty)((x2.shape[0], Kp), dtype=BF16, device=x.device)
+        if x2.requires_grad:
+            xp = TF.pad(x2.to(BF16), (0, Kp - K)) if Kp != K else x2.to(BF16).contiguous()
+        else:
+            xp[:, :K].copy_(x2)
+        x2 = xp if Kp == K else xp[:, :K]
+    y = _LinearFn.apply(x2, weight, bias, ACT_IDS[act], float(slope))
+    return y.reshape(*lead, weight.shape[0])

@@ -1,0 +1,281 @@
+"""Fused optimizers over one flat fp32 parameter buffer.
+
+All parameters of a group live in a single contiguous fp32 buffer (the ``nn.Parameter``s become
+views into it) and their ``.grad``s are views into a matching flat gradient buffer. One kernel
+launch (csrc/loss_optim.hip) updates the whole model per step, and the data-parallel layer
+all-reduces slices of the same flat gradient buffer in place (no bucket copies).
+
+Update rules match torch.optim.SGD / Adam / RMSprop exactly (same state names, same
+``state_dict`` format), as used by the reference configs (R/ResNet/pytorch/train.py:26-215:
+SGD momentum .9 + wd, RMSprop for MobileNet; Adam for LeNet/YOLO/Hourglass/GANs).
+On CPU the same classes run the identical math with torch ops.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .._ext import lib, ptr, stream_handle
+
+
+class _FlatOptimizer(torch.optim.Optimizer):
+    STATE_NAMES: tuple = ()
+
+    def __init__(self, params, defaults):
+        super().__init__(params, defaults)
+        self._flat = []  # per group: dict(param, grad, views, gviews, offsets, states)
+        for group in self.param_groups:
+            self._flat.append(self._flatten_group(group))
+
+    # ---------------- flat storage ----------------
+    def _flatten_group(self, group):
+        ps = group["params"]
+        if not ps:
+            return None
+        dev = ps[0].device
+        for p in ps:
+            if p.dtype != torch.float32:
+                raise TypeError("fused optimizers keep fp32 master parameters")
+            if p.device != dev:
+                raise ValueError("all parameters of a group must live on one device")
+        # reuse an existing flat buffer (parallel.flat.flatten_parameters) when every param of
+        # the group is a view into it and the group covers the buffer exactly
+        sizes = [p.numel() for p in ps]
+        total = sum(sizes)
+        shared = getattr(ps[0], "_dv_flat", None)
+        reuse = (shared is not None and all(getattr(p, "_dv_flat", None) is shared for p in ps)
+                 and shared[0].numel() == total)
+        views, gviews, offs = [], [], []
+        if reuse:
+            pflat, gflat = shared
+            for p, n in zip(ps, sizes):
+                off = p._dv_off
+                views.append(pflat[off:off + n].view(p.shape))
+                gviews.append(gflat[off:off + n].view(p.shape))
+                if p.grad is not None and p.grad.data_ptr() != gviews[-1].data_ptr():
+                    gviews[-1].copy_(p.grad)
+                p.data = views[-1]
+                p.grad = gviews[-1]
+                offs.append((off, n))
+        else:
+            pflat = torch.empty(total, dtype=torch.float32, device=dev)
+            gflat = torch.zeros(total, dtype=torch.float32, device=dev)
+            off = 0
+            for p, n in zip(ps, sizes):
+                pv = pflat[off:off + n].view(p.shape)
+                gv = gflat[off:off + n].view(p.shape)
+                pv.copy_(p.data)
+                p.data = pv
+                if p.grad is not None:
+                    gv.copy_(p.grad)
+                p.grad = gv
+                p._dv_flat = (pflat, gflat)
+                p._dv_off = off
+                views.append(pv)
+                gviews.append(gv)
+                offs.append((off, n))
+                off += n
+        states = {name: torch.zeros(total, dtype=torch.float32, device=dev) for name in self.STATE_NAMES}
+        return dict(param=pflat, grad=gflat, views=views, gviews=gviews, offsets=offs, states=states, step=0,
+                    first=True)
+
+    def param_views(self):
+        return [v for f in self._flat if f for v in f["views"]]
+
+    def flat_grads(self):
+        return [f["grad"] for f in self._flat if f]
+
+    @torch.no_grad()
+    def zero_grad(self, set_to_none: bool = False):
+        for group, f in zip(self.param_groups, self._flat):
+            if f is None:
+                continue
+            f["grad"].zero_()
+            for p, gv in zip(group["params"], f["gviews"]):
+                if p.grad is not gv:
+                    p.grad = gv
+
+    def _sync_grads(self, group, f):
+        """Ensure every .grad is the flat view; returns active (offset, n) segments."""
+        segs = []
+        all_active = True
+        for p, gv, (off, n) in zip(group["params"], f["gviews"], f["offsets"]):
+            g = p.grad
+            if g is None:
+                all_active = False
+                p.grad = gv
+                gv.zero_()
+                continue
+            if g is not gv:
+                gv.copy_(g)
+                p.grad = gv
+            segs.append((off, n))
+        if all_active:
+            return [(0, f["param"].numel())]
+        # merge adjacent segments
+        merged = []
+        for off, n in sorted(segs):
+            if merged and merged[-1][0] + merged[-1][1] == off:
+                merged[-1] = (merged[-1][0], merged[-1][1] + n)
+            else:
+                merged.append((off, n))
+        return merged
+
+    @torch.no_grad()
+    def step(self, closure=None, grad_scale: float = 1.0):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group, f in zip(self.param_groups, self._flat):
+            if f is None:
+                continue
+            segs = self._sync_grads(group, f)
+            f["step"] += 1
+            for off, n in segs:
+                self._update(group, f, off, n, grad_scale)
+            f["first"] = False
+        return loss
+
+    def _update(self, group, f, off, n, gs):  # pragma: no cover - abstract
+        raise NotImplementedError
+
+    @staticmethod
+    def _slice(t, off, n):
+        return t[off:off + n]
+
+    # ---------------- torch-compatible state_dict ----------------
+    def state_dict(self):
+        sd = super().state_dict()
+        state = {}
+        idx = 0
+        for group, f in zip(self.param_groups, self._flat):
+            if f is None:
+                continue
+            for (off, n), p in zip(f["offsets"], group["params"]):
+                st = {}
+                for name, buf in f["states"].items():
+                    st[name] = buf[off:off + n].view(p.shape).clone()
+                if self.STATE_NAMES and not f["first"]:
+                    st["step"] = torch.tensor(float(f["step"]))
+                    state[idx] = st
+                idx += 1
+        sd["state"] = state
+        for g, f in zip(sd["param_groups"], self._flat):
+            g["_dv_step"] = f["step"] if f else 0
+        return sd
+
+    def load_state_dict(self, state_dict):
+        groups = state_dict["param_groups"]
+        for g, sg in zip(self.param_groups, groups):
+            for k, v in sg.items():
+                if k not in ("params", "_dv_step"):
+                    g[k] = v
+        idx = 0
+        for sg, group, f in zip(groups, self.param_groups, self._flat):
+            if f is None:
+                continue
+            f["step"] = int(sg.get("_dv_step", 0))
+            any_state = False
+            for (off, n), p in zip(f["offsets"], group["params"]):
+                st = state_dict["state"].get(idx, state_dict["state"].get(str(idx)))
+                if st:
+                    any_state = True
+                    for name in self.STATE_NAMES:
+                        if name in st:
+                            f["states"][name][off:off + n].copy_(st[name].reshape(-1).to(f["param"].device))
+                    if "step" in st and f["step"] == 0:
+                        f["step"] = int(float(st["step"]))
+                idx += 1
+            f["first"] = not any_state
+
+
+class FusedSGD(_FlatOptimizer):
+    STATE_NAMES = ("momentum_buffer",)
+
+    def __init__(self, params, lr=0.1, momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False):
+        super().__init__(params, dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
+                                      nesterov=nesterov))
+
+    def _update(self, g, f, off, n, gs):
+        p = f["param"][off:off + n]
+        gr = f["grad"][off:off + n]
+        buf = f["states"]["momentum_buffer"][off:off + n]
+        if p.is_cuda:
+            lib().sgd(ptr(p), ptr(gr), ptr(buf), n, float(g["lr"]), float(g["momentum"]), float(g["dampening"]),
+                      float(g["weight_decay"]), int(g["nesterov"]), int(f["first"]), float(gs), stream_handle())
+            return
+        d = gr * gs + g["weight_decay"] * p
+        if g["momentum"] != 0:
+            if f["first"]:
+                buf.copy_(d)
+            else:
+                buf.mul_(g["momentum"]).add_(d, alpha=1 - g["dampening"])
+            d = d + g["momentum"] * buf if g["nesterov"] else buf
+        p.add_(d, alpha=-g["lr"])
+
+
+class FusedAdam(_FlatOptimizer):
+    STATE_NAMES = ("exp_avg", "exp_avg_sq")
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, decoupled=False):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, decoupled=decoupled))
+
+    def _update(self, g, f, off, n, gs):
+        b1, b2 = g["betas"]
+        t = f["step"]
+        bc1 = 1 - b1 ** t
+        bc2 = 1 - b2 ** t
+        p = f["param"][off:off + n]
+        gr = f["grad"][off:off + n]
+        m = f["states"]["exp_avg"][off:off + n]
+        v = f["states"]["exp_avg_sq"][off:off + n]
+        if p.is_cuda:
+            lib().adam(ptr(p), ptr(gr), ptr(m), ptr(v), n, float(g["lr"]), float(b1), float(b2), float(g["eps"]),
+                       float(g["weight_decay"]), int(g["decoupled"]), float(bc1), float(bc2), float(gs), stream_handle())
+            return
+        grad = gr * gs
+        if g["decoupled"]:
+            p.mul_(1 - g["lr"] * g["weight_decay"])
+        else:
+            grad = grad + g["weight_decay"] * p
+        m.mul_(b1).add_(grad, alpha=1 - b1)
+        v.mul_(b2).addcmul_(grad, grad, value=1 - b2)
+        denom = (v / bc2).sqrt_().add_(g["eps"])
+        p.addcdiv_(m, denom, value=-g["lr"] / bc1)
+
+
+class FusedRMSprop(_FlatOptimizer):
+    STATE_NAMES = ("square_avg", "momentum_buffer", "grad_avg")
+
+    def __init__(self, params, lr=1e-2, alpha=0.99, eps=1e-8, weight_decay=0.0, momentum=0.0, centered=False):
+        super().__init__(params, dict(lr=lr, alpha=alpha, eps=eps, weight_decay=weight_decay, momentum=momentum,
+                                      centered=centered))
+
+    def _update(self, g, f, off, n, gs):
+        p = f["param"][off:off + n]
+        gr = f["grad"][off:off + n]
+        sq = f["states"]["square_avg"][off:off + n]
+        mom = f["states"]["momentum_buffer"][off:off + n]
+        ga = f["states"]["grad_avg"][off:off + n]
+        if p.is_cuda:
+            lib().rmsprop(ptr(p), ptr(gr), ptr(sq), ptr(mom), ptr(ga), n, float(g["lr"]), float(g["alpha"]),
+                          float(g["eps"]), float(g["weight_decay"]), float(g["momentum"]), int(g["centered"]), float(gs),
+                          stream_handle())
+            return
+        grad = gr * gs + g["weight_decay"] * p
+        sq.mul_(g["alpha"]).addcmul_(grad, grad, value=1 - g["alpha"])
+        if g["centered"]:
+            ga.mul_(g["alpha"]).add_(grad, alpha=1 - g["alpha"])
+            avg = (sq - ga * ga).sqrt_().add_(g["eps"])
+        else:
+            avg = sq.sqrt().add_(g["eps"])
+        if g["momentum"] > 0:
+            mom.mul_(g["momentum"]).addcdiv_(grad, avg)
+            p.add_(mom, alpha=-g["lr"])
+        else:
+            p.addcdiv_(grad, avg, value=-g["lr"])
+
+
+OPTIMIZERS = {"SGD": FusedSGD, "Adam": FusedAdam, "RMSprop": FusedRMSprop}

@@ -1,0 +1,287 @@
+"""Numerics of every native gfx950 kernel against a plain PyTorch fp32 reference of the same op.
+
+Inputs are rounded to bf16 first so the reference sees exactly the operands the kernel sees;
+tolerances cover bf16 output rounding and fp32 accumulation-order differences.
+"""
+import pytest
+import torch
+import torch.nn.functional as TF
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+
+
+def _cos(a, b):
+    a = a.float().flatten()
+    b = b.float().flatten()
+    return (a @ b / (a.norm() * b.norm()).clamp_min(1e-12)).item()
+
+
+def _nhwc(t):
+    return t.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _ext():
+    from deep_vision_amd._ext import lib
+
+    lib()
+    torch.manual_seed(0)
+
+
+CONV_CASES = [
+    # N, C, H, W, K, R, stride, pad, groups
+    (2, 64, 14, 14, 64, 1, 1, 0, 1),
+    (2, 64, 14, 14, 128, 3, 1, 1, 1),
+    (2, 256, 14, 14, 128, 1, 2, 0, 1),
+    (2, 3, 32, 32, 64, 7, 2, 3, 1),      # stem, C padded 3 -> 8
+    (2, 32, 17, 15, 48, 3, 2, 1, 1),     # stride-2 3x3: divisibility-gather dgrad
+    (2, 64, 9, 9, 255, 1, 1, 0, 1),      # YOLO head: 255 outputs (padded channel stride)
+    (2, 96, 13, 13, 256, 5, 1, 2, 1),    # 5x5, C % 64 != 0 (generic K decode)
+    (2, 128, 8, 8, 128, 3, 1, 1, 2),     # grouped
+    (3, 200, 7, 7, 520, 1, 1, 0, 1),     # odd M / N tails
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_bwd(case):
+    from deep_vision_amd import ops as F
+
+    N, C, H, W, K, R, s, p, g = case
+    x32 = torch.randn(N, C, H, W, device=DEV).bfloat16().float()
+    w = (torch.randn(K, C // g, R, R, device=DEV) * (2.0 / (C * R * R / g)) ** 0.5).requires_grad_(True)
+    x = _nhwc(x32).requires_grad_(True)
+    y = F.conv2d(x, w, None, s, p, 1, g)
+    xr = x32.clone().requires_grad_(True)
+    wr = w.detach().bfloat16().float().requires_grad_(True)
+    yr = TF.conv2d(xr, wr, None, s, p, 1, g)
+    assert y.shape == yr.shape
+    assert _rel(y, yr) < 2e-2
+    dy32 = torch.randn_like(yr).bfloat16().float()
+    y.backward(_nhwc(dy32))
+    yr.backward(dy32)
+    assert _rel(x.grad, xr.grad) < 3e-2
+    assert _rel(w.grad, wr.grad) < 3e-2
+
+
+def test_conv_bias_relu_epilogue():
+    from deep_vision_amd import ops as F
+
+    x32 = torch.randn(2, 32, 12, 12, device=DEV).bfloat16().float()
+    w = torch.randn(40, 32, 3, 3, device=DEV) * 0.1
+    b = torch.randn(40, device=DEV)
+    y = F.conv2d(_nhwc(x32), w, b, 1, 1, act="relu")
+    yr = TF.relu(TF.conv2d(x32, w.bfloat16().float(), b, 1, 1))
+    assert _rel(y, yr) < 2e-2
+
+
+def test_conv_stats_epilogue_and_bn():
+    from deep_vision_amd import nn, ops as F
+
+    conv = nn.Conv2d(64, 128, 3, padding=1, bias=False).to(DEV)
+    bn = nn.BatchNorm2d(128).to(DEV)
+    bn.weight.data.uniform_(0.5, 1.5)
+    bn.bias.data.uniform_(-0.5, 0.5)
+    conv_r = torch.nn.Conv2d(64, 128, 3, padding=1, bias=False).to(DEV)
+    bn_r = torch.nn.BatchNorm2d(128).to(DEV)
+    conv_r.weight.data.copy_(conv.weight.data.bfloat16().float())
+    bn_r.load_state_dict(bn.state_dict())
+    x32 = torch.randn(4, 64, 16, 16, device=DEV).bfloat16().float()
+    res32 = torch.randn(4, 128, 16, 16, device=DEV).bfloat16().float()
+    x = _nhwc(x32).requires_grad_(True)
+    res = _nhwc(res32).requires_grad_(True)
+    y = F.conv_bn_act(x, conv, bn, "relu", residual=res)
+    xr = x32.clone().requires_grad_(True)
+    rr = res32.clone().requires_grad_(True)
+    yr = TF.relu(bn_r(conv_r(xr)) + rr)
+    assert _rel(y, yr) < 3e-2
+    assert torch.allclose(bn.running_mean, bn_r.running_mean, atol=1e-2, rtol=1e-2)
+    assert torch.allclose(bn.running_var, bn_r.running_var, atol=1e-2, rtol=2e-2)
+    dy32 = torch.randn_like(yr).bfloat16().float()
+    y.backward(_nhwc(dy32))
+    yr.backward(dy32)
+    assert _rel(x.grad, xr.grad) < 8e-2 and _cos(x.grad, xr.grad) > 0.999
+    # ReLU-mask boundary elements (z ~ 0) can flip under bf16 rounding: compare globally
+    assert _cos(res.grad, rr.grad) > 0.999
+    mism = ((res.grad.float() - rr.grad).abs() > 0.05).float().mean().item()
+    assert mism < 5e-3
+    for a, b in ((bn.weight.grad, bn_r.weight.grad), (bn.bias.grad, bn_r.bias.grad),
+                 (conv.weight.grad, conv_r.weight.grad)):
+        assert _rel(a, b) < 8e-2 and _cos(a, b) > 0.999
+
+
+def test_bn_eval():
+    from deep_vision_amd import nn
+
+    bn = nn.BatchNorm2d(48).to(DEV).eval()
+    bn.running_mean.uniform_(-1, 1)
+    bn.running_var.uniform_(0.5, 2)
+    x32 = torch.randn(2, 48, 5, 5, device=DEV).bfloat16().float()
+    y = bn(_nhwc(x32))
+    yr = torch.nn.functional.batch_norm(x32, bn.running_mean, bn.running_var, bn.weight, bn.bias, False)
+    assert _rel(y, yr) < 1e-2
+
+
+@pytest.mark.parametrize("cfg", [(3, 2, 1, False), (3, 2, 0, True), (2, 2, 0, False), (3, 1, 1, False)])
+def test_maxpool(cfg):
+    from deep_vision_amd import ops as F
+
+    k, s, p, ceil = cfg
+    x32 = torch.randn(2, 64, 15, 15, device=DEV).bfloat16().float()
+    x = _nhwc(x32).requires_grad_(True)
+    xr = x32.clone().requires_grad_(True)
+    y = F.max_pool2d(x, k, s, p, ceil)
+    yr = TF.max_pool2d(xr, k, s, p, ceil_mode=ceil)
+    assert y.shape == yr.shape
+    assert _rel(y, yr) == 0.0
+    dy = torch.randn_like(yr).bfloat16().float()
+    y.backward(_nhwc(dy))
+    yr.backward(dy)
+    assert _rel(x.grad, xr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("cfg", [(7, 1, 0, False, True), (5, 3, 0, False, True), (3, 2, 1, True, False)])
+def test_avgpool(cfg):
+    from deep_vision_amd import ops as F
+
+    k, s, p, ceil, cip = cfg
+    x32 = torch.randn(2, 32, 14, 14, device=DEV).bfloat16().float()
+    x = _nhwc(x32).requires_grad_(True)
+    xr = x32.clone().requires_grad_(True)
+    y = F.avg_pool2d(x, k, s, p, ceil, cip)
+    yr = TF.avg_pool2d(xr, k, s, p, ceil, cip)
+    assert y.shape == yr.shape
+    assert _rel(y, yr) < 1e-2
+    dy = torch.randn_like(yr).bfloat16().float()
+    y.backward(_nhwc(dy))
+    yr.backward(dy)
+    assert _rel(x.grad, xr.grad) < 1e-2
+
+
+def test_gap_linear_xent():
+    from deep_vision_amd import ops as F
+
+    x32 = torch.randn(8, 256, 7, 7, device=DEV).bfloat16().float()
+    w = (torch.randn(100, 256, device=DEV) * 0.05).requires_grad_(True)
+    b = torch.randn(100, device=DEV).requires_grad_(True)
+    lab = torch.randint(0, 100, (8,), device=DEV)
+    x = _nhwc(x32).requires_grad_(True)
+    h = F.adaptive_avg_pool2d(x, 1).flatten(1)
+    logits = F.linear(h, w, b)
+    loss = F.cross_entropy(logits, lab)
+    xr = x32.clone().requires_grad_(True)
+    wr = w.detach().bfloat16().float().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True)
+    hr = TF.adaptive_avg_pool2d(xr, 1).flatten(1).bfloat16().float()
+    lr = TF.linear(hr, wr, br)
+    lossr = TF.cross_entropy(lr, lab)
+    assert abs(loss.item() - lossr.item()) < 2e-2 * max(1.0, abs(lossr.item()))
+    loss.backward()
+    lossr.backward()
+    assert _rel(x.grad, xr.grad) < 5e-2
+    assert _rel(w.grad, wr.grad) < 5e-2
+    assert _rel(b.grad, br.grad) < 5e-2
+
+
+def test_linear_odd_sizes():
+    from deep_vision_amd import ops as F
+
+    x32 = torch.randn(5, 100, device=DEV).bfloat16().float()
+    w = (torch.randn(37, 100, device=DEV) * 0.1).requires_grad_(True)
+    x = x32.clone().requires_grad_(True)
+    y = F.linear(x, w, None, act="relu")
+    wr = w.detach().bfloat16().float().requires_grad_(True)
+    xr = x32.clone().requires_grad_(True)
+    yr = TF.relu(TF.linear(xr, wr))
+    assert _rel(y, yr) < 2e-2
+    g = torch.randn_like(yr)
+    y.backward(g)
+    yr.backward(g.bfloat16().float())
+    assert _rel(x.grad, xr.grad) < 5e-2
+    assert _rel(w.grad, wr.grad) < 5e-2
+
+
+def test_conv_transpose():
+    from deep_vision_amd import ops as F
+
+    for (cin, cout, k, s, p, op) in [(64, 32, 3, 2, 1, 1), (32, 16, 5, 1, 2, 0), (16, 8, 4, 2, 1, 0)]:
+        x32 = torch.randn(2, cin, 7, 7, device=DEV).bfloat16().float()
+        w = (torch.randn(cin, cout, k, k, device=DEV) * 0.1).requires_grad_(True)
+        x = _nhwc(x32).requires_grad_(True)
+        y = F.conv_transpose2d(x, w, None, s, p, op)
+        xr = x32.clone().requires_grad_(True)
+        wr = w.detach().bfloat16().float().requires_grad_(True)
+        yr = TF.conv_transpose2d(xr, wr, None, s, p, op)
+        assert y.shape == yr.shape, (y.shape, yr.shape)
+        assert _rel(y, yr) < 2e-2
+        dy = torch.randn_like(yr).bfloat16().float()
+        y.backward(_nhwc(dy))
+        yr.backward(dy)
+        assert _rel(x.grad, xr.grad) < 3e-2
+        assert _rel(w.grad, wr.grad) < 3e-2
+
+
+def test_activations_add_upsample():
+    from deep_vision_amd import ops as F
+
+    x32 = torch.randn(2, 16, 6, 6, device=DEV).bfloat16().float()
+    for act, ref in [("relu", TF.relu), ("tanh", torch.tanh), ("sigmoid", torch.sigmoid),
+                     ("leaky", lambda t: TF.leaky_relu(t, 0.1))]:
+        x = _nhwc(x32).requires_grad_(True)
+        y = F.activation(x, act, 0.1)
+        xr = x32.clone().requires_grad_(True)
+        yr = ref(xr)
+        assert _rel(y, yr) < 1e-2
+        y.sum().backward()
+        yr.sum().backward()
+        assert _rel(x.grad, xr.grad) < 2e-2
+    a = _nhwc(x32)
+    y = F.add(a, a, act="relu")
+    assert _rel(y, TF.relu(2 * x32)) < 1e-2
+    x = _nhwc(x32).requires_grad_(True)
+    u = F.upsample_nearest(x, 2)
+    ur = TF.interpolate(x32, scale_factor=2, mode="nearest")
+    assert _rel(u, ur) == 0.0
+    u.sum().backward()
+    assert torch.allclose(x.grad.float(), torch.full_like(x32, 4.0))
+
+
+def test_dropout_mask_consistency():
+    from deep_vision_amd import ops as F
+
+    x = torch.ones(4096, device=DEV, dtype=torch.bfloat16).requires_grad_(True)
+    y = F.dropout(x, 0.5, True)
+    kept = (y != 0).float().mean().item()
+    assert 0.45 < kept < 0.55
+    y.sum().backward()
+    assert torch.equal((x.grad != 0), (y != 0))
+
+
+def test_optimizers_match_torch():
+    from deep_vision_amd.train.optim import FusedAdam, FusedRMSprop, FusedSGD
+
+    for cls, ref_cls, kw in [
+        (FusedSGD, torch.optim.SGD, dict(lr=0.1, momentum=0.9, weight_decay=1e-4)),
+        (FusedAdam, torch.optim.Adam, dict(lr=1e-3)),
+        (FusedRMSprop, torch.optim.RMSprop, dict(lr=0.045, alpha=0.9, eps=1.0)),
+    ]:
+        p1 = [torch.randn(33, 7, device=DEV, requires_grad=True), torch.randn(5, device=DEV, requires_grad=True)]
+        p2 = [p.detach().clone().requires_grad_(True) for p in p1]
+        o1 = cls(p1, **kw)
+        o2 = ref_cls(p2, **kw)
+        for _ in range(3):
+            for a, b in zip(p1, p2):
+                g = torch.randn_like(a)
+                a.grad = g.clone()
+                b.grad = g.clone()
+            o1.step()
+            o2.step()
+        for a, b in zip(o1.param_views(), p2):
+            assert torch.allclose(a, b, atol=1e-5, rtol=1e-4), cls.__name__
