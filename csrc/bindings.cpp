@@ -58,14 +58,14 @@ PYBIND11_MODULE(_C, m) {
                             uptr acc, uptr st) {
     dv_bn_bwd_reduce(CP(dout), CP(out), CP(x), rows, C, CFP(mean), CFP(invstd), act, slope, FP(acc), ST(st)); check_last("bn_bwd_reduce");
   });
-  m.def("bn_bwd_finalize", [](uptr acc, int C, double count, uptr gamma, uptr invstd, uptr dgamma, uptr dbeta, uptr kmdz,
-                              uptr kmdzx, uptr kscale, uptr st) {
-    dv_bn_bwd_finalize(CFP(acc), C, count, CFP(gamma), CFP(invstd), FP(dgamma), FP(dbeta), FP(kmdz), FP(kmdzx), FP(kscale), ST(st));
+  m.def("bn_bwd_finalize", [](uptr acc, int C, double count, uptr gamma, uptr mean, uptr invstd, uptr dgamma, uptr dbeta,
+                              uptr kA, uptr kB, uptr kC, uptr st) {
+    dv_bn_bwd_finalize(CFP(acc), C, count, CFP(gamma), CFP(mean), CFP(invstd), FP(dgamma), FP(dbeta), FP(kA), FP(kB), FP(kC), ST(st));
     check_last("bn_bwd_finalize");
   });
-  m.def("bn_bwd_apply", [](uptr dout, uptr out, uptr x, uptr dx, uptr dres, int64_t n, int C, uptr mean, uptr invstd,
-                           uptr kmdz, uptr kmdzx, uptr kscale, int act, float slope, uptr st) {
-    dv_bn_bwd_apply(CP(dout), CP(out), CP(x), P(dx), P(dres), n, C, CFP(mean), CFP(invstd), CFP(kmdz), CFP(kmdzx), CFP(kscale), act, slope, ST(st));
+  m.def("bn_bwd_apply", [](uptr dout, uptr out, uptr x, uptr dx, uptr dres, int64_t n, int C, uptr kA, uptr kB, uptr kC,
+                           int act, float slope, uptr st) {
+    dv_bn_bwd_apply(CP(dout), CP(out), CP(x), P(dx), P(dres), n, C, CFP(kA), CFP(kB), CFP(kC), act, slope, ST(st));
     check_last("bn_bwd_apply");
   });
   m.def("bn_bwd_eval", [](uptr dout, uptr out, uptr dx, uptr dres, int64_t n, int C, uptr scale, int act, float slope, uptr st) {

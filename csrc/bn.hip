@@ -138,25 +138,44 @@ __global__ void bn_eval_prep_kernel(int C, float eps, const float* gamma, const 
   scale[c] = g * inv; shift[c] = b - rm[c] * g * inv;
 }
 
+// Row x channel-group tiling shared by the memory-bound BN passes: TPR = C/VEC threads cover
+// one pixel row (16-B vectors, fully coalesced), RPI = NT/TPR rows per iteration; every
+// thread keeps its VEC channels' parameters in registers for the whole block (no per-element
+// channel index arithmetic, no parameter reloads).
+struct RowTile {
+  int cg, tpr, rpi, lane_c, lane_r;
+  DV_DEVICE RowTile(int C, int VEC) {
+    cg = C / VEC; tpr = cg < NT ? cg : NT; rpi = NT / tpr;
+    lane_c = threadIdx.x % tpr; lane_r = threadIdx.x / tpr;
+  }
+};
+
 // ---- out = act(x*scale + shift (+res)) ----
 template <int VEC>
 __global__ __launch_bounds__(NT) void bn_apply_kernel(const u16* __restrict__ x, const u16* __restrict__ res,
-                                                        u16* __restrict__ out, int64_t nvec, int C,
+                                                        u16* __restrict__ out, int64_t rows, int C, int64_t rows_per_block,
                                                         const float* __restrict__ scale, const float* __restrict__ shift,
                                                         int act, float slope) {
-  const int cg = C / VEC;
-  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * NT) {
-    const int c0 = (int)(i % cg) * VEC;
-    float v[VEC], r[VEC];
-    VecIO<VEC>::load(x + i * VEC, v);
-    if (res) VecIO<VEC>::load(res + i * VEC, r);
+  RowTile t(C, VEC);
+  if (t.lane_r >= t.rpi) return;
+  const int64_t r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
+  for (int g = t.lane_c; g < t.cg; g += t.tpr) {
+    float sc[VEC], sf[VEC];
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-      float z = v[k] * scale[c0 + k] + shift[c0 + k];
-      if (res) z += r[k];
-      v[k] = act_fwd(z, act, slope);
+    for (int k = 0; k < VEC; ++k) { sc[k] = scale[g * VEC + k]; sf[k] = shift[g * VEC + k]; }
+    for (int64_t r = r0 + t.lane_r; r < r1; r += t.rpi) {
+      const int64_t o = r * C + g * VEC;
+      float v[VEC], rv[VEC];
+      VecIO<VEC>::load(x + o, v);
+      if (res) VecIO<VEC>::load(res + o, rv);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) {
+        float z = fmaf(v[k], sc[k], sf[k]);
+        if (res) z += rv[k];
+        v[k] = act_fwd(z, act, slope);
+      }
+      VecIO<VEC>::store(out + o, v);
     }
-    VecIO<VEC>::store(out + i * VEC, v);
   }
 }
 
@@ -210,79 +229,99 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(const u16* __restrict
   }
 }
 
-// fold backward shards: dbeta = sum dz, dgamma = sum dz*xhat; coef1/coef2 for the apply pass
+// fold backward shards: dbeta = sum dz, dgamma = sum dz*xhat, and the per-channel affine form
+// of the input gradient  dx = kA*dz + kB*x + kC  (kA = gamma*invstd,
+// kB = -kA*invstd*mean(dz*xhat), kC = kA*(mean*invstd*mean(dz*xhat) - mean(dz)))
 __global__ void bn_bwd_finalize_kernel(const float* __restrict__ acc, int C, double count, const float* __restrict__ gamma,
-                                       const float* __restrict__ invstd, float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                       float* __restrict__ k_mean_dz, float* __restrict__ k_mean_dzx, float* __restrict__ k_scale) {
+                                       const float* __restrict__ mean, const float* __restrict__ invstd,
+                                       float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ kA,
+                                       float* __restrict__ kB, float* __restrict__ kC) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   double s = 0.0, q = 0.0;
   for (int i = 0; i < SHARDS; ++i) { s += acc[(int64_t)i * 2 * C + c]; q += acc[(int64_t)i * 2 * C + C + c]; }
   if (dbeta) dbeta[c] = (float)s;
   if (dgamma) dgamma[c] = (float)q;
-  k_mean_dz[c] = (float)(s / count);
-  k_mean_dzx[c] = (float)(q / count);
-  k_scale[c] = (gamma ? gamma[c] : 1.f) * invstd[c];
+  const double mdz = s / count, mdzx = q / count;
+  const double is = invstd[c], a = (double)(gamma ? gamma[c] : 1.f) * is;
+  kA[c] = (float)a;
+  kB[c] = (float)(-a * is * mdzx);
+  kC[c] = (float)(a * ((double)mean[c] * is * mdzx - mdz));
 }
 
-// dx = k_scale * (dz - mean_dz - xhat * mean_dzx); optionally dres = dz
+// dx = kA*dz + kB*x + kC ; optionally dres = dz
 template <int VEC>
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const u16* __restrict__ dout, const u16* __restrict__ out,
                                                             const u16* __restrict__ x, u16* __restrict__ dx, u16* __restrict__ dres,
-                                                            int64_t nvec, int C, const float* __restrict__ mean,
-                                                            const float* __restrict__ invstd, const float* __restrict__ k_mean_dz,
-                                                            const float* __restrict__ k_mean_dzx, const float* __restrict__ k_scale,
+                                                            int64_t rows, int C, int64_t rows_per_block, const float* __restrict__ kA,
+                                                            const float* __restrict__ kB, const float* __restrict__ kC,
                                                             int act, float slope) {
-  const int cg = C / VEC;
-  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * NT) {
-    const int c0 = (int)(i % cg) * VEC;
-    float d[VEC], o[VEC], xv[VEC], r[VEC];
-    VecIO<VEC>::load(dout + i * VEC, d);
-    if (act) VecIO<VEC>::load(out + i * VEC, o);
-    VecIO<VEC>::load(x + i * VEC, xv);
+  RowTile t(C, VEC);
+  if (t.lane_r >= t.rpi) return;
+  const int64_t r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
+  for (int g = t.lane_c; g < t.cg; g += t.tpr) {
+    float a[VEC], b[VEC], cc[VEC];
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-      const int c = c0 + k;
-      const float dz = act ? act_bwd(d[k], o[k], act, slope) : d[k];
-      const float xh = (xv[k] - mean[c]) * invstd[c];
-      r[k] = dz;
-      d[k] = k_scale[c] * (dz - k_mean_dz[c] - xh * k_mean_dzx[c]);
+    for (int k = 0; k < VEC; ++k) { a[k] = kA[g * VEC + k]; b[k] = kB[g * VEC + k]; cc[k] = kC[g * VEC + k]; }
+    for (int64_t r = r0 + t.lane_r; r < r1; r += t.rpi) {
+      const int64_t o = r * C + g * VEC;
+      float d[VEC], ov[VEC], xv[VEC], rr[VEC];
+      VecIO<VEC>::load(dout + o, d);
+      if (act) VecIO<VEC>::load(out + o, ov);
+      VecIO<VEC>::load(x + o, xv);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) {
+        const float dz = act ? act_bwd(d[k], ov[k], act, slope) : d[k];
+        rr[k] = dz;
+        d[k] = fmaf(a[k], dz, fmaf(b[k], xv[k], cc[k]));
+      }
+      VecIO<VEC>::store(dx + o, d);
+      if (dres) VecIO<VEC>::store(dres + o, rr);
     }
-    VecIO<VEC>::store(dx + i * VEC, d);
-    if (dres) VecIO<VEC>::store(dres + i * VEC, r);
   }
 }
 
 // eval-mode / frozen-stat backward: dx = scale * dz
 template <int VEC>
 __global__ __launch_bounds__(NT) void bn_bwd_eval_kernel(const u16* __restrict__ dout, const u16* __restrict__ out,
-                                                           u16* __restrict__ dx, u16* __restrict__ dres, int64_t nvec, int C,
-                                                           const float* __restrict__ scale, int act, float slope) {
-  const int cg = C / VEC;
-  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * NT) {
-    const int c0 = (int)(i % cg) * VEC;
-    float d[VEC], o[VEC], r[VEC];
-    VecIO<VEC>::load(dout + i * VEC, d);
-    if (act) VecIO<VEC>::load(out + i * VEC, o);
+                                                           u16* __restrict__ dx, u16* __restrict__ dres, int64_t rows, int C,
+                                                           int64_t rows_per_block, const float* __restrict__ scale, int act,
+                                                           float slope) {
+  RowTile t(C, VEC);
+  if (t.lane_r >= t.rpi) return;
+  const int64_t r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
+  for (int g = t.lane_c; g < t.cg; g += t.tpr) {
+    float sc[VEC];
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-      const float dz = act ? act_bwd(d[k], o[k], act, slope) : d[k];
-      r[k] = dz; d[k] = dz * scale[c0 + k];
+    for (int k = 0; k < VEC; ++k) sc[k] = scale[g * VEC + k];
+    for (int64_t r = r0 + t.lane_r; r < r1; r += t.rpi) {
+      const int64_t o = r * C + g * VEC;
+      float d[VEC], ov[VEC], rr[VEC];
+      VecIO<VEC>::load(dout + o, d);
+      if (act) VecIO<VEC>::load(out + o, ov);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) {
+        const float dz = act ? act_bwd(d[k], ov[k], act, slope) : d[k];
+        rr[k] = dz; d[k] = dz * sc[k];
+      }
+      VecIO<VEC>::store(dx + o, d);
+      if (dres) VecIO<VEC>::store(dres + o, rr);
     }
-    VecIO<VEC>::store(dx + i * VEC, d);
-    if (dres) VecIO<VEC>::store(dres + i * VEC, r);
   }
 }
 
 inline int vec_for(int C) { return (C % 8 == 0) ? 8 : (C % 4 == 0) ? 4 : (C % 2 == 0) ? 2 : 1; }
-inline int grid_for(int64_t nvec) {
-  int64_t g = (nvec + NT - 1) / NT;
-  return (int)std::min<int64_t>(std::max<int64_t>(g, 1), 256 * 8);
-}
 inline int reduce_grid(int64_t rows) {
   // >= 4 blocks/CU worth of parallelism but at least ~32 rows per block
   int64_t g = std::min<int64_t>(1024, std::max<int64_t>(1, rows / 32));
   return (int)g;
+}
+// rows per block for the row-tiled apply passes: ~4096 blocks, a multiple of rows/iteration
+inline int64_t apply_rows_per_block(int64_t rows, int C, int v) {
+  const int cg = C / v, tpr = cg < NT ? cg : NT, rpi = NT / tpr;
+  int64_t rpb = (rows + 4095) / 4096;
+  rpb = ((rpb + rpi - 1) / rpi) * rpi;
+  return std::max<int64_t>(rpb, rpi);
 }
 }  // namespace
 
@@ -314,9 +353,10 @@ void dv_bn_eval_prep(int C, float eps, const float* gamma, const float* beta, co
 void dv_bn_apply(const void* x, const void* res, void* out, int64_t n, int C, const float* scale, const float* shift,
                  int act, float slope, hipStream_t st) {
   const int v = vec_for(C);
-  const int64_t nvec = n / v;
-  const int g = grid_for(nvec);
-  DISPATCH_VEC(C, bn_apply_kernel, <<<g, NT, 0, st>>>((const u16*)x, (const u16*)res, (u16*)out, nvec, C, scale, shift, act, slope))
+  const int64_t rows = n / C;
+  const int64_t rpb = apply_rows_per_block(rows, C, v);
+  const int g = (int)((rows + rpb - 1) / rpb);
+  DISPATCH_VEC(C, bn_apply_kernel, <<<g, NT, 0, st>>>((const u16*)x, (const u16*)res, (u16*)out, rows, C, rpb, scale, shift, act, slope))
 }
 
 void dv_bn_bwd_reduce(const void* dout, const void* out, const void* x, int64_t rows, int C, const float* mean,
@@ -325,25 +365,25 @@ void dv_bn_bwd_reduce(const void* dout, const void* out, const void* x, int64_t 
   DISPATCH_VEC(C, bn_bwd_reduce_kernel, <<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, rows, C, mean, invstd, act, slope, acc))
 }
 
-void dv_bn_bwd_finalize(const float* acc, int C, double count, const float* gamma, const float* invstd, float* dgamma,
-                        float* dbeta, float* k_mean_dz, float* k_mean_dzx, float* k_scale, hipStream_t st) {
-  bn_bwd_finalize_kernel<<<(C + 255) / 256, 256, 0, st>>>(acc, C, count, gamma, invstd, dgamma, dbeta, k_mean_dz,
-                                                          k_mean_dzx, k_scale);
+void dv_bn_bwd_finalize(const float* acc, int C, double count, const float* gamma, const float* mean, const float* invstd,
+                        float* dgamma, float* dbeta, float* kA, float* kB, float* kC, hipStream_t st) {
+  bn_bwd_finalize_kernel<<<(C + 255) / 256, 256, 0, st>>>(acc, C, count, gamma, mean, invstd, dgamma, dbeta, kA, kB, kC);
 }
 
 void dv_bn_bwd_apply(const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t n, int C,
-                     const float* mean, const float* invstd, const float* k_mean_dz, const float* k_mean_dzx,
-                     const float* k_scale, int act, float slope, hipStream_t st) {
+                     const float* kA, const float* kB, const float* kC, int act, float slope, hipStream_t st) {
   const int v = vec_for(C);
-  const int64_t nvec = n / v;
-  const int g = grid_for(nvec);
-  DISPATCH_VEC(C, bn_bwd_apply_kernel, <<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, (u16*)dx, (u16*)dres, nvec, C, mean, invstd, k_mean_dz, k_mean_dzx, k_scale, act, slope))
+  const int64_t rows = n / C;
+  const int64_t rpb = apply_rows_per_block(rows, C, v);
+  const int g = (int)((rows + rpb - 1) / rpb);
+  DISPATCH_VEC(C, bn_bwd_apply_kernel, <<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, (u16*)dx, (u16*)dres, rows, C, rpb, kA, kB, kC, act, slope))
 }
 
 void dv_bn_bwd_eval(const void* dout, const void* out, void* dx, void* dres, int64_t n, int C, const float* scale,
                     int act, float slope, hipStream_t st) {
   const int v = vec_for(C);
-  const int64_t nvec = n / v;
-  const int g = grid_for(nvec);
-  DISPATCH_VEC(C, bn_bwd_eval_kernel, <<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (u16*)dx, (u16*)dres, nvec, C, scale, act, slope))
+  const int64_t rows = n / C;
+  const int64_t rpb = apply_rows_per_block(rows, C, v);
+  const int g = (int)((rows + rpb - 1) / rpb);
+  DISPATCH_VEC(C, bn_bwd_eval_kernel, <<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (u16*)dx, (u16*)dres, rows, C, rpb, scale, act, slope))
 }

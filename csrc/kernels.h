@@ -46,11 +46,10 @@ void dv_bn_apply(const void* x, const void* res, void* out, int64_t n, int C, co
                  int act, float slope, hipStream_t st);
 void dv_bn_bwd_reduce(const void* dout, const void* out, const void* x, int64_t rows, int C, const float* mean,
                       const float* invstd, int act, float slope, float* acc, hipStream_t st);
-void dv_bn_bwd_finalize(const float* acc, int C, double count, const float* gamma, const float* invstd, float* dgamma,
-                        float* dbeta, float* k_mean_dz, float* k_mean_dzx, float* k_scale, hipStream_t st);
+void dv_bn_bwd_finalize(const float* acc, int C, double count, const float* gamma, const float* mean, const float* invstd,
+                        float* dgamma, float* dbeta, float* kA, float* kB, float* kC, hipStream_t st);
 void dv_bn_bwd_apply(const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t n, int C,
-                     const float* mean, const float* invstd, const float* k_mean_dz, const float* k_mean_dzx,
-                     const float* k_scale, int act, float slope, hipStream_t st);
+                     const float* kA, const float* kB, const float* kC, int act, float slope, hipStream_t st);
 void dv_bn_bwd_eval(const void* dout, const void* out, void* dx, void* dres, int64_t n, int C, const float* scale,
                     int act, float slope, hipStream_t st);
 

@@ -81,13 +81,11 @@ class _BNActFn(torch.autograd.Function):
             L.bn_bwd_reduce(ptr(dout), ptr(out), ptr(x), rows, C, ptr(mean), ptr(invstd), act, float(slope), ptr(acc), st)
             dgamma = torch.empty(C, dtype=F32, device=dev) if weight is not None else None
             dbeta = torch.empty(C, dtype=F32, device=dev) if weight is not None else None
-            kmdz = torch.empty(C, dtype=F32, device=dev)
-            kmdzx = torch.empty(C, dtype=F32, device=dev)
-            kscale = torch.empty(C, dtype=F32, device=dev)
-            L.bn_bwd_finalize(ptr(acc), C, float(rows), ptr(weight.detach() if weight is not None else None), ptr(invstd),
-                              ptr(dgamma), ptr(dbeta), ptr(kmdz), ptr(kmdzx), ptr(kscale), st)
-            L.bn_bwd_apply(ptr(dout), ptr(out), ptr(x), ptr(dx), ptr(dres), x.numel(), C, ptr(mean), ptr(invstd),
-                           ptr(kmdz), ptr(kmdzx), ptr(kscale), act, float(slope), st)
+            coef = torch.empty((3, C), dtype=F32, device=dev)
+            L.bn_bwd_finalize(ptr(acc), C, float(rows), ptr(weight.detach() if weight is not None else None), ptr(mean),
+                              ptr(invstd), ptr(dgamma), ptr(dbeta), ptr(coef[0]), ptr(coef[1]), ptr(coef[2]), st)
+            L.bn_bwd_apply(ptr(dout), ptr(out), ptr(x), ptr(dx), ptr(dres), x.numel(), C, ptr(coef[0]), ptr(coef[1]),
+                           ptr(coef[2]), act, float(slope), st)
         else:
             L.bn_bwd_eval(ptr(dout), ptr(out), ptr(dx), ptr(dres), x.numel(), C, ptr(scale), act, float(slope), st)
             # frozen statistics: dgamma = sum(dz * xhat), dbeta = sum(dz) are not needed in eval mode
