@@ -75,8 +75,24 @@ DV_DEVICE int xcd_remap(int bid, int nwg) {
   return base + loc;
 }
 
+// Magic-number unsigned division for 0 <= n < 2^31 (Granlund-Montgomery): q = (umulhi(n,m)+n) >> s.
+// Replaces the ~40-instruction integer division in index decodes (pixel -> (img, p, q)).
+struct FastDiv {
+  uint32_t mul, shr, d;
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f{0u, 0u, d};
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  f.shr = l;
+  f.mul = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1ull);
+  return f;
+}
+DV_DEVICE uint32_t fdiv(uint32_t n, const FastDiv& f) { return (__umulhi(n, f.mul) + n) >> f.shr; }
+
 // 16-byte aligned zero page used as the source address of padded / out-of-range
-// LDS-DMA lanes (global_load_lds cannot predicate a lane to "write zeros").
-extern __device__ __attribute__((aligned(16))) char dv_zero_page[256];
+// LDS-DMA lanes (global_load_lds cannot predicate a lane to "write zeros"). One copy per
+// translation unit: device code is not relocatable across TUs (no -fgpu-rdc).
+static __device__ __attribute__((aligned(16))) char dv_zero_page[256];
 
 #define DV_CHECK_LAUNCH() (void)hipGetLastError()

@@ -1,0 +1,355 @@
+// Implicit-GEMM convolution FORWARD on gfx950 MFMA (bf16 in, fp32 accumulate).
+// Also serves conv dgrad, ConvTranspose forward and Linear forward/dgrad (SURVEY §2.7 K1-K4,
+// K9, K13).
+//
+//   C[m = out pixel][n = out channel] = sum_k im2col(X)[m][k] * W[n][k],  k = (r, s, c)
+//
+// Structure (see /opt/skills/guides/cdna_hip_programming.md §5):
+//   * block tile BM x BN x 64, 256 threads = 4 waves, each wave a 64x64 sub-tile of
+//     4x4 v_mfma_f32_16x16x32_bf16. Tile variants: 128x128 (2x2 waves) and 256x64 (4x1 waves,
+//     for 64-channel layers that would waste half of a 128-wide tile).
+//   * operands staged global->LDS by LDS-DMA (global_load_lds_dwordx4); out-of-range /
+//     padding lanes read a zero page, so the im2col halo costs no branches.
+//   * K-contiguous LDS images, 128-B rows, XOR-swizzled on the SOURCE address (chunk ^
+//     (row>>1)&7) and read back with ds_read_b128 conflict-free.
+//   * 2-stage double buffer, one barrier per K-tile; a single stage (and so twice the
+//     blocks per CU) when K fits one tile — the HBM-bound 1x1 layers.
+//   * loader for C % 64 == 0 ("FASTC"): every K-tile is one filter tap (r, s) and a 64-channel
+//     slice, so each lane keeps a per-row base pointer and a tap-validity bitmask; per K-tile
+//     the address is base + a wave-uniform scalar offset (a few VALU per DMA instruction).
+//   * epilogue: +bias, ReLU/LeakyReLU, per-channel BatchNorm partial statistics (DPP row
+//     reductions + sharded atomics), then the tile is staged through LDS and written with
+//     16-byte stores covering whole 128-B lines of the NHWC output (any channel slice).
+//   * XCD-aware logical tile order: N-tiles of one M-panel run on one XCD (shared L2).
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int EPI_PITCH = 72;                      // bf16 elements per staged row (64 + 8 pad)
+constexpr int EPI_WAVE_BYTES = 64 * EPI_PITCH * 2;  // 9216
+constexpr int EPI_BYTES = 4 * EPI_WAVE_BYTES;       // 36864
+constexpr int STAT_BYTES = 2048;
+
+enum { KM_FAST = 0, KM_GENERIC = 1, KM_TGATHER = 2 };
+enum { ACT_NONE = 0, ACT_RELU = 1, ACT_LEAKY = 2 };
+
+struct FwdParams {
+  const u16* x;
+  const u16* w;
+  u16* y;
+  const float* bias;
+  float* stats;
+  int M, N, K, G;
+  int Hin, Win, Cg, ldx;
+  int P, Q;
+  int R, S, sh, sw, ph, pw, dh, dw;
+  int OH, OW, osh, osw, oph, opw, ldy;
+  int act; float slope;
+  int identity_map;
+  FastDiv div_pq, div_q;
+};
+
+DV_DEVICE void glds16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(GLB_PTR(src), LDS_PTR(lds_wave_base), 16, 0, 0);
+}
+// K-contiguous LDS image, rows of BK bf16 (128 B for BK=64, 64 B for BK=32), XOR-swizzled on
+// the 16-B chunk index; both swizzles are conflict-free for the ds_read_b128 lane groups.
+template <int BK_>
+DV_DEVICE int kc_swz(int row) {
+  if constexpr (BK_ == 64) return (row >> 1) & 7;
+  else return ((row >> 2) & 1) << 1;
+}
+template <int BK_>
+DV_DEVICE bf16x8 read_kc(const char* img, int row, int chunk) {
+  return *reinterpret_cast<const bf16x8*>(img + row * (BK_ * 2) + ((chunk ^ kc_swz<BK_>(row)) << 4));
+}
+
+template <int BM_, int BN_, int BK_>
+constexpr int stage_bytes() { return (BM_ + BN_) * BK_ * 2; }
+
+template <int BM_, int BN_, int BK_, int KMODE>
+__global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
+  constexpr int WN = BN_ / 64, WM = BM_ / 64;
+  static_assert(WN * WM == 4, "4 waves of 64x64");
+  constexpr int CH = BK_ / 8;          // 16-B chunks per LDS row
+  constexpr int RPI = 64 / CH;         // rows written by one 1-KB DMA wave-instruction
+  constexpr int MI = BM_ / RPI / 4;    // M-operand DMA instructions per wave per K-tile
+  constexpr int NI = BN_ / RPI / 4;    // N-operand DMA instructions per wave per K-tile
+  constexpr int KK = BK_ / 32;         // 32-deep MFMA steps per K-tile
+  constexpr int STAGE = stage_bytes<BM_, BN_, BK_>();
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wave_m = wid / WN, wave_n = wid % WN;
+
+  const int tiles_m = (p.M + BM_ - 1) / BM_, tiles_n = (p.N + BN_ - 1) / BN_;
+  int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int tn = logical % tiles_n; logical /= tiles_n;
+  const int tm = logical % tiles_m;
+  const int grp = logical / tiles_m;
+  const int m0 = tm * BM_, n0 = tn * BN_;
+  const char* zero = dv_zero_page;
+  const int64_t goff_x = (int64_t)grp * p.Cg;
+
+  // ---------------- per-lane load descriptors (fixed for the whole K loop) ----------------
+  const u16* wrow[NI];
+  bool wok[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int row = (wid * NI + j) * RPI + lane / CH;
+    const int lc = (lane % CH) ^ kc_swz<BK_>(row);
+    const int n = n0 + row;
+    wok[j] = n < p.N;
+    wrow[j] = p.w + ((int64_t)grp * p.N + (wok[j] ? n : 0)) * p.K + lc * 8;
+  }
+  const u16* xrow[MI];      // KM_FAST: pointer at (pixel origin, channel lc*8)
+  uint32_t tapmask[MI];     // KM_FAST: bit r (h valid) | bit 16+s (w valid); 0 for m >= M
+  int64_t pixbase[MI];      // generic: img*Hin*Win
+  int hb[MI], wb[MI];
+  bool mok[MI];
+#pragma unroll
+  for (int j = 0; j < MI; ++j) {
+    const int row = (wid * MI + j) * RPI + lane / CH;
+    const int lc = (lane % CH) ^ kc_swz<BK_>(row);
+    const int m = m0 + row;
+    mok[j] = m < p.M;
+    const int mm = mok[j] ? m : 0;
+    const int img = (int)fdiv((uint32_t)mm, p.div_pq), rem = mm - img * (p.P * p.Q);
+    const int pp = (int)fdiv((uint32_t)rem, p.div_q), qq = rem - pp * p.Q;
+    pixbase[j] = (int64_t)img * p.Hin * p.Win;
+    if (KMODE == KM_TGATHER) { hb[j] = pp + p.ph; wb[j] = qq + p.pw; }
+    else { hb[j] = pp * p.sh - p.ph; wb[j] = qq * p.sw - p.pw; }
+    if (KMODE == KM_FAST) {
+      uint32_t mk = 0;
+      for (int r = 0; r < p.R; ++r) { const int h = hb[j] + r * p.dh; mk |= (uint32_t)(h >= 0 && h < p.Hin) << r; }
+      for (int s = 0; s < p.S; ++s) { const int w = wb[j] + s * p.dw; mk |= (uint32_t)(w >= 0 && w < p.Win) << (16 + s); }
+      tapmask[j] = mok[j] ? mk : 0u;
+      xrow[j] = p.x + (pixbase[j] + (int64_t)hb[j] * p.Win + wb[j]) * p.ldx + goff_x + lc * 8;
+    }
+  }
+
+  // FASTC tap walker (wave-uniform)
+  int t_r = 0, t_s = 0, t_c = 0;
+  auto stage = [&](int kt, int buf) {
+    char* img_n = smem + buf * STAGE;
+    char* img_m = img_n + BN_ * BK_ * 2;
+    const int k0 = kt * BK_;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int row = (wid * NI + j) * RPI + lane / CH;
+      const int lc = (lane % CH) ^ kc_swz<BK_>(row);
+      const bool ok = wok[j] && (KMODE == KM_FAST || k0 + lc * 8 < p.K);
+      glds16(ok ? (const void*)(wrow[j] + k0) : (const void*)zero, img_n + (wid * NI + j) * 1024);
+    }
+    if (KMODE == KM_FAST) {
+      const int64_t koff = ((int64_t)(t_r * p.dh) * p.Win + t_s * p.dw) * p.ldx + t_c;
+      const int sh_r = t_r, sh_s = 16 + t_s;
+#pragma unroll
+      for (int j = 0; j < MI; ++j) {
+        const bool ok = (tapmask[j] >> sh_r) & (tapmask[j] >> sh_s) & 1u;
+        glds16(ok ? (const void*)(xrow[j] + koff) : (const void*)zero, img_m + (wid * MI + j) * 1024);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < MI; ++j) {
+        const int row = (wid * MI + j) * RPI + lane / CH;
+        const int lc = (lane % CH) ^ kc_swz<BK_>(row);
+        const int k = k0 + lc * 8;
+        const int rs = k / p.Cg, c = k - rs * p.Cg;
+        const int r = rs / p.S, s = rs - r * p.S;
+        bool ok = mok[j] && k < p.K;
+        int h, w;
+        if (KMODE == KM_TGATHER) {
+          const int hn = hb[j] - r * p.dh, wn = wb[j] - s * p.dw;
+          ok = ok && hn >= 0 && wn >= 0 && (hn % p.sh) == 0 && (wn % p.sw) == 0;
+          h = hn / p.sh; w = wn / p.sw;
+        } else {
+          h = hb[j] + r * p.dh; w = wb[j] + s * p.dw;
+        }
+        ok = ok && h >= 0 && h < p.Hin && w >= 0 && w < p.Win;
+        const void* src = zero;
+        if (ok) src = p.x + (pixbase[j] + (int64_t)h * p.Win + w) * p.ldx + goff_x + c;
+        glds16(src, img_m + (wid * MI + j) * 1024);
+      }
+    }
+  };
+  auto advance = [&]() {
+    if (KMODE == KM_FAST) {
+      t_c += BK_;
+      if (t_c >= p.Cg) { t_c = 0; if (++t_s == p.S) { t_s = 0; ++t_r; } }
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nt = (p.K + BK_ - 1) / BK_;
+  stage(0, 0);
+  advance();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nt) { stage(t + 1, cur ^ 1); advance(); }
+    const char* img_n = smem + cur * STAGE;
+    const char* img_m = img_n + BN_ * BK_ * 2;
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        fa[j] = read_kc<BK_>(img_n, wave_n * 64 + j * 16 + (lane & 15), kk * 4 + (lane >> 4));
+        fb[j] = read_kc<BK_>(img_m, wave_m * 64 + j * 16 + (lane & 15), kk * 4 + (lane >> 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[j], fb[i], acc[j][i], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---------------- epilogue ----------------
+  // acc[j][i][r]: n_local = j*16 + (lane>>4)*4 + r, m_local = i*16 + (lane&15) within the wave tile
+  const int nw0 = n0 + wave_n * 64;  // first channel of this wave
+  float bsum[4][4], bsq[4][4];
+  u16* st = reinterpret_cast<u16*>(smem + wid * EPI_WAVE_BYTES);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float bv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = nw0 + j * 16 + (lane >> 4) * 4 + r;
+      bv[r] = (p.bias && n < p.N) ? p.bias[grp * p.N + n] : 0.f;
+      bsum[j][r] = 0.f; bsq[j][r] = 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ml = i * 16 + (lane & 15);
+      const bool mv = m0 + wave_m * 64 + ml < p.M;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float t = acc[j][i][r] + bv[r];
+        if (p.act == ACT_RELU) t = fmaxf(t, 0.f);
+        else if (p.act == ACT_LEAKY) t = t > 0.f ? t : t * p.slope;
+        v[r] = t;
+        if (mv) { bsum[j][r] += t; bsq[j][r] += t * t; }
+      }
+      uint2 pk; pk.x = pack2bf(v[0], v[1]); pk.y = pack2bf(v[2], v[3]);
+      *reinterpret_cast<uint2*>(st + ml * EPI_PITCH + j * 16 + (lane >> 4) * 4) = pk;
+    }
+  }
+  if (p.stats) {
+    float* sh = reinterpret_cast<float*>(smem + EPI_BYTES);  // [WM][BN_][2]
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float s1 = row16_sum(bsum[j][r]);
+        const float s2 = row16_sum(bsq[j][r]);
+        if ((lane & 15) == 0) {
+          const int nl = wave_n * 64 + j * 16 + (lane >> 4) * 4 + r;
+          sh[(wave_m * BN_ + nl) * 2 + 0] = s1;
+          sh[(wave_m * BN_ + nl) * 2 + 1] = s2;
+        }
+      }
+  }
+  __syncthreads();
+  if (p.stats && threadIdx.x < BN_) {
+    const float* sh = reinterpret_cast<const float*>(smem + EPI_BYTES);
+    const int n = n0 + threadIdx.x;
+    if (n < p.N) {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) { s1 += sh[(w * BN_ + threadIdx.x) * 2]; s2 += sh[(w * BN_ + threadIdx.x) * 2 + 1]; }
+      const int64_t ncols = (int64_t)p.G * p.N;
+      float* a = p.stats + (int64_t)(tm % DV_STAT_SHARDS) * 2 * ncols;
+      atomicAdd(a + grp * p.N + n, s1);
+      atomicAdd(a + ncols + grp * p.N + n, s2);
+    }
+  }
+  // staged tile -> global: each wave writes its 64 rows x 64 channels as 16-B pieces
+  const int64_t goff_y = (int64_t)grp * p.N;
+  const bool vec = ((p.N & 7) == 0) && ((p.ldy & 7) == 0) && ((goff_y & 7) == 0);
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int rl = it * 8 + (lane >> 3), ch = (lane & 7) * 8;
+    const int m = m0 + wave_m * 64 + rl;
+    const int n = nw0 + ch;
+    if (m >= p.M || n >= p.N) continue;
+    int64_t opix;
+    if (p.identity_map) opix = m;
+    else {
+      const int img = (int)fdiv((uint32_t)m, p.div_pq), rem = m - img * (p.P * p.Q);
+      const int pp = (int)fdiv((uint32_t)rem, p.div_q), qq = rem - pp * p.Q;
+      opix = ((int64_t)img * p.OH + pp * p.osh + p.oph) * p.OW + qq * p.osw + p.opw;
+    }
+    u16* dst = p.y + opix * p.ldy + goff_y + n;
+    const u16* src = st + rl * EPI_PITCH + ch;
+    if (vec) {
+      *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) if (n + e < p.N) dst[e] = src[e];
+    }
+  }
+}
+
+template <int BM_, int BN_, int BK_>
+constexpr int lds_bytes(int stages) {
+  return (stages * stage_bytes<BM_, BN_, BK_>() > EPI_BYTES ? stages * stage_bytes<BM_, BN_, BK_>() : EPI_BYTES) +
+         STAT_BYTES;
+}
+
+template <int BM_, int BN_, int BK_, int KMODE>
+void launch_fwd(const FwdParams& p, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)conv_fwd_kernel<BM_, BN_, BK_, KMODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        lds_bytes<BM_, BN_, BK_>(2));
+    attr = true;
+  }
+  const int nt = (p.K + BK_ - 1) / BK_;
+  const size_t lds = lds_bytes<BM_, BN_, BK_>(nt > 1 ? 2 : 1);
+  const int blocks = ((p.M + BM_ - 1) / BM_) * ((p.N + BN_ - 1) / BN_) * p.G;
+  conv_fwd_kernel<BM_, BN_, BK_, KMODE><<<dim3(blocks), dim3(NT), lds, st>>>(p);
+}
+
+template <int KMODE>
+void dispatch_tile(const FwdParams& p, hipStream_t st) {
+  // 64-channel outputs: a 256x64 tile keeps every MFMA useful; BK=32 keeps two stages at
+  // 40 KB so three blocks share a CU.
+  if (p.N <= 64) launch_fwd<256, 64, 32, KMODE>(p, st);
+  else launch_fwd<128, 128, 64, KMODE>(p, st);
+}
+
+}  // namespace
+
+int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
+  FwdParams p{};
+  p.x = (const u16*)a.x; p.w = (const u16*)a.w; p.y = (u16*)a.y;
+  p.bias = a.bias; p.stats = a.stats;
+  p.G = a.G; p.M = a.Nb * a.P * a.Q; p.N = a.Kout; p.K = a.R * a.S * a.Cg;
+  p.Hin = a.H; p.Win = a.W; p.Cg = a.Cg; p.ldx = a.ldx;
+  p.P = a.P; p.Q = a.Q; p.R = a.R; p.S = a.S;
+  p.sh = a.sh; p.sw = a.sw; p.ph = a.ph; p.pw = a.pw; p.dh = a.dh; p.dw = a.dw;
+  p.OH = a.OH; p.OW = a.OW; p.osh = a.osh; p.osw = a.osw; p.oph = a.oph; p.opw = a.opw; p.ldy = a.ldy;
+  p.act = a.act; p.slope = a.slope;
+  p.identity_map = (a.OH == a.P && a.OW == a.Q && a.osh == 1 && a.osw == 1 && a.oph == 0 && a.opw == 0);
+  if (p.Cg % 8 != 0 || p.ldx % 8 != 0) return -1;
+  p.div_pq = make_fastdiv((uint32_t)(a.P * a.Q));
+  p.div_q = make_fastdiv((uint32_t)a.Q);
+  // the fast loader needs every K-tile inside one filter tap: Cg % 64 == 0 covers both BKs
+  if (a.tgather) dispatch_tile<KM_TGATHER>(p, st);
+  else if (p.Cg % 64 == 0 && p.R <= 16 && p.S <= 16) dispatch_tile<KM_FAST>(p, st);
+  else dispatch_tile<KM_GENERIC>(p, st);
+  return 0;
+}

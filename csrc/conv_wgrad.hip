@@ -1,0 +1,294 @@
+// Implicit-GEMM convolution WEIGHT GRADIENT on gfx950 MFMA (also ConvTranspose
+// and Linear wgrad).
+//
+//   dW[m = out channel][n = (r, s, c)] = sum_{pix} dY[pix][m] * im2col(X)[pix][n]
+//
+// The reduction runs over every output pixel of the batch (up to N*H*W = 802,816 for ResNet-50
+// at batch 256), so the K dimension is split over blocks ("split-K") and each block adds its
+// fp32 tile into dW with 256-B-row atomics staged through LDS (Guideline 12: the atomic traffic
+// per FLOP is bounded by giving every split >= 2048 pixels).
+//
+// Both operands are MN-contiguous in NHWC (pixels are rows, channels contiguous), so they are
+// staged by LDS-DMA as [64 pixels][cols] images and fed to MFMA through the hardware-transposed
+// read ds_read_b64_tr_b16. The column XOR swizzle (on 8-byte units, keyed by the pixel row) makes
+// those reads conflict-free for any row length that is a multiple of 256 B.
+//
+// Tile variants (4 waves of 64x64): 128x128, and 64x256 for 64-output-channel layers.
+// A plain-row fast path serves 1x1 / stride-1 / pad-0 convs and Linear (no spatial decode).
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr int BK = 64;  // pixels per K-tile
+constexpr int NT = 256;
+constexpr int F32_PAD = 4;
+
+struct WgParams {
+  const u16* x;   // im2col source (N operand)
+  const u16* dy;  // M operand rows
+  float* dw;      // [G][M][N]
+  int M, N, K, G;
+  int Hin, Win, Cg, ldx, ldm;
+  int P, Q;
+  int R, S, sh, sw, ph, pw, dh, dw_;
+  int splits, ktiles_per_split, atomic_out;
+  FastDiv div_pq, div_q, div_cg, div_s;
+};
+
+DV_DEVICE void glds16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(GLB_PTR(src), LDS_PTR(lds_wave_base), 16, 0, 0);
+}
+// 16-byte-chunk XOR key of pixel row k (multiples of 2 chunks = 32-B blocks). Rows of >= 256 B
+// take 8 keys; 128-B rows (64 columns) take 4 keys and rely on the row parity for the other
+// half of the bank row. Both verified conflict-free for the tr-read lane groups.
+template <int COLS>
+DV_DEVICE int mn_swz(int k) {
+  if constexpr (COLS >= 128) return ((k & 3) | ((k >> 1) & 4)) << 1;
+  else return (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 1;
+}
+
+// 8-element MFMA fragment from an MN image [64 k][COLS] via two transposed reads.
+template <int COLS>
+DV_DEVICE bf16x8 read_mn(const char* img, int col0, int kbase, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int k1 = kbase + 8 * g + q, k2 = k1 + 4;
+  const int u = (col0 >> 2) + p;
+  const char* a1 = img + k1 * (COLS * 2) + ((u ^ (mn_swz<COLS>(k1) << 1)) << 3);
+  const char* a2 = img + k2 * (COLS * 2) + ((u ^ (mn_swz<COLS>(k2) << 1)) << 3);
+  i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((i16x4 __attribute__((address_space(3)))*)LDS_PTR(a1));
+  i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((i16x4 __attribute__((address_space(3)))*)LDS_PTR(a2));
+  i16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+template <int BM_, int BN_, bool PLAIN>
+__global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgParams p) {
+  constexpr int WN = BN_ / 64, WM = BM_ / 64;
+  static_assert(WN * WM == 4, "4 waves of 64x64");
+  constexpr int MCH = BM_ / 8, NCH = BN_ / 8;        // 16-B chunks per image row
+  constexpr int MRPI = 64 / MCH, NRPI = 64 / NCH;    // image rows per 1-KB DMA instruction
+  constexpr int MI = (BK / MRPI) / 4, NI = (BK / NRPI) / 4;  // DMA instructions per wave per tile
+  constexpr int MBYTES = BK * BM_ * 2, STAGE = BK * (BM_ + BN_) * 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wave_m = wid / WN, wave_n = wid % WN;
+
+  const int tiles_m = (p.M + BM_ - 1) / BM_, tiles_n = (p.N + BN_ - 1) / BN_;
+  int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int tn = logical % tiles_n; logical /= tiles_n;
+  const int tm = logical % tiles_m; logical /= tiles_m;
+  const int split = logical % p.splits, grp = logical / p.splits;
+  const int m0 = tm * BM_, n0 = tn * BN_;
+  const char* zero = dv_zero_page;
+  const int kt0 = split * p.ktiles_per_split;
+  const int kt1 = min((p.K + BK - 1) / BK, kt0 + p.ktiles_per_split);
+  const int nt = kt1 - kt0;
+  const int64_t goff_x = (int64_t)grp * p.Cg;
+
+  // ---- M operand (dY): per instruction a fixed 8-channel chunk; pixel row = k0 + row ----
+  const u16* mrow[MI];
+  bool mok[MI];
+#pragma unroll
+  for (int j = 0; j < MI; ++j) {
+    const int row = (wid * MI + j) * MRPI + lane / MCH;
+    const int lc = (lane % MCH) ^ mn_swz<BM_>(row);
+    const int m = m0 + lc * 8;
+    mok[j] = m < p.M;
+    mrow[j] = p.dy + (int64_t)row * p.ldm + (int64_t)grp * p.M + (mok[j] ? m : 0);
+  }
+  // ---- N operand (im2col X): fixed column chunk (r, s, c), pixel decode walked per tile ----
+  int n_r[NI], n_s[NI], n_c[NI];
+  bool nok[NI];
+  int w_img[NI], w_p[NI], w_q[NI];
+  const u16* nrow[NI];  // PLAIN: pointer at (pixel row, channel)
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int row = (wid * NI + j) * NRPI + lane / NCH;
+    const int lc = (lane % NCH) ^ mn_swz<BN_>(row);
+    const int n = n0 + lc * 8;
+    nok[j] = n < p.N;
+    const int nn = nok[j] ? n : 0;
+    if (PLAIN) {
+      n_c[j] = nn;
+      nrow[j] = p.x + (int64_t)row * p.ldx + goff_x + nn;
+    } else {
+      const int rs = (int)fdiv((uint32_t)nn, p.div_cg);
+      n_c[j] = nn - rs * p.Cg;
+      n_r[j] = (int)fdiv((uint32_t)rs, p.div_s);
+      n_s[j] = rs - n_r[j] * p.S;
+      const int pix = kt0 * BK + row;
+      w_img[j] = (int)fdiv((uint32_t)pix, p.div_pq);
+      const int rem = pix - w_img[j] * p.P * p.Q;
+      w_p[j] = (int)fdiv((uint32_t)rem, p.div_q);
+      w_q[j] = rem - w_p[j] * p.Q;
+    }
+  }
+  const int d_q = BK % p.Q, d_p = (BK / p.Q) % p.P, d_img = BK / (p.P * p.Q);
+
+  auto stage = [&](int kt, int buf) {
+    char* img_m = smem + buf * STAGE;
+    char* img_n = img_m + MBYTES;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int j = 0; j < MI; ++j) {
+      const int row = (wid * MI + j) * MRPI + lane / MCH;
+      const bool ok = mok[j] && (k0 + row < p.K);
+      glds16(ok ? (const void*)(mrow[j] + (int64_t)k0 * p.ldm) : (const void*)zero, img_m + (wid * MI + j) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int row = (wid * NI + j) * NRPI + lane / NCH;
+      const void* src = zero;
+      if (PLAIN) {
+        if (nok[j] && k0 + row < p.K) src = nrow[j] + (int64_t)k0 * p.ldx;
+      } else {
+        const int h = w_p[j] * p.sh - p.ph + n_r[j] * p.dh;
+        const int w = w_q[j] * p.sw - p.pw + n_s[j] * p.dw_;
+        if (nok[j] && k0 + row < p.K && (unsigned)h < (unsigned)p.Hin && (unsigned)w < (unsigned)p.Win)
+          src = p.x + (((int64_t)w_img[j] * p.Hin + h) * p.Win + w) * p.ldx + goff_x + n_c[j];
+      }
+      glds16(src, img_n + (wid * NI + j) * 1024);
+    }
+  };
+  auto advance = [&]() {
+    if (!PLAIN) {
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        int q = w_q[j] + d_q, pp = w_p[j] + d_p, im = w_img[j] + d_img;
+        if (q >= p.Q) { q -= p.Q; ++pp; }
+        if (pp >= p.P) { pp -= p.P; ++im; }
+        w_q[j] = q; w_p[j] = pp; w_img[j] = im;
+      }
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nt > 0) {
+    stage(kt0, 0);
+    advance();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int t = 0; t < nt; ++t) {
+      const int cur = t & 1;
+      if (t + 1 < nt) { stage(kt0 + t + 1, cur ^ 1); advance(); }
+      const char* img_m = smem + cur * STAGE;
+      const char* img_n = img_m + MBYTES;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 fa[4], fb[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          fa[j] = read_mn<BN_>(img_n, wave_n * 64 + j * 16, kk * 32, lane);
+          fb[j] = read_mn<BM_>(img_m, wave_m * 64 + j * 16, kk * 32, lane);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[j], fb[i], acc[j][i], 0, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: fp32 tile through LDS, then 256-B row segments (atomic or plain) ----
+  // acc[j][i][r]: n_local = wave_n*64 + j*16 + (lane>>4)*4 + r ; m_local = wave_m*64 + i*16 + (lane&15)
+  constexpr int LD = BN_ + F32_PAD;
+  float* T = reinterpret_cast<float*>(smem);  // [BM_][LD]
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int nl = wave_n * 64 + j * 16 + (lane >> 4) * 4;
+      const int ml = wave_m * 64 + i * 16 + (lane & 15);
+      *reinterpret_cast<f32x4*>(&T[ml * LD + nl]) = acc[j][i];
+    }
+  __syncthreads();
+  float* dwp = p.dw + (int64_t)grp * p.M * p.N;
+  for (int rr = wid; rr < BM_; rr += 4) {
+    const int m = m0 + rr;
+    if (m >= p.M) break;
+#pragma unroll
+    for (int h = 0; h < BN_ / 64; ++h) {
+      const int nl = h * 64 + lane, n = n0 + nl;
+      if (n < p.N) {
+        const float v = T[rr * LD + nl];
+        float* dst = dwp + (int64_t)m * p.N + n;
+        if (p.atomic_out) atomicAdd(dst, v); else *dst = v;
+      }
+    }
+  }
+}
+
+template <int BM_, int BN_>
+constexpr int wg_lds_bytes() {
+  constexpr int st = 2 * BK * (BM_ + BN_) * 2, ep = BM_ * (BN_ + F32_PAD) * 4;
+  return st > ep ? st : ep;
+}
+
+template <int BM_, int BN_, bool PLAIN>
+void launch_wg(const WgParams& p, int blocks, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)conv_wgrad_kernel<BM_, BN_, PLAIN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        wg_lds_bytes<BM_, BN_>());
+    attr = true;
+  }
+  constexpr int lds = wg_lds_bytes<BM_, BN_>();
+  conv_wgrad_kernel<BM_, BN_, PLAIN><<<dim3(blocks), dim3(NT), lds, st>>>(p);
+}
+
+inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+}  // namespace
+
+int dv_conv_wgrad_splits(const ConvWgradArgs& a) {
+  const int M = a.Kout, N = a.R * a.S * a.Cg, K = a.Nb * a.P * a.Q;
+  const bool narrow = M <= 64;
+  const int tiles = cdiv(M, narrow ? 64 : 128) * cdiv(N, narrow ? 256 : 128) * a.G;
+  const int ktiles = cdiv(K, BK);
+  int splits = cdiv(768, tiles);                        // ~3 blocks per CU
+  splits = std::min(splits, std::max(1, ktiles / 32));  // >= 2048 pixels per split (atomic budget)
+  return std::max(1, std::min(splits, ktiles));
+}
+
+int dv_conv_stats_tiles(int Nb, int P, int Q) { return cdiv(Nb * P * Q, 128); }
+
+int dv_conv_wgrad(const ConvWgradArgs& a, hipStream_t st) {
+  WgParams p{};
+  p.x = (const u16*)a.x; p.dy = (const u16*)a.dy; p.dw = a.dw;
+  p.G = a.G; p.M = a.Kout; p.N = a.R * a.S * a.Cg; p.K = a.Nb * a.P * a.Q;
+  p.Hin = a.H; p.Win = a.W; p.Cg = a.Cg; p.ldx = a.ldx; p.ldm = a.ldy;
+  p.P = a.P; p.Q = a.Q; p.R = a.R; p.S = a.S;
+  p.sh = a.sh; p.sw = a.sw; p.ph = a.ph; p.pw = a.pw; p.dh = a.dh; p.dw_ = a.dw_;
+  if (p.Cg % 8 != 0 || p.ldx % 8 != 0 || p.ldm % 8 != 0) return -1;
+  p.div_pq = make_fastdiv((uint32_t)(a.P * a.Q));
+  p.div_q = make_fastdiv((uint32_t)a.Q);
+  p.div_cg = make_fastdiv((uint32_t)a.Cg);
+  p.div_s = make_fastdiv((uint32_t)a.S);
+  const int ktiles = cdiv(p.K, BK);
+  const int splits = a.splits > 0 ? a.splits : dv_conv_wgrad_splits(a);
+  p.ktiles_per_split = cdiv(ktiles, splits);
+  p.splits = cdiv(ktiles, p.ktiles_per_split);
+  p.atomic_out = p.splits > 1 ? 1 : 0;
+  if (p.atomic_out) (void)hipMemsetAsync(a.dw, 0, (size_t)p.G * p.M * p.N * sizeof(float), st);
+  // plain rows: the im2col of a 1x1 / stride-1 / pad-0 conv is X itself (pixel grid == input grid)
+  const bool plain = a.R == 1 && a.S == 1 && a.sh == 1 && a.sw == 1 && a.ph == 0 && a.pw == 0 && a.P == a.H &&
+                     a.Q == a.W;
+  const bool narrow = p.M <= 64;
+  const int blocks = cdiv(p.M, narrow ? 64 : 128) * cdiv(p.N, narrow ? 256 : 128) * p.G * p.splits;
+  if (narrow) {
+    if (plain) launch_wg<64, 256, true>(p, blocks, st); else launch_wg<64, 256, false>(p, blocks, st);
+  } else {
+    if (plain) launch_wg<128, 128, true>(p, blocks, st); else launch_wg<128, 128, false>(p, blocks, st);
+  }
+  return p.splits;
+}
