@@ -34,8 +34,10 @@ PYBIND11_MODULE(_C, m) {
     check_last("conv_fwd");
   });
   m.def("conv_wgrad", [](uptr x, uptr dy, uptr dw, int Nb, int H, int W, int Cg, int ldx, int G, int Kout, int P_, int Q,
-                         int ldy, int R, int S, int sh, int sw, int ph, int pw, int dh, int dwl, int splits, uptr st) {
-    ConvWgradArgs a{CP(x), CP(dy), FP(dw), Nb, H, W, Cg, ldx, G, Kout, P_, Q, ldy, R, S, sh, sw, ph, pw, dh, dwl, splits};
+                         int ldy, int R, int S, int sh, int sw, int ph, int pw, int dh, int dwl, int splits, int accumulate,
+                         uptr st) {
+    ConvWgradArgs a{CP(x), CP(dy), FP(dw), Nb, H, W, Cg, ldx, G, Kout, P_, Q, ldy, R, S, sh, sw, ph, pw, dh, dwl, splits,
+                    accumulate};
     int r = dv_conv_wgrad(a, ST(st));
     if (r < 0) throw std::runtime_error("conv_wgrad: unsupported geometry (channels must be a multiple of 8)");
     check_last("conv_wgrad");
@@ -45,7 +47,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_stats", [](uptr x, int64_t rows, int C, uptr acc, uptr st) { dv_bn_stats(CP(x), rows, C, FP(acc), ST(st)); check_last("bn_stats"); });
   m.def("bn_finalize", [](uptr acc, int C, double count, float eps, float mom, uptr gamma, uptr beta, uptr rm, uptr rv,
                           uptr smean, uptr sinv, uptr scale, uptr shift, uptr st) {
-    dv_bn_finalize(CFP(acc), C, count, eps, mom, CFP(gamma), CFP(beta), FP(rm), FP(rv), FP(smean), FP(sinv), FP(scale), FP(shift), ST(st));
+    dv_bn_finalize(FP(acc), C, count, eps, mom, CFP(gamma), CFP(beta), FP(rm), FP(rv), FP(smean), FP(sinv), FP(scale), FP(shift), ST(st));
     check_last("bn_finalize");
   });
   m.def("bn_eval_prep", [](int C, float eps, uptr gamma, uptr beta, uptr rm, uptr rv, uptr scale, uptr shift, uptr st) {
@@ -54,18 +56,19 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_apply", [](uptr x, uptr res, uptr out, int64_t n, int C, uptr scale, uptr shift, int act, float slope, uptr st) {
     dv_bn_apply(CP(x), CP(res), P(out), n, C, CFP(scale), CFP(shift), act, slope, ST(st)); check_last("bn_apply");
   });
-  m.def("bn_bwd_reduce", [](uptr dout, uptr out, uptr x, int64_t rows, int C, uptr mean, uptr invstd, int act, float slope,
-                            uptr acc, uptr st) {
-    dv_bn_bwd_reduce(CP(dout), CP(out), CP(x), rows, C, CFP(mean), CFP(invstd), act, slope, FP(acc), ST(st)); check_last("bn_bwd_reduce");
+  m.def("bn_bwd_reduce", [](uptr dout, uptr out, uptr x, int64_t rows, int C, uptr mean, uptr invstd, uptr mscale,
+                            uptr mshift, int act, float slope, uptr acc, uptr st) {
+    dv_bn_bwd_reduce(CP(dout), CP(out), CP(x), rows, C, CFP(mean), CFP(invstd), CFP(mscale), CFP(mshift), act, slope, FP(acc), ST(st));
+    check_last("bn_bwd_reduce");
   });
   m.def("bn_bwd_finalize", [](uptr acc, int C, double count, uptr gamma, uptr mean, uptr invstd, uptr dgamma, uptr dbeta,
-                              uptr kA, uptr kB, uptr kC, uptr st) {
-    dv_bn_bwd_finalize(CFP(acc), C, count, CFP(gamma), CFP(mean), CFP(invstd), FP(dgamma), FP(dbeta), FP(kA), FP(kB), FP(kC), ST(st));
+                              int accumulate, uptr kA, uptr kB, uptr kC, uptr st) {
+    dv_bn_bwd_finalize(FP(acc), C, count, CFP(gamma), CFP(mean), CFP(invstd), FP(dgamma), FP(dbeta), accumulate, FP(kA), FP(kB), FP(kC), ST(st));
     check_last("bn_bwd_finalize");
   });
   m.def("bn_bwd_apply", [](uptr dout, uptr out, uptr x, uptr dx, uptr dres, int64_t n, int C, uptr kA, uptr kB, uptr kC,
-                           int act, float slope, uptr st) {
-    dv_bn_bwd_apply(CP(dout), CP(out), CP(x), P(dx), P(dres), n, C, CFP(kA), CFP(kB), CFP(kC), act, slope, ST(st));
+                           uptr mscale, uptr mshift, int act, float slope, uptr st) {
+    dv_bn_bwd_apply(CP(dout), CP(out), CP(x), P(dx), P(dres), n, C, CFP(kA), CFP(kB), CFP(kC), CFP(mscale), CFP(mshift), act, slope, ST(st));
     check_last("bn_bwd_apply");
   });
   m.def("bn_bwd_eval", [](uptr dout, uptr out, uptr dx, uptr dres, int64_t n, int C, uptr scale, int act, float slope, uptr st) {

@@ -80,6 +80,7 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(const u16* __restrict__ x,
 #pragma unroll
     for (int i = 0; i < VEC; ++i) { s[i] = 0.f; q[i] = 0.f; }
     if (lane_r < rpi && g < cg) {
+#pragma unroll 2
       for (int64_t r = r0 + lane_r; r < r1; r += rpi) {
         float v[VEC];
         VecIO<VEC>::load(x + r * C + g * VEC, v);
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(const u16* __restrict__ x,
 }
 
 // ---- fold shards -> mean/invstd/scale/shift, update running stats ----
-__global__ void bn_finalize_kernel(const float* __restrict__ acc, int C, double count, float eps,
+__global__ void bn_finalize_kernel(float* __restrict__ acc, int C, double count, float eps,
                                    float momentum, const float* __restrict__ gamma, const float* __restrict__ beta,
                                    float* __restrict__ running_mean, float* __restrict__ running_var,
                                    float* __restrict__ save_mean, float* __restrict__ save_invstd,
@@ -113,7 +114,11 @@ __global__ void bn_finalize_kernel(const float* __restrict__ acc, int C, double 
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   double s = 0.0, q = 0.0;
-  for (int i = 0; i < SHARDS; ++i) { s += acc[(int64_t)i * 2 * C + c]; q += acc[(int64_t)i * 2 * C + C + c]; }
+  // fold and re-zero the shards: the accumulator is persistent and self-cleaning (no memset launch)
+  for (int i = 0; i < SHARDS; ++i) {
+    float* a = acc + (int64_t)i * 2 * C + c;
+    s += a[0]; q += a[C]; a[0] = 0.f; a[C] = 0.f;
+  }
   const double mean = s / count;
   double var = q / count - mean * mean;
   if (var < 0) var = 0;
@@ -163,6 +168,7 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const u16* __restrict__ x,
     float sc[VEC], sf[VEC];
 #pragma unroll
     for (int k = 0; k < VEC; ++k) { sc[k] = scale[g * VEC + k]; sf[k] = shift[g * VEC + k]; }
+#pragma unroll 2
     for (int64_t r = r0 + t.lane_r; r < r1; r += t.rpi) {
       const int64_t o = r * C + g * VEC;
       float v[VEC], rv[VEC];
@@ -180,10 +186,15 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const u16* __restrict__ x,
 }
 
 // ---- backward reduce: sum dz, sum dz*xhat (xhat = (x-mean)*invstd) ----
-template <int VEC>
+// The activation mask comes from the saved output `out` when present (residual blocks), else it
+// is recomputed from the BN input: z = x*mscale + mshift (one tensor read less per pass).
+enum { MM_NONE = 0, MM_OUT = 1, MM_X = 2 };  // activation-mask source (compile time: no branchy loads)
+
+template <int VEC, int MM>
 __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(const u16* __restrict__ dout, const u16* __restrict__ out,
                                                              const u16* __restrict__ x, int64_t rows, int C,
                                                              const float* __restrict__ mean, const float* __restrict__ invstd,
+                                                             const float* __restrict__ mscale, const float* __restrict__ mshift,
                                                              int act, float slope, float* __restrict__ acc) {
   __shared__ float sh[2][NT * VEC];
   const int cg = C / VEC;
@@ -195,20 +206,27 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(const u16* __restrict
   const int64_t r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
   for (int cb = 0; cb < cg; cb += tpr) {
     const int g = cb + lane_c;
-    float s[VEC], q[VEC], mu[VEC], is[VEC];
+    float s[VEC], q[VEC], mu[VEC], is[VEC], ms[VEC], mh[VEC];
 #pragma unroll
     for (int i = 0; i < VEC; ++i) { s[i] = 0.f; q[i] = 0.f; }
     if (lane_r < rpi && g < cg) {
 #pragma unroll
-      for (int i = 0; i < VEC; ++i) { mu[i] = mean[g * VEC + i]; is[i] = invstd[g * VEC + i]; }
+      for (int i = 0; i < VEC; ++i) {
+        mu[i] = mean[g * VEC + i]; is[i] = invstd[g * VEC + i];
+        ms[i] = MM == MM_X ? mscale[g * VEC + i] : 0.f;
+        mh[i] = MM == MM_X ? mshift[g * VEC + i] : 0.f;
+      }
+#pragma unroll 2
       for (int64_t r = r0 + lane_r; r < r1; r += rpi) {
         float d[VEC], o[VEC], xv[VEC];
         VecIO<VEC>::load(dout + r * C + g * VEC, d);
-        if (act) VecIO<VEC>::load(out + r * C + g * VEC, o);
         VecIO<VEC>::load(x + r * C + g * VEC, xv);
+        if constexpr (MM == MM_OUT) VecIO<VEC>::load(out + r * C + g * VEC, o);
 #pragma unroll
         for (int i = 0; i < VEC; ++i) {
-          const float dz = act ? act_bwd(d[i], o[i], act, slope) : d[i];
+          float dz = d[i];
+          if constexpr (MM == MM_OUT) dz = act_bwd(d[i], o[i], act, slope);
+          if constexpr (MM == MM_X) dz = act_bwd(d[i], fmaf(xv[i], ms[i], mh[i]), act, slope);
           s[i] += dz; q[i] += dz * (xv[i] - mu[i]) * is[i];
         }
       }
@@ -229,19 +247,23 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(const u16* __restrict
   }
 }
 
-// fold backward shards: dbeta = sum dz, dgamma = sum dz*xhat, and the per-channel affine form
-// of the input gradient  dx = kA*dz + kB*x + kC  (kA = gamma*invstd,
+// fold backward shards (and re-zero them): dbeta = sum dz, dgamma = sum dz*xhat (written, or
+// added into the live gradient buffer when `accumulate`), and the per-channel affine form of
+// the input gradient  dx = kA*dz + kB*x + kC  (kA = gamma*invstd,
 // kB = -kA*invstd*mean(dz*xhat), kC = kA*(mean*invstd*mean(dz*xhat) - mean(dz)))
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ acc, int C, double count, const float* __restrict__ gamma,
+__global__ void bn_bwd_finalize_kernel(float* __restrict__ acc, int C, double count, const float* __restrict__ gamma,
                                        const float* __restrict__ mean, const float* __restrict__ invstd,
-                                       float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ kA,
-                                       float* __restrict__ kB, float* __restrict__ kC) {
+                                       float* __restrict__ dgamma, float* __restrict__ dbeta, int accumulate,
+                                       float* __restrict__ kA, float* __restrict__ kB, float* __restrict__ kC) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   double s = 0.0, q = 0.0;
-  for (int i = 0; i < SHARDS; ++i) { s += acc[(int64_t)i * 2 * C + c]; q += acc[(int64_t)i * 2 * C + C + c]; }
-  if (dbeta) dbeta[c] = (float)s;
-  if (dgamma) dgamma[c] = (float)q;
+  for (int i = 0; i < SHARDS; ++i) {
+    float* a = acc + (int64_t)i * 2 * C + c;
+    s += a[0]; q += a[C]; a[0] = 0.f; a[C] = 0.f;
+  }
+  if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)s : (float)s;
+  if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)q : (float)q;
   const double mdz = s / count, mdzx = q / count;
   const double is = invstd[c], a = (double)(gamma ? gamma[c] : 1.f) * is;
   kA[c] = (float)a;
@@ -250,28 +272,36 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ acc, int C, dou
 }
 
 // dx = kA*dz + kB*x + kC ; optionally dres = dz
-template <int VEC>
+template <int VEC, int MM>
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const u16* __restrict__ dout, const u16* __restrict__ out,
                                                             const u16* __restrict__ x, u16* __restrict__ dx, u16* __restrict__ dres,
                                                             int64_t rows, int C, int64_t rows_per_block, const float* __restrict__ kA,
                                                             const float* __restrict__ kB, const float* __restrict__ kC,
+                                                            const float* __restrict__ mscale, const float* __restrict__ mshift,
                                                             int act, float slope) {
   RowTile t(C, VEC);
   if (t.lane_r >= t.rpi) return;
   const int64_t r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
   for (int g = t.lane_c; g < t.cg; g += t.tpr) {
-    float a[VEC], b[VEC], cc[VEC];
+    float a[VEC], b[VEC], cc[VEC], ms[VEC], mh[VEC];
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) { a[k] = kA[g * VEC + k]; b[k] = kB[g * VEC + k]; cc[k] = kC[g * VEC + k]; }
+    for (int k = 0; k < VEC; ++k) {
+      a[k] = kA[g * VEC + k]; b[k] = kB[g * VEC + k]; cc[k] = kC[g * VEC + k];
+      ms[k] = MM == MM_X ? mscale[g * VEC + k] : 0.f;
+      mh[k] = MM == MM_X ? mshift[g * VEC + k] : 0.f;
+    }
+#pragma unroll 2
     for (int64_t r = r0 + t.lane_r; r < r1; r += t.rpi) {
       const int64_t o = r * C + g * VEC;
       float d[VEC], ov[VEC], xv[VEC], rr[VEC];
       VecIO<VEC>::load(dout + o, d);
-      if (act) VecIO<VEC>::load(out + o, ov);
       VecIO<VEC>::load(x + o, xv);
+      if constexpr (MM == MM_OUT) VecIO<VEC>::load(out + o, ov);
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
-        const float dz = act ? act_bwd(d[k], ov[k], act, slope) : d[k];
+        float dz = d[k];
+        if constexpr (MM == MM_OUT) dz = act_bwd(d[k], ov[k], act, slope);
+        if constexpr (MM == MM_X) dz = act_bwd(d[k], fmaf(xv[k], ms[k], mh[k]), act, slope);
         rr[k] = dz;
         d[k] = fmaf(a[k], dz, fmaf(b[k], xv[k], cc[k]));
       }
@@ -294,6 +324,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_eval_kernel(const u16* __restrict__
     float sc[VEC];
 #pragma unroll
     for (int k = 0; k < VEC; ++k) sc[k] = scale[g * VEC + k];
+#pragma unroll 2
     for (int64_t r = r0 + t.lane_r; r < r1; r += t.rpi) {
       const int64_t o = r * C + g * VEC;
       float d[VEC], ov[VEC], rr[VEC];
@@ -338,7 +369,7 @@ void dv_bn_stats(const void* x, int64_t rows, int C, float* acc, hipStream_t st)
   DISPATCH_VEC(C, bn_stats_kernel, <<<g, NT, 0, st>>>((const u16*)x, rows, C, acc))
 }
 
-void dv_bn_finalize(const float* acc, int C, double count, float eps, float momentum, const float* gamma,
+void dv_bn_finalize(float* acc, int C, double count, float eps, float momentum, const float* gamma,
                     const float* beta, float* rm, float* rv, float* save_mean, float* save_invstd, float* scale,
                     float* shift, hipStream_t st) {
   bn_finalize_kernel<<<(C + 255) / 256, 256, 0, st>>>(acc, C, count, eps, momentum, gamma, beta, rm, rv, save_mean,
@@ -359,24 +390,57 @@ void dv_bn_apply(const void* x, const void* res, void* out, int64_t n, int C, co
   DISPATCH_VEC(C, bn_apply_kernel, <<<g, NT, 0, st>>>((const u16*)x, (const u16*)res, (u16*)out, rows, C, rpb, scale, shift, act, slope))
 }
 
-void dv_bn_bwd_reduce(const void* dout, const void* out, const void* x, int64_t rows, int C, const float* mean,
-                      const float* invstd, int act, float slope, float* acc, hipStream_t st) {
-  const int g = reduce_grid(rows);
-  DISPATCH_VEC(C, bn_bwd_reduce_kernel, <<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, rows, C, mean, invstd, act, slope, acc))
+template <int MM>
+static void bwd_reduce_launch(int g, const void* dout, const void* out, const void* x, int64_t rows, int C, const float* mean,
+                              const float* invstd, const float* mscale, const float* mshift, int act, float slope, float* acc,
+                              hipStream_t st) {
+  switch (vec_for(C)) {
+    case 8: bn_bwd_reduce_kernel<8, MM><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, rows, C, mean, invstd, mscale, mshift, act, slope, acc); break;
+    case 4: bn_bwd_reduce_kernel<4, MM><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, rows, C, mean, invstd, mscale, mshift, act, slope, acc); break;
+    case 2: bn_bwd_reduce_kernel<2, MM><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, rows, C, mean, invstd, mscale, mshift, act, slope, acc); break;
+    default: bn_bwd_reduce_kernel<1, MM><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, rows, C, mean, invstd, mscale, mshift, act, slope, acc); break;
+  }
 }
 
-void dv_bn_bwd_finalize(const float* acc, int C, double count, const float* gamma, const float* mean, const float* invstd,
-                        float* dgamma, float* dbeta, float* kA, float* kB, float* kC, hipStream_t st) {
-  bn_bwd_finalize_kernel<<<(C + 255) / 256, 256, 0, st>>>(acc, C, count, gamma, mean, invstd, dgamma, dbeta, kA, kB, kC);
+void dv_bn_bwd_reduce(const void* dout, const void* out, const void* x, int64_t rows, int C, const float* mean,
+                      const float* invstd, const float* mscale, const float* mshift, int act, float slope, float* acc,
+                      hipStream_t st) {
+  const int g = reduce_grid(rows);
+  if (!act) bwd_reduce_launch<MM_NONE>(g, dout, out, x, rows, C, mean, invstd, mscale, mshift, act, slope, acc, st);
+  else if (out) bwd_reduce_launch<MM_OUT>(g, dout, out, x, rows, C, mean, invstd, mscale, mshift, act, slope, acc, st);
+  else bwd_reduce_launch<MM_X>(g, dout, out, x, rows, C, mean, invstd, mscale, mshift, act, slope, acc, st);
+}
+
+void dv_bn_bwd_finalize(float* acc, int C, double count, const float* gamma, const float* mean, const float* invstd,
+                        float* dgamma, float* dbeta, int accumulate, float* kA, float* kB, float* kC, hipStream_t st) {
+  bn_bwd_finalize_kernel<<<(C + 255) / 256, 256, 0, st>>>(acc, C, count, gamma, mean, invstd, dgamma, dbeta, accumulate,
+                                                          kA, kB, kC);
+}
+
+template <int MM>
+static void bwd_apply_launch(int g, const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t rows,
+                             int C, int64_t rpb, const float* kA, const float* kB, const float* kC, const float* mscale,
+                             const float* mshift, int act, float slope, hipStream_t st) {
+#define BA_ARGS <<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, (u16*)dx, (u16*)dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope)
+  switch (vec_for(C)) {
+    case 8: bn_bwd_apply_kernel<8, MM> BA_ARGS; break;
+    case 4: bn_bwd_apply_kernel<4, MM> BA_ARGS; break;
+    case 2: bn_bwd_apply_kernel<2, MM> BA_ARGS; break;
+    default: bn_bwd_apply_kernel<1, MM> BA_ARGS; break;
+  }
+#undef BA_ARGS
 }
 
 void dv_bn_bwd_apply(const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t n, int C,
-                     const float* kA, const float* kB, const float* kC, int act, float slope, hipStream_t st) {
+                     const float* kA, const float* kB, const float* kC, const float* mscale, const float* mshift, int act,
+                     float slope, hipStream_t st) {
   const int v = vec_for(C);
   const int64_t rows = n / C;
   const int64_t rpb = apply_rows_per_block(rows, C, v);
   const int g = (int)((rows + rpb - 1) / rpb);
-  DISPATCH_VEC(C, bn_bwd_apply_kernel, <<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, (u16*)dx, (u16*)dres, rows, C, rpb, kA, kB, kC, act, slope))
+  if (!act) bwd_apply_launch<MM_NONE>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, st);
+  else if (out) bwd_apply_launch<MM_OUT>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, st);
+  else bwd_apply_launch<MM_X>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, st);
 }
 
 void dv_bn_bwd_eval(const void* dout, const void* out, void* dx, void* dres, int64_t n, int C, const float* scale,

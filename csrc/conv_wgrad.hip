@@ -32,7 +32,7 @@ struct WgParams {
   int Hin, Win, Cg, ldx, ldm;
   int P, Q;
   int R, S, sh, sw, ph, pw, dh, dw_;
-  int splits, ktiles_per_split, atomic_out;
+  int splits, ktiles_per_split, atomic_out, accumulate;
   FastDiv div_pq, div_q, div_cg, div_s;
 };
 
@@ -222,7 +222,8 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgParams p) {
       if (n < p.N) {
         const float v = T[rr * LD + nl];
         float* dst = dwp + (int64_t)m * p.N + n;
-        if (p.atomic_out) atomicAdd(dst, v); else *dst = v;
+        if (p.atomic_out) atomicAdd(dst, v);
+        else *dst = p.accumulate ? *dst + v : v;
       }
     }
   }
@@ -279,7 +280,8 @@ int dv_conv_wgrad(const ConvWgradArgs& a, hipStream_t st) {
   p.ktiles_per_split = cdiv(ktiles, splits);
   p.splits = cdiv(ktiles, p.ktiles_per_split);
   p.atomic_out = p.splits > 1 ? 1 : 0;
-  if (p.atomic_out) (void)hipMemsetAsync(a.dw, 0, (size_t)p.G * p.M * p.N * sizeof(float), st);
+  p.accumulate = a.accumulate;
+  if (p.atomic_out && !a.accumulate) (void)hipMemsetAsync(a.dw, 0, (size_t)p.G * p.M * p.N * sizeof(float), st);
   // plain rows: the im2col of a 1x1 / stride-1 / pad-0 conv is X itself (pixel grid == input grid)
   const bool plain = a.R == 1 && a.S == 1 && a.sh == 1 && a.sw == 1 && a.ph == 0 && a.pw == 0 && a.P == a.H &&
                      a.Q == a.W;

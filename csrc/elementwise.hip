@@ -141,21 +141,30 @@ __global__ void wgrad_unprep_kernel(const float* __restrict__ src, float* __rest
   }
 }
 
-// NCHW (fp32 or bf16) -> NHWC bf16 with channel padding
+// NCHW (fp32 or bf16) -> NHWC bf16 with channel padding. One thread per pixel and group of 8
+// output channels: reads are coalesced across threads (consecutive w), writes are 16-B vectors.
 template <typename T>
 __global__ void to_nhwc_kernel(const T* __restrict__ x, u16* __restrict__ y, int N, int C, int H, int W, int Cp) {
-  const int64_t total = (int64_t)N * H * W * Cp;
+  const int64_t HW = (int64_t)H * W;
+  const int cg = Cp / 8;
+  const int64_t total = (int64_t)N * HW * cg;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    int64_t u = t;
-    const int c = (int)(u % Cp); u /= Cp;
-    const int w = (int)(u % W); u /= W;
-    const int h = (int)(u % H); const int n = (int)(u / H);
-    float v = 0.f;
-    if (c < C) {
-      const int64_t src = (((int64_t)n * C + c) * H + h) * W + w;
-      if constexpr (sizeof(T) == 4) v = x[src]; else v = bf2f(x[src]);
+    const int64_t pix = t % (N * HW);  // pixel fastest -> coalesced reads
+    const int g = (int)(t / (N * HW));
+    const int64_t n = pix / HW, hw = pix - n * HW;
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = g * 8 + k;
+      v[k] = 0.f;
+      if (c < C) {
+        const int64_t src = (n * C + c) * HW + hw;
+        if constexpr (sizeof(T) == 4) v[k] = x[src]; else v[k] = bf2f(x[src]);
+      }
     }
-    y[t] = f2bf(v);
+    uint4 r;
+    r.x = pack2bf(v[0], v[1]); r.y = pack2bf(v[2], v[3]); r.z = pack2bf(v[4], v[5]); r.w = pack2bf(v[6], v[7]);
+    *reinterpret_cast<uint4*>(y + pix * Cp + g * 8) = r;
   }
 }
 
@@ -194,7 +203,7 @@ void dv_wgrad_unprep(const float* src, float* dst, int G, int Og, int Ig, int R,
   wgrad_unprep_kernel<<<grid_for(total), NT, 0, st>>>(src, dst, G, Og, Ig, R, S, Ipad, alpha, accumulate);
 }
 void dv_to_nhwc(const void* x, int x_is_f32, void* y, int N, int C, int H, int W, int Cp, hipStream_t st) {
-  const int64_t total = (int64_t)N * H * W * Cp;
+  const int64_t total = (int64_t)N * H * W * (Cp / 8);
   if (x_is_f32) to_nhwc_kernel<float><<<grid_for(total), NT, 0, st>>>((const float*)x, (u16*)y, N, C, H, W, Cp);
   else to_nhwc_kernel<u16><<<grid_for(total), NT, 0, st>>>((const u16*)x, (u16*)y, N, C, H, W, Cp);
 }

@@ -28,6 +28,7 @@ struct ConvWgradArgs {
   int Kout, P, Q, ldy;
   int R, S, sh, sw, ph, pw, dh, dw_;
   int splits;      // 0 = heuristic
+  int accumulate;  // add into dw (live gradient buffer) instead of overwriting
 };
 
 int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st);
@@ -37,7 +38,7 @@ int dv_conv_stats_tiles(int Nb, int P, int Q);
 
 // ---- batchnorm (bn.hip) ----
 void dv_bn_stats(const void* x, int64_t rows, int C, float* acc, hipStream_t st);
-void dv_bn_finalize(const float* acc, int C, double count, float eps, float momentum, const float* gamma,
+void dv_bn_finalize(float* acc, int C, double count, float eps, float momentum, const float* gamma,
                     const float* beta, float* rm, float* rv, float* save_mean, float* save_invstd, float* scale,
                     float* shift, hipStream_t st);
 void dv_bn_eval_prep(int C, float eps, const float* gamma, const float* beta, const float* rm, const float* rv,
@@ -45,11 +46,13 @@ void dv_bn_eval_prep(int C, float eps, const float* gamma, const float* beta, co
 void dv_bn_apply(const void* x, const void* res, void* out, int64_t n, int C, const float* scale, const float* shift,
                  int act, float slope, hipStream_t st);
 void dv_bn_bwd_reduce(const void* dout, const void* out, const void* x, int64_t rows, int C, const float* mean,
-                      const float* invstd, int act, float slope, float* acc, hipStream_t st);
-void dv_bn_bwd_finalize(const float* acc, int C, double count, const float* gamma, const float* mean, const float* invstd,
-                        float* dgamma, float* dbeta, float* kA, float* kB, float* kC, hipStream_t st);
+                      const float* invstd, const float* mscale, const float* mshift, int act, float slope, float* acc,
+                      hipStream_t st);
+void dv_bn_bwd_finalize(float* acc, int C, double count, const float* gamma, const float* mean, const float* invstd,
+                        float* dgamma, float* dbeta, int accumulate, float* kA, float* kB, float* kC, hipStream_t st);
 void dv_bn_bwd_apply(const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t n, int C,
-                     const float* kA, const float* kB, const float* kC, int act, float slope, hipStream_t st);
+                     const float* kA, const float* kB, const float* kC, const float* mscale, const float* mshift, int act,
+                     float slope, hipStream_t st);
 void dv_bn_bwd_eval(const void* dout, const void* out, void* dx, void* dres, int64_t n, int C, const float* scale,
                     int act, float slope, hipStream_t st);
 

@@ -18,7 +18,8 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as TF
 
-from .common import ACT_IDS, BF16, F32, grad_nhwc, is_nhwc, ld_of, lib, native, ptr, stream_handle
+from .common import (ACT_IDS, BF16, F32, grad_nhwc, grad_sink, is_nhwc, ld_of, lib, native, notify_grad_ready, ptr,
+                     stream_handle, workspace)
 
 STAT_SHARDS = 64
 
@@ -31,40 +32,41 @@ def _nrows(x):
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, stats, weight, bias, running_mean, running_var, residual, training, momentum, eps, act,
-                slope):
+                slope, ws_fwd, ws_bwd):
         N, C, H, W = x.shape
-        ld = ld_of(x)
-        if ld != C:
+        if ld_of(x) != C:
             raise NotImplementedError("BatchNorm on a padded channel view")
         dev = x.device
         st = stream_handle()
         L = lib()
-        scale = torch.empty(C, dtype=F32, device=dev)
-        shift = torch.empty(C, dtype=F32, device=dev)
+        prm = torch.empty((4, C), dtype=F32, device=dev)  # scale, shift, mean, invstd
+        scale, shift, mean, invstd = prm[0], prm[1], prm[2], prm[3]
         rows = N * H * W
         g = weight.detach() if weight is not None else None
         b = bias.detach() if bias is not None else None
         if training:
             if stats is None:
-                stats = torch.zeros((STAT_SHARDS, 2, C), dtype=F32, device=dev)
+                stats = ws_fwd
                 L.bn_stats(ptr(x), rows, C, ptr(stats), st)
-            mean = torch.empty(C, dtype=F32, device=dev)
-            invstd = torch.empty(C, dtype=F32, device=dev)
             L.bn_finalize(ptr(stats), C, float(rows), float(eps), float(momentum), ptr(g), ptr(b), ptr(running_mean),
                           ptr(running_var), ptr(mean), ptr(invstd), ptr(scale), ptr(shift), st)
         else:
-            mean = invstd = None
             L.bn_eval_prep(C, float(eps), ptr(g), ptr(b), ptr(running_mean), ptr(running_var), ptr(scale), ptr(shift), st)
         out = torch.empty_like(x)
         L.bn_apply(ptr(x), ptr(residual), ptr(out), x.numel(), C, ptr(scale), ptr(shift), act, float(slope), st)
-        ctx.save_for_backward(x, out if act else None, weight, mean, invstd, scale)
+        # activation mask in backward: from the saved output when a residual was added, else
+        # recomputed from x (z = x*scale + shift) so the output is not kept alive / re-read
+        keep_out = bool(act) and residual is not None
+        ctx.save_for_backward(x, out if keep_out else None, weight, bias, prm)
         ctx.cfg = (training, act, slope, residual is not None)
+        ctx.ws_bwd = ws_bwd
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        x, out, weight, mean, invstd, scale = ctx.saved_tensors
+        x, out, weight, bias, prm = ctx.saved_tensors
         training, act, slope, has_res = ctx.cfg
+        scale, shift, mean, invstd = prm[0], prm[1], prm[2], prm[3]
         N, C, H, W = x.shape
         dout = grad_nhwc(dout)
         if ld_of(dout) != C:
@@ -76,20 +78,31 @@ class _BNActFn(torch.autograd.Function):
         dres = torch.empty_like(x) if (has_res and ctx.needs_input_grad[6]) else None
         dgamma = dbeta = None
         if training:
-            acc = torch.zeros((STAT_SHARDS, 2, C), dtype=F32, device=dev)
+            acc = ctx.ws_bwd
             rows = N * H * W
-            L.bn_bwd_reduce(ptr(dout), ptr(out), ptr(x), rows, C, ptr(mean), ptr(invstd), act, float(slope), ptr(acc), st)
-            dgamma = torch.empty(C, dtype=F32, device=dev) if weight is not None else None
-            dbeta = torch.empty(C, dtype=F32, device=dev) if weight is not None else None
+            L.bn_bwd_reduce(ptr(dout), ptr(out), ptr(x), rows, C, ptr(mean), ptr(invstd), ptr(scale), ptr(shift), act,
+                            float(slope), ptr(acc), st)
+            sg = grad_sink(weight) if ctx.needs_input_grad[2] else None
+            sb = grad_sink(bias) if ctx.needs_input_grad[3] else None
+            direct = sg is not None and sb is not None
+            if weight is not None and not direct:
+                dgamma = torch.empty(C, dtype=F32, device=dev)
+                dbeta = torch.empty(C, dtype=F32, device=dev)
             coef = torch.empty((3, C), dtype=F32, device=dev)
             L.bn_bwd_finalize(ptr(acc), C, float(rows), ptr(weight.detach() if weight is not None else None), ptr(mean),
-                              ptr(invstd), ptr(dgamma), ptr(dbeta), ptr(coef[0]), ptr(coef[1]), ptr(coef[2]), st)
+                              ptr(invstd), ptr(sg if direct else dgamma), ptr(sb if direct else dbeta), int(direct),
+                              ptr(coef[0]), ptr(coef[1]), ptr(coef[2]), st)
             L.bn_bwd_apply(ptr(dout), ptr(out), ptr(x), ptr(dx), ptr(dres), x.numel(), C, ptr(coef[0]), ptr(coef[1]),
-                           ptr(coef[2]), act, float(slope), st)
+                           ptr(coef[2]), ptr(scale), ptr(shift), act, float(slope), st)
+            if direct:
+                notify_grad_ready(weight)
+                notify_grad_ready(bias)
         else:
+            if act and out is None:  # eval backward needs the mask: rebuild the output
+                out = torch.empty_like(x)
+                L.bn_apply(ptr(x), 0, ptr(out), x.numel(), C, ptr(scale), ptr(shift), act, float(slope), st)
             L.bn_bwd_eval(ptr(dout), ptr(out), ptr(dx), ptr(dres), x.numel(), C, ptr(scale), act, float(slope), st)
-            # frozen statistics: dgamma = sum(dz * xhat), dbeta = sum(dz) are not needed in eval mode
-        return dx, None, dgamma, dbeta, None, None, dres, None, None, None, None, None
+        return dx, None, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None
 
 
 def _torch_bn_act(x, bn, act, slope, residual):
@@ -122,8 +135,11 @@ def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None):
     rv = bn.running_var if bn.track_running_stats else None
     if residual is not None and not (is_nhwc(residual) and ld_of(residual) == residual.shape[1]):
         residual = residual.to(dtype=BF16).contiguous(memory_format=torch.channels_last)
+    C = x.shape[1]
+    ws_fwd = workspace(bn, "bn_fwd", (STAT_SHARDS, 2, C), x.device) if training else None
+    ws_bwd = workspace(bn, "bn_bwd", (STAT_SHARDS, 2, C), x.device) if training else None
     return _BNActFn.apply(x, stats, bn.weight, bn.bias, rm, rv, residual, training, mom,
-                          bn.eps, ACT_IDS[act], float(slope))
+                          bn.eps, ACT_IDS[act], float(slope), ws_fwd, ws_bwd)
 
 
 def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None):
@@ -132,8 +148,12 @@ def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None):
 
     if not native(x):
         return _torch_bn_act(conv(x), bn, act, slope, residual)
-    want = bn.training or not bn.track_running_stats
-    r = conv2d(x, conv.weight, conv.bias, conv.stride, conv.padding, conv.dilation, conv.groups, want_stats=want)
+    # BN kernels need dense channels: a channel count that is not a multiple of 8 comes back as a
+    # padded view, which is compacted below and gets its statistics from a separate pass
+    want = (bn.training or not bn.track_running_stats) and conv.out_channels % 8 == 0
+    sbuf = workspace(bn, "bn_fwd", (STAT_SHARDS, 2, conv.out_channels), x.device) if want else None
+    r = conv2d(x, conv.weight, conv.bias, conv.stride, conv.padding, conv.dilation, conv.groups, want_stats=want,
+               stats_buf=sbuf)
     y, stats = r if want else (r, None)
     if y.shape[1] % 8 != 0:  # padded view: BN kernels require dense channels
         y = y.contiguous(memory_format=torch.channels_last)

@@ -83,7 +83,7 @@ def as_nhwc(x: torch.Tensor, pad_to8: bool = True) -> torch.Tensor:
     if is_nhwc(x) and (not pad_to8 or ld_of(x) % 8 == 0):
         return x
     N, C, H, W = x.shape
-    if not x.requires_grad and x.dtype in (F32, BF16) and x.is_contiguous():
+    if not x.requires_grad and x.dtype in (F32, BF16) and x.is_contiguous() and (pad_to8 or C % 8 == 0):
         Cp = round8(C) if pad_to8 else C
         y = torch.empty((N, Cp, H, W), dtype=BF16, device=x.device, memory_format=CL)
         lib().to_nhwc(ptr(x), int(x.dtype == F32), ptr(y), N, C, H, W, Cp, stream_handle())
@@ -102,3 +102,38 @@ def grad_nhwc(g: torch.Tensor) -> torch.Tensor:
     out = empty_nhwc(N, C, H, W, g.device, zero=(C % 8 != 0))
     out.copy_(g)
     return out
+
+
+# ---------------------------------------------------------------------------------------------
+# Gradient sinks: native backward kernels write parameter gradients straight into the live
+# ``param.grad`` buffer (a view into the flat gradient buffer of parallel.flat / train.optim)
+# with accumulate semantics — exactly AccumulateGrad's in-place ``grad += g`` without the
+# extra pass — and then signal readiness to the data-parallel bucketing layer.
+# ---------------------------------------------------------------------------------------------
+def grad_sink(param):
+    """The tensor to accumulate ``param``'s gradient into, or None (fall back to autograd)."""
+    if param is None or not param.requires_grad:
+        return None
+    g = param.grad
+    if g is None or g.dtype != F32 or not g.is_contiguous() or g.shape != param.shape or g.device != param.device:
+        return None
+    if torch.is_grad_enabled():  # double-backward: keep autograd semantics
+        return None
+    return g
+
+
+def notify_grad_ready(param):
+    hook = getattr(param, "_dv_ready_hook", None)
+    if hook is not None:
+        hook(param)
+
+
+def workspace(owner, key, shape, device, dtype=F32):
+    """Persistent zero-initialised buffer owned by a module (self-cleaning accumulators)."""
+    ws = owner.__dict__.setdefault("_dv_ws", {})
+    k = (key, tuple(shape), str(device), dtype)
+    t = ws.get(k)
+    if t is None:
+        t = torch.zeros(shape, dtype=dtype, device=device)
+        ws[k] = t
+    return t

@@ -14,8 +14,8 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as TF
 
-from .common import (ACT_IDS, BF16, CL, F32, alloc_cl, as_nhwc, empty_nhwc, grad_nhwc, ld_of, lib, native, ptr, round8,
-                     stream_handle)
+from .common import (ACT_IDS, BF16, CL, F32, alloc_cl, as_nhwc, empty_nhwc, grad_nhwc, grad_sink, ld_of, lib, native,
+                     notify_grad_ready, ptr, round8, stream_handle)
 
 STAT_SHARDS = 64
 
@@ -108,7 +108,8 @@ def _dgrad(dy, weight, x_shape, Cg_x, G, stride, padding, dilation, device):
     return dX
 
 
-def _wgrad(x, dy, weight, Cg_x, G, stride, padding, dilation):
+def _wgrad(x, dy, weight, Cg_x, G, stride, padding, dilation, out=None):
+    """Weight gradient (OIHW fp32). With ``out`` the result is ADDED into ``out`` (live grad)."""
     N, _, H, W = x.shape
     O, Ig, R, S = weight.shape
     Og = O // G
@@ -116,19 +117,25 @@ def _wgrad(x, dy, weight, Cg_x, G, stride, padding, dilation):
     sh, sw = stride
     ph, pw = padding
     dh, dw = dilation
-    buf = torch.empty(G * Og * R * S * Cg_x, dtype=F32, device=x.device)
+    direct = R == 1 and S == 1 and Cg_x == Ig
+    if direct:
+        buf = out if out is not None else torch.empty((O, Ig, 1, 1), dtype=F32, device=x.device)
+        acc = int(out is not None)
+    else:
+        buf = torch.empty(G * Og * R * S * Cg_x, dtype=F32, device=x.device)
+        acc = 0
     lib().conv_wgrad(ptr(x), ptr(dy), ptr(buf), N, H, W, Cg_x, ld_of(x), G, Og, P, Q, ld_of(dy), R, S, sh, sw, ph, pw,
-                     dh, dw, 0, stream_handle())
-    if R == 1 and S == 1 and Cg_x == Ig:
-        return buf.view(O, Ig, 1, 1)
-    dW = torch.empty((O, Ig, R, S), dtype=F32, device=x.device)
-    lib().wgrad_unprep(ptr(buf), ptr(dW), G, Og, Ig, R, S, Cg_x, 1.0, 0, stream_handle())
+                     dh, dw, 0, acc, stream_handle())
+    if direct:
+        return buf
+    dW = out if out is not None else torch.empty((O, Ig, R, S), dtype=F32, device=x.device)
+    lib().wgrad_unprep(ptr(buf), ptr(dW), G, Og, Ig, R, S, Cg_x, 1.0, int(out is not None), stream_handle())
     return dW
 
 
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats):
+    def forward(ctx, x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats, stats_buf=None):
         N, Cx, H, W = x.shape
         O, Ig, R, S = weight.shape
         G = groups
@@ -138,7 +145,9 @@ class _ConvFn(torch.autograd.Function):
         P, Q = out_size(H, W, R, S, stride, padding, dilation)
         wk = _prep_weight(weight, G, Cg_x, mode=0)
         y = empty_nhwc(N, O, P, Q, x.device)
-        stats = torch.zeros((STAT_SHARDS, 2, O), dtype=F32, device=x.device) if want_stats else None
+        stats = None
+        if want_stats:
+            stats = stats_buf if stats_buf is not None else torch.zeros((STAT_SHARDS, 2, O), dtype=F32, device=x.device)
         b = bias.detach().float().contiguous() if bias is not None else None
         conv_fwd_raw(x, wk, y, b, stats, N, H, W, Cg_x, ldx, G, Og, P, Q, R, S, stride, padding, dilation,
                      act=act, slope=slope)
@@ -165,14 +174,18 @@ class _ConvFn(torch.autograd.Function):
             if dx.shape[1] != x.shape[1]:
                 dx = dx[:, : x.shape[1]]
         if ctx.needs_input_grad[1]:
-            dw = _wgrad(x, dy, weight, Cg_x, G, stride, padding, dilation)
+            sink = grad_sink(weight)
+            dw = _wgrad(x, dy, weight, Cg_x, G, stride, padding, dilation, out=sink)
+            if sink is not None:
+                dw = None
+                notify_grad_ready(weight)
         if has_bias and ctx.needs_input_grad[2]:
             db = _channel_sum(dy)
-        return dx, dw, db, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None, None
 
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=None, slope=0.0,
-           want_stats=False):
+           want_stats=False, stats_buf=None):
     """Conv2d (+fused bias/activation). Returns y, or (y, stats) when want_stats (GPU only)."""
     stride, padding, dilation = _pair(stride), _pair(padding), _pair(dilation)
     if not native(x):
@@ -185,7 +198,8 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=
     if isinstance(padding, str):
         raise NotImplementedError("string padding: use ops.conv.same_padding")
     x = as_nhwc(x, pad_to8=(groups == 1))
-    return _ConvFn.apply(x, weight, bias, stride, padding, dilation, groups, ACT_IDS[act], float(slope), want_stats)
+    return _ConvFn.apply(x, weight, bias, stride, padding, dilation, groups, ACT_IDS[act], float(slope), want_stats,
+                         stats_buf)
 
 
 # ---------------------------------------------------------------------------------------
@@ -276,13 +290,13 @@ class _LinearFn(torch.autograd.Function):
         conv_fwd_raw(x, wk, y_full, b, None, N, 1, 1, Kp, Kp, 1, O, 1, 1, 1, 1, (1, 1), (0, 0), (1, 1), act=act,
                      slope=slope, ldy=Op)
         y = y_full if Op == O else y_full[:, :O]
-        ctx.save_for_backward(x, weight, y if act else None)
+        ctx.save_for_backward(x, weight, bias, y if act else None)
         ctx.cfg = (act, slope, bias is not None, Kp, Op)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, weight, y = ctx.saved_tensors
+        x, weight, bias, y = ctx.saved_tensors
         act, slope, has_bias, Kp, Op = ctx.cfg
         N, K = x.shape
         O, _ = weight.shape
@@ -302,12 +316,22 @@ class _LinearFn(torch.autograd.Function):
                          ldy=Kp)
             dx = dx_full if Kp == K else dx_full[:, :K]
         if ctx.needs_input_grad[1]:
-            buf = torch.empty(O * Kp, dtype=F32, device=dy.device)
+            sink = grad_sink(weight) if Kp == K else None
+            buf = sink if sink is not None else torch.empty(O * Kp, dtype=F32, device=dy.device)
             lib().conv_wgrad(ptr(x), ptr(dy), ptr(buf), N, 1, 1, Kp, Kp, 1, O, 1, 1, Op, 1, 1, 1, 1, 0, 0, 1, 1, 0,
-                             stream_handle())
-            dw = buf.view(O, Kp)[:, :K].contiguous() if Kp != K else buf.view(O, K)
+                             int(sink is not None), stream_handle())
+            if sink is not None:
+                dw = None
+                notify_grad_ready(weight)
+            else:
+                dw = buf.view(O, Kp)[:, :K].contiguous() if Kp != K else buf.view(O, K)
         if has_bias and ctx.needs_input_grad[2]:
             db = dy.float().sum(0)
+            sink = grad_sink(bias)
+            if sink is not None:
+                sink.add_(db)
+                db = None
+                notify_grad_ready(bias)
         return dx, dw, db, None, None
 
 

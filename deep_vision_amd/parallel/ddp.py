@@ -69,7 +69,13 @@ class DataParallel(torch.nn.Module):
         for bi, b in enumerate(self.buckets):
             for p in b.params:
                 self._bucket_of[id(p)] = bi
-        self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(p)) for p, _, _ in layout]
+        self._hooks = []
+        for p, _, _ in layout:
+            h = self._make_hook(p)
+            self._hooks.append(p.register_post_accumulate_grad_hook(h))
+            # native backward kernels write gradients straight into the flat buffer and signal
+            # readiness through this attribute instead of autograd's AccumulateGrad
+            p._dv_ready_hook = h
         self.comm_stats = {"allreduce_calls": 0, "allreduce_bytes": 0}
         self._reset()
 
