@@ -122,5 +122,31 @@ PYBIND11_MODULE(_C, m) {
                       float momentum, int centered, float gscale, uptr st) {
     dv_rmsprop(FP(p), CFP(g), FP(sq), FP(mom), FP(gavg), n, lr, alpha, eps, wd, momentum, centered, gscale, ST(st)); check_last("rmsprop");
   });
+  m.def("dw_fwd", [](uptr x, uptr w, uptr bias, uptr y, int N, int H, int W, int C, int ldx, int P_, int Q, int ldy, int K,
+                     int sh, int sw, int ph, int pw, int act, float slope, uptr stats, uptr st) {
+    if (dv_dw_fwd(CP(x), CFP(w), CFP(bias), P(y), N, H, W, C, ldx, P_, Q, ldy, K, sh, sw, ph, pw, act, slope, FP(stats), ST(st)))
+      throw std::runtime_error("dw_fwd: unsupported shape");
+    check_last("dw_fwd");
+  });
+  m.def("dw_dgrad", [](uptr dy, uptr w, uptr dx, int N, int H, int W, int C, int ldx, int P_, int Q, int ldy, int K, int sh,
+                       int sw, int ph, int pw, uptr st) {
+    if (dv_dw_dgrad(CP(dy), CFP(w), P(dx), N, H, W, C, ldx, P_, Q, ldy, K, sh, sw, ph, pw, ST(st)))
+      throw std::runtime_error("dw_dgrad: unsupported shape");
+    check_last("dw_dgrad");
+  });
+  m.def("dw_wgrad", [](uptr x, uptr dy, uptr dw, int N, int H, int W, int C, int ldx, int P_, int Q, int ldy, int K, int sh,
+                       int sw, int ph, int pw, int accumulate, uptr st) {
+    if (dv_dw_wgrad(CP(x), CP(dy), FP(dw), N, H, W, C, ldx, P_, Q, ldy, K, sh, sw, ph, pw, accumulate, ST(st)))
+      throw std::runtime_error("dw_wgrad: unsupported shape");
+    check_last("dw_wgrad");
+  });
+  m.def("lrn_fwd", [](uptr x, uptr y, int64_t npix, int C, int lo, int hi, float alpha, float beta, float k, uptr st) {
+    if (dv_lrn_fwd(CP(x), P(y), npix, C, lo, hi, alpha, beta, k, ST(st))) throw std::runtime_error("lrn_fwd: C > 1024");
+    check_last("lrn_fwd");
+  });
+  m.def("lrn_bwd", [](uptr x, uptr dy, uptr dx, int64_t npix, int C, int lo, int hi, float alpha, float beta, float k, uptr st) {
+    if (dv_lrn_bwd(CP(x), CP(dy), P(dx), npix, C, lo, hi, alpha, beta, k, ST(st))) throw std::runtime_error("lrn_bwd: C > 1024");
+    check_last("lrn_bwd");
+  });
   m.def("sumsq", [](uptr x, int64_t n, uptr out, uptr st) { dv_sumsq(CFP(x), n, FP(out), ST(st)); check_last("sumsq"); });
 }

@@ -91,3 +91,17 @@ void dv_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, 
 void dv_rmsprop(float* p, const float* g, float* sq, float* mom, float* gavg, int64_t n, float lr, float alpha, float eps,
                 float wd, float momentum, int centered, float gscale, hipStream_t st);
 void dv_sumsq(const float* x, int64_t n, float* out, hipStream_t st);
+
+// ---- depthwise conv (depthwise.hip) ----
+int dv_dw_fwd(const void* x, const float* w, const float* bias, void* y, int N, int H, int W, int C, int ldx, int P,
+              int Q, int ldy, int K, int sh, int sw, int ph, int pw, int act, float slope, float* stats, hipStream_t st);
+int dv_dw_dgrad(const void* dy, const float* w, void* dx, int N, int H, int W, int C, int ldx, int P, int Q, int ldy,
+                int K, int sh, int sw, int ph, int pw, hipStream_t st);
+int dv_dw_wgrad(const void* x, const void* dy, float* dw, int N, int H, int W, int C, int ldx, int P, int Q, int ldy,
+                int K, int sh, int sw, int ph, int pw, int accumulate, hipStream_t st);
+
+// ---- local response normalisation (lrn.hip) ----
+int dv_lrn_fwd(const void* x, void* y, int64_t npix, int C, int lo, int hi, float alpha, float beta, float k,
+               hipStream_t st);
+int dv_lrn_bwd(const void* x, const void* dy, void* dx, int64_t npix, int C, int lo, int hi, float alpha, float beta,
+               float k, hipStream_t st);

@@ -196,10 +196,36 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=
             y = TF.leaky_relu(y, slope)
         return (y, None) if want_stats else y
     if isinstance(padding, str):
-        raise NotImplementedError("string padding: use ops.conv.same_padding")
+        raise NotImplementedError("string padding: use nn.Conv2d(padding='same_keras')")
+    if _is_depthwise(x, weight, groups, stride, dilation):
+        return depthwise_conv2d(x, weight, bias, stride, padding, act, slope, want_stats, stats_buf)
+    if groups > 1 and ((x.shape[1] // groups) % 8 != 0 or (weight.shape[0] // groups) % 8 != 0):
+        return _grouped_padded_conv(x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats)
     x = as_nhwc(x, pad_to8=(groups == 1))
     return _ConvFn.apply(x, weight, bias, stride, padding, dilation, groups, ACT_IDS[act], float(slope), want_stats,
                          stats_buf)
+
+
+def _grouped_padded_conv(x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats):
+    """Grouped conv whose channels per group are not multiples of 8 (ShuffleNet V1 g=3: 20/40/80
+    channels per group). Input channels and output channels of every group are zero-padded to a
+    multiple of 8 (differentiable copies), the MFMA kernel runs with the padded group strides,
+    and the padding channels are dropped from the output. Statistics are left to the BN pass."""
+    N, C, H, W = x.shape
+    G = groups
+    Cg, O = C // G, weight.shape[0]
+    Og = O // G
+    Cgp, Ogp = round8(Cg), round8(Og)
+    xg = x.to(BF16).reshape(N, G, Cg, H, W)
+    xg = TF.pad(xg, (0, 0, 0, 0, 0, Cgp - Cg)).reshape(N, G * Cgp, H, W).contiguous(memory_format=CL)
+    R, S = weight.shape[2], weight.shape[3]
+    wp = TF.pad(weight.view(G, Og, Cg, R, S), (0, 0, 0, 0, 0, Cgp - Cg, 0, Ogp - Og)).reshape(G * Ogp, Cgp, R, S)
+    bp = TF.pad(bias.view(G, Og), (0, Ogp - Og)).reshape(-1) if bias is not None else None
+    y = _ConvFn.apply(xg, wp, bp, stride, padding, dilation, groups, ACT_IDS[act], float(slope), False, None)
+    if Ogp != Og:
+        P, Q = y.shape[2], y.shape[3]
+        y = y.reshape(N, G, Ogp, P, Q)[:, :, :Og].reshape(N, O, P, Q).contiguous(memory_format=CL)
+    return (y, None) if want_stats else y
 
 
 # ---------------------------------------------------------------------------------------
@@ -356,3 +382,72 @@ def linear(x, weight, bias=None, act=None, slope=0.0):
         x2 = xp if Kp == K else xp[:, :K]
     y = _LinearFn.apply(x2, weight, bias, ACT_IDS[act], float(slope))
     return y.reshape(*lead, weight.shape[0])
+
+
+# ---------------------------------------------------------------------------------------
+# Depthwise conv (groups == in == out channels): csrc/depthwise.hip
+# ---------------------------------------------------------------------------------------
+class _DWConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, padding, act, slope, want_stats, stats_buf):
+        N, C, H, W = x.shape
+        K = weight.shape[2]
+        P, Q = out_size(H, W, K, K, stride, padding, (1, 1))
+        y = empty_nhwc(N, C, P, Q, x.device)
+        w = weight.detach().float().contiguous()
+        b = bias.detach().float().contiguous() if bias is not None else None
+        stats = None
+        if want_stats:
+            stats = stats_buf if stats_buf is not None else torch.zeros((STAT_SHARDS, 2, C), dtype=F32, device=x.device)
+        lib().dw_fwd(ptr(x), ptr(w), ptr(b), ptr(y), N, H, W, C, ld_of(x), P, Q, ld_of(y), K, stride[0], stride[1],
+                     padding[0], padding[1], act, float(slope), ptr(stats), stream_handle())
+        ctx.save_for_backward(x, weight, y if act else None)
+        ctx.cfg = (stride, padding, act, slope, bias is not None)
+        if want_stats:
+            ctx.mark_non_differentiable(stats)
+            return y, stats
+        return y
+
+    @staticmethod
+    def backward(ctx, dy, *unused):
+        x, weight, y = ctx.saved_tensors
+        stride, padding, act, slope, has_bias = ctx.cfg
+        dy = grad_nhwc(dy)
+        if act:
+            g = torch.empty_like(dy)
+            lib().act_bwd(ptr(dy), ptr(y), ptr(g), dy.numel(), act, float(slope), stream_handle())
+            dy = g
+        N, C, H, W = x.shape
+        K = weight.shape[2]
+        P, Q = dy.shape[2], dy.shape[3]
+        w = weight.detach().float().contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = empty_nhwc(N, C, H, W, x.device)
+            lib().dw_dgrad(ptr(dy), ptr(w), ptr(dx), N, H, W, C, ld_of(dx), P, Q, ld_of(dy), K, stride[0], stride[1],
+                           padding[0], padding[1], stream_handle())
+        if ctx.needs_input_grad[1]:
+            sink = grad_sink(weight)
+            buf = sink if sink is not None else torch.empty_like(w)
+            lib().dw_wgrad(ptr(x), ptr(dy), ptr(buf), N, H, W, C, ld_of(x), P, Q, ld_of(dy), K, stride[0], stride[1],
+                           padding[0], padding[1], int(sink is not None), stream_handle())
+            if sink is not None:
+                notify_grad_ready(weight)
+            else:
+                dw = buf
+        if has_bias and ctx.needs_input_grad[2]:
+            db = _channel_sum(dy)
+        return dx, dw, db, None, None, None, None, None, None
+
+
+def _is_depthwise(x, weight, groups, stride, dilation):
+    O, Ig, R, S = weight.shape
+    return (groups > 1 and groups == x.shape[1] and O == groups and Ig == 1 and R == S and R in (1, 3, 5, 7)
+            and dilation == (1, 1) and x.shape[1] % 8 == 0)
+
+
+def depthwise_conv2d(x, weight, bias=None, stride=1, padding=0, act=None, slope=0.0, want_stats=False,
+                     stats_buf=None):
+    stride, padding = _pair(stride), _pair(padding)
+    x = as_nhwc(x, pad_to8=False)
+    return _DWConvFn.apply(x, weight, bias, stride, padding, ACT_IDS[act], float(slope), want_stats, stats_buf)

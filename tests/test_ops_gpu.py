@@ -285,3 +285,77 @@ def test_optimizers_match_torch():
             o2.step()
         for a, b in zip(o1.param_views(), p2):
             assert torch.allclose(a, b, atol=1e-5, rtol=1e-4), cls.__name__
+
+
+@pytest.mark.parametrize("cfg", [(32, 3, 1, 1), (64, 3, 2, 1), (128, 3, 1, 1), (1024, 3, 1, 1), (48, 5, 2, 2)])
+def test_depthwise(cfg):
+    from deep_vision_amd import ops as F
+
+    C, k, s, p = cfg
+    x32 = torch.randn(2, C, 15, 13, device=DEV).bfloat16().float()
+    w = (torch.randn(C, 1, k, k, device=DEV) * 0.3).requires_grad_(True)
+    x = _nhwc(x32).requires_grad_(True)
+    y = F.conv2d(x, w, None, s, p, 1, C)
+    xr = x32.clone().requires_grad_(True)
+    wr = w.detach().clone().requires_grad_(True)
+    yr = TF.conv2d(xr, wr, None, s, p, 1, C)
+    assert y.shape == yr.shape
+    assert _rel(y, yr) < 2e-2
+    dy = torch.randn_like(yr).bfloat16().float()
+    y.backward(_nhwc(dy))
+    yr.backward(dy)
+    assert _rel(x.grad, xr.grad) < 2e-2
+    assert _rel(w.grad, wr.grad) < 2e-2
+
+
+def test_depthwise_bn_stats_fusion():
+    from deep_vision_amd import nn, ops as F
+
+    conv = nn.Conv2d(64, 64, 3, padding=1, groups=64, bias=False).to(DEV)
+    bn = nn.BatchNorm2d(64).to(DEV)
+    x32 = torch.randn(4, 64, 14, 14, device=DEV).bfloat16().float()
+    y = F.conv_bn_act(_nhwc(x32), conv, bn, "relu")
+    bn_r = torch.nn.BatchNorm2d(64).to(DEV)
+    yr = TF.relu(bn_r(TF.conv2d(x32, conv.weight.detach(), None, 1, 1, 1, 64)))
+    assert _rel(y, yr) < 3e-2
+
+
+@pytest.mark.parametrize("mode", ["torch", "tf"])
+def test_lrn(mode):
+    from deep_vision_amd.ops import lrn
+
+    for C, size in [(96, 96), (64, 5), (192, 192)]:
+        x32 = torch.randn(2, C, 6, 5, device=DEV).bfloat16().float()
+        x = _nhwc(x32).requires_grad_(True)
+        xr = x32.clone().requires_grad_(True)
+        if mode == "torch":
+            y = lrn.local_response_norm(x, size, 1e-4, 0.75, 1.0)
+            yr = TF.local_response_norm(xr, size, 1e-4, 0.75, 1.0)
+        else:
+            y = lrn.tf_local_response_norm(x, 5, 1.0, 1.0, 0.5)
+            yr = lrn.tf_local_response_norm(xr, 5, 1.0, 1.0, 0.5)
+        assert _rel(y, yr) < 2e-2
+        dy = torch.randn_like(yr).bfloat16().float()
+        y.backward(_nhwc(dy))
+        yr.backward(dy)
+        assert _rel(x.grad, xr.grad) < 3e-2
+
+
+def test_grouped_padded_conv():
+    from deep_vision_amd import ops as F
+
+    for (C, O, G) in [(240, 60, 3), (60, 240, 3), (24, 48, 2)]:
+        x32 = torch.randn(2, C, 9, 9, device=DEV).bfloat16().float()
+        w = (torch.randn(O, C // G, 1, 1, device=DEV) * 0.1).requires_grad_(True)
+        x = _nhwc(x32).requires_grad_(True)
+        y = F.conv2d(x, w, None, 1, 0, 1, G)
+        xr = x32.clone().requires_grad_(True)
+        wr = w.detach().bfloat16().float().requires_grad_(True)
+        yr = TF.conv2d(xr, wr, None, 1, 0, 1, G)
+        assert y.shape == yr.shape
+        assert _rel(y, yr) < 2e-2
+        dy = torch.randn_like(yr).bfloat16().float()
+        y.backward(_nhwc(dy))
+        yr.backward(dy)
+        assert _rel(x.grad, xr.grad) < 3e-2
+        assert _rel(w.grad, wr.grad) < 3e-2
