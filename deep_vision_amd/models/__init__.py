@@ -1,11 +1,34 @@
 """Model zoo (reference parity: SURVEY §2.2) and a name -> constructor registry."""
+from .classic import VGG16, VGG19, AlexNetV1, AlexNetV2, AlexNetV2TF, LeNet5, LeNet5TF  # noqa: F401
+from .inception import InceptionV1, InceptionV3  # noqa: F401
+from .mobilenet import MobileNetV1, MobileNetV1TF, ShuffleNetV1  # noqa: F401
 from .resnet import ResNet34, ResNet50, ResNet152  # noqa: F401
 
 MODELS = {
+    "lenet5": LeNet5,
+    "lenet5_tf": LeNet5TF,
+    "alexnet1": AlexNetV1,
+    "alexnet2": AlexNetV2,
+    "alexnet2_tf": AlexNetV2TF,
+    "vgg16": VGG16,
+    "vgg19": VGG19,
+    "inception1": InceptionV1,
+    "inception3": InceptionV3,
     "resnet34": ResNet34,
     "resnet50": ResNet50,
     "resnet152": ResNet152,
+    "mobilenet1": MobileNetV1,
+    "mobilenet1_tf": MobileNetV1TF,
+    "shufflenet1": ShuffleNetV1,
 }
+
+
+def register(name):
+    def deco(cls):
+        MODELS[name] = cls
+        return cls
+
+    return deco
 
 
 def get_model(name: str, **kw):

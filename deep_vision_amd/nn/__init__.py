@@ -17,7 +17,7 @@ from ..ops.common import native
 __all__ = [
     "Conv2d", "ConvTranspose2d", "Linear", "BatchNorm2d", "ReLU", "LeakyReLU", "Tanh", "Sigmoid", "MaxPool2d",
     "AvgPool2d", "AdaptiveAvgPool2d", "Dropout", "Upsample", "LocalResponseNorm", "Flatten", "Sequential",
-    "ZeroPad2d", "ReflectionPad2d", "ChannelShuffle", "Identity",
+    "ZeroPad2d", "ReflectionPad2d", "ChannelShuffle", "Identity", "FusedSequential",
 ]
 
 Sequential = tnn.Sequential
@@ -177,3 +177,53 @@ class ChannelShuffle(tnn.Module):
         if native(x):
             y = y.contiguous(memory_format=torch.channels_last)
         return y
+
+
+_ACTS = {tnn.ReLU: ("relu", None), tnn.LeakyReLU: ("leaky", "negative_slope")}
+
+
+def _act_of(m):
+    for cls, (name, attr) in _ACTS.items():
+        if isinstance(m, cls):
+            return name, (getattr(m, attr) if attr else 0.0)
+    return None, 0.0
+
+
+class FusedSequential(tnn.Sequential):
+    """torch.nn.Sequential that, on native GPU tensors, fuses producer -> activation chains:
+
+    Conv2d [-> BatchNorm2d] [-> ReLU/LeakyReLU]  -> one conv (+BN statistics epilogue, +apply)
+    Linear -> ReLU/LeakyReLU                     -> one GEMM with a fused activation epilogue
+
+    Module indices (and therefore state_dict keys) are exactly those of nn.Sequential.
+    """
+
+    def forward(self, x):
+        if not native(x):
+            return super().forward(x)
+        mods = list(self._modules.values())
+        i = 0
+        while i < len(mods):
+            m = mods[i]
+            nxt = mods[i + 1] if i + 1 < len(mods) else None
+            if isinstance(m, tnn.Conv2d) and not isinstance(m, tnn.ConvTranspose2d) and m.padding_mode == "zeros" \
+                    and not getattr(m, "keras_same", False):
+                if isinstance(nxt, tnn.BatchNorm2d):
+                    act, slope = _act_of(mods[i + 2]) if i + 2 < len(mods) else (None, 0.0)
+                    x = F.conv_bn_act(x, m, nxt, act, slope)
+                    i += 3 if act else 2
+                    continue
+                act, slope = _act_of(nxt)
+                if act:
+                    x = F.conv2d(x, m.weight, m.bias, m.stride, m.padding, m.dilation, m.groups, act=act, slope=slope)
+                    i += 2
+                    continue
+            if isinstance(m, tnn.Linear):
+                act, slope = _act_of(nxt)
+                if act:
+                    x = F.linear(x, m.weight, m.bias, act=act, slope=slope)
+                    i += 2
+                    continue
+            x = m(x)
+            i += 1
+        return x

@@ -1,0 +1,112 @@
+"""Model-zoo parity on CPU (SURVEY §2.2 golden parameter counts, reference state_dict keys).
+
+When the read-only reference tree is mounted, the reference PyTorch modules are imported and
+compared key-for-key and output-for-output (same weights, eval mode). The parameter counts
+are pinned independently so the test is meaningful without the reference too.
+"""
+import importlib.util
+import os
+
+import pytest
+import torch
+
+from deep_vision_amd import models as M
+
+REF = "/root/reference"
+
+PINNED = {
+    "lenet5": 61_706,
+    "lenet5_tf": 61_706,
+    "alexnet1": 62_378_344,
+    "alexnet2": 61_838_248,
+    "vgg16": 138_357_544,
+    "vgg19": 143_667_240,
+    "inception1": 13_378_280,
+    "resnet34": 11_693_736,
+    "resnet50": 25_557_032,
+    "resnet152": 60_192_808,
+    "mobilenet1": 4_231_976,
+    "mobilenet1_tf": 4_242_856,  # reference comment R/MobileNet/tensorflow/train.py:35
+}
+
+
+def nparams(m):
+    return sum(p.numel() for p in m.parameters())
+
+
+@pytest.mark.parametrize("name", sorted(PINNED))
+def test_param_counts(name):
+    assert nparams(M.get_model(name)) == PINNED[name]
+
+
+REF_MODULES = [
+    ("lenet5", "LeNet/pytorch/models/lenet5.py", "LeNet5", (2, 1, 32, 32)),
+    ("alexnet1", "AlexNet/pytorch/models/alexnet_v1.py", "AlexNetV1", (1, 3, 224, 224)),
+    ("alexnet2", "AlexNet/pytorch/models/alexnet_v2.py", "AlexNetV2", (1, 3, 224, 224)),
+    ("vgg16", "VGG/pytorch/models/vgg16.py", "VGG16", (1, 3, 224, 224)),
+    ("inception1", "Inception/pytorch/models/inception_v1.py", "InceptionV1", (1, 3, 224, 224)),
+    ("resnet34", "ResNet/pytorch/models/resnet34.py", "ResNet34", (1, 3, 224, 224)),
+    ("resnet50", "ResNet/pytorch/models/resnet50.py", "ResNet50", (1, 3, 224, 224)),
+    ("mobilenet1", "MobileNet/pytorch/models/mobilenet_v1.py", "MobileNetV1", (1, 3, 224, 224)),
+]
+
+
+def _load_ref(rel, name):
+    path = os.path.join(REF, rel)
+    if not os.path.exists(path):
+        pytest.skip("reference tree not mounted")
+    spec = importlib.util.spec_from_file_location("ref_" + name, path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+@pytest.mark.parametrize("key,rel,cls,shape", REF_MODULES)
+def test_reference_state_dict_and_outputs(key, rel, cls, shape):
+    torch.manual_seed(0)
+    ref = getattr(_load_ref(rel, cls), cls)()
+    mine = M.get_model(key)
+    a, b = mine.state_dict(), ref.state_dict()
+    assert list(a.keys()) == list(b.keys())
+    assert all(a[k].shape == b[k].shape for k in a)
+    mine.load_state_dict(b)
+    mine.eval()
+    ref.eval()
+    x = torch.randn(*shape)
+    with torch.no_grad():
+        assert torch.allclose(mine(x), ref(x), atol=1e-5, rtol=1e-5)
+
+
+def test_inception_train_mode_returns_aux():
+    m = M.get_model("inception1").train()
+    out = m(torch.randn(2, 3, 224, 224))
+    assert isinstance(out, tuple) and len(out) == 3
+    assert all(o.shape == (2, 1000) for o in out)
+
+
+@pytest.mark.parametrize("name,shape,out", [("shufflenet1", (2, 3, 224, 224), (2, 1000)),
+                                            ("alexnet2_tf", (1, 3, 224, 224), (1, 1000)),
+                                            ("mobilenet1_tf", (1, 3, 224, 224), (1, 1000))])
+def test_extra_models_forward(name, shape, out):
+    m = M.get_model(name).eval()
+    with torch.no_grad():
+        assert m(torch.randn(*shape)).shape == out
+
+
+def test_resnet_train_step_cpu():
+    from deep_vision_amd import ops as F
+    from deep_vision_amd.train.optim import FusedSGD
+
+    torch.manual_seed(0)
+    m = M.get_model("resnet34")
+    opt = FusedSGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    x = torch.randn(4, 3, 64, 64)
+    y = torch.randint(0, 1000, (4,))
+    losses = []
+    for _ in range(4):
+        opt.zero_grad()
+        loss = F.cross_entropy(m(x), y)
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert losses[-1] < losses[0]
