@@ -3,7 +3,9 @@
 // extension only depends on the HIP runtime that torch itself loaded.
 #include <pybind11/pybind11.h>
 #include <hip/hip_runtime.h>
+#include <pybind11/stl.h>
 #include <string>
+#include <vector>
 #include "kernels.h"
 
 namespace py = pybind11;
@@ -149,4 +151,34 @@ PYBIND11_MODULE(_C, m) {
     check_last("lrn_bwd");
   });
   m.def("sumsq", [](uptr x, int64_t n, uptr out, uptr st) { dv_sumsq(CFP(x), n, FP(out), ST(st)); check_last("sumsq"); });
+
+  m.def("yolo_gather_boxes", [](uptr yt, int N, int cells, int D, uptr boxes, uptr counts, uptr st) {
+    dv_yolo_gather_boxes(CFP(yt), N, cells, D, FP(boxes), reinterpret_cast<int*>(counts), ST(st));
+    check_last("yolo_gather_boxes");
+  });
+  m.def("yolo_loss", [](uptr pred, int ldp, uptr yt, uptr boxes, uptr counts, uptr grad, uptr gw, uptr losses, int N, int g,
+                        int C, std::vector<float> anchors, float grad_scale, float lambda_coord, float lambda_noobj,
+                        float ignore_thresh, uptr st) {
+    if (anchors.size() != 6) throw std::runtime_error("yolo_loss: 3 anchors (w, h) expected");
+    dv_yolo_loss(CP(pred), ldp, CFP(yt), CFP(boxes), reinterpret_cast<const int*>(counts), P(grad), CFP(gw), FP(losses), N, g, C,
+                 anchors.data(), grad_scale, lambda_coord, lambda_noobj, ignore_thresh, ST(st));
+    check_last("yolo_loss");
+  });
+  m.def("yolo_decode", [](uptr pred, int ldp, int N, int g, int C, std::vector<float> anchors, uptr out, int rows_total,
+                          int row_off, uptr st) {
+    if (anchors.size() != 6) throw std::runtime_error("yolo_decode: 3 anchors (w, h) expected");
+    dv_yolo_decode(CP(pred), ldp, N, g, C, anchors.data(), FP(out), rows_total, row_off, ST(st));
+    check_last("yolo_decode");
+  });
+  m.def("nms", [](uptr cand, int N, int M, int D, float iou_thresh, float score_thresh, int max_det, uptr out, uptr st) {
+    if (dv_nms(CFP(cand), N, M, D, iou_thresh, score_thresh, max_det, FP(out), ST(st)))
+      throw std::runtime_error("nms: more than 32768 candidate rows per image");
+    check_last("nms");
+  });
+  m.def("pw_loss", [](int kind, uptr pred, int pred_bf16, uptr tgt, int tgt_type, float tval, int64_t rows, int C,
+                      int ldp, int ldt, float a, float b, uptr sums, uptr grad, uptr gscale, float hscale, uptr st) {
+    dv_pw_loss(kind, CP(pred), pred_bf16, CP(tgt), tgt_type, tval, rows, C, ldp, ldt, a, b, FP(sums), P(grad),
+               CFP(gscale), hscale, ST(st));
+    check_last("pw_loss");
+  });
 }

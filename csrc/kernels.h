@@ -105,3 +105,18 @@ int dv_lrn_fwd(const void* x, void* y, int64_t npix, int C, int lo, int hi, floa
                hipStream_t st);
 int dv_lrn_bwd(const void* x, const void* dy, void* dx, int64_t npix, int C, int lo, int hi, float alpha, float beta,
                float k, hipStream_t st);
+
+// ---- YOLOv3 head: loss + grad, decode, NMS (yolo.hip) ----
+void dv_yolo_gather_boxes(const float* y_true, int N, int cells, int D, float* boxes, int* counts, hipStream_t st);
+void dv_yolo_loss(const void* pred, int ldp, const float* y_true, const float* boxes, const int* counts, void* grad,
+                  const float* gw, float* losses, int N, int g, int C, const float* anchors6, float grad_scale, float lambda_coord,
+                  float lambda_noobj, float ignore_thresh, hipStream_t st);
+void dv_yolo_decode(const void* pred, int ldp, int N, int g, int C, const float* anchors6, float* out, int rows_total,
+                    int row_off, hipStream_t st);
+int dv_nms(const float* cand, int N, int M, int D, float iou_thresh, float score_thresh, int max_det, float* out,
+           hipStream_t st);
+
+// ---- pointwise losses with gradient (losses.hip) ----
+void dv_pw_loss(int kind, const void* pred, int pred_bf16, const void* tgt, int tgt_type, float tval, int64_t rows,
+                int C, int ldp, int ldt, float a, float b, float* sums, void* grad, const float* gscale, float hscale,
+                hipStream_t st);

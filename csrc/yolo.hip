@@ -1,0 +1,303 @@
+// YOLOv3 head kernels: fused per-scale loss + gradient, box decode, greedy NMS.
+//
+// Semantics follow R/YOLO/tensorflow/yolov3.py:234-371 (YoloLoss) and utils.py (clipped BCE,
+// broadcast IoU with the +1e-7 union guard), R/YOLO/tensorflow/postprocess.py (multi-label greedy
+// NMS: score = objectness, at most `max_det` detections, the count stored in row max_det).
+//
+// Layouts
+//   pred   : bf16 head conv output, NHWC rows of 3*(5+C) channels with row stride ldp
+//            (= the (N, g, g, 3, 5+C) view of the reference), padding channels get zero grads
+//   y_true : fp32 (N, g, g, 3, 5+C): (cx, cy, w, h, obj, one-hot classes) as encoded by
+//            deep_vision_amd.data.yolo.encode_labels
+//
+// Loss kernel: one wave per grid cell (3 anchors x (5+C) channels), block = 4 cells of one image
+// (blockIdx.y = image), grid-stride over the cells. Per anchor, the ignore-mask IoU against the
+// image's ground-truth boxes (staged in LDS) is split across the 64 lanes and max-reduced; the
+// class BCE channels are spread over the lanes. Loss and d(loss)/d(pred) come out of the same pass
+// (the reference differentiates the same graph with GradientTape); per-image loss components
+// [xy, wh, class, obj] are block-reduced then atomically added. The autograd forward runs it
+// without a gradient; the backward re-runs it with the upstream (N, 4) weights, so any
+// combination of the per-image components differentiates exactly. (losses may be null then.)
+//
+// Ignore mask: the reference sorts y_true boxes per coordinate (tf.sort on axis 1 scrambles
+// x1/y1/x2/y2 of different boxes, yolov3.py:292) before the top-100 IoU; here the IoU is taken
+// against the first 100 real ground-truth boxes of the scale in cell order (the intended set).
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+constexpr int NT = 256;
+constexpr int MAXB = 100;
+constexpr float BCE_EPS = 1e-7f;
+
+DV_DEVICE float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+
+// clipped BCE of probability p (reference utils.binary_cross_entropy) and d/dlogit (0 when clipped)
+DV_DEVICE float bce(float p, float t, float& dz) {
+  const float pc = fminf(fmaxf(p, BCE_EPS), 1.f - BCE_EPS);
+  dz = (p > BCE_EPS && p < 1.f - BCE_EPS) ? (p - t) : 0.f;
+  return -(t * __logf(pc) + (1.f - t) * __logf(1.f - pc));
+}
+
+DV_DEVICE float iou(float ax1, float ay1, float ax2, float ay2, const float* b) {
+  const float iw = fminf(fmaxf(fminf(ax2, b[2]) - fmaxf(ax1, b[0]), 0.f), 1.f);
+  const float ih = fminf(fmaxf(fminf(ay2, b[3]) - fmaxf(ay1, b[1]), 0.f), 1.f);
+  const float i = iw * ih;
+  const float u = (ax2 - ax1) * (ay2 - ay1) + (b[2] - b[0]) * (b[3] - b[1]) - i;
+  return i / (u + 1e-7f);
+}
+
+__global__ __launch_bounds__(NT) void yolo_gather_kernel(const float* __restrict__ yt, int cells, int D,
+                                                         float* __restrict__ boxes, int* __restrict__ counts) {
+  __shared__ int wcnt[NT / 64];
+  __shared__ int total;
+  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float* base = yt + (int64_t)n * cells * D;
+  if (tid == 0) total = 0;
+  __syncthreads();
+  for (int c0 = 0; c0 < cells; c0 += NT) {
+    const int c = c0 + tid;
+    const bool obj = c < cells && base[(int64_t)c * D + 4] > 0.f;
+    const uint64_t m = __ballot(obj);
+    if (lane == 0) wcnt[w] = __popcll(m);
+    __syncthreads();
+    int off = total;
+    for (int i = 0; i < w; ++i) off += wcnt[i];
+    off += __popcll(m & ((1ull << lane) - 1ull));
+    if (obj && off < MAXB) {
+      const float* r = base + (int64_t)c * D;
+      float* o = boxes + ((int64_t)n * MAXB + off) * 4;
+      o[0] = r[0] - r[2] * 0.5f;
+      o[1] = r[1] - r[3] * 0.5f;
+      o[2] = r[0] + r[2] * 0.5f;
+      o[3] = r[1] + r[3] * 0.5f;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int s = 0;
+      for (int i = 0; i < NT / 64; ++i) s += wcnt[i];
+      total += s;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) counts[n] = min(total, MAXB);
+}
+
+struct YoloArgs {
+  const u16* pred; int ldp;
+  const float* yt;
+  const float* boxes; const int* counts;
+  u16* grad;        // may be null (forward / validation)
+  const float* gw;  // [N][4] upstream weights of (xy, wh, class, obj) for the gradient
+  float* losses;    // [N][4] (xy, wh, class, obj), accumulated
+  int g, C;
+  float aw[3], ah[3];
+  float grad_scale, lambda_coord, lambda_noobj, ignore_thresh;
+};
+
+__global__ __launch_bounds__(NT) void yolo_loss_kernel(YoloArgs a) {
+  __shared__ float sb[MAXB][4];
+  __shared__ float red[4][NT / 64];
+  const int n = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nb = a.counts[n];
+  for (int i = threadIdx.x; i < nb * 4; i += NT) sb[i >> 2][i & 3] = a.boxes[(int64_t)n * MAXB * 4 + i];
+  __syncthreads();
+  const int D = 5 + a.C, cells = a.g * a.g;
+  const float gf = (float)a.g;
+  float lxy = 0.f, lwh = 0.f, lcls = 0.f, lobj = 0.f;
+  for (int cell = blockIdx.x * (NT / 64) + w; cell < cells; cell += gridDim.x * (NT / 64)) {
+    const int gy = cell / a.g, gx = cell - gy * a.g;
+    const int64_t row = (int64_t)n * cells + cell;
+    const u16* p = a.pred + row * a.ldp;
+    const float* t = a.yt + row * 3 * D;
+    u16* gr = a.grad ? a.grad + row * a.ldp : nullptr;
+    float wxy = 0.f, wwh = 0.f, wcl = 0.f, wob = 0.f;
+    if (gr) {
+      wxy = a.gw[n * 4 + 0] * a.grad_scale; wwh = a.gw[n * 4 + 1] * a.grad_scale;
+      wcl = a.gw[n * 4 + 2] * a.grad_scale; wob = a.gw[n * 4 + 3] * a.grad_scale;
+    }
+#pragma unroll
+    for (int an = 0; an < 3; ++an) {
+      const u16* pa = p + an * D;
+      const float* ta = t + an * D;
+      const float tx = bf2f(pa[0]), ty = bf2f(pa[1]), tw = bf2f(pa[2]), th = bf2f(pa[3]), to = bf2f(pa[4]);
+      const float sx = sigm(tx), sy = sigm(ty);
+      const float bx = (sx + gx) / gf, by = (sy + gy) / gf;
+      const float bw = __expf(tw) * a.aw[an], bh = __expf(th) * a.ah[an];
+      const float x1 = bx - 0.5f * bw, y1 = by - 0.5f * bh, x2 = bx + 0.5f * bw, y2 = by + 0.5f * bh;
+      float best = 0.f;
+      for (int j = lane; j < nb; j += 64) best = fmaxf(best, iou(x1, y1, x2, y2, sb[j]));
+      best = wave_max(best);
+      const float ignore = best < a.ignore_thresh ? 1.f : 0.f;
+      const float cx = ta[0], cy = ta[1], cw = ta[2], ch = ta[3], tobj = ta[4];
+      const float wgt = 2.f - cw * ch;
+      const float rx = cx * gf - gx, ry = cy * gf - gy;
+      float rw = __logf(cw / a.aw[an]), rh = __logf(ch / a.ah[an]);
+      if (!isfinite(rw)) rw = 0.f;
+      if (!isfinite(rh)) rh = 0.f;
+      const float kc = a.lambda_coord * tobj * wgt;
+      // box / objectness channels: lanes 0..4 own one each
+      const float po = sigm(to);
+      float dobj;
+      const float eobj = bce(po, tobj, dobj);
+      const float fobj = tobj + (1.f - tobj) * ignore * a.lambda_noobj;
+      if (lane == 0) {
+        lxy += kc * ((rx - sx) * (rx - sx) + (ry - sy) * (ry - sy));
+        lwh += kc * ((rw - tw) * (rw - tw) + (rh - th) * (rh - th));
+        lobj += fobj * eobj;
+      }
+      if (gr && lane < 5) {
+        float gv;
+        if (lane == 0) gv = wxy * kc * 2.f * (sx - rx) * sx * (1.f - sx);
+        else if (lane == 1) gv = wxy * kc * 2.f * (sy - ry) * sy * (1.f - sy);
+        else if (lane == 2) gv = wwh * kc * 2.f * (tw - rw);
+        else if (lane == 3) gv = wwh * kc * 2.f * (th - rh);
+        else gv = wob * fobj * dobj;
+        gr[an * D + lane] = f2bf(gv);
+      }
+      // class channels
+      if (tobj != 0.f) {
+        for (int c = lane; c < a.C; c += 64) {
+          float dz;
+          const float e = bce(sigm(bf2f(pa[5 + c])), ta[5 + c], dz);
+          lcls += tobj * e;
+          if (gr) gr[an * D + 5 + c] = f2bf(wcl * tobj * dz);
+        }
+      } else if (gr) {
+        for (int c = lane; c < a.C; c += 64) gr[an * D + 5 + c] = 0;
+      }
+    }
+    if (gr)
+      for (int c = 3 * D + lane; c < a.ldp; c += 64) gr[c] = 0;
+  }
+  lcls = wave_sum(lcls);
+  if (lane == 0) {
+    red[0][w] = lxy; red[1][w] = lwh; red[2][w] = lcls; red[3][w] = lobj;
+  }
+  __syncthreads();
+  if (a.losses && threadIdx.x < 4) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) s += red[threadIdx.x][i];
+    atomicAdd(a.losses + n * 4 + threadIdx.x, s);
+  }
+}
+
+// decode: out row (n, row_off + cell*3 + anchor) = [x1, y1, x2, y2, sigmoid(obj), sigmoid(classes)]
+__global__ __launch_bounds__(NT) void yolo_decode_kernel(const u16* __restrict__ pred, int ldp, int N, int g, int C,
+                                                         float aw0, float ah0, float aw1, float ah1, float aw2, float ah2,
+                                                         float* __restrict__ out, int rows_total, int row_off) {
+  const int D = 5 + C;
+  const int64_t total = (int64_t)N * g * g * 3 * D;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
+    const int j = (int)(i % D);
+    const int64_t r = i / D;  // (n, cell, anchor)
+    const int an = (int)(r % 3);
+    const int64_t nc = r / 3;
+    const int cell = (int)(nc % (g * g));
+    const int n = (int)(nc / (g * g));
+    const u16* pa = pred + nc * ldp + an * D;
+    float v;
+    if (j < 4) {
+      const float aw = an == 0 ? aw0 : (an == 1 ? aw1 : aw2);
+      const float ah = an == 0 ? ah0 : (an == 1 ? ah1 : ah2);
+      const int gy = cell / g, gx = cell - gy * g;
+      const float bx = (sigm(bf2f(pa[0])) + gx) / g, by = (sigm(bf2f(pa[1])) + gy) / g;
+      const float bw = __expf(bf2f(pa[2])) * aw, bh = __expf(bf2f(pa[3])) * ah;
+      v = j == 0 ? bx - 0.5f * bw : j == 1 ? by - 0.5f * bh : j == 2 ? bx + 0.5f * bw : by + 0.5f * bh;
+    } else {
+      v = sigm(bf2f(pa[j]));
+    }
+    out[((int64_t)n * rows_total + row_off + (int64_t)cell * 3 + an) * D + j] = v;
+  }
+}
+
+// Greedy NMS, one block per image, candidates = rows with score >= score_thresh (scores staged in
+// LDS, -inf once taken or suppressed). Each round: block argmax (lowest index on ties, as
+// tf.argmax), emit the row, suppress rows with IoU > iou_thresh.
+constexpr int NMS_MAXM = 32768;  // 128 KB of LDS: 608x608 inputs give 22743 rows
+__global__ __launch_bounds__(NT) void nms_kernel(const float* __restrict__ cand, int M, int D, float iou_thresh,
+                                                 float score_thresh, int max_det, float* __restrict__ out) {
+  __shared__ float sc[NMS_MAXM];
+  __shared__ float rv[NT / 64];
+  __shared__ int ri[NT / 64];
+  __shared__ int pick;
+  const int n = blockIdx.x, tid = threadIdx.x;
+  const float* c = cand + (int64_t)n * M * D;
+  float* o = out + (int64_t)n * (max_det + 1) * D;
+  for (int i = tid; i < M; i += NT) {
+    const float s = c[(int64_t)i * D + 4];
+    sc[i] = s >= score_thresh ? s : -INFINITY;
+  }
+  __syncthreads();
+  int count = 0;
+  for (; count < max_det; ++count) {
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int i = tid; i < M; i += NT) {
+      const float s = sc[i];
+      if (s > bv) { bv = s; bi = i; }  // strided scan visits increasing i: ties keep the first
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const float ov = __shfl_xor(bv, off, 64);
+      const int oi = __shfl_xor(bi, off, 64);
+      if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+    }
+    if ((tid & 63) == 0) { rv[tid >> 6] = bv; ri[tid >> 6] = bi; }
+    __syncthreads();
+    if (tid == 0) {
+      float v = rv[0]; int id = ri[0];
+      for (int k = 1; k < NT / 64; ++k)
+        if (rv[k] > v || (rv[k] == v && ri[k] < id)) { v = rv[k]; id = ri[k]; }
+      pick = (v == -INFINITY) ? -1 : id;
+    }
+    __syncthreads();
+    const int pk = pick;
+    if (pk < 0) break;
+    const float* b = c + (int64_t)pk * D;
+    for (int j = tid; j < D; j += NT) o[(int64_t)count * D + j] = b[j];
+    const float x1 = b[0], y1 = b[1], x2 = b[2], y2 = b[3];
+    for (int i = tid; i < M; i += NT) {
+      if (sc[i] == -INFINITY) continue;
+      if (i == pk || iou(x1, y1, x2, y2, c + (int64_t)i * D) > iou_thresh) sc[i] = -INFINITY;
+    }
+    __syncthreads();
+  }
+  if (tid == 0 && count > 0)
+    for (int j = 0; j < D; ++j) o[(int64_t)max_det * D + j] = (float)count;
+}
+}  // namespace
+
+void dv_yolo_gather_boxes(const float* y_true, int N, int cells, int D, float* boxes, int* counts, hipStream_t st) {
+  yolo_gather_kernel<<<N, NT, 0, st>>>(y_true, cells, D, boxes, counts);
+}
+
+void dv_yolo_loss(const void* pred, int ldp, const float* y_true, const float* boxes, const int* counts, void* grad,
+                  const float* gw, float* losses, int N, int g, int C, const float* anchors6, float grad_scale, float lambda_coord,
+                  float lambda_noobj, float ignore_thresh, hipStream_t st) {
+  YoloArgs a;
+  a.pred = (const u16*)pred; a.ldp = ldp; a.yt = y_true; a.boxes = boxes; a.counts = counts;
+  a.grad = (u16*)grad; a.gw = gw; a.losses = losses; a.g = g; a.C = C;
+  for (int i = 0; i < 3; ++i) { a.aw[i] = anchors6[2 * i]; a.ah[i] = anchors6[2 * i + 1]; }
+  a.grad_scale = grad_scale; a.lambda_coord = lambda_coord; a.lambda_noobj = lambda_noobj;
+  a.ignore_thresh = ignore_thresh;
+  const int cells = g * g;
+  const int bx = std::max(1, std::min((cells + 3) / 4, 2048 / std::max(N, 1) + 1));
+  yolo_loss_kernel<<<dim3(bx, N), NT, 0, st>>>(a);
+}
+
+void dv_yolo_decode(const void* pred, int ldp, int N, int g, int C, const float* anchors6, float* out, int rows_total,
+                    int row_off, hipStream_t st) {
+  const int64_t total = (int64_t)N * g * g * 3 * (5 + C);
+  const int blocks = (int)std::min<int64_t>((total + NT - 1) / NT, 8192);
+  yolo_decode_kernel<<<blocks, NT, 0, st>>>((const u16*)pred, ldp, N, g, C, anchors6[0], anchors6[1], anchors6[2],
+                                            anchors6[3], anchors6[4], anchors6[5], out, rows_total, row_off);
+}
+
+int dv_nms(const float* cand, int N, int M, int D, float iou_thresh, float score_thresh, int max_det, float* out,
+           hipStream_t st) {
+  if (M > NMS_MAXM) return -1;
+  nms_kernel<<<N, NT, 0, st>>>(cand, M, D, iou_thresh, score_thresh, max_det, out);
+  return 0;
+}

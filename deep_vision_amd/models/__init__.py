@@ -3,6 +3,11 @@ from .classic import VGG16, VGG19, AlexNetV1, AlexNetV2, AlexNetV2TF, LeNet5, Le
 from .inception import InceptionV1, InceptionV3  # noqa: F401
 from .mobilenet import MobileNetV1, MobileNetV1TF, ShuffleNetV1  # noqa: F401
 from .resnet import ResNet34, ResNet50, ResNet152  # noqa: F401
+from .yolov3 import YoloV3, Darknet53  # noqa: F401
+from .hourglass import StackedHourglassNetwork  # noqa: F401
+from .centernet import ObjectsAsPoints  # noqa: F401
+from .gan import (CycleGANDiscriminator, CycleGANGenerator, DCGANDiscriminator, DCGANGenerator,  # noqa: F401
+                  cyclegan, dcgan)
 
 MODELS = {
     "lenet5": LeNet5,
@@ -20,6 +25,14 @@ MODELS = {
     "mobilenet1": MobileNetV1,
     "mobilenet1_tf": MobileNetV1TF,
     "shufflenet1": ShuffleNetV1,
+    "yolov3": YoloV3,
+    "darknet53": Darknet53,
+    "hourglass104": StackedHourglassNetwork,
+    "centernet": ObjectsAsPoints,
+    "dcgan_generator": DCGANGenerator,
+    "dcgan_discriminator": DCGANDiscriminator,
+    "cyclegan_generator": CycleGANGenerator,
+    "cyclegan_discriminator": CycleGANDiscriminator,
 }
 
 

@@ -1,0 +1,103 @@
+"""Stacked Hourglass network (R/Hourglass/tensorflow/hourglass104.py:19-159).
+
+* BottleneckBlock: pre-activation BN(momentum .9 -> torch .1, eps 1e-3) -> ReLU -> 1x1 (C/2) ->
+  BN -> ReLU -> 3x3 (C/2) -> BN -> ReLU -> 1x1 (C), all convs with bias (Keras default), plus an
+  identity or 1x1 projection (``downsample``) (:19-67).
+* HourglassModule: recursive order-4 module with 2x2 max-pool down and nearest 2x up (:70-98).
+* StackedHourglassNetwork: 7x7/2 stem, 4 stacks, 16 heatmaps per stack; every stack output is
+  returned (intermediate supervision) and re-injected through two 1x1 convs (:101-159).
+
+The reference's loop variable ``i`` is shadowed by the inner residual loop (:136/:138), so its
+Keras graph also creates re-injection convs after the last stack. They reach no output, and a
+Keras functional Model only holds layers on an input->output path, so they are not part of the
+reference model and are not built here: 16,290,752 trainable parameters (pinned in tests).
+SURVEY §2.2 lists 16,360,896, which counts those two dead convs (+70,144); the CenterNet
+notebook summary (R/ObjectsAsPoints/tensorflow/test.ipynb cell 2) confirms that dead branches
+are excluded -- models/centernet.py matches it exactly only without its dead layers.
+
+GPU path: the BN -> ReLU prologue of each block runs as one native BN pass (statistics from a
+separate reduction because the block input is a sum), the inner conv -> BN -> ReLU pairs take
+their statistics from the conv epilogue.
+"""
+from __future__ import annotations
+
+import torch.nn as tnn
+
+from .. import nn
+from .. import ops as F
+
+
+def _bn(c):
+    return nn.BatchNorm2d(c, eps=1e-3, momentum=0.1)
+
+
+class BottleneckBlock(tnn.Module):
+    def __init__(self, cin, filters, downsample=False):
+        super().__init__()
+        self.downsample = nn.Conv2d(cin, filters, 1) if downsample else None
+        self.bn1 = _bn(cin)
+        self.conv1 = nn.Conv2d(cin, filters // 2, 1)
+        self.bn2 = _bn(filters // 2)
+        self.conv2 = nn.Conv2d(filters // 2, filters // 2, 3, padding=1)
+        self.bn3 = _bn(filters // 2)
+        self.conv3 = nn.Conv2d(filters // 2, filters, 1)
+
+    def forward(self, x):
+        identity = self.downsample(x) if self.downsample is not None else x
+        y = F.batch_norm_act(x, self.bn1, "relu")
+        y = F.conv_bn_act(y, self.conv1, self.bn2, "relu")
+        y = F.conv_bn_act(y, self.conv2, self.bn3, "relu")
+        return F.add(self.conv3(y), identity)
+
+
+class HourglassModule(tnn.Module):
+    def __init__(self, order, filters, num_residual):
+        super().__init__()
+        self.order = order
+        self.up1 = tnn.Sequential(*[BottleneckBlock(filters, filters) for _ in range(num_residual + 1)])
+        self.low1 = tnn.Sequential(*[BottleneckBlock(filters, filters) for _ in range(num_residual)])
+        if order > 1:
+            self.low2 = HourglassModule(order - 1, filters, num_residual)
+        else:
+            self.low2 = tnn.Sequential(*[BottleneckBlock(filters, filters) for _ in range(num_residual)])
+        self.low3 = tnn.Sequential(*[BottleneckBlock(filters, filters) for _ in range(num_residual)])
+
+    def forward(self, x):
+        up1 = self.up1(x)
+        low = self.low3(self.low2(self.low1(F.max_pool2d(x, 2, 2))))
+        return F.add(F.upsample_nearest(low, 2), up1)
+
+
+class StackedHourglassNetwork(tnn.Module):
+    def __init__(self, num_stack=4, num_residual=1, num_heatmap=16, input_size=256):
+        super().__init__()
+        self.num_stack = num_stack
+        self.input_size = input_size
+        self.stem = nn.Conv2d(3, 64, 7, stride=2, padding="same_keras")
+        self.stem_bn = _bn(64)
+        self.pre = tnn.Sequential(BottleneckBlock(64, 128, downsample=True))
+        self.pre2 = tnn.Sequential(BottleneckBlock(128, 128), BottleneckBlock(128, 256, downsample=True))
+        self.hourglass = tnn.ModuleList(HourglassModule(4, 256, num_residual) for _ in range(num_stack))
+        self.residual = tnn.ModuleList(tnn.Sequential(*[BottleneckBlock(256, 256) for _ in range(num_residual)])
+                                       for _ in range(num_stack))
+        self.linear = tnn.ModuleList(tnn.ModuleDict({"conv": nn.Conv2d(256, 256, 1), "bn": _bn(256)})
+                                     for _ in range(num_stack))
+        self.heatmap = tnn.ModuleList(nn.Conv2d(256, num_heatmap, 1) for _ in range(num_stack))
+        self.inter_x = tnn.ModuleList(nn.Conv2d(256, 256, 1) for _ in range(num_stack - 1))
+        self.inter_y = tnn.ModuleList(nn.Conv2d(num_heatmap, 256, 1) for _ in range(num_stack - 1))
+
+    def forward(self, x):
+        x = F.conv_bn_act(x, self.stem, self.stem_bn, "relu")
+        x = self.pre(x)
+        x = F.max_pool2d(x, 2, 2)
+        x = self.pre2(x)
+        ys = []
+        for i in range(self.num_stack):
+            x = self.residual[i](self.hourglass[i](x))
+            lin = self.linear[i]
+            x = F.conv_bn_act(x, lin["conv"], lin["bn"], "relu")
+            y = self.heatmap[i](x)
+            ys.append(y)
+            if i < self.num_stack - 1:
+                x = F.add(self.inter_x[i](x), self.inter_y[i](y))
+        return ys

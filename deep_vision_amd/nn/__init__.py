@@ -25,11 +25,6 @@ Flatten = tnn.Flatten
 Identity = tnn.Identity
 
 
-def _same_pad(k, s, d=1):
-    """Keras 'same' padding: total = max((ceil(i/s)-1)*s + (k-1)*d + 1 - i, 0) — input dependent."""
-    return k, s, d
-
-
 class Conv2d(tnn.Conv2d):
     """torch.nn.Conv2d; ``padding='same_keras'`` reproduces TF/Keras asymmetric 'same' padding
     (extra row/col at the bottom/right at stride 2)."""
@@ -38,22 +33,24 @@ class Conv2d(tnn.Conv2d):
         self.keras_same = padding == "same_keras"
         super().__init__(*args, padding=0 if self.keras_same else padding, **kw)
 
-    def _keras_pads(self, H, W):
+    def native_padding(self, H, W):
+        """Padding for ops.conv2d: ``self.padding``, or the Keras 'same' (top, bottom, left,
+        right) pads for an H x W input: total = max((ceil(i/s)-1)*s + (k-1)*d + 1 - i, 0), the
+        odd pixel at the bottom/right."""
+        if not self.keras_same:
+            return self.padding
         out = []
         for i, k, s, d in ((H, self.kernel_size[0], self.stride[0], self.dilation[0]),
                            (W, self.kernel_size[1], self.stride[1], self.dilation[1])):
             o = -(-i // s)
             tot = max((o - 1) * s + (k - 1) * d + 1 - i, 0)
-            out.append((tot // 2, tot - tot // 2))
-        return out
+            out += [tot // 2, tot - tot // 2]
+        return tuple(out) if out[0] != out[1] or out[2] != out[3] else (out[0], out[2])
 
     def forward(self, x):
         if self.keras_same:
-            (pt, pb), (pl, pr) = self._keras_pads(x.shape[2], x.shape[3])
-            if pt == pb and pl == pr:
-                return F.conv2d(x, self.weight, self.bias, self.stride, (pt, pl), self.dilation, self.groups)
-            x = pad2d(x, (pl, pr, pt, pb))
-            return F.conv2d(x, self.weight, self.bias, self.stride, 0, self.dilation, self.groups)
+            return F.conv2d(x, self.weight, self.bias, self.stride, self.native_padding(x.shape[2], x.shape[3]),
+                            self.dilation, self.groups)
         if self.padding_mode != "zeros":
             return super().forward(x) if not native(x) else F.conv2d(
                 tnn.functional.pad(x, self._reversed_padding_repeated_twice, mode=self.padding_mode), self.weight,
@@ -70,7 +67,21 @@ def pad2d(x, pads, mode="constant"):
 
 
 class ConvTranspose2d(tnn.ConvTranspose2d):
+    """torch.nn.ConvTranspose2d; ``padding='same_keras'`` gives Keras Conv2DTranspose 'same'
+    semantics (output = input * stride, top/left pad (k - s) // 2 -- e.g. k3/s2 differs from
+    torch's padding=1, output_padding=1 by a one-pixel shift)."""
+
+    def __init__(self, *args, padding=0, **kw):
+        self.keras_same = padding == "same_keras"
+        super().__init__(*args, padding=0 if self.keras_same else padding, **kw)
+
     def forward(self, x, output_size=None):
+        if self.keras_same:
+            from ..ops.conv import keras_same_transpose
+
+            pad, out = keras_same_transpose(x.shape[2], x.shape[3], self.kernel_size, self.stride)
+            return F.conv_transpose2d(x, self.weight, self.bias, self.stride, pad, 0, self.groups, self.dilation,
+                                      output_size=out)
         if output_size is not None or not native(x):
             return super().forward(x, output_size)
         return F.conv_transpose2d(x, self.weight, self.bias, self.stride, self.padding, self.output_padding,
@@ -206,8 +217,8 @@ class FusedSequential(tnn.Sequential):
         while i < len(mods):
             m = mods[i]
             nxt = mods[i + 1] if i + 1 < len(mods) else None
-            if isinstance(m, tnn.Conv2d) and not isinstance(m, tnn.ConvTranspose2d) and m.padding_mode == "zeros" \
-                    and not getattr(m, "keras_same", False):
+            if isinstance(m, Conv2d) and m.padding_mode == "zeros":
+                pad = m.native_padding(x.shape[2], x.shape[3])
                 if isinstance(nxt, tnn.BatchNorm2d):
                     act, slope = _act_of(mods[i + 2]) if i + 2 < len(mods) else (None, 0.0)
                     x = F.conv_bn_act(x, m, nxt, act, slope)
@@ -215,7 +226,7 @@ class FusedSequential(tnn.Sequential):
                     continue
                 act, slope = _act_of(nxt)
                 if act:
-                    x = F.conv2d(x, m.weight, m.bias, m.stride, m.padding, m.dilation, m.groups, act=act, slope=slope)
+                    x = F.conv2d(x, m.weight, m.bias, m.stride, pad, m.dilation, m.groups, act=act, slope=slope)
                     i += 2
                     continue
             if isinstance(m, tnn.Linear):

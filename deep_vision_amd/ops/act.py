@@ -21,7 +21,7 @@ def _prep(x):
     if _native_layout(x):
         return x
     if x.dim() == 4:
-        return x.to(dtype=BF16, memory_format=CL)
+        return x.to(dtype=BF16).contiguous(memory_format=CL)  # .to() keeps non-dense CL-strided views
     return x.to(dtype=BF16).contiguous()
 
 

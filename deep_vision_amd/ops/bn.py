@@ -52,6 +52,9 @@ class _BNActFn(torch.autograd.Function):
                           ptr(running_var), ptr(mean), ptr(invstd), ptr(scale), ptr(shift), st)
         else:
             L.bn_eval_prep(C, float(eps), ptr(g), ptr(b), ptr(running_mean), ptr(running_var), ptr(scale), ptr(shift), st)
+            if weight is not None and weight.requires_grad:  # dgamma needs xhat of the running stats
+                mean.copy_(running_mean)
+                torch.rsqrt(running_var + eps, out=invstd)
         out = torch.empty_like(x)
         L.bn_apply(ptr(x), ptr(residual), ptr(out), x.numel(), C, ptr(scale), ptr(shift), act, float(slope), st)
         # activation mask in backward: from the saved output when a residual was added, else
@@ -77,9 +80,12 @@ class _BNActFn(torch.autograd.Function):
         dx = torch.empty_like(x)
         dres = torch.empty_like(x) if (has_res and ctx.needs_input_grad[6]) else None
         dgamma = dbeta = None
-        if training:
-            acc = ctx.ws_bwd
+        want_affine = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
+        direct = False
+        if training or want_affine:
+            # sum dz and sum dz*xhat (xhat from the batch statistics, or the running ones in eval)
             rows = N * H * W
+            acc = ctx.ws_bwd if ctx.ws_bwd is not None else torch.zeros((STAT_SHARDS, 2, C), dtype=F32, device=dev)
             L.bn_bwd_reduce(ptr(dout), ptr(out), ptr(x), rows, C, ptr(mean), ptr(invstd), ptr(scale), ptr(shift), act,
                             float(slope), ptr(acc), st)
             sg = grad_sink(weight) if ctx.needs_input_grad[2] else None
@@ -92,16 +98,17 @@ class _BNActFn(torch.autograd.Function):
             L.bn_bwd_finalize(ptr(acc), C, float(rows), ptr(weight.detach() if weight is not None else None), ptr(mean),
                               ptr(invstd), ptr(sg if direct else dgamma), ptr(sb if direct else dbeta), int(direct),
                               ptr(coef[0]), ptr(coef[1]), ptr(coef[2]), st)
+        if training:
             L.bn_bwd_apply(ptr(dout), ptr(out), ptr(x), ptr(dx), ptr(dres), x.numel(), C, ptr(coef[0]), ptr(coef[1]),
                            ptr(coef[2]), ptr(scale), ptr(shift), act, float(slope), st)
-            if direct:
-                notify_grad_ready(weight)
-                notify_grad_ready(bias)
         else:
             if act and out is None:  # eval backward needs the mask: rebuild the output
                 out = torch.empty_like(x)
                 L.bn_apply(ptr(x), 0, ptr(out), x.numel(), C, ptr(scale), ptr(shift), act, float(slope), st)
             L.bn_bwd_eval(ptr(dout), ptr(out), ptr(dx), ptr(dres), x.numel(), C, ptr(scale), act, float(slope), st)
+        if direct:
+            notify_grad_ready(weight)
+            notify_grad_ready(bias)
         return dx, None, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None
 
 
@@ -152,7 +159,8 @@ def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None):
     # padded view, which is compacted below and gets its statistics from a separate pass
     want = (bn.training or not bn.track_running_stats) and conv.out_channels % 8 == 0
     sbuf = workspace(bn, "bn_fwd", (STAT_SHARDS, 2, conv.out_channels), x.device) if want else None
-    r = conv2d(x, conv.weight, conv.bias, conv.stride, conv.padding, conv.dilation, conv.groups, want_stats=want,
+    pad = conv.native_padding(x.shape[2], x.shape[3]) if hasattr(conv, "native_padding") else conv.padding
+    r = conv2d(x, conv.weight, conv.bias, conv.stride, pad, conv.dilation, conv.groups, want_stats=want,
                stats_buf=sbuf)
     y, stats = r if want else (r, None)
     if y.shape[1] % 8 != 0:  # padded view: BN kernels require dense channels

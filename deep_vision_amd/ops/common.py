@@ -88,7 +88,7 @@ def as_nhwc(x: torch.Tensor, pad_to8: bool = True) -> torch.Tensor:
         y = torch.empty((N, Cp, H, W), dtype=BF16, device=x.device, memory_format=CL)
         lib().to_nhwc(ptr(x), int(x.dtype == F32), ptr(y), N, C, H, W, Cp, stream_handle())
         return y  # padded channels are written as zeros by the kernel
-    y = x.to(dtype=BF16, memory_format=CL)
+    y = x.to(dtype=BF16).contiguous(memory_format=CL)
     if pad_to8 and C % 8 != 0:
         y = torch.nn.functional.pad(y, (0, 0, 0, 0, 0, round8(C) - C)).contiguous(memory_format=CL)
     return y

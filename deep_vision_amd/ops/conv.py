@@ -33,6 +33,22 @@ def out_size(H, W, R, S, stride, padding, dilation):
     return P, Q
 
 
+def norm_padding(padding):
+    """int | (ph, pw) | (top, bottom, left, right) -> ((pt, pl), (eb, er)).
+
+    The 4-tuple form is TF/Keras asymmetric 'same' padding: the kernels take the top/left pad and
+    an output size that includes the ``eb``/``er`` extra bottom/right rows, whose reads fall
+    outside the image and are zero-filled by the gather -- no padded copy of the input."""
+    if isinstance(padding, int):
+        return (padding, padding), (0, 0)
+    if len(padding) == 4:
+        pt, pb, pl, pr = padding
+        if pb < pt or pr < pl:
+            raise NotImplementedError("asymmetric padding larger at top/left")
+        return (pt, pl), (pb - pt, pr - pl)
+    return tuple(padding), (0, 0)
+
+
 def _prep_weight(weight: torch.Tensor, G: int, pad: int, mode: int) -> torch.Tensor:
     """fp32 OIHW -> bf16 kernel operand.
 
@@ -135,14 +151,15 @@ def _wgrad(x, dy, weight, Cg_x, G, stride, padding, dilation, out=None):
 
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats, stats_buf=None):
+    def forward(ctx, x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats, stats_buf=None,
+                extra=(0, 0)):
         N, Cx, H, W = x.shape
         O, Ig, R, S = weight.shape
         G = groups
         Og = O // G
         ldx = ld_of(x)
         Cg_x = _gather_channels(x, Cx // G, G)  # padded channels (G == 1) are zeros
-        P, Q = out_size(H, W, R, S, stride, padding, dilation)
+        P, Q = out_size(H + extra[0], W + extra[1], R, S, stride, padding, dilation)
         wk = _prep_weight(weight, G, Cg_x, mode=0)
         y = empty_nhwc(N, O, P, Q, x.device)
         stats = None
@@ -181,29 +198,37 @@ class _ConvFn(torch.autograd.Function):
                 notify_grad_ready(weight)
         if has_bias and ctx.needs_input_grad[2]:
             db = _channel_sum(dy)
-        return dx, dw, db, None, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None, None, None
 
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=None, slope=0.0,
            want_stats=False, stats_buf=None):
-    """Conv2d (+fused bias/activation). Returns y, or (y, stats) when want_stats (GPU only)."""
-    stride, padding, dilation = _pair(stride), _pair(padding), _pair(dilation)
+    """Conv2d (+fused bias/activation). Returns y, or (y, stats) when want_stats (GPU only).
+
+    ``padding`` may be (top, bottom, left, right) for TF/Keras asymmetric 'same' padding."""
+    if isinstance(padding, str):
+        raise NotImplementedError("string padding: use nn.Conv2d(padding='same_keras')")
+    stride, dilation = _pair(stride), _pair(dilation)
+    padding, extra = norm_padding(padding)
     if not native(x):
+        if extra != (0, 0):
+            x = TF.pad(x, (padding[1], padding[1] + extra[1], padding[0], padding[0] + extra[0]))
+            padding = (0, 0)
         y = TF.conv2d(x, weight, bias, stride, padding, dilation, groups)
         if act in ("relu",):
             y = TF.relu(y)
         elif act in ("leaky", "leaky_relu"):
             y = TF.leaky_relu(y, slope)
         return (y, None) if want_stats else y
-    if isinstance(padding, str):
-        raise NotImplementedError("string padding: use nn.Conv2d(padding='same_keras')")
     if _is_depthwise(x, weight, groups, stride, dilation):
-        return depthwise_conv2d(x, weight, bias, stride, padding, act, slope, want_stats, stats_buf)
+        return depthwise_conv2d(x, weight, bias, stride, padding, act, slope, want_stats, stats_buf, extra)
     if groups > 1 and ((x.shape[1] // groups) % 8 != 0 or (weight.shape[0] // groups) % 8 != 0):
+        if extra != (0, 0):
+            raise NotImplementedError("asymmetric padding on a channel-padded grouped conv")
         return _grouped_padded_conv(x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats)
     x = as_nhwc(x, pad_to8=(groups == 1))
     return _ConvFn.apply(x, weight, bias, stride, padding, dilation, groups, ACT_IDS[act], float(slope), want_stats,
-                         stats_buf)
+                         stats_buf, extra)
 
 
 def _grouped_padded_conv(x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats):
@@ -233,9 +258,11 @@ def _grouped_padded_conv(x, weight, bias, stride, padding, dilation, groups, act
 # ---------------------------------------------------------------------------------------
 class _ConvTFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, padding, output_padding, dilation, groups):
+    def forward(ctx, x, weight, bias, stride, padding, output_padding, dilation, groups, out_hw=None):
         # x (N, Cin, H, W), weight (Cin, Cout/G, R, S). Equivalent conv: W_conv = weight with
         # O := Cin, I := Cout/G; output = dgrad(x) of that conv with output size (OH, OW).
+        # ``out_hw`` overrides the output size (Keras 'same': H*stride with a top/left pad of
+        # (k - s) // 2, i.e. the torch result cropped at the bottom/right).
         N, Cin, H, W = x.shape
         Ci, Cog, R, S = weight.shape
         G = groups
@@ -244,6 +271,8 @@ class _ConvTFn(torch.autograd.Function):
         dh, dw = dilation
         OH = (H - 1) * sh - 2 * ph + dh * (R - 1) + output_padding[0] + 1
         OW = (W - 1) * sw - 2 * pw + dw * (S - 1) + output_padding[1] + 1
+        if out_hw is not None:
+            OH, OW = out_hw
         Cout = Cog * G
         if G > 1 and (Cog % 8 != 0):
             raise NotImplementedError("grouped ConvTranspose requires out-channels-per-group % 8 == 0")
@@ -287,15 +316,28 @@ class _ConvTFn(torch.autograd.Function):
             dw = _wgrad(dy, x, weight, Cg_dy, G, stride, padding, dilation)
         if has_bias and ctx.needs_input_grad[2]:
             db = _channel_sum(dy)
-        return dx, dw, db, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None
 
 
-def conv_transpose2d(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1, dilation=1):
+def keras_same_transpose(H, W, kernel_size, stride):
+    """Keras Conv2DTranspose(padding='same'): output (H*s, W*s), top/left pad (k - s) // 2."""
+    (kh, kw), (sh, sw) = _pair(kernel_size), _pair(stride)
+    return (max(kh - sh, 0) // 2, max(kw - sw, 0) // 2), (H * sh, W * sw)
+
+
+def conv_transpose2d(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1, dilation=1,
+                     output_size=None):
+    """torch.nn.functional.conv_transpose2d; ``output_size=(OH, OW)`` crops / fixes the output
+    grid (used for Keras 'same' transposed convs whose size torch cannot express)."""
     stride, padding, output_padding, dilation = _pair(stride), _pair(padding), _pair(output_padding), _pair(dilation)
     if not native(x):
-        return TF.conv_transpose2d(x, weight, bias, stride, padding, output_padding, groups, dilation)
+        if output_size is None:
+            return TF.conv_transpose2d(x, weight, bias, stride, padding, output_padding, groups, dilation)
+        y = TF.conv_transpose2d(x, weight, bias, stride, 0, 0, groups, dilation)
+        return y[:, :, padding[0]:padding[0] + output_size[0], padding[1]:padding[1] + output_size[1]]
     x = as_nhwc(x, pad_to8=(groups == 1))
-    return _ConvTFn.apply(x, weight, bias, stride, padding, output_padding, dilation, groups)
+    return _ConvTFn.apply(x, weight, bias, stride, padding, output_padding, dilation, groups,
+                          tuple(output_size) if output_size is not None else None)
 
 
 # ---------------------------------------------------------------------------------------
@@ -389,10 +431,10 @@ def linear(x, weight, bias=None, act=None, slope=0.0):
 # ---------------------------------------------------------------------------------------
 class _DWConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, padding, act, slope, want_stats, stats_buf):
+    def forward(ctx, x, weight, bias, stride, padding, act, slope, want_stats, stats_buf, extra=(0, 0)):
         N, C, H, W = x.shape
         K = weight.shape[2]
-        P, Q = out_size(H, W, K, K, stride, padding, (1, 1))
+        P, Q = out_size(H + extra[0], W + extra[1], K, K, stride, padding, (1, 1))
         y = empty_nhwc(N, C, P, Q, x.device)
         w = weight.detach().float().contiguous()
         b = bias.detach().float().contiguous() if bias is not None else None
@@ -437,7 +479,7 @@ class _DWConvFn(torch.autograd.Function):
                 dw = buf
         if has_bias and ctx.needs_input_grad[2]:
             db = _channel_sum(dy)
-        return dx, dw, db, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None
 
 
 def _is_depthwise(x, weight, groups, stride, dilation):
@@ -447,7 +489,8 @@ def _is_depthwise(x, weight, groups, stride, dilation):
 
 
 def depthwise_conv2d(x, weight, bias=None, stride=1, padding=0, act=None, slope=0.0, want_stats=False,
-                     stats_buf=None):
+                     stats_buf=None, extra=(0, 0)):
     stride, padding = _pair(stride), _pair(padding)
     x = as_nhwc(x, pad_to8=False)
-    return _DWConvFn.apply(x, weight, bias, stride, padding, ACT_IDS[act], float(slope), want_stats, stats_buf)
+    return _DWConvFn.apply(x, weight, bias, stride, padding, ACT_IDS[act], float(slope), want_stats, stats_buf,
+                           extra)

@@ -27,7 +27,18 @@ PINNED = {
     "resnet152": 60_192_808,
     "mobilenet1": 4_231_976,
     "mobilenet1_tf": 4_242_856,  # reference comment R/MobileNet/tensorflow/train.py:35
+    "yolov3": 61_949_149,  # trainable; 62,001,757 with BN moving statistics
+    # Keras drops layers that reach no output (verified by centernet below against the notebook
+    # summary); SURVEY §2.2's 16,360,896 counts the two dead re-injection convs (+70,144)
+    "hourglass104": 16_290_752,
+    "centernet": 94_553_384,  # R/ObjectsAsPoints/tensorflow/test.ipynb: trainable 94,553,384
+    "dcgan_generator": 2_305_472,
+    "dcgan_discriminator": 212_865,
+    "cyclegan_generator": 11_383_427,
+    "cyclegan_discriminator": 2_765_633,
 }
+
+TOTAL_WITH_BN_STATS = {"yolov3": 62_001_757, "centernet": 94_654_504}  # Keras "Total params"
 
 
 def nparams(m):
@@ -37,6 +48,13 @@ def nparams(m):
 @pytest.mark.parametrize("name", sorted(PINNED))
 def test_param_counts(name):
     assert nparams(M.get_model(name)) == PINNED[name]
+
+
+@pytest.mark.parametrize("name", sorted(TOTAL_WITH_BN_STATS))
+def test_keras_total_params(name):
+    m = M.get_model(name)
+    stats = sum(b.numel() for k, b in m.named_buffers() if "running" in k)
+    assert nparams(m) + stats == TOTAL_WITH_BN_STATS[name]
 
 
 REF_MODULES = [
