@@ -1,0 +1,10 @@
+"""LeNet PT trainer: `python train.py -m <model> [-c <ckpt>]` (same CLI as R/LeNet/pytorch/train.py)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.abspath(os.path.join(os.path.dirname(__file__), "..", "..")))
+
+from deep_vision_amd.train.classification import main  # noqa: E402
+
+if __name__ == "__main__":
+    main(choices=['lenet5'], default="lenet5")

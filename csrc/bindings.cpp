@@ -175,9 +175,9 @@ PYBIND11_MODULE(_C, m) {
       throw std::runtime_error("nms: more than 32768 candidate rows per image");
     check_last("nms");
   });
-  m.def("pw_loss", [](int kind, uptr pred, int pred_bf16, uptr tgt, int tgt_type, float tval, int64_t rows, int C,
-                      int ldp, int ldt, float a, float b, uptr sums, uptr grad, uptr gscale, float hscale, uptr st) {
-    dv_pw_loss(kind, CP(pred), pred_bf16, CP(tgt), tgt_type, tval, rows, C, ldp, ldt, a, b, FP(sums), P(grad),
+  m.def("pw_loss", [](int kind, uptr pred, int pred_bf16, uptr tgt, int tgt_type, float tval, uptr wt, int64_t rows,
+                      int C, int ldp, int ldt, float a, float b, uptr sums, uptr grad, uptr gscale, float hscale, uptr st) {
+    dv_pw_loss(kind, CP(pred), pred_bf16, CP(tgt), tgt_type, tval, CFP(wt), rows, C, ldp, ldt, a, b, FP(sums), P(grad),
                CFP(gscale), hscale, ST(st));
     check_last("pw_loss");
   });

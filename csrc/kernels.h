@@ -117,6 +117,6 @@ int dv_nms(const float* cand, int N, int M, int D, float iou_thresh, float score
            hipStream_t st);
 
 // ---- pointwise losses with gradient (losses.hip) ----
-void dv_pw_loss(int kind, const void* pred, int pred_bf16, const void* tgt, int tgt_type, float tval, int64_t rows,
-                int C, int ldp, int ldt, float a, float b, float* sums, void* grad, const float* gscale, float hscale,
-                hipStream_t st);
+void dv_pw_loss(int kind, const void* pred, int pred_bf16, const void* tgt, int tgt_type, float tval, const float* wt,
+                int64_t rows, int C, int ldp, int ldt, float a, float b, float* sums, void* grad, const float* gscale,
+                float hscale, hipStream_t st);

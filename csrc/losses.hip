@@ -13,7 +13,8 @@
 //
 // Layout: pred / target / grad are row-major (rows, ld) with C valid channels per row (padded NHWC
 // channel strides are honoured, padding channels of the gradient are written as zeros). The
-// target is fp32, bf16 or a scalar constant (GAN labels).
+// target is fp32, bf16 or a scalar constant (GAN labels); an optional fp32 weight tensor (target
+// layout) scales each element's loss and gradient (CenterNet's masked size / offset L1).
 #include "common.h"
 #include "kernels.h"
 
@@ -63,9 +64,10 @@ DV_DEVICE void pw_eval(int kind, float p, float t, float a, float b, float& l, f
 
 template <typename TP, typename TT>
 __global__ __launch_bounds__(NT) void pw_loss_kernel(int kind, const TP* __restrict__ pred, const TT* __restrict__ tgt,
-                                                     float tval, int64_t rows, int C, int ldp, int ldt, float a,
-                                                     float b, float* __restrict__ sums, TP* __restrict__ grad,
-                                                     const float* __restrict__ gscale, float hscale) {
+                                                     float tval, const float* __restrict__ wt, int64_t rows, int C,
+                                                     int ldp, int ldt, float a, float b, float* __restrict__ sums,
+                                                     TP* __restrict__ grad, const float* __restrict__ gscale,
+                                                     float hscale) {
   __shared__ float sh[NT / 64];
   const int ldg = ldp;
   const int64_t total = rows * ldg;
@@ -82,6 +84,10 @@ __global__ __launch_bounds__(NT) void pw_loss_kernel(int kind, const TP* __restr
     const float t = tgt ? ldv<TT>(tgt, r * ldt + c) : tval;
     float l, g, pos;
     pw_eval(kind, p, t, a, b, l, g, pos);
+    if (wt) {
+      const float w = wt[r * ldt + c];
+      l *= w; g *= w;
+    }
     ls += l; ps += pos;
     if (grad) stv<TP>(grad, i, g * sc);
   }
@@ -96,24 +102,25 @@ __global__ __launch_bounds__(NT) void pw_loss_kernel(int kind, const TP* __restr
 }
 
 template <typename TP, typename TT>
-void launch(int kind, const void* pred, const void* tgt, float tval, int64_t rows, int C, int ldp, int ldt, float a,
-            float b, float* sums, void* grad, const float* gscale, float hscale, hipStream_t st) {
+void launch(int kind, const void* pred, const void* tgt, float tval, const float* wt, int64_t rows, int C, int ldp,
+            int ldt, float a, float b, float* sums, void* grad, const float* gscale, float hscale, hipStream_t st) {
   const int64_t total = rows * ldp;
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((total + NT - 1) / NT, 2048));
-  pw_loss_kernel<TP, TT><<<blocks, NT, 0, st>>>(kind, (const TP*)pred, (const TT*)tgt, tval, rows, C, ldp, ldt, a, b,
-                                                sums, (TP*)grad, gscale, hscale);
+  pw_loss_kernel<TP, TT><<<blocks, NT, 0, st>>>(kind, (const TP*)pred, (const TT*)tgt, tval, wt, rows, C, ldp, ldt, a,
+                                                b, sums, (TP*)grad, gscale, hscale);
 }
 }  // namespace
 
-// tgt_type: 0 fp32, 1 bf16, 2 scalar (tval)
-void dv_pw_loss(int kind, const void* pred, int pred_bf16, const void* tgt, int tgt_type, float tval, int64_t rows,
-                int C, int ldp, int ldt, float a, float b, float* sums, void* grad, const float* gscale, float hscale,
-                hipStream_t st) {
+// tgt_type: 0 fp32, 1 bf16, 2 scalar (tval). wt: optional fp32 per-element weight in the target's layout.
+void dv_pw_loss(int kind, const void* pred, int pred_bf16, const void* tgt, int tgt_type, float tval, const float* wt,
+                int64_t rows, int C, int ldp, int ldt, float a, float b, float* sums, void* grad, const float* gscale,
+                float hscale, hipStream_t st) {
+  const void* t = tgt_type == 2 ? nullptr : tgt;
   if (pred_bf16) {
-    if (tgt_type == 1) launch<u16, u16>(kind, pred, tgt, tval, rows, C, ldp, ldt, a, b, sums, grad, gscale, hscale, st);
-    else launch<u16, float>(kind, pred, tgt_type == 2 ? nullptr : tgt, tval, rows, C, ldp, ldt, a, b, sums, grad, gscale, hscale, st);
+    if (tgt_type == 1) launch<u16, u16>(kind, pred, t, tval, wt, rows, C, ldp, ldt, a, b, sums, grad, gscale, hscale, st);
+    else launch<u16, float>(kind, pred, t, tval, wt, rows, C, ldp, ldt, a, b, sums, grad, gscale, hscale, st);
   } else {
-    if (tgt_type == 1) launch<float, u16>(kind, pred, tgt, tval, rows, C, ldp, ldt, a, b, sums, grad, gscale, hscale, st);
-    else launch<float, float>(kind, pred, tgt_type == 2 ? nullptr : tgt, tval, rows, C, ldp, ldt, a, b, sums, grad, gscale, hscale, st);
+    if (tgt_type == 1) launch<float, u16>(kind, pred, t, tval, wt, rows, C, ldp, ldt, a, b, sums, grad, gscale, hscale, st);
+    else launch<float, float>(kind, pred, t, tval, wt, rows, C, ldp, ldt, a, b, sums, grad, gscale, hscale, st);
   }
 }

@@ -46,7 +46,7 @@ def _torch_lib() -> str:
 def _sources():
     out = []
     for f in sorted(os.listdir(CSRC)):
-        if f.endswith((".hip", ".cpp")):
+        if f.endswith((".hip", ".cpp")) and os.path.isfile(os.path.join(CSRC, f)):
             out.append(os.path.join(CSRC, f))
     return out
 
@@ -106,6 +106,33 @@ def build(force: bool = False, jobs: int | None = None, debug: bool = False, ver
     return out
 
 
+def io_ext_path() -> str:
+    return os.path.join(PKG, "_io" + _ext_suffix())
+
+
+def build_host(force: bool = False, verbose: bool = True) -> str:
+    """Host-only native runtime (csrc/host/*.cpp -> deep_vision_amd._io): g++, SSE4.2 CRC32C."""
+    import pybind11
+
+    srcs = sorted(os.path.join(CSRC, "host", f) for f in os.listdir(os.path.join(CSRC, "host")) if f.endswith(".cpp"))
+    out = io_ext_path()
+    if not force and os.path.exists(out) and all(os.path.getmtime(s) <= os.path.getmtime(out) for s in srcs):
+        return out
+    cmd = ["g++", "-O3", "-msse4.2", "-std=c++17", "-shared", "-fPIC", "-pthread", *srcs, "-o", out,
+           f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"host build failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    if verbose:
+        print(f"[deep_vision_amd] built {out}", flush=True)
+    return out
+
+
+def build_all(force: bool = False, verbose: bool = True) -> None:
+    build(force=force, verbose=verbose)
+    build_host(force=force, verbose=verbose)
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
@@ -113,6 +140,7 @@ def main(argv=None):
     ap.add_argument("--debug", action="store_true")
     a = ap.parse_args(argv)
     build(force=a.force, jobs=a.j, debug=a.debug)
+    build_host(force=a.force)
 
 
 if __name__ == "__main__":

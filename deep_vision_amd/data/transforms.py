@@ -1,0 +1,159 @@
+"""Sample transforms of the PT ImageNet pipeline (R/ResNet/pytorch/data_load.py:72-297), operating
+on ``{'image': HWC uint8 ndarray, 'annotation': int}`` samples like the reference.
+
+The reference decodes with cv2; PIL is used here (cv2 is not part of this stack): bilinear
+resize, RGB order, alpha dropped, grayscale expanded to 3 channels in ToTensor.
+Reference quirks kept for trained-model parity: ``Rescale`` truncates the new size with int();
+``RandomCrop`` draws ``randint(0, h - new_h)`` (exclusive upper bound); ``ToTensor`` does **not**
+divide by 255, so ``Normalize`` with the ImageNet mean/std acts on 0-255 values
+(R/ResNet/pytorch/train.py:315-331); ``ColorJitter`` runs before ToTensor through PIL in a
+random order (A21).
+"""
+from __future__ import annotations
+
+import random
+
+import numpy as np
+import torch
+from PIL import Image, ImageEnhance
+
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+class Compose:
+    def __init__(self, transforms):
+        self.transforms = list(transforms)
+
+    def __call__(self, sample):
+        for t in self.transforms:
+            sample = t(sample)
+        return sample
+
+
+def _resize(image: np.ndarray, new_h: int, new_w: int) -> np.ndarray:
+    return np.asarray(Image.fromarray(image).resize((new_w, new_h), Image.BILINEAR))
+
+
+class Rescale:
+    def __init__(self, output_size):
+        assert isinstance(output_size, (int, tuple))
+        self.output_size = output_size
+
+    def __call__(self, sample):
+        image = sample["image"]
+        h, w = image.shape[:2]
+        if isinstance(self.output_size, int):
+            if h > w:
+                new_h, new_w = self.output_size * h / w, self.output_size
+            else:
+                new_h, new_w = self.output_size, self.output_size * w / h
+        else:
+            new_h, new_w = self.output_size
+        return {**sample, "image": _resize(image, int(new_h), int(new_w))}
+
+
+class RandomHorizontalFlip:
+    def __init__(self, p=0.5):
+        self.p = p
+
+    def __call__(self, sample):
+        if random.random() < self.p:
+            return {**sample, "image": np.ascontiguousarray(np.fliplr(sample["image"]))}
+        return sample
+
+
+def _pair(v):
+    return (v, v) if isinstance(v, int) else tuple(v)
+
+
+class RandomCrop:
+    def __init__(self, output_size):
+        self.output_size = _pair(output_size)
+
+    def __call__(self, sample):
+        image = sample["image"]
+        h, w = image.shape[:2]
+        nh, nw = self.output_size
+        top = np.random.randint(0, h - nh) if h > nh else 0
+        left = np.random.randint(0, w - nw) if w > nw else 0
+        return {**sample, "image": image[top:top + nh, left:left + nw]}
+
+
+class CenterCrop:
+    def __init__(self, output_size):
+        self.output_size = _pair(output_size)
+
+    def __call__(self, sample):
+        image = sample["image"]
+        h, w = image.shape[:2]
+        nh, nw = self.output_size
+        top, left = (h - nh) // 2, (w - nw) // 2
+        return {**sample, "image": image[top:top + nh, left:left + nw]}
+
+
+class ToTensor:
+    """HWC ndarray -> CHW float tensor (values kept in 0-255, like the reference)."""
+
+    def __call__(self, sample):
+        image = sample["image"]
+        if image.ndim == 2:
+            image = np.stack((image,) * 3, axis=-1)
+        return {**sample, "image": torch.from_numpy(np.ascontiguousarray(image.transpose(2, 0, 1))).float()}
+
+
+class Normalize:
+    def __init__(self, mean, std):
+        self.mean = torch.tensor(mean).view(-1, 1, 1)
+        self.std = torch.tensor(std).view(-1, 1, 1)
+
+    def __call__(self, sample):
+        return {**sample, "image": (sample["image"] - self.mean) / self.std}
+
+
+class ColorJitter:
+    """Brightness / contrast / saturation (/ hue) jitter in random order through PIL."""
+
+    def __init__(self, brightness=0, contrast=0, saturation=0, hue=0):
+        self.brightness, self.contrast, self.saturation, self.hue = brightness, contrast, saturation, hue
+
+    @staticmethod
+    def _hue(img, f):
+        h, s, v = img.convert("HSV").split()
+        h = h.point(lambda x: (x + int(f * 255)) % 256)
+        return Image.merge("HSV", (h, s, v)).convert("RGB")
+
+    def get_params(self):
+        ts = []
+        if self.brightness > 0:
+            b = random.uniform(max(0, 1 - self.brightness), 1 + self.brightness)
+            ts.append(lambda im: ImageEnhance.Brightness(im).enhance(b))
+        if self.contrast > 0:
+            c = random.uniform(max(0, 1 - self.contrast), 1 + self.contrast)
+            ts.append(lambda im: ImageEnhance.Contrast(im).enhance(c))
+        if self.saturation > 0:
+            s = random.uniform(max(0, 1 - self.saturation), 1 + self.saturation)
+            ts.append(lambda im: ImageEnhance.Color(im).enhance(s))
+        if self.hue > 0:
+            hf = random.uniform(-self.hue, self.hue)
+            ts.append(lambda im: self._hue(im, hf))
+        random.shuffle(ts)
+        return ts
+
+    def __call__(self, sample):
+        image = Image.fromarray(sample["image"], mode="RGB")
+        for t in self.get_params():
+            image = t(image)
+        return {**sample, "image": np.asarray(image)}
+
+
+def imagenet_train_transform():
+    """R/ResNet/pytorch/train.py:315-324."""
+    return Compose([Rescale(256), RandomHorizontalFlip(0.5), RandomCrop(224),
+                    ColorJitter(brightness=0.2, contrast=0.2, saturation=0.2, hue=0), ToTensor(),
+                    Normalize(IMAGENET_MEAN, IMAGENET_STD)])
+
+
+def imagenet_val_transform():
+    """R/ResNet/pytorch/train.py:326-331."""
+    return Compose([Rescale(256), CenterCrop(224), ToTensor(), Normalize(IMAGENET_MEAN, IMAGENET_STD)])

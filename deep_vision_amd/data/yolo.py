@@ -89,3 +89,78 @@ def synthetic_sample(rng, num_classes=80, size=416, max_boxes=8):
     classes = rng.integers(0, num_classes, k)
     img = rng.uniform(-1, 1, (3, size, size)).astype(np.float32)
     return img, boxes, classes
+
+
+# ------------------------------------------------------------------ datasets
+def decode_image(encoded: bytes) -> np.ndarray:
+    import io
+
+    from PIL import Image
+
+    with Image.open(io.BytesIO(encoded)) as im:
+        return np.asarray(im.convert("RGB"))
+
+
+def resize(image: np.ndarray, size) -> np.ndarray:
+    from PIL import Image
+
+    return np.asarray(Image.fromarray(image).resize((size[1], size[0]), Image.BILINEAR))
+
+
+class YoloTFRecordDataset:
+    """COCO / VOC TFRecords (schema of R/Datasets/MSCOCO/tfrecords.py:37-100) -> (image CHW float32 in
+    [-1, 1], (y_small, y_medium, y_large)) exactly as Preprocessor.__call__ (preprocess.py:13-35):
+    decode, random flip and box-preserving crop when training, resize to 416, /127.5 - 1, encode."""
+
+    def __init__(self, files, is_train, num_classes=80, output_shape=(416, 416), seed=0):
+        from .tfrecord import TFRecordIndex
+
+        self.index = TFRecordIndex(files)
+        self.is_train = is_train
+        self.num_classes = num_classes
+        self.output_shape = tuple(output_shape)
+        self.seed = seed
+        self.grids = tuple(output_shape[0] // s for s in (8, 16, 32))
+
+    def __len__(self):
+        return len(self.index)
+
+    def __getitem__(self, i):
+        from .tfrecord import decode_example, example_values
+
+        ex = decode_example(self.index[i])
+        image = decode_image(example_values(ex, "image/encoded")[0])
+        classes = np.asarray(example_values(ex, "image/object/class/label", []), np.int64)
+        boxes = np.stack([np.asarray(example_values(ex, f"image/object/bbox/{k}", []), np.float32)
+                          for k in ("xmin", "ymin", "xmax", "ymax")], 1) if len(classes) else np.zeros((0, 4), np.float32)
+        if self.is_train:
+            rng = np.random.default_rng((self.seed, i, np.random.randint(1 << 30)))
+            image, boxes = random_flip(image, boxes, rng)
+            image, boxes = random_crop(image, boxes, rng)
+        image = resize(image, self.output_shape).astype(np.float32) / 127.5 - 1
+        labels = encode_labels(boxes, classes, self.num_classes, self.grids)
+        return np.ascontiguousarray(image.transpose(2, 0, 1)), labels
+
+
+class SyntheticYoloDataset:
+    """Random images + random ground truth of the training shapes (--synthetic)."""
+
+    def __init__(self, n=64, num_classes=80, size=416, seed=0):
+        self.n, self.num_classes, self.size, self.seed = n, num_classes, size, seed
+        self.grids = tuple(size // s for s in (8, 16, 32))
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        rng = np.random.default_rng((self.seed, i))
+        img, boxes, classes = synthetic_sample(rng, self.num_classes, self.size)
+        return img, encode_labels(boxes, classes, self.num_classes, self.grids)
+
+
+def collate(batch):
+    import torch
+
+    imgs = torch.from_numpy(np.stack([b[0] for b in batch]))
+    labels = tuple(torch.from_numpy(np.stack([b[1][k] for b in batch])) for k in range(3))
+    return imgs, labels

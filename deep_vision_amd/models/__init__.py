@@ -3,6 +3,7 @@ from .classic import VGG16, VGG19, AlexNetV1, AlexNetV2, AlexNetV2TF, LeNet5, Le
 from .inception import InceptionV1, InceptionV3  # noqa: F401
 from .mobilenet import MobileNetV1, MobileNetV1TF, ShuffleNetV1  # noqa: F401
 from .resnet import ResNet34, ResNet50, ResNet152  # noqa: F401
+from .resnet_tf import ResNet50TF, ResNet50V2, ResNet152TF  # noqa: F401
 from .yolov3 import YoloV3, Darknet53  # noqa: F401
 from .hourglass import StackedHourglassNetwork  # noqa: F401
 from .centernet import ObjectsAsPoints  # noqa: F401
@@ -25,6 +26,9 @@ MODELS = {
     "mobilenet1": MobileNetV1,
     "mobilenet1_tf": MobileNetV1TF,
     "shufflenet1": ShuffleNetV1,
+    "resnet50_tf": ResNet50TF,
+    "resnet152_tf": ResNet152TF,
+    "resnet50v2_tf": ResNet50V2,
     "yolov3": YoloV3,
     "darknet53": Darknet53,
     "hourglass104": StackedHourglassNetwork,
@@ -33,6 +37,8 @@ MODELS = {
     "dcgan_discriminator": DCGANDiscriminator,
     "cyclegan_generator": CycleGANGenerator,
     "cyclegan_discriminator": CycleGANDiscriminator,
+    "dcgan": dcgan,
+    "cyclegan": cyclegan,
 }
 
 

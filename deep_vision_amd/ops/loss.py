@@ -82,7 +82,7 @@ def _match_target(t, pred):
 
 class _PWLossFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, pred, target, tval, kind, a, b, norm):
+    def forward(ctx, pred, target, tval, kind, a, b, norm, weight=None):
         rows, C, ld = _rows(pred)
         dev = pred.device
         sums = torch.zeros(2, dtype=F32, device=dev)
@@ -90,19 +90,21 @@ class _PWLossFn(torch.autograd.Function):
             target, ttype = _match_target(target, pred)
         else:
             ttype = 2
-        lib().pw_loss(kind, ptr(pred), int(pred.dtype == BF16), ptr(target), ttype, float(tval), rows, C, ld, C, a, b,
-                      ptr(sums), 0, 0, 1.0, stream_handle())
+        if weight is not None:
+            weight = _match_target(weight.float(), pred)[0]
+        lib().pw_loss(kind, ptr(pred), int(pred.dtype == BF16), ptr(target), ttype, float(tval), ptr(weight), rows, C,
+                      ld, C, a, b, ptr(sums), 0, 0, 1.0, stream_handle())
         if kind == _KINDS["focal"]:
             scale = 1.0 / sums[1].clamp(min=1.0)
         else:
             scale = torch.full((), norm, dtype=F32, device=dev)
-        ctx.save_for_backward(pred, target, scale)
+        ctx.save_for_backward(pred, target, scale, weight)
         ctx.cfg = (tval, kind, a, b, ttype)
         return sums[0] * scale
 
     @staticmethod
     def backward(ctx, gout):
-        pred, target, scale = ctx.saved_tensors
+        pred, target, scale, weight = ctx.saved_tensors
         tval, kind, a, b, ttype = ctx.cfg
         rows, C, ld = _rows(pred)
         gs = (gout.float() * scale).reshape(1).contiguous()
@@ -112,19 +114,22 @@ class _PWLossFn(torch.autograd.Function):
             grad = empty_nhwc(*pred.shape, pred.device)
         else:
             grad = torch.empty_like(pred)
-        lib().pw_loss(kind, ptr(pred), int(pred.dtype == BF16), ptr(target), ttype, float(tval), rows, C, ld, C, a, b,
-                      0, ptr(grad), ptr(gs), 1.0, stream_handle())
-        return grad, None, None, None, None, None, None
+        lib().pw_loss(kind, ptr(pred), int(pred.dtype == BF16), ptr(target), ttype, float(tval), ptr(weight), rows, C,
+                      ld, C, a, b, 0, ptr(grad), ptr(gs), 1.0, stream_handle())
+        return grad, None, None, None, None, None, None, None
 
 
-def _pw(pred, target, kind, a=0.0, b=0.0, reduction="mean"):
+def _pw(pred, target, kind, a=0.0, b=0.0, reduction="mean", weight=None, norm=None):
     if isinstance(target, (int, float)):
         tval, target_t = float(target), None
     else:
         tval, target_t = 0.0, target
+    if weight is not None and target_t is None:
+        target_t = torch.full(pred.shape, tval, dtype=F32, device=pred.device)
     pred = _native_pred(pred)
-    norm = 1.0 / pred.numel() if reduction == "mean" else 1.0
-    return _PWLossFn.apply(pred, target_t, tval, _KINDS[kind], float(a), float(b), norm)
+    if norm is None:
+        norm = 1.0 / pred.numel() if reduction == "mean" else 1.0
+    return _PWLossFn.apply(pred, target_t, tval, _KINDS[kind], float(a), float(b), norm, weight)
 
 
 def _full_like(t, v):
@@ -174,3 +179,12 @@ def focal_loss(logits, target, alpha=2.0, beta=4.0):
         ln = -((1 - t) ** beta) * p ** alpha * torch.log(1 - p) * (1 - pos)
         return (lp.sum() + ln.sum()) / pos.sum().clamp(min=1)
     return _pw(logits, target, "focal", a=alpha, b=beta, reduction="sum")
+
+
+def masked_l1(pred, target, mask, num=None):
+    """sum(|p - t| * mask) / max(num, 1) -- CenterNet size / offset regression at object centres
+    (``mask`` in the target's shape; ``num`` a host count, default ``mask.sum()`` synced)."""
+    n = float(max(1.0, float(mask.sum()) if num is None else num))
+    if not native(pred):
+        return ((pred.float() - target.float()).abs() * mask.float()).sum() / n
+    return _pw(pred, target, "l1", weight=mask, norm=1.0 / n)

@@ -113,6 +113,11 @@ class DataParallel(torch.nn.Module):
         self._reset()
         return self.module(*args, **kw)
 
+    def prepare(self):
+        """Arm the buckets for a backward pass when submodules are called directly instead of
+        through ``forward`` (multi-network steps, e.g. CycleGAN's generator pair)."""
+        self._reset()
+
     @contextlib.contextmanager
     def no_sync(self):
         """Gradient accumulation without communication (grads accumulate in the flat buffer)."""

@@ -1,0 +1,243 @@
+"""Supervised classification trainer (PT ImageNet / MNIST trainers E1-E3, TF1-Keras E4/E5, the
+MobileNet TF2 skeleton E6 made runnable).
+
+Same control flow and stdout protocol as R/ResNet/pytorch/train.py:310-538:
+``validate(epoch 0)`` then per epoch ``train`` -> ``validate`` -> scheduler step (Plateau on
+validation top-1, or on val_loss for the Keras configs) -> full checkpoint
+``{name}-{ts}-epoch-{e}.pt``; every 10 batches
+``Time, {ts}, Epoch: {e}, Batch: {b}, Training Loss: {avg10}, LR: {lr}``; after validation
+``Epoch: {e}, Validation Top 1 acc: ...`` / ``Top 5 acc`` / ``Set Loss``.
+
+MI355X-first differences: one process per GPU (global batch split across ranks, bucketed RCCL
+all-reduce overlapped with backward), losses accumulate on the device and are read every 10
+batches only, the 10-batch loss and validation sums are all-reduced in one packed
+collective, Inception's auxiliary heads are trained with the GoogLeNet 0.3 weighting (A3).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import time
+
+import torch
+
+from .. import ops as F
+from ..config import TrainConfig, get_config
+from ..data import transforms as T
+from ..data.datasets import ImageNet2012Dataset, MnistDataset, SyntheticClassification
+from ..data.loader import DevicePrefetcher, make_loader, set_epoch
+from . import checkpoint as C
+from .engine import Engine, seed_everything
+from .schedulers import make_scheduler, plateau_metric
+
+
+def accuracy(output, target, topk=(1,)):
+    """R/ResNet/pytorch/train.py:524-538 (pytorch/examples): percent correct in the top k."""
+    with torch.no_grad():
+        maxk = max(topk)
+        batch = target.size(0)
+        _, pred = output.float().topk(maxk, 1, True, True)
+        pred = pred.t()
+        correct = pred.eq(target.view(1, -1).expand_as(pred))
+        return [correct[:k].reshape(-1).float().sum(0, keepdim=True).mul_(100.0 / batch) for k in topk]
+
+
+def model_summary(model, input_shape) -> str:
+    """A torchsummary-like header: parameter counts (trainable / total incl. BN statistics)."""
+    n = sum(p.numel() for p in model.parameters())
+    nt = sum(p.numel() for p in model.parameters() if p.requires_grad)
+    nb = sum(b.numel() for k, b in model.named_buffers() if "running" in k)
+    return (f"Model: {type(model).__name__}  input: {tuple(input_shape)}\n"
+            f"Total params: {n + nb:,}\nTrainable params: {nt:,}\nNon-trainable params: {n + nb - nt:,}")
+
+
+def _label_key(cfg):
+    return "label" if cfg.dataset == "mnist" else "annotation"
+
+
+def build_datasets(cfg: TrainConfig, data_dir=None, synthetic=False, synthetic_size=512, num_classes=None):
+    key = _label_key(cfg)
+    nc = num_classes or (10 if cfg.dataset == "mnist" else 1000)
+    if cfg.dataset == "mnist":
+        root = data_dir or "../dataset"
+        mk = lambda split: MnistDataset(os.path.join(root, f"{split}-images-idx3-ubyte"),  # noqa: E731
+                                        os.path.join(root, f"{split}-labels-idx1-ubyte"),
+                                        synthetic_images=True,
+                                        scale=255.0 if cfg.extras.get("scale_only") else 1.0,
+                                        mean=(0.0,) if cfg.extras.get("scale_only") else (0.1307,),
+                                        std=(1.0,) if cfg.extras.get("scale_only") else (0.3081,))
+        if synthetic or not os.path.exists(os.path.join(root, "train-labels-idx1-ubyte")):
+            return (SyntheticClassification(synthetic_size, cfg.input_shape, nc, key, seed=1),
+                    SyntheticClassification(max(64, synthetic_size // 4), cfg.input_shape, nc, key, seed=2))
+        return mk("train"), mk("t10k")
+    if cfg.dataset == "imagenet" and not synthetic:
+        root = data_dir or "../dataset"
+        labels = os.path.join(root, "synsets.txt")
+        tr, va = os.path.join(root, "train_flatten"), os.path.join(root, "val_flatten")
+        if os.path.isdir(tr) and os.path.isfile(labels):
+            return (ImageNet2012Dataset(tr, labels, T.imagenet_train_transform()),
+                    ImageNet2012Dataset(va, labels, T.imagenet_val_transform()))
+    return (SyntheticClassification(synthetic_size, cfg.input_shape, nc, key, seed=1),
+            SyntheticClassification(max(64, synthetic_size // 4), cfg.input_shape, nc, key, seed=2))
+
+
+def _criterion(output, target, aux_weight):
+    if isinstance(output, tuple):  # Inception V1 train mode: (main, aux1, aux2)
+        main, *aux = output
+        loss = F.cross_entropy(main, target)
+        for a in aux:
+            loss = loss + aux_weight * F.cross_entropy(a, target)
+        return loss, main
+    return F.cross_entropy(output, target), output
+
+
+def train(loader, net, optimizer, epoch, loggers, eng: Engine, cfg: TrainConfig, max_steps=None, scheduler=None):
+    net.train()
+    key = _label_key(cfg)
+    aux_w = cfg.extras.get("aux_weight", 0.3)
+    eng.log("Start training epoch {}".format(epoch))
+    acc = torch.zeros((), device=eng.device)
+    seen = 0
+    for batch_i, data in enumerate(loader):
+        if max_steps is not None and batch_i >= max_steps:
+            break
+        image = data["image"].to(eng.device, non_blocking=True)
+        target = data[key].to(eng.device, dtype=torch.long, non_blocking=True)
+        with eng.timer.step(samples=image.shape[0]):
+            with eng.timer.phase("fwd"):
+                loss, _ = _criterion(net(image), target, aux_w)
+            lr = C.get_lr(optimizer)
+            eng.backward_step(loss, net, optimizer)
+        acc += loss.detach().float()
+        seen += 1
+        if batch_i % 10 == 9:
+            avg = eng.reduce_sum([acc.item() / 10.0])[0] / eng.world
+            eng.log("Time, {}, Epoch: {}, Batch: {}, Training Loss: {}, LR: {}".format(
+                C.timestamp(), epoch, batch_i + 1, avg, lr))
+            C.log_metrics(loggers, "train_loss", avg, epoch)
+            acc.zero_()
+    return seen
+
+
+def validate(loader, net, epoch, loggers, eng: Engine, cfg: TrainConfig, max_steps=None):
+    net.eval()
+    key = _label_key(cfg)
+    tot = torch.zeros(6, dtype=torch.float64, device=eng.device)  # loss, top1, top5 (per-batch sums), n, c1, c5
+    nbatches = 0
+    with torch.no_grad():
+        for batch_i, data in enumerate(loader):
+            if max_steps is not None and batch_i >= max_steps:
+                break
+            image = data["image"].to(eng.device, non_blocking=True)
+            target = data[key].to(eng.device, dtype=torch.long, non_blocking=True)
+            out = net(image)
+            out = out[0] if isinstance(out, tuple) else out
+            loss = F.cross_entropy(out, target)
+            a1, a5 = accuracy(out, target, topk=(1, min(5, out.shape[1])))
+            n = target.numel()
+            nbatches += 1
+            tot += torch.stack([loss.double(), a1[0].double(), a5[0].double(), torch.tensor(float(n), device=eng.device,
+                                dtype=torch.float64), a1[0].double() * n / 100, a5[0].double() * n / 100])
+    vals = eng.reduce_sum(tot.tolist() + [nbatches])
+    nb = max(1, vals[6])
+    val_loss, top1, top5 = vals[0] / nb, vals[1] / nb, vals[2] / nb  # per-batch average
+    eng.log("Epoch: {}, Validation Top 1 acc: {}".format(epoch, top1))
+    eng.log("Epoch: {}, Validation Top 5 acc: {}".format(epoch, top5))
+    eng.log("Epoch: {}, Validation Set Loss: {}".format(epoch, val_loss))
+    if vals[3] > 0:
+        eng.log("Epoch: {}, Validation exact Top 1 acc: {} ({} samples)".format(epoch, 100 * vals[4] / vals[3],
+                                                                                  int(vals[3])))
+    C.log_metrics(loggers, "val_top1_acc", top1, epoch)
+    C.log_metrics(loggers, "val_top5_acc", top5, epoch)
+    C.log_metrics(loggers, "val_loss", val_loss, epoch)
+    return val_loss, top1, top5
+
+
+def run_epochs(config: TrainConfig, checkpoint_path=None, *, device=None, data_dir=None, synthetic=False,
+               epochs=None, max_steps=None, val_steps=None, synthetic_size=512, num_workers=None, seed=0,
+               checkpoint_dir=None, profile=False, batch_size=None):
+    eng = Engine(device=device, profile=profile)
+    seed_everything(seed, eng.rank)
+    eng.log("CUDA is available: {}".format(torch.cuda.is_available()))
+    cfg = config
+    if batch_size is not None:
+        cfg = cfg.replace(batch_size=batch_size)
+    bs = cfg.per_rank_batch(eng.world)
+    train_ds, val_ds = build_datasets(cfg, data_dir, synthetic, synthetic_size)
+    workers = cfg.num_workers if num_workers is None else num_workers
+    train_loader = make_loader(train_ds, bs, shuffle=True, num_workers=workers, seed=seed)
+    val_loader = make_loader(val_ds, bs, shuffle=False, num_workers=workers)
+    model = eng.build_model(cfg.model, **cfg.model_params)
+    eng.log(model_summary(model, cfg.input_shape))
+    net = eng.wrap(model)
+    if eng.world > 1:
+        eng.log("Using {} GPUs!".format(eng.world) if eng.device.type == "cuda" else f"Using {eng.world} ranks (gloo)")
+    optimizer = eng.optimizer(cfg.optimizer, net.parameters(), cfg.optimizer_params)
+    scheduler = make_scheduler(cfg.scheduler, optimizer, cfg.scheduler_params)
+    loggers = C.initialize_loggers()
+    model_dir = checkpoint_dir or cfg.checkpoint_dir
+    model_id = time.strftime("%Y-%m-%dT%H:%M:%S", time.localtime())
+    start_epoch = 1
+    if checkpoint_path is not None:
+        net, optimizer, scheduler, loggers, start_epoch = C.load_checkpoint(checkpoint_path, net, optimizer, scheduler,
+                                                                            loggers)
+    device_loader = DevicePrefetcher(train_loader, eng.device)
+    validate(val_loader, net, 0, loggers, eng, cfg, val_steps)
+    total = epochs if epochs is not None else cfg.total_epochs
+    last = None
+    for epoch in range(start_epoch, total + 1):
+        set_epoch(train_loader, epoch)
+        train(device_loader, net, optimizer, epoch, loggers, eng, cfg, max_steps)
+        val_loss, top1, top5 = validate(val_loader, net, epoch, loggers, eng, cfg, val_steps)
+        if isinstance(scheduler, torch.optim.lr_scheduler.ReduceLROnPlateau):
+            scheduler.step(val_loss if plateau_metric(cfg.scheduler_params) == "val_loss" else top1)
+        elif scheduler is not None:
+            scheduler.step()
+        path = os.path.join(model_dir, C.classifier_checkpoint_name(cfg.name, model_id, epoch))
+        last = C.atomic_save(C.training_state(epoch, net, optimizer, scheduler, loggers, config=cfg.name), path)
+        if eng.timer.enabled:
+            eng.log("[dv-profile] epoch {}: {}".format(epoch, eng.timer.summary()))
+            eng.timer.reset()
+    eng.barrier()
+    eng.close()
+    return last, loggers
+
+
+def add_common_args(ap: argparse.ArgumentParser):
+    ap.add_argument("-c", "--checkpoint", default=None, help="checkpoint to resume from ('latest' scans the dir)")
+    ap.add_argument("--synthetic", action="store_true", help="synthetic data of the configured shape")
+    ap.add_argument("--synthetic-size", type=int, default=512)
+    ap.add_argument("--data-dir", default=None)
+    ap.add_argument("--epochs", type=int, default=None, help="override total_epochs")
+    ap.add_argument("--max-steps", type=int, default=None, help="batches per epoch (smoke runs)")
+    ap.add_argument("--val-steps", type=int, default=None)
+    ap.add_argument("--batch-size", type=int, default=None, help="override the configured batch")
+    ap.add_argument("--workers", type=int, default=None)
+    ap.add_argument("--device", default=None, help="cuda | cpu (default: cuda when available)")
+    ap.add_argument("--checkpoint-dir", default=None)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--profile", action="store_true", help="per-phase HIP-event step timing")
+    ap.add_argument("--nproc", type=int, default=None, help="spawn N ranks (one per GPU) via torch.distributed.run")
+    return ap
+
+
+def resolve_checkpoint(arg, cfg, checkpoint_dir=None):
+    if arg == "latest":
+        return C.latest(checkpoint_dir or cfg.checkpoint_dir, f"{cfg.name}-*.pt")
+    return arg
+
+
+def main(argv=None, choices=None, default=None):
+    """``train.py -m <model> [-c <checkpoint>]`` (R/ResNet/pytorch/train.py:541-562)."""
+    from ..launch import maybe_spawn
+
+    ap = argparse.ArgumentParser(description="deep_vision_amd classification trainer")
+    ap.add_argument("-m", "--model", choices=choices, default=default, required=default is None)
+    add_common_args(ap)
+    a = ap.parse_args(argv)
+    maybe_spawn(a.nproc)
+    cfg = get_config(a.model)
+    ck = resolve_checkpoint(a.checkpoint, cfg, a.checkpoint_dir)
+    run_epochs(cfg, ck, device=a.device, data_dir=a.data_dir, synthetic=a.synthetic, epochs=a.epochs,
+               max_steps=a.max_steps, val_steps=a.val_steps, synthetic_size=a.synthetic_size, num_workers=a.workers,
+               seed=a.seed, checkpoint_dir=a.checkpoint_dir, profile=a.profile, batch_size=a.batch_size)

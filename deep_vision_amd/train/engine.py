@@ -1,0 +1,122 @@
+"""Shared training runtime of every family trainer (replaces DataParallel / MirroredStrategy glue).
+
+``Engine`` owns: the process group (one rank per GPU, RCCL; gloo on CPU), the device, the model
+(optionally wrapped in parallel.DataParallel -- bucketed RCCL all-reduce overlapped with
+backward), the fused flat-buffer optimizer, the optimizer step with the 1/world averaging fused
+in, the non-finite guard, the fault injector, the watchdog heartbeat and the step timer.
+
+Loss scaling follows the reference per family: PT classifiers average over the *local* batch
+(``nn.CrossEntropyLoss`` mean; DataParallel computed it over the global batch on GPU0, which
+equals the mean of per-rank means for equal shards), TF2 loops sum per-example losses and
+divide by the *global* batch (MirroredStrategy) -- ``Engine.world`` and
+``TrainConfig.global_batch`` give both.
+"""
+from __future__ import annotations
+
+import os
+import random
+
+import numpy as np
+import torch
+
+from .. import models as M
+from ..parallel import dist as D
+from ..parallel.ddp import DataParallel
+from ..profiling import StepTimer
+from ..utils.fault import FaultInjector, NonFiniteGuard, Watchdog
+from .optim import FusedAdam, FusedRMSprop, FusedSGD
+
+OPTIMIZERS = {"sgd": FusedSGD, "adam": FusedAdam, "rmsprop": FusedRMSprop}
+
+
+def seed_everything(seed: int, rank: int = 0):
+    random.seed(seed + rank)
+    np.random.seed(seed + rank)
+    torch.manual_seed(seed + rank)
+
+
+def make_optimizer(name, params, kw):
+    kw = dict(kw)
+    if "betas" in kw:
+        kw["betas"] = tuple(kw["betas"])
+    return OPTIMIZERS[name](params, **kw)
+
+
+class Engine:
+    def __init__(self, device: str | None = None, backend: str | None = None, bucket_mb: float = 64.0,
+                 log_every: int = 10, watchdog_s: float | None = None, profile: bool = False):
+        if device == "cpu":
+            backend = backend or "gloo"
+        self.world, self.rank, self.local_rank, dev = D.init_distributed(backend)
+        self.device = torch.device(device) if device and device != "cuda" else dev
+        self.bucket_mb = bucket_mb
+        self.is_main = self.rank == 0
+        self.guard = NonFiniteGuard(every=log_every)
+        self.faults = FaultInjector(rank=self.rank)
+        self.timer = StepTimer(enabled=profile)
+        wd = float(os.environ.get("DV_WATCHDOG_S", watchdog_s or 0))
+        self.watchdog = Watchdog(wd).start() if wd > 0 else None
+        self.step_count = 0
+
+    def log(self, *a, **kw):
+        if self.is_main:
+            print(*a, **kw, flush=True)
+
+    # ---------------- model / optimizer ----------------
+    def build_model(self, name, **kw):
+        return M.get_model(name, **kw)
+
+    def wrap(self, model: torch.nn.Module) -> torch.nn.Module:
+        model = model.to(self.device)
+        if self.world > 1:
+            return DataParallel(model, bucket_mb=self.bucket_mb)
+        return model
+
+    @staticmethod
+    def unwrap(model):
+        return model.module if isinstance(model, DataParallel) else model
+
+    def optimizer(self, name, params, kw):
+        return make_optimizer(name, params, kw)
+
+    # ---------------- one optimisation step ----------------
+    def backward_step(self, loss, model, optimizer, zero_grad=True):
+        """backward -> all-reduce completion -> (guarded) fused optimizer step. Returns False when
+        the step was skipped because the loss / gradients were not finite."""
+        self.step_count += 1
+        s = self.step_count
+        self.faults.process(s)
+        loss = self.faults.loss(loss, s)
+        if zero_grad:
+            optimizer.zero_grad()
+        with self.timer.phase("bwd"):
+            loss.backward()
+        flat = optimizer.flat_grads() if hasattr(optimizer, "flat_grads") else None
+        self.faults.grads(flat[0] if flat else None, s)
+        with self.timer.phase("comm"):
+            if isinstance(model, DataParallel):
+                model.finish()
+        ok = True
+        if self.guard.should_check(s):
+            ok = self.guard.ok(loss, flat[0] if flat else None)
+        if ok:
+            with self.timer.phase("opt"):
+                gs = model.grad_scale if isinstance(model, DataParallel) else 1.0
+                optimizer.step(grad_scale=gs)
+        else:
+            optimizer.zero_grad()
+            self.log(f"[dv] non-finite loss/gradients at step {s}: step skipped ({self.guard.skipped} so far)")
+        if self.watchdog is not None:
+            self.watchdog.beat()
+        return ok
+
+    def reduce_sum(self, values):
+        return D.all_reduce_scalars(list(values), device=self.device if self.device.type == "cuda" else "cpu")
+
+    def barrier(self):
+        D.barrier()
+
+    def close(self):
+        if self.watchdog is not None:
+            self.watchdog.stop()
+        D.destroy()

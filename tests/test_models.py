@@ -38,7 +38,8 @@ PINNED = {
     "cyclegan_discriminator": 2_765_633,
 }
 
-TOTAL_WITH_BN_STATS = {"yolov3": 62_001_757, "centernet": 94_654_504}  # Keras "Total params"
+# Keras "Total params" (trainable + BN moving statistics); resnet50v2_tf = keras-applications ResNet50V2
+TOTAL_WITH_BN_STATS = {"yolov3": 62_001_757, "centernet": 94_654_504, "resnet50v2_tf": 25_613_800}
 
 
 def nparams(m):
