@@ -111,13 +111,15 @@ class _DropoutFn(torch.autograd.Function):
     def forward(ctx, x, p, seed):
         y = torch.empty_like(x)
         lib().dropout(ptr(x), ptr(y), x.numel(), float(p), seed, stream_handle())
-        ctx.cfg = (p, seed)
+        ctx.cfg = (p, seed, x.stride())
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        p, seed = ctx.cfg
+        p, seed, stride = ctx.cfg
         dy = _prep(dy)
+        if dy.stride() != stride:  # the mask is indexed by flat position: match the forward layout
+            dy = torch.empty_strided(dy.shape, stride, dtype=dy.dtype, device=dy.device).copy_(dy)
         dx = torch.empty_like(dy)
         lib().dropout(ptr(dy), ptr(dx), dy.numel(), float(p), seed, stream_handle())  # same mask
         return dx, None, None

@@ -104,6 +104,33 @@ def grad_nhwc(g: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def like_layout(t: torch.Tensor, ref: torch.Tensor) -> torch.Tensor:
+    """``t`` (same logical shape as the NHWC tensor ``ref``) in exactly ``ref``'s physical layout,
+    copying when needed. Elementwise kernels that walk two tensors as flat arrays (activation
+    backward: dY against the saved Y) need identical strides -- an incoming gradient can be a
+    channel slice of a concat (Inception / YOLO route), whose pixel stride is the concat width."""
+    if t.dtype == ref.dtype and t.stride() == ref.stride() and t.shape == ref.shape:
+        return t
+    out = empty_layout(ref)
+    out.copy_(t)
+    return out
+
+
+def empty_layout(ref: torch.Tensor) -> torch.Tensor:
+    """Uninitialised tensor with ``ref``'s NHWC layout (a dense channels_last tensor, or an
+    ``empty_nhwc`` padded view whose whole padded buffer is allocated and zero-padded)."""
+    N, C, H, W = ref.shape
+    if ld_of(ref) == C:
+        return torch.empty_like(ref, memory_format=CL)
+    return empty_nhwc(N, C, H, W, ref.device)
+
+
+def nhwc_numel(t: torch.Tensor) -> int:
+    """Elements spanned by an NHWC tensor including channel padding (flat kernel length)."""
+    N, C, H, W = t.shape
+    return N * H * W * ld_of(t)
+
+
 # ---------------------------------------------------------------------------------------------
 # Gradient sinks: native backward kernels write parameter gradients straight into the live
 # ``param.grad`` buffer (a view into the flat gradient buffer of parallel.flat / train.optim)

@@ -14,8 +14,8 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as TF
 
-from .common import (ACT_IDS, BF16, CL, F32, alloc_cl, as_nhwc, empty_nhwc, grad_nhwc, grad_sink, ld_of, lib, native,
-                     notify_grad_ready, ptr, round8, stream_handle)
+from .common import (ACT_IDS, BF16, CL, F32, alloc_cl, as_nhwc, empty_nhwc, grad_nhwc, grad_sink, ld_of, lib,
+                     like_layout, empty_layout, native, nhwc_numel, notify_grad_ready, ptr, round8, stream_handle)
 
 STAT_SHARDS = 64
 
@@ -181,9 +181,9 @@ class _ConvFn(torch.autograd.Function):
         stride, padding, dilation, G, act, slope, Cg_x, has_bias = ctx.cfg
         dy = grad_nhwc(dy)
         if act:
-            g = torch.empty_like(dy) if ld_of(dy) == dy.shape[1] else empty_nhwc(*dy.shape, dy.device)
-            n = dy.numel() if ld_of(dy) == dy.shape[1] else dy.shape[0] * dy.shape[2] * dy.shape[3] * ld_of(dy)
-            lib().act_bwd(ptr(dy), ptr(y), ptr(g), n, act, float(slope), stream_handle())
+            dy = like_layout(dy, y)  # the saved output's exact layout (dy may be a concat slice)
+            g = empty_layout(y)
+            lib().act_bwd(ptr(dy), ptr(y), ptr(g), nhwc_numel(y), act, float(slope), stream_handle())
             dy = g
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
@@ -456,8 +456,9 @@ class _DWConvFn(torch.autograd.Function):
         stride, padding, act, slope, has_bias = ctx.cfg
         dy = grad_nhwc(dy)
         if act:
-            g = torch.empty_like(dy)
-            lib().act_bwd(ptr(dy), ptr(y), ptr(g), dy.numel(), act, float(slope), stream_handle())
+            dy = like_layout(dy, y)
+            g = empty_layout(y)
+            lib().act_bwd(ptr(dy), ptr(y), ptr(g), nhwc_numel(y), act, float(slope), stream_handle())
             dy = g
         N, C, H, W = x.shape
         K = weight.shape[2]

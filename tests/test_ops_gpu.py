@@ -359,3 +359,23 @@ def test_grouped_padded_conv():
         yr.backward(dy)
         assert _rel(x.grad, xr.grad) < 3e-2
         assert _rel(w.grad, wr.grad) < 3e-2
+
+
+def test_conv_act_grad_from_concat_slice():
+    """A fused conv+ReLU whose output feeds a channel concat receives a channel-slice gradient
+    (pixel stride = concat width) -- Inception / YOLO routes."""
+    from deep_vision_amd import ops as F
+
+    x32 = torch.randn(2, 32, 9, 9, device=DEV).bfloat16().float()
+    w1 = (torch.randn(24, 32, 1, 1, device=DEV) * 0.2).requires_grad_(True)
+    w2 = (torch.randn(40, 32, 3, 3, device=DEV) * 0.1).requires_grad_(True)
+    x = _nhwc(x32).requires_grad_(True)
+    y = torch.cat([F.conv2d(x, w1, act="relu"), F.conv2d(x, w2, padding=1, act="relu")], 1)
+    g = torch.randn(2, 64, 9, 9, device=DEV)
+    y.backward(_nhwc(g))
+    xr = x32.clone().requires_grad_(True)
+    w1r, w2r = w1.detach().clone().requires_grad_(True), w2.detach().clone().requires_grad_(True)
+    yr = torch.cat([TF.relu(TF.conv2d(xr, w1r)), TF.relu(TF.conv2d(xr, w2r, padding=1))], 1)
+    yr.backward(g)
+    assert _cos(x.grad, xr.grad) > 0.999
+    assert _cos(w1.grad, w1r.grad) > 0.999 and _cos(w2.grad, w2r.grad) > 0.999
