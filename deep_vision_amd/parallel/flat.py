@@ -22,13 +22,14 @@ def flatten_parameters(model: torch.nn.Module, reverse: bool = True):
     gflat = torch.zeros(total, dtype=torch.float32, device=dev)
     off = 0
     layout = []
+    shared = (pflat, gflat)  # one object: the optimizer recognises the layout by identity
     with torch.no_grad():
         for p in order:
             n = p.numel()
             pflat[off:off + n].view_as(p).copy_(p.data)
             p.data = pflat[off:off + n].view(p.shape)
             p.grad = gflat[off:off + n].view(p.shape)
-            p._dv_flat = (pflat, gflat)
+            p._dv_flat = shared
             p._dv_off = off
             layout.append((p, off, n))
             off += n

@@ -44,8 +44,9 @@ class _FlatOptimizer(torch.optim.Optimizer):
         sizes = [p.numel() for p in ps]
         total = sum(sizes)
         shared = getattr(ps[0], "_dv_flat", None)
-        reuse = (shared is not None and all(getattr(p, "_dv_flat", None) is shared for p in ps)
-                 and shared[0].numel() == total)
+        reuse = (shared is not None and shared[0].numel() == total
+                 and all(getattr(p, "_dv_flat", None) is not None and p._dv_flat[0].data_ptr() == shared[0].data_ptr()
+                         for p in ps))
         views, gviews, offs = [], [], []
         if reuse:
             pflat, gflat = shared

@@ -1,0 +1,139 @@
+"""Distributed data parallelism on CPU (gloo, world size 2; SURVEY §7.5 4a/4b semantics).
+
+* DP-2 over half batches == one process over the full batch (BN-free model: identical gradient
+  averaging and identical optimizer updates, incl. the fused 1/world grad scale)
+* bucket bookkeeping: several buckets, every one issued once per step; unused parameters do
+  not deadlock (issued in ``finish``); ``no_sync`` accumulation
+* broadcast of initial parameters from rank 0
+* packed scalar all-reduce
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class Net(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.a = torch.nn.Linear(16, 64)
+        self.b = torch.nn.Linear(64, 64)
+        self.unused = torch.nn.Linear(8, 8)  # never receives a gradient
+        self.c = torch.nn.Linear(64, 4)
+
+    def forward(self, x):
+        return self.c(torch.tanh(self.b(torch.relu(self.a(x)))))
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+
+    from deep_vision_amd.parallel.ddp import DataParallel
+    from deep_vision_amd.parallel.dist import all_reduce_scalars, init_distributed
+    from deep_vision_amd.train.optim import FusedSGD
+
+    init_distributed("gloo")
+    torch.manual_seed(100 + rank)  # different init per rank: broadcast must fix it
+    net = Net()
+    ddp = DataParallel(net, bucket_mb=0.01)  # tiny buckets -> several all-reduces
+    opt = FusedSGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    g = torch.Generator().manual_seed(0)
+    xs = [torch.randn(8, 16, generator=g) for _ in range(3)]
+    ys = [torch.randn(8, 4, generator=g) for _ in range(3)]
+    for x, y in zip(xs, ys):
+        xl, yl = x[rank * 4:(rank + 1) * 4], y[rank * 4:(rank + 1) * 4]
+        opt.zero_grad()
+        loss = ((ddp(xl) - yl) ** 2).mean()
+        loss.backward()
+        ddp.finish()
+        opt.step(grad_scale=ddp.grad_scale)
+    issued = ddp.comm_stats["allreduce_calls"]
+    # no_sync: local accumulation only
+    with ddp.no_sync():
+        opt.zero_grad()
+        ((ddp(xs[0][rank * 4:(rank + 1) * 4]) - ys[0][rank * 4:(rank + 1) * 4]) ** 2).mean().backward()
+        ddp.finish()
+    s = all_reduce_scalars([float(rank + 1)], device="cpu")[0]
+    # numpy copies: pickled by value (tensors would be shared through fds of an exiting process)
+    q.put((rank, {k: v.detach().numpy().copy() for k, v in net.state_dict().items()}, issued, len(ddp.buckets), s,
+           net.a.weight.grad.numpy().copy()))
+    dist.destroy_process_group()
+
+
+def test_ddp_gloo_matches_single_process():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r = q.get(timeout=240)
+        res[r[0]] = r[1:]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sd0, issued, nb, s, _ = res[0]
+    sd1 = res[1][0]
+    sd0 = {k: torch.from_numpy(v) for k, v in sd0.items()}
+    sd1 = {k: torch.from_numpy(v) for k, v in sd1.items()}
+    for k in sd0:
+        assert torch.equal(sd0[k], sd1[k]), k  # replicas stay identical
+    assert nb >= 3 and issued == 3 * nb  # every bucket issued exactly once per step
+    assert s == 3.0
+    # reference: one process, full batch, same (rank-0) initial weights
+    from deep_vision_amd.train.optim import FusedSGD
+
+    torch.manual_seed(100)
+    ref = Net()
+    opt = FusedSGD(ref.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    g = torch.Generator().manual_seed(0)
+    xs = [torch.randn(8, 16, generator=g) for _ in range(3)]
+    ys = [torch.randn(8, 4, generator=g) for _ in range(3)]
+    for x, y in zip(xs, ys):
+        opt.zero_grad()
+        ((ref(x) - y) ** 2).mean().backward()
+        opt.step()
+    for k, v in ref.state_dict().items():
+        assert torch.allclose(sd0[k], v, atol=1e-6, rtol=1e-5), k
+    # no_sync left the two ranks' gradients different (local halves)
+    assert not torch.allclose(torch.from_numpy(res[0][4]), torch.from_numpy(res[1][4]))
+
+
+def _trainer_worker(rank, world, port, tmp, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from deep_vision_amd.config import get_config
+    from deep_vision_amd.train.classification import run_epochs
+
+    last, loggers = run_epochs(get_config("lenet5"), None, device="cpu", synthetic=True, synthetic_size=128,
+                               num_workers=0, checkpoint_dir=tmp + "/", epochs=1, max_steps=3, val_steps=1)
+    q.put((rank, last, loggers["val_loss"]["value"]))
+
+
+def test_classification_trainer_two_ranks(tmp_path):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_trainer_worker, args=(r, world, port, str(tmp_path), q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=300) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][0] is not None and res[1][0] is None  # rank 0 writes the checkpoint
+    assert res[0][1] == pytest.approx(res[1][1])  # validation metrics are all-reduced
