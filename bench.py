@@ -32,7 +32,7 @@ def main():
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--backend", default="native", choices=["native", "torch"],
                     help="torch = PyTorch/MIOpen reference path (for comparison only)")
-    ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--profile-steps", type=int, default=0)
     args = ap.parse_args()
 

@@ -20,8 +20,11 @@ def env_world():
 def init_distributed(backend: str | None = None, timeout_s: int = 600):
     """Initialise the default process group if WORLD_SIZE > 1. Returns (world, rank, local_rank, device)."""
     world, rank, local = env_world()
-    use_cuda = torch.cuda.is_available() and backend != "gloo"
-    device = torch.device(f"cuda:{local}") if use_cuda else torch.device("cpu")
+    backend = backend or os.environ.get("DV_DIST_BACKEND") or None
+    use_cuda = torch.cuda.is_available() and (backend != "gloo" or os.environ.get("DV_DIST_BACKEND") == "gloo")
+    # ranks beyond the visible device count share devices (rehearsing N ranks on fewer GPUs with
+    # DV_DIST_BACKEND=gloo; RCCL itself requires one rank per GPU)
+    device = torch.device(f"cuda:{local % max(1, torch.cuda.device_count())}") if use_cuda else torch.device("cpu")
     if use_cuda:
         torch.cuda.set_device(device)
     if world > 1 and not dist.is_initialized():
