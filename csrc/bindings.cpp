@@ -28,9 +28,10 @@ PYBIND11_MODULE(_C, m) {
 
   m.def("conv_fwd", [](uptr x, uptr w, uptr y, uptr bias, uptr stats, int Nb, int H, int W, int Cg, int ldx, int G,
                        int Kout, int P_, int Q, int R, int S, int sh, int sw, int ph, int pw, int dh, int dw, int tgather,
-                       int OH, int OW, int osh, int osw, int oph, int opw, int ldy, int act, float slope, uptr st) {
+                       int OH, int OW, int osh, int osw, int oph, int opw, int ldy, int act, float slope, uptr res,
+                       uptr st) {
     ConvFwdArgs a{CP(x), CP(w), P(y), CFP(bias), FP(stats), Nb, H, W, Cg, ldx, G, Kout, P_, Q, R, S, sh, sw, ph, pw,
-                  dh, dw, tgather, OH, OW, osh, osw, oph, opw, ldy, act, slope};
+                  dh, dw, tgather, OH, OW, osh, osw, oph, opw, ldy, act, slope, CP(res)};
     int r = dv_conv_fwd(a, ST(st));
     if (r != 0) throw std::runtime_error("conv_fwd: unsupported geometry (channels must be a multiple of 8)");
     check_last("conv_fwd");
@@ -181,4 +182,10 @@ PYBIND11_MODULE(_C, m) {
                CFP(gscale), hscale, ST(st));
     check_last("pw_loss");
   });
+  m.def("wprep_batched", [](uptr descs, uptr chunks, int nchunks, uptr st) {
+    dv_wprep_batched(CP(descs), CP(chunks), nchunks, ST(st));
+    check_last("wprep_batched");
+  });
+  m.attr("WPREP_CHUNK") = WPREP_CHUNK;
+  m.attr("WPREP_DESC_BYTES") = (int)sizeof(WprepDesc);
 }

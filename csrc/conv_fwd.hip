@@ -41,6 +41,7 @@ struct FwdParams {
   u16* y;
   const float* bias;
   float* stats;
+  const u16* res;  // optional: y = conv + res (same layout as y; may alias y -> in-place accumulate)
   int M, N, K, G;
   int Hin, Win, Cg, ldx;
   int P, Q;
@@ -294,7 +295,24 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
     }
     u16* dst = p.y + opix * p.ldy + goff_y + n;
     const u16* src = st + rl * EPI_PITCH + ch;
-    if (vec) {
+    if (p.res) {  // residual-gradient join: dX += stashed gradient (fused instead of an add pass)
+      const u16* rp = p.res + opix * p.ldy + goff_y + n;
+      if (vec) {
+        uint4 a = *reinterpret_cast<const uint4*>(src), b = *reinterpret_cast<const uint4*>(rp);
+        const u16* av = reinterpret_cast<const u16*>(&a);
+        const u16* bw = reinterpret_cast<const u16*>(&b);
+        uint4 o;
+        uint32_t* ov = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          ov[e] = pack2bf(bf2f(av[2 * e]) + bf2f(bw[2 * e]), bf2f(av[2 * e + 1]) + bf2f(bw[2 * e + 1]));
+        *reinterpret_cast<uint4*>(dst) = o;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (n + e < p.N) dst[e] = f2bf(bf2f(src[e]) + bf2f(rp[e]));
+      }
+    } else if (vec) {
       *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
     } else {
 #pragma unroll
@@ -336,7 +354,7 @@ void dispatch_tile(const FwdParams& p, hipStream_t st) {
 int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
   FwdParams p{};
   p.x = (const u16*)a.x; p.w = (const u16*)a.w; p.y = (u16*)a.y;
-  p.bias = a.bias; p.stats = a.stats;
+  p.bias = a.bias; p.stats = a.stats; p.res = (const u16*)a.res;
   p.G = a.G; p.M = a.Nb * a.P * a.Q; p.N = a.Kout; p.K = a.R * a.S * a.Cg;
   p.Hin = a.H; p.Win = a.W; p.Cg = a.Cg; p.ldx = a.ldx;
   p.P = a.P; p.Q = a.Q; p.R = a.R; p.S = a.S;

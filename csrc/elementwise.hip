@@ -127,6 +127,36 @@ __global__ void wprep_kernel(const float* __restrict__ w, u16* __restrict__ out,
   }
 }
 
+// Batched weight prep: every conv / linear weight of the model re-laid-out in ONE launch after the
+// optimizer step (one block per 4096-element chunk of one descriptor), instead of one launch per
+// layer per call. Descriptors / chunk table live in device memory (built once on the host).
+__global__ __launch_bounds__(256) void wprep_batched_kernel(const WprepDesc* __restrict__ descs,
+                                                            const int2* __restrict__ chunks) {
+  const int2 ch = chunks[blockIdx.x];
+  const WprepDesc d = descs[ch.x];
+  const int64_t t0 = (int64_t)ch.y * WPREP_CHUNK;
+  const int64_t t1 = min(d.total, t0 + WPREP_CHUNK);
+  for (int64_t t = t0 + threadIdx.x; t < t1; t += 256) {
+    int64_t u = t;
+    int g, o, i, r, s;
+    bool ok;
+    if (d.mode == 0) {
+      i = (int)(u % d.pad); u /= d.pad;
+      s = (int)(u % d.S); u /= d.S;
+      r = (int)(u % d.R); u /= d.R;
+      o = (int)(u % d.Og); g = (int)(u / d.Og);
+      ok = i < d.Ig;
+    } else {
+      o = (int)(u % d.pad); u /= d.pad;
+      s = (int)(u % d.S); u /= d.S;
+      r = (int)(u % d.R); u /= d.R;
+      i = (int)(u % d.Ig); g = (int)(u / d.Ig);
+      ok = o < d.Og;
+    }
+    d.out[t] = ok ? f2bf(d.w[((((int64_t)(g * d.Og + o)) * d.Ig + i) * d.R + r) * d.S + s]) : (u16)0;
+  }
+}
+
 // fp32 [G][O][R][S][Ipad] gradient (kernel layout) -> fp32 OIHW param-grad layout (drop padding)
 __global__ void wgrad_unprep_kernel(const float* __restrict__ src, float* __restrict__ dst, int G, int Og, int Ig,
                                     int R, int S, int Ipad, float alpha, int accumulate) {
@@ -196,6 +226,10 @@ void dv_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, hipSt
 void dv_wprep(const float* w, void* out, int G, int Og, int Ig, int R, int S, int pad, int mode, hipStream_t st) {
   const int64_t total = (int64_t)G * (mode == 0 ? Og : Ig) * pad * R * S;
   wprep_kernel<<<grid_for(total), NT, 0, st>>>(w, (u16*)out, G, Og, Ig, R, S, pad, mode);
+}
+void dv_wprep_batched(const void* descs, const void* chunks, int nchunks, hipStream_t st) {
+  if (nchunks > 0)
+    wprep_batched_kernel<<<nchunks, 256, 0, st>>>((const WprepDesc*)descs, (const int2*)chunks);
 }
 void dv_wgrad_unprep(const float* src, float* dst, int G, int Og, int Ig, int R, int S, int Ipad, float alpha,
                      int accumulate, hipStream_t st) {

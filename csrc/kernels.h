@@ -18,6 +18,7 @@ struct ConvFwdArgs {
   int tgather;        // transposed-conv gather (dgrad with stride > 1)
   int OH, OW, osh, osw, oph, opw, ldy;  // output pixel mapping
   int act; float slope;
+  const void* res;    // optional residual added in the epilogue (layout of y, may alias y)
 };
 
 struct ConvWgradArgs {
@@ -120,3 +121,13 @@ int dv_nms(const float* cand, int N, int M, int D, float iou_thresh, float score
 void dv_pw_loss(int kind, const void* pred, int pred_bf16, const void* tgt, int tgt_type, float tval, const float* wt,
                 int64_t rows, int C, int ldp, int ldt, float a, float b, float* sums, void* grad, const float* gscale,
                 float hscale, hipStream_t st);
+
+// ---- batched weight prep (elementwise.hip) ----
+#define WPREP_CHUNK 4096
+struct WprepDesc {  // 48 bytes, mirrored by deep_vision_amd/ops/wcache.py
+  const float* w;
+  unsigned short* out;
+  int64_t total;
+  int G, Og, Ig, R, S, pad, mode, _unused;
+};
+void dv_wprep_batched(const void* descs, const void* chunks, int nchunks, hipStream_t st);

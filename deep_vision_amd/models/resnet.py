@@ -16,6 +16,7 @@ import torch.nn as tnn
 
 from .. import nn
 from .. import ops as F
+from ..ops.conv import GradJoin
 
 
 def _init(model):
@@ -43,9 +44,15 @@ class BasicBlock(tnn.Module):
                 nn.Conv2d(in_channels, out_channels, 1, stride=stride, bias=False), nn.BatchNorm2d(out_channels))
 
     def forward(self, x):
-        identity = F.conv_bn_act(x, self.projection[0], self.projection[1]) if self.downsample else x
-        out = F.conv_bn_act(x, self.conv1, self.bn1, "relu")
-        return F.conv_bn_act(out, self.conv2, self.bn2, "relu", residual=identity)
+        # GradJoin: the gradient of x from the shortcut (identity or projection) is folded into
+        # conv1's dgrad epilogue instead of a separate autograd add (ops.conv.GradJoin)
+        j = GradJoin() if F.native(x) else None
+        out = F.conv_bn_act(x, self.conv1, self.bn1, "relu", join=j, join_role="consumer")
+        if self.downsample:
+            identity, rj = F.conv_bn_act(x, self.projection[0], self.projection[1], join=j, join_role="producer"), None
+        else:
+            identity, rj = x, j
+        return F.conv_bn_act(out, self.conv2, self.bn2, "relu", residual=identity, residual_join=rj)
 
 
 class BottleneckBlock(tnn.Module):
@@ -65,10 +72,15 @@ class BottleneckBlock(tnn.Module):
                 nn.Conv2d(in_channels, out2, 1, stride=stride, bias=False), nn.BatchNorm2d(out2))
 
     def forward(self, x):
-        identity = F.conv_bn_act(x, self.projection[0], self.projection[1]) if self.downsample else x
-        out = F.conv_bn_act(x, self.conv1, self.bn1, "relu")
+        j = GradJoin() if F.native(x) else None
+        out = F.conv_bn_act(x, self.conv1, self.bn1, "relu", join=j, join_role="consumer")
         out = F.conv_bn_act(out, self.conv2, self.bn2, "relu")
-        return F.conv_bn_act(out, self.conv3, self.bn3, "relu", residual=identity)
+        # projection created after the main path: its backward runs first and stashes its dx
+        if self.downsample:
+            identity, rj = F.conv_bn_act(x, self.projection[0], self.projection[1], join=j, join_role="producer"), None
+        else:
+            identity, rj = x, j
+        return F.conv_bn_act(out, self.conv3, self.bn3, "relu", residual=identity, residual_join=rj)
 
 
 class _ResNetBase(tnn.Module):

@@ -32,7 +32,7 @@ def _nrows(x):
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, stats, weight, bias, running_mean, running_var, residual, training, momentum, eps, act,
-                slope, ws_fwd, ws_bwd):
+                slope, ws_fwd, ws_bwd, join=None):
         N, C, H, W = x.shape
         if ld_of(x) != C:
             raise NotImplementedError("BatchNorm on a padded channel view")
@@ -63,6 +63,7 @@ class _BNActFn(torch.autograd.Function):
         ctx.save_for_backward(x, out if keep_out else None, weight, bias, prm)
         ctx.cfg = (training, act, slope, residual is not None)
         ctx.ws_bwd = ws_bwd
+        ctx.join = join
         return out
 
     @staticmethod
@@ -109,7 +110,9 @@ class _BNActFn(torch.autograd.Function):
         if direct:
             notify_grad_ready(weight)
             notify_grad_ready(bias)
-        return dx, None, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None
+        if ctx.join is not None and dres is not None:
+            dres = ctx.join.produce(dres)  # folded into the shortcut consumer's dgrad epilogue
+        return dx, None, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None, None
 
 
 def _torch_bn_act(x, bn, act, slope, residual):
@@ -130,7 +133,7 @@ def bn_momentum(bn) -> float:
     return bn.momentum
 
 
-def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None):
+def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None, residual_join=None):
     """act(BN(x) (+ residual)) with ``bn`` an nn.BatchNorm2d (parameters, buffers, mode)."""
     if not native(x):
         return _torch_bn_act(x, bn, act, slope, residual)
@@ -142,15 +145,20 @@ def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None):
     rv = bn.running_var if bn.track_running_stats else None
     if residual is not None and not (is_nhwc(residual) and ld_of(residual) == residual.shape[1]):
         residual = residual.to(dtype=BF16).contiguous(memory_format=torch.channels_last)
+        residual_join = None  # the residual reaches its source through a copy
     C = x.shape[1]
     ws_fwd = workspace(bn, "bn_fwd", (STAT_SHARDS, 2, C), x.device) if training else None
     ws_bwd = workspace(bn, "bn_bwd", (STAT_SHARDS, 2, C), x.device) if training else None
     return _BNActFn.apply(x, stats, bn.weight, bn.bias, rm, rv, residual, training, mom,
-                          bn.eps, ACT_IDS[act], float(slope), ws_fwd, ws_bwd)
+                          bn.eps, ACT_IDS[act], float(slope), ws_fwd, ws_bwd, residual_join)
 
 
-def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None):
-    """Fused conv -> BN (batch stats from the conv epilogue) -> (+residual) -> activation."""
+def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None, join=None, join_role=None, residual_join=None):
+    """Fused conv -> BN (batch stats from the conv epilogue) -> (+residual) -> activation.
+
+    ``join`` / ``join_role`` ('consumer' | 'producer') and ``residual_join``: a conv.GradJoin
+    shared by the two consumers of a block input (see models/resnet.py) so the gradient sum
+    is folded into the consumer conv's dgrad epilogue."""
     from .conv import conv2d
 
     if not native(x):
@@ -161,9 +169,9 @@ def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None):
     sbuf = workspace(bn, "bn_fwd", (STAT_SHARDS, 2, conv.out_channels), x.device) if want else None
     pad = conv.native_padding(x.shape[2], x.shape[3]) if hasattr(conv, "native_padding") else conv.padding
     r = conv2d(x, conv.weight, conv.bias, conv.stride, pad, conv.dilation, conv.groups, want_stats=want,
-               stats_buf=sbuf)
+               stats_buf=sbuf, join=join, join_role=join_role)
     y, stats = r if want else (r, None)
     if y.shape[1] % 8 != 0:  # padded view: BN kernels require dense channels
         y = y.contiguous(memory_format=torch.channels_last)
         stats = None
-    return batch_norm_act(y, bn, act, slope, residual, stats)
+    return batch_norm_act(y, bn, act, slope, residual, stats, residual_join=residual_join)

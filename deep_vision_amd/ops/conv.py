@@ -14,6 +14,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as TF
 
+from . import wcache
 from .common import (ACT_IDS, BF16, CL, F32, alloc_cl, as_nhwc, empty_nhwc, grad_nhwc, grad_sink, ld_of, lib,
                      like_layout, empty_layout, native, nhwc_numel, notify_grad_ready, ptr, round8, stream_handle)
 
@@ -49,21 +50,30 @@ def norm_padding(padding):
     return tuple(padding), (0, 0)
 
 
-def _prep_weight(weight: torch.Tensor, G: int, pad: int, mode: int) -> torch.Tensor:
-    """fp32 OIHW -> bf16 kernel operand.
+def _prep_weight(weight: torch.Tensor, G: int, pad: int, mode: int, param=None) -> torch.Tensor:
+    """fp32 OIHW -> bf16 kernel operand (cached per parameter, see ops/wcache.py).
 
     mode 0: [G][Og][R][S][pad]  (inner = input channels, zero-padded to ``pad``)
     mode 1: [G][Ig][R][S][pad]  (inner = output channels per group, zero-padded to ``pad``)
+    ``param``: the nn.Parameter behind ``weight`` when ``weight`` is a view of it (Linear).
     """
     O, Ig, R, S = weight.shape
-    w = weight.detach()
-    if w.dtype != F32 or not w.is_contiguous():
-        w = w.float().contiguous()
     Og = O // G
     n = G * (Og if mode == 0 else Ig) * R * S * pad
-    out = torch.empty(n, dtype=BF16, device=w.device)
-    lib().wprep(ptr(w), ptr(out), G, Og, Ig, R, S, pad, mode, stream_handle())
-    return out
+
+    def compute(out):
+        w = weight.detach()
+        if w.dtype != F32 or not w.is_contiguous():
+            w = w.float().contiguous()
+        if out is None:
+            out = torch.empty(n, dtype=BF16, device=w.device)
+        lib().wprep(ptr(w), ptr(out), G, Og, Ig, R, S, pad, mode, stream_handle())
+        return out
+
+    key = param if param is not None else weight
+    if isinstance(key, torch.nn.Parameter) and key.dtype == F32 and key.is_contiguous():
+        return wcache.get(key, G, pad, mode, compute)
+    return compute(None)
 
 
 def _channel_sum(dy: torch.Tensor) -> torch.Tensor:
@@ -76,14 +86,14 @@ def _channel_sum(dy: torch.Tensor) -> torch.Tensor:
 
 
 def conv_fwd_raw(x, wk, y, bias, stats, N, H, W, Cg, ldx, G, Kout, P, Q, R, S, stride, padding, dilation,
-                 act=0, slope=0.0, tgather=0, omap=None, ldy=None):
+                 act=0, slope=0.0, tgather=0, omap=None, ldy=None, res=None):
     sh, sw = stride
     ph, pw = padding
     dh, dw = dilation
     OH, OW, osh, osw, oph, opw = omap if omap is not None else (P, Q, 1, 1, 0, 0)
     lib().conv_fwd(ptr(x), ptr(wk), ptr(y), ptr(bias), ptr(stats), N, H, W, Cg, ldx, G, Kout, P, Q, R, S, sh, sw, ph,
                    pw, dh, dw, tgather, OH, OW, osh, osw, oph, opw, ldy if ldy is not None else ld_of(y), act, float(slope),
-                   stream_handle())
+                   ptr(res), stream_handle())
 
 
 def _gather_channels(t: torch.Tensor, per_group: int, G: int) -> int:
@@ -98,8 +108,18 @@ def _gather_channels(t: torch.Tensor, per_group: int, G: int) -> int:
     raise NotImplementedError(f"grouped conv with {per_group} channels per group (needs % 8 == 0)")
 
 
-def _dgrad(dy, weight, x_shape, Cg_x, G, stride, padding, dilation, device):
-    """dX (N, G*Cg_x, H, W) from dY; Cg_x may include zero-padding channels."""
+def _accumulable(t, shape):
+    """True when ``t`` can serve as the in-place accumulation target of a dgrad (dense NHWC)."""
+    return (t is not None and t.dtype == BF16 and tuple(t.shape) == tuple(shape)
+            and t.is_contiguous(memory_format=CL))
+
+
+def _dgrad(dy, weight, x_shape, Cg_x, G, stride, padding, dilation, device, accum=None):
+    """dX (N, G*Cg_x, H, W) from dY; Cg_x may include zero-padding channels.
+
+    ``accum``: a dense gradient of the same input from another consumer (residual shortcut /
+    projection); the dgrad kernel adds into it in place (epilogue ``res`` aliasing ``y``),
+    replacing autograd's separate gradient-sum pass."""
     N, _, H, W = x_shape
     O, Ig, R, S = weight.shape
     Og = O // G
@@ -111,17 +131,48 @@ def _dgrad(dy, weight, x_shape, Cg_x, G, stride, padding, dilation, device):
     wd = _prep_weight(weight, G, Cg_dy, mode=1)  # [G][Ig][R][S][Cg_dy]
     ldy_in = ld_of(dy)
     scatter = (sh, sw) != (1, 1) and R == 1 and S == 1 and (ph, pw) == (0, 0)
-    dX = alloc_cl((N, G * Cg_x, H, W), zero=(scatter or Cg_x != Ig), device=device)
+    if accum is not None and Cg_x == Ig and _accumulable(accum, (N, G * Cg_x, H, W)):
+        dX, res = accum, accum  # scattered positions get res + val, the others keep res
+    else:
+        dX, res = alloc_cl((N, G * Cg_x, H, W), zero=(scatter or Cg_x != Ig), device=device), None
     if (sh, sw) == (1, 1):
         conv_fwd_raw(dy, wd, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, H, W, R, S, (1, 1), (-ph, -pw),
-                     (-dh, -dw), ldy=G * Cg_x)
+                     (-dh, -dw), ldy=G * Cg_x, res=res)
     elif scatter:
         conv_fwd_raw(dy, wd, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, P, Q, 1, 1, (1, 1), (0, 0), (1, 1),
-                     omap=(H, W, sh, sw, 0, 0), ldy=G * Cg_x)
+                     omap=(H, W, sh, sw, 0, 0), ldy=G * Cg_x, res=res)
     else:
         conv_fwd_raw(dy, wd, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, H, W, R, S, stride, padding, dilation,
-                     tgather=1, ldy=G * Cg_x)
+                     tgather=1, ldy=G * Cg_x, res=res)
+    if accum is not None and res is None:  # layout mismatch: plain add
+        dX = dX[:, : accum.shape[1]] + accum if dX.shape[1] != accum.shape[1] else dX + accum
     return dX
+
+
+class GradJoin:
+    """Meeting point of two gradients of one tensor (a block input used by a conv and by a
+    residual add / projection conv). Whichever backward runs first stashes or announces itself;
+    the second folds the sum into the consumer conv's dgrad epilogue (no separate add pass).
+    Order-independent: the producer only stashes while the consumer has not run yet."""
+
+    __slots__ = ("grad", "consumer_done")
+
+    def __init__(self):
+        self.grad = None
+        self.consumer_done = False
+
+    def produce(self, g):
+        """Producer side: returns the gradient to hand to autograd (None when stashed)."""
+        if g is None or self.consumer_done:
+            return g
+        self.grad = g if self.grad is None else self.grad + g
+        return None
+
+    def take(self):
+        """Consumer side: the stashed gradient (or None), marking the consumer as done."""
+        g, self.grad = self.grad, None
+        self.consumer_done = True
+        return g
 
 
 def _wgrad(x, dy, weight, Cg_x, G, stride, padding, dilation, out=None):
@@ -152,7 +203,7 @@ def _wgrad(x, dy, weight, Cg_x, G, stride, padding, dilation, out=None):
 class _ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats, stats_buf=None,
-                extra=(0, 0)):
+                extra=(0, 0), join=None, join_role=None):
         N, Cx, H, W = x.shape
         O, Ig, R, S = weight.shape
         G = groups
@@ -170,6 +221,7 @@ class _ConvFn(torch.autograd.Function):
                      act=act, slope=slope)
         ctx.save_for_backward(x, weight, y if act else None)
         ctx.cfg = (stride, padding, dilation, G, act, slope, Cg_x, bias is not None)
+        ctx.join = (join, join_role)
         if want_stats:
             ctx.mark_non_differentiable(stats)
             return y, stats
@@ -186,10 +238,14 @@ class _ConvFn(torch.autograd.Function):
             lib().act_bwd(ptr(dy), ptr(y), ptr(g), nhwc_numel(y), act, float(slope), stream_handle())
             dy = g
         dx = dw = db = None
+        join, role = ctx.join
         if ctx.needs_input_grad[0]:
-            dx = _dgrad(dy, weight, x.shape, Cg_x, G, stride, padding, dilation, x.device)
+            accum = join.take() if (join is not None and role == "consumer") else None
+            dx = _dgrad(dy, weight, x.shape, Cg_x, G, stride, padding, dilation, x.device, accum=accum)
             if dx.shape[1] != x.shape[1]:
                 dx = dx[:, : x.shape[1]]
+            if join is not None and role == "producer":
+                dx = join.produce(dx)
         if ctx.needs_input_grad[1]:
             sink = grad_sink(weight)
             dw = _wgrad(x, dy, weight, Cg_x, G, stride, padding, dilation, out=sink)
@@ -198,11 +254,11 @@ class _ConvFn(torch.autograd.Function):
                 notify_grad_ready(weight)
         if has_bias and ctx.needs_input_grad[2]:
             db = _channel_sum(dy)
-        return dx, dw, db, None, None, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None, None, None, None, None
 
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=None, slope=0.0,
-           want_stats=False, stats_buf=None):
+           want_stats=False, stats_buf=None, join=None, join_role=None):
     """Conv2d (+fused bias/activation). Returns y, or (y, stats) when want_stats (GPU only).
 
     ``padding`` may be (top, bottom, left, right) for TF/Keras asymmetric 'same' padding."""
@@ -210,6 +266,8 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=
         raise NotImplementedError("string padding: use nn.Conv2d(padding='same_keras')")
     stride, dilation = _pair(stride), _pair(dilation)
     padding, extra = norm_padding(padding)
+    if join is not None and join_role == "consumer" and not native(x):
+        join.consumer_done = True
     if not native(x):
         if extra != (0, 0):
             x = TF.pad(x, (padding[1], padding[1] + extra[1], padding[0], padding[0] + extra[0]))
@@ -220,15 +278,23 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=
         elif act in ("leaky", "leaky_relu"):
             y = TF.leaky_relu(y, slope)
         return (y, None) if want_stats else y
-    if _is_depthwise(x, weight, groups, stride, dilation):
+    dw = _is_depthwise(x, weight, groups, stride, dilation)
+    padded_groups = groups > 1 and ((x.shape[1] // groups) % 8 != 0 or (weight.shape[0] // groups) % 8 != 0)
+    if join is not None and join_role == "consumer" and (dw or padded_groups):
+        join.consumer_done = True  # these paths do not fold the join: producers hand grads to autograd
+    if dw:
         return depthwise_conv2d(x, weight, bias, stride, padding, act, slope, want_stats, stats_buf, extra)
-    if groups > 1 and ((x.shape[1] // groups) % 8 != 0 or (weight.shape[0] // groups) % 8 != 0):
+    if padded_groups:
         if extra != (0, 0):
             raise NotImplementedError("asymmetric padding on a channel-padded grouped conv")
         return _grouped_padded_conv(x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats)
-    x = as_nhwc(x, pad_to8=(groups == 1))
-    return _ConvFn.apply(x, weight, bias, stride, padding, dilation, groups, ACT_IDS[act], float(slope), want_stats,
-                         stats_buf, extra)
+    xn = as_nhwc(x, pad_to8=(groups == 1))
+    if xn is not x and join is not None:
+        if join_role == "consumer":  # the gradient reaches x through the layout copy: no join
+            join.consumer_done = True
+        join = None
+    return _ConvFn.apply(xn, weight, bias, stride, padding, dilation, groups, ACT_IDS[act], float(slope), want_stats,
+                         stats_buf, extra, join, join_role)
 
 
 def _grouped_padded_conv(x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats):
@@ -351,7 +417,7 @@ class _LinearFn(torch.autograd.Function):
         N, K = x.shape
         O, _ = weight.shape
         Kp = x.stride(0)  # zero-padded row stride, multiple of 8
-        wk = _prep_weight(weight.view(O, K, 1, 1), 1, Kp, mode=0)
+        wk = _prep_weight(weight.view(O, K, 1, 1), 1, Kp, mode=0, param=weight)
         Op = round8(O)
         y_full = (torch.zeros if Op != O else torch.empty)((N, Op), dtype=BF16, device=x.device)
         b = bias.detach().float().contiguous() if bias is not None else None
@@ -378,7 +444,7 @@ class _LinearFn(torch.autograd.Function):
             dy = g[:, :O]
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            wd = _prep_weight(weight.view(O, K, 1, 1), 1, Op, mode=1)  # [K][Op]
+            wd = _prep_weight(weight.view(O, K, 1, 1), 1, Op, mode=1, param=weight)  # [K][Op]
             dx_full = (torch.zeros if Kp != K else torch.empty)((N, Kp), dtype=BF16, device=dy.device)
             conv_fwd_raw(dy, wd, dx_full, None, None, N, 1, 1, Op, Op, 1, K, 1, 1, 1, 1, (1, 1), (0, 0), (1, 1),
                          ldy=Kp)

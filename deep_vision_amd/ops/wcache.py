@@ -1,0 +1,113 @@
+"""Cache of the bf16 MFMA operand layouts of every conv / linear weight.
+
+The kernels consume weights as bf16 ``[G][Og][R][S][Cpad]`` (forward) and ``[G][Ig][R][S][Opad]``
+(dgrad). Re-laying them out per layer per call costs one launch each (107 per ResNet-50 step).
+Here each (parameter, layout) gets a persistent buffer:
+
+* a hit needs the same global *weights epoch*, the same parameter ``_version`` (user in-place
+  edits bump it) and the same storage pointer;
+* the fused optimizers call ``after_step()`` once per step: the epoch advances and ONE batched
+  kernel (csrc/elementwise.hip ``wprep_batched_kernel``) refreshes every registered buffer on the
+  current stream, right after the parameter update -- so the next forward / backward only hit.
+"""
+from __future__ import annotations
+
+import struct
+import weakref
+
+import torch
+
+from .._ext import lib, ptr, stream_handle
+
+_entries = {}  # key -> [param weakref, buf, epoch, version, data_ptr, geometry]
+_epoch = 0
+_tables = {}  # device -> (n_entries_snapshot, descs, chunks, nchunks)
+ENABLED = True
+
+
+def _key(param, G, pad, mode):
+    return (id(param), G, pad, mode)
+
+
+def get(param, G, pad, mode, compute):
+    """bf16 operand of ``param`` in layout (G, pad, mode); ``compute(out)`` fills a buffer."""
+    if not ENABLED:
+        return compute(None)
+    k = _key(param, G, pad, mode)
+    e = _entries.get(k)
+    if e is not None and e[0]() is param:
+        if e[2] == _epoch and e[3] == param._version and e[4] == param.data_ptr():
+            return e[1]
+        buf = compute(e[1])
+    else:
+        buf = compute(None)
+        _tables.pop(buf.device, None)
+    _entries[k] = [weakref.ref(param), buf, _epoch, param._version, param.data_ptr(), (G, pad, mode)]
+    return buf
+
+
+def _build_table(device):
+    descs, chunks = [], []
+    chunk = int(lib().WPREP_CHUNK)
+    live = []
+    for k, e in list(_entries.items()):
+        p = e[0]()
+        if p is None:
+            del _entries[k]
+            continue
+        if e[1].device != device or p.dtype != torch.float32 or not p.is_contiguous():
+            continue
+        G, pad, mode = e[5]
+        shp = p.shape if p.dim() == 4 else (p.shape[0], p.shape[1], 1, 1)
+        O, Ig, R, S = shp
+        Og = O // G
+        total = G * (Og if mode == 0 else Ig) * R * S * pad
+        di = len(descs)
+        descs.append(struct.pack("<qqqiiiiiiii", p.data_ptr(), e[1].data_ptr(), total, G, Og, Ig, R, S, pad, mode, 0))
+        chunks += [(di, c) for c in range((total + chunk - 1) // chunk)]
+        live.append(k)
+    if not descs:
+        return None
+    assert len(descs[0]) == int(lib().WPREP_DESC_BYTES)
+    dbuf = torch.frombuffer(bytearray(b"".join(descs)), dtype=torch.uint8).to(device)
+    cbuf = torch.tensor(chunks, dtype=torch.int32).reshape(-1, 2).to(device)
+    return (len(_entries), dbuf, cbuf, len(chunks), live)
+
+
+def _table_valid(t) -> bool:
+    if t[0] != len(_entries):
+        return False
+    for k in t[4]:
+        e = _entries.get(k)
+        if e is None:
+            return False
+        p = e[0]()
+        if p is None or p.data_ptr() != e[4]:
+            return False
+    return True
+
+
+def after_step(device=None):
+    """Advance the weights epoch and refresh every cached operand of ``device`` in one launch."""
+    global _epoch
+    _epoch += 1
+    if not ENABLED or not _entries:
+        return
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    t = _tables.get(device)
+    if t is None or not _table_valid(t):
+        t = _build_table(device)  # (drops dead entries; bakes in the current data pointers)
+        if t is None:
+            _tables.pop(device, None)
+            return
+        _tables[device] = t
+    lib().wprep_batched(ptr(t[1]), ptr(t[2]), t[3], stream_handle())
+    for k in t[4]:
+        e = _entries[k]
+        p = e[0]()
+        e[2], e[3], e[4] = _epoch, p._version, p.data_ptr()
+
+
+def clear():
+    _entries.clear()
+    _tables.clear()

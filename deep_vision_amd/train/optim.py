@@ -137,6 +137,10 @@ class _FlatOptimizer(torch.optim.Optimizer):
             for off, n in segs:
                 self._update(group, f, off, n, grad_scale)
             f["first"] = False
+        if any(f is not None and f["param"].is_cuda for f in self._flat):
+            from ..ops import wcache
+
+            wcache.after_step()  # one batched re-layout of every cached bf16 weight operand
         return loss
 
     def _update(self, group, f, off, n, gs):  # pragma: no cover - abstract

@@ -170,41 +170,69 @@ def test_pointwise_losses(kind):
 
 
 # ----------------------------------- whole models -----------------------------------
-def _compare_model(make, inputs, loss_fn, out_cos=0.99, grad_cos=0.97, train=True):
-    """Native bf16 vs torch fp32 on identical weights. Deep random-init nets in train mode amplify
-    bf16 rounding through batch-statistics BN on tiny inner feature maps (hourglass / CenterNet
-    reach 1x1-2x2), so those are compared tightly in eval mode and loosely in train mode."""
+def _run_variant(make, inputs, loss_fn, train, variant):
     from deep_vision_amd.ops.common import set_backend
 
     torch.manual_seed(0)
     m = make().to(DEV).train(train)
-    ref = copy.deepcopy(m)
-    out = m(*inputs)
-    loss_fn(out).backward()
-    set_backend("torch")
+    set_backend("native" if variant == "native" else "torch")
     try:
-        out_r = ref(*inputs)
-        loss_fn(out_r).backward()
+        if variant == "bf16":
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                out = m(*inputs)
+                loss = loss_fn(out)
+        else:
+            out = m(*inputs)
+            loss = loss_fn(out)
+        loss.backward()
     finally:
         set_backend("native")
-    flat = lambda o: [t for t in (o if isinstance(o, (list, tuple)) else [o]) for t in (flat(t) if isinstance(t, (list, tuple)) else [t])]
-    for a, b in zip(flat(out), flat(out_r)):
+    return m, out
+
+
+def _flat(o):
+    return [t for t in (o if isinstance(o, (list, tuple)) else [o]) for t in (_flat(t) if isinstance(t, (list, tuple)) else [t])]
+
+
+def _compare_model(make, inputs, loss_fn, out_cos=0.99, grad_cos=0.97, train=True):
+    """Native bf16 vs torch fp32 on identical weights.
+
+    Eval mode: direct thresholds. Train mode: random-init nets with batch-statistics BN at
+    small batch amplify *any* bf16 rounding (PyTorch's own autocast-bf16 path reaches only
+    ~0.2-0.4 median gradient cosine to fp32 on ResNet-50 / MobileNet there, see
+    tools/debug_gradcmp.py), so the native path is held to the torch-bf16 baseline instead."""
+    m, out = _run_variant(make, inputs, loss_fn, train, "native")
+    ref, out_r = _run_variant(make, inputs, loss_fn, train, "fp32")
+    base = _run_variant(make, inputs, loss_fn, train, "bf16") if train else None
+    for k, (a, b) in enumerate(zip(_flat(out), _flat(out_r))):
         assert a.shape == b.shape
-        assert _cos(a, b) > out_cos
-    bad, n_checked = [], 0
-    for (n, pa), pb in zip(m.named_parameters(), ref.parameters()):
-        if grad_cos is None:
-            break
-        if pb.grad is None:
+        c = _cos(a, b)
+        if base is None:
+            assert c > out_cos, c
+        else:
+            cb = _cos(_flat(base[1])[k], b)
+            assert c > min(out_cos, cb - 0.01), (c, cb)
+    if grad_cos is None:
+        return
+    pa_all = dict(m.named_parameters())
+    rows = []
+    for (n, pr) in ref.named_parameters():
+        pa = pa_all[n]
+        if pr.grad is None:
             assert pa.grad is None or pa.grad.abs().max() == 0
             continue
-        n_checked += 1
-        c = _cos(pa.grad, pb.grad)
-        if c < grad_cos:
-            bad.append((n, c))
-    # small per-channel reductions (BN gamma over a 4x4 map) can lose a few digits to cancellation
-    # of bf16 terms: allow 2% outliers, none below 0.5
-    assert len(bad) <= max(1, n_checked // 50) and all(c > 0.5 for _, c in bad), bad[:10]
+        cb = _cos(dict(base[0].named_parameters())[n].grad, pr.grad) if base is not None else None
+        rows.append((n, _cos(pa.grad, pr.grad), cb))
+    if base is None:
+        bad = [(n, c) for n, c, _ in rows if c < grad_cos]
+        # small per-channel reductions (BN gamma over a 4x4 map) can lose digits to cancellation
+        assert len(bad) <= max(1, len(rows) // 50) and all(c > 0.5 for _, c in bad), bad[:10]
+    else:
+        med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
+        mn, mb = med([c for _, c, _ in rows]), med([c for _, _, c in rows])
+        assert mn >= min(grad_cos, mb - 0.05), (mn, mb)
+        worse = [(n, c, b) for n, c, b in rows if c < b - 0.3]
+        assert len(worse) <= max(2, len(rows) // 10), worse[:10]
 
 
 def test_yolov3_model():
@@ -218,7 +246,15 @@ def test_yolov3_model():
         return sum(D.yolo_loss(h, y, ANCHORS_WH[list(m)], 80).sum() for h, y, m in zip(heads, ys, ANCHOR_MASKS)) / 2
 
     _compare_model(lambda: YoloV3(80), (x,), loss, out_cos=0.995, grad_cos=0.98, train=False)
-    _compare_model(lambda: YoloV3(80), (x,), loss, out_cos=0.95, grad_cos=0.7)
+    # train mode at 256 px / batch 4: the deepest BN layers see 256 samples per channel (at
+    # 128 px / batch 2 only 32, where batch statistics amplify bf16 rounding into the grads)
+    x2 = torch.randn(4, 3, 256, 256, device=DEV)
+    ys2 = [_yolo_batch(4, 80, g, seed=g) for g in (32, 16, 8)]
+
+    def loss2(heads):
+        return sum(D.yolo_loss(h, y, ANCHORS_WH[list(m)], 80).sum() for h, y, m in zip(heads, ys2, ANCHOR_MASKS)) / 4
+
+    _compare_model(lambda: YoloV3(80), (x2,), loss2, out_cos=0.98, grad_cos=0.8)
 
 
 def test_hourglass_model():
@@ -301,3 +337,48 @@ def test_classifiers_train_step_native_vs_torch():
     # default-initialised nets vanish (~0.4x per layer), making any comparison meaningless
     _compare_model(lambda: M.get_model("mobilenet1"), (x,), ce, out_cos=0.99, grad_cos=0.9)
     _compare_model(lambda: M.get_model("shufflenet1"), (x,), ce, out_cos=0.99, grad_cos=0.9)
+
+
+def test_resnet_grad_join_and_weight_cache():
+    """ResNet blocks fold the shortcut gradient into conv1's dgrad epilogue (GradJoin) and the
+    bf16 weight operands are refreshed by one batched launch after each optimizer step: a
+    3-step SGD trajectory must track torch fp32 as closely as torch's own autocast-bf16 does."""
+    from deep_vision_amd import models as M
+    from deep_vision_amd import ops as F
+    from deep_vision_amd.ops.common import set_backend
+    from deep_vision_amd.train.optim import FusedSGD
+
+    x = torch.randn(8, 3, 128, 128, device=DEV)
+    y = torch.randint(0, 1000, (8,), device=DEV)
+    for name in ("resnet50", "resnet34"):
+        torch.manual_seed(0)
+        base = M.get_model(name).to(DEV)
+        runs = {}
+        for variant in ("native", "fp32", "bf16"):
+            m = copy.deepcopy(base)
+            opt = FusedSGD(m.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
+            outs = []
+            set_backend("native" if variant == "native" else "torch")
+            try:
+                for _ in range(3):
+                    opt.zero_grad()
+                    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=variant == "bf16"):
+                        out = m(x)
+                        loss = F.cross_entropy(out, y) if variant == "native" else \
+                            torch.nn.functional.cross_entropy(out.float(), y)
+                    loss.backward()
+                    opt.step()
+                    outs.append(out.detach().float())
+            finally:
+                set_backend("native")
+            runs[variant] = (m, outs)
+        for k in range(3):
+            cn = _cos(runs["native"][1][k], runs["fp32"][1][k])
+            cb = _cos(runs["bf16"][1][k], runs["fp32"][1][k])
+            assert cn > cb - 0.02, (name, k, cn, cb)
+        # aggregate parameter update over the 3 steps (per-parameter updates of bias-like
+        # parameters are rounding noise in every bf16 path)
+        upd = {v: torch.cat([(p.detach() - q.detach()).flatten() for p, q in
+                             zip(runs[v][0].parameters(), base.parameters())]) for v in runs}
+        cn, cb = _cos(upd["native"], upd["fp32"]), _cos(upd["bf16"], upd["fp32"])
+        assert cn > cb - 0.05, (name, cn, cb)
