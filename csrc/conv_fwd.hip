@@ -70,7 +70,7 @@ DV_DEVICE bf16x8 read_kc(const char* img, int row, int chunk) {
 template <int BM_, int BN_, int BK_>
 constexpr int stage_bytes() { return (BM_ + BN_) * BK_ * 2; }
 
-template <int BM_, int BN_, int BK_, int KMODE>
+template <int BM_, int BN_, int BK_, int KMODE, bool RES>
 __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
   constexpr int WN = BN_ / 64, WM = BM_ / 64;
   static_assert(WN * WM == 4, "4 waves of 64x64");
@@ -295,7 +295,7 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
     }
     u16* dst = p.y + opix * p.ldy + goff_y + n;
     const u16* src = st + rl * EPI_PITCH + ch;
-    if (p.res) {  // residual-gradient join: dX += stashed gradient (fused instead of an add pass)
+    if constexpr (RES) {  // residual-gradient join: dX += stashed gradient (fused instead of an add pass)
       const u16* rp = p.res + opix * p.ldy + goff_y + n;
       if (vec) {
         uint4 a = *reinterpret_cast<const uint4*>(src), b = *reinterpret_cast<const uint4*>(rp);
@@ -327,26 +327,31 @@ constexpr int lds_bytes(int stages) {
          STAT_BYTES;
 }
 
-template <int BM_, int BN_, int BK_, int KMODE>
+template <int BM_, int BN_, int BK_, int KMODE, bool RES>
 void launch_fwd(const FwdParams& p, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)conv_fwd_kernel<BM_, BN_, BK_, KMODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipFuncSetAttribute((const void*)conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         lds_bytes<BM_, BN_, BK_>(2));
     attr = true;
   }
   const int nt = (p.K + BK_ - 1) / BK_;
   const size_t lds = lds_bytes<BM_, BN_, BK_>(nt > 1 ? 2 : 1);
   const int blocks = ((p.M + BM_ - 1) / BM_) * ((p.N + BN_ - 1) / BN_) * p.G;
-  conv_fwd_kernel<BM_, BN_, BK_, KMODE><<<dim3(blocks), dim3(NT), lds, st>>>(p);
+  conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES><<<dim3(blocks), dim3(NT), lds, st>>>(p);
 }
 
 template <int KMODE>
 void dispatch_tile(const FwdParams& p, hipStream_t st) {
   // 64-channel outputs: a 256x64 tile keeps every MFMA useful; BK=32 keeps two stages at
   // 40 KB so three blocks share a CU.
-  if (p.N <= 64) launch_fwd<256, 64, 32, KMODE>(p, st);
-  else launch_fwd<128, 128, 64, KMODE>(p, st);
+  if (p.res) {  // in-place gradient accumulation epilogue (compile-time: no cost for the others)
+    if (p.N <= 64) launch_fwd<256, 64, 32, KMODE, true>(p, st);
+    else launch_fwd<128, 128, 64, KMODE, true>(p, st);
+  } else {
+    if (p.N <= 64) launch_fwd<256, 64, 32, KMODE, false>(p, st);
+    else launch_fwd<128, 128, 64, KMODE, false>(p, st);
+  }
 }
 
 }  // namespace

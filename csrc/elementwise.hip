@@ -130,29 +130,34 @@ __global__ void wprep_kernel(const float* __restrict__ w, u16* __restrict__ out,
 // Batched weight prep: every conv / linear weight of the model re-laid-out in ONE launch after the
 // optimizer step (one block per 4096-element chunk of one descriptor), instead of one launch per
 // layer per call. Descriptors / chunk table live in device memory (built once on the host).
+DV_DEVICE FastDiv fastdiv_dev(uint32_t d) {
+  FastDiv f{0u, 0u, d};
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  f.shr = l;
+  f.mul = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1ull);
+  return f;
+}
+
 __global__ __launch_bounds__(256) void wprep_batched_kernel(const WprepDesc* __restrict__ descs,
                                                             const int2* __restrict__ chunks) {
   const int2 ch = chunks[blockIdx.x];
   const WprepDesc d = descs[ch.x];
-  const int64_t t0 = (int64_t)ch.y * WPREP_CHUNK;
-  const int64_t t1 = min(d.total, t0 + WPREP_CHUNK);
-  for (int64_t t = t0 + threadIdx.x; t < t1; t += 256) {
-    int64_t u = t;
-    int g, o, i, r, s;
+  // per-block magic divisors: 32-bit mul-hi decode instead of five 64-bit divisions per element
+  const FastDiv fpad = fastdiv_dev(d.pad), fs = fastdiv_dev(d.S), fr = fastdiv_dev(d.R);
+  const FastDiv fo = fastdiv_dev(d.mode == 0 ? d.Og : d.Ig);
+  const uint32_t t0 = (uint32_t)ch.y * WPREP_CHUNK;
+  const uint32_t t1 = (uint32_t)min(d.total, (int64_t)t0 + WPREP_CHUNK);
+  for (uint32_t t = t0 + threadIdx.x; t < t1; t += 256) {
+    uint32_t u = t, q;
+    q = fdiv(u, fpad); const int inner = (int)(u - q * d.pad); u = q;
+    q = fdiv(u, fs); const int s = (int)(u - q * d.S); u = q;
+    q = fdiv(u, fr); const int r = (int)(u - q * d.R); u = q;
+    q = fdiv(u, fo); const int outer = (int)(u - q * (d.mode == 0 ? d.Og : d.Ig)); const int g = (int)q;
+    int o, i;
     bool ok;
-    if (d.mode == 0) {
-      i = (int)(u % d.pad); u /= d.pad;
-      s = (int)(u % d.S); u /= d.S;
-      r = (int)(u % d.R); u /= d.R;
-      o = (int)(u % d.Og); g = (int)(u / d.Og);
-      ok = i < d.Ig;
-    } else {
-      o = (int)(u % d.pad); u /= d.pad;
-      s = (int)(u % d.S); u /= d.S;
-      r = (int)(u % d.R); u /= d.R;
-      i = (int)(u % d.Ig); g = (int)(u / d.Ig);
-      ok = o < d.Og;
-    }
+    if (d.mode == 0) { i = inner; o = outer; ok = i < d.Ig; }
+    else { o = inner; i = outer; ok = o < d.Og; }
     d.out[t] = ok ? f2bf(d.w[((((int64_t)(g * d.Og + o)) * d.Ig + i) * d.R + r) * d.S + s]) : (u16)0;
   }
 }

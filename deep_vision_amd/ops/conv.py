@@ -222,6 +222,7 @@ class _ConvFn(torch.autograd.Function):
         ctx.save_for_backward(x, weight, y if act else None)
         ctx.cfg = (stride, padding, dilation, G, act, slope, Cg_x, bias is not None)
         ctx.join = (join, join_role)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics output
         if want_stats:
             ctx.mark_non_differentiable(stats)
             return y, stats
@@ -231,6 +232,12 @@ class _ConvFn(torch.autograd.Function):
     def backward(ctx, dy, *unused):
         x, weight, y = ctx.saved_tensors
         stride, padding, dilation, G, act, slope, Cg_x, has_bias = ctx.cfg
+        if dy is None:
+            join, role = ctx.join
+            if join is not None and role == "consumer":
+                g = join.take()  # nothing to add to: hand a stashed shortcut gradient through
+                return (g, None, None) + (None,) * 11
+            return (None,) * 14
         dy = grad_nhwc(dy)
         if act:
             dy = like_layout(dy, y)  # the saved output's exact layout (dy may be a concat slice)
@@ -511,6 +518,7 @@ class _DWConvFn(torch.autograd.Function):
                      padding[0], padding[1], act, float(slope), ptr(stats), stream_handle())
         ctx.save_for_backward(x, weight, y if act else None)
         ctx.cfg = (stride, padding, act, slope, bias is not None)
+        ctx.set_materialize_grads(False)
         if want_stats:
             ctx.mark_non_differentiable(stats)
             return y, stats
@@ -520,6 +528,8 @@ class _DWConvFn(torch.autograd.Function):
     def backward(ctx, dy, *unused):
         x, weight, y = ctx.saved_tensors
         stride, padding, act, slope, has_bias = ctx.cfg
+        if dy is None:
+            return (None,) * 10
         dy = grad_nhwc(dy)
         if act:
             dy = like_layout(dy, y)

@@ -1,6 +1,8 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R && mkdir -p gpurun_out
-timeout -k 10 300 python bench.py --backend torch --steps 10 --warmup 3 > gpurun_out/bench_torch.log 2>&1 && \
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1 && \
 cd /tmp && export TMPDIR=/tmp && \
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof1 -o run --output-format csv -- python3 $R/bench.py --steps 5 --warmup 2 > $R/gpurun_out/prof1.log 2>&1
+echo rc=$?
+tail -1 $R/gpurun_out/bench.log
