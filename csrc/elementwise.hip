@@ -141,24 +141,41 @@ DV_DEVICE FastDiv fastdiv_dev(uint32_t d) {
 
 __global__ __launch_bounds__(256) void wprep_batched_kernel(const WprepDesc* __restrict__ descs,
                                                             const int2* __restrict__ chunks) {
+  __shared__ float tile[64][65];
   const int2 ch = chunks[blockIdx.x];
   const WprepDesc d = descs[ch.x];
-  // per-block magic divisors: 32-bit mul-hi decode instead of five 64-bit divisions per element
+  if (d.mode == 1) {
+    // dgrad layout = per-group transpose: out[g][k][o] (o padded to pad) <- w[g*Og + o][k], k = (i, r, s).
+    // 64x64 tiles through LDS: coalesced reads along k and coalesced writes along o.
+    const int K = d.Ig * d.R * d.S;
+    const int tk = (K + 63) / 64, to = (d.pad + 63) / 64;
+    const int tid = ch.y, g = tid / (tk * to), rem = tid - g * tk * to;
+    const int k0 = (rem / to) * 64, o0 = (rem % to) * 64;
+    const float* w = d.w + (int64_t)g * d.Og * K;
+    for (int e = threadIdx.x; e < 4096; e += 256) {
+      const int r = e >> 6, c = e & 63;  // r: o offset, c: k offset
+      tile[r][c] = (o0 + r < d.Og && k0 + c < K) ? w[(int64_t)(o0 + r) * K + k0 + c] : 0.f;
+    }
+    __syncthreads();
+    u16* out = d.out + (int64_t)g * K * d.pad;
+    for (int e = threadIdx.x; e < 4096; e += 256) {
+      const int r = e >> 6, c = e & 63;  // r: k offset, c: o offset
+      if (k0 + r < K && o0 + c < d.pad) out[(int64_t)(k0 + r) * d.pad + o0 + c] = f2bf(tile[c][r]);
+    }
+    return;
+  }
+  // forward layout: out[g][o][r][s][i] (i padded) -- reads stay inside one filter row (cached)
   const FastDiv fpad = fastdiv_dev(d.pad), fs = fastdiv_dev(d.S), fr = fastdiv_dev(d.R);
-  const FastDiv fo = fastdiv_dev(d.mode == 0 ? d.Og : d.Ig);
+  const FastDiv fo = fastdiv_dev(d.Og);
   const uint32_t t0 = (uint32_t)ch.y * WPREP_CHUNK;
   const uint32_t t1 = (uint32_t)min(d.total, (int64_t)t0 + WPREP_CHUNK);
   for (uint32_t t = t0 + threadIdx.x; t < t1; t += 256) {
     uint32_t u = t, q;
-    q = fdiv(u, fpad); const int inner = (int)(u - q * d.pad); u = q;
+    q = fdiv(u, fpad); const int i = (int)(u - q * d.pad); u = q;
     q = fdiv(u, fs); const int s = (int)(u - q * d.S); u = q;
     q = fdiv(u, fr); const int r = (int)(u - q * d.R); u = q;
-    q = fdiv(u, fo); const int outer = (int)(u - q * (d.mode == 0 ? d.Og : d.Ig)); const int g = (int)q;
-    int o, i;
-    bool ok;
-    if (d.mode == 0) { i = inner; o = outer; ok = i < d.Ig; }
-    else { o = inner; i = outer; ok = o < d.Og; }
-    d.out[t] = ok ? f2bf(d.w[((((int64_t)(g * d.Og + o)) * d.Ig + i) * d.R + r) * d.S + s]) : (u16)0;
+    q = fdiv(u, fo); const int o = (int)(u - q * d.Og); const int g = (int)q;
+    d.out[t] = i < d.Ig ? f2bf(d.w[((((int64_t)(g * d.Og + o)) * d.Ig + i) * d.R + r) * d.S + s]) : (u16)0;
   }
 }
 

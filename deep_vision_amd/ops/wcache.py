@@ -64,7 +64,12 @@ def _build_table(device):
         total = G * (Og if mode == 0 else Ig) * R * S * pad
         di = len(descs)
         descs.append(struct.pack("<qqqiiiiiiii", p.data_ptr(), e[1].data_ptr(), total, G, Og, Ig, R, S, pad, mode, 0))
-        chunks += [(di, c) for c in range((total + chunk - 1) // chunk)]
+        if mode == 1:  # 64x64 transpose tiles per group (wprep_batched_kernel)
+            K = Ig * R * S
+            ntiles = G * ((K + 63) // 64) * ((pad + 63) // 64)
+        else:
+            ntiles = (total + chunk - 1) // chunk
+        chunks += [(di, c) for c in range(ntiles)]
         live.append(k)
     if not descs:
         return None

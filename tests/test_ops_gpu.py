@@ -379,3 +379,32 @@ def test_conv_act_grad_from_concat_slice():
     yr.backward(g)
     assert _cos(x.grad, xr.grad) > 0.999
     assert _cos(w1.grad, w1r.grad) > 0.999 and _cos(w2.grad, w2r.grad) > 0.999
+
+
+def test_batched_weight_prep_matches_per_layer():
+    """ops.wcache: one batched launch after the optimizer step == the per-layer wprep kernel."""
+    from deep_vision_amd.ops import wcache
+    from deep_vision_amd.ops.common import ptr, stream_handle
+    from deep_vision_amd.ops.conv import _prep_weight
+    from deep_vision_amd._ext import lib
+
+    wcache.clear()
+    cases = [((64, 32, 3, 3), 1, 32, 0), ((64, 32, 3, 3), 1, 64, 1), ((48, 24, 1, 1), 2, 24, 0),
+             ((48, 24, 1, 1), 2, 24, 1), ((100, 3, 7, 7), 1, 8, 0), ((100, 3, 7, 7), 1, 104, 1),
+             ((1000, 2048, 1, 1), 1, 2048, 0), ((1000, 2048, 1, 1), 1, 1000, 1)]
+    params = []
+    for shape, G, pad, mode in cases:
+        p = torch.nn.Parameter(torch.randn(*shape, device=DEV))
+        _prep_weight(p, G, pad, mode)  # registers the cache entry
+        params.append((p, G, pad, mode))
+    with torch.no_grad():
+        for p, *_ in params:
+            p.mul_(-1.5)  # version bump: the batched refresh must rewrite everything
+    wcache.after_step()
+    for p, G, pad, mode in params:
+        O, Ig, R, S = p.shape
+        ref = torch.empty(G * (O // G if mode == 0 else Ig) * R * S * pad, dtype=torch.bfloat16, device=DEV)
+        lib().wprep(ptr(p.detach()), ptr(ref), G, O // G, Ig, R, S, pad, mode, stream_handle())
+        got = _prep_weight(p, G, pad, mode)  # cache hit
+        assert torch.equal(got, ref), (p.shape, G, pad, mode)
+    wcache.clear()
