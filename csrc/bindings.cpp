@@ -56,12 +56,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_eval_prep", [](int C, float eps, uptr gamma, uptr beta, uptr rm, uptr rv, uptr scale, uptr shift, uptr st) {
     dv_bn_eval_prep(C, eps, CFP(gamma), CFP(beta), CFP(rm), CFP(rv), FP(scale), FP(shift), ST(st)); check_last("bn_eval_prep");
   });
-  m.def("bn_apply", [](uptr x, uptr res, uptr out, int64_t n, int C, uptr scale, uptr shift, int act, float slope, uptr st) {
-    dv_bn_apply(CP(x), CP(res), P(out), n, C, CFP(scale), CFP(shift), act, slope, ST(st)); check_last("bn_apply");
+  m.def("bn_apply", [](uptr x, uptr res, uptr out, int64_t n, int C, uptr scale, uptr shift, int act, float slope,
+                       uptr mask, uptr st) {
+    dv_bn_apply(CP(x), CP(res), P(out), n, C, CFP(scale), CFP(shift), act, slope, P(mask), ST(st)); check_last("bn_apply");
   });
   m.def("bn_bwd_reduce", [](uptr dout, uptr out, uptr x, int64_t rows, int C, uptr mean, uptr invstd, uptr mscale,
-                            uptr mshift, int act, float slope, uptr acc, uptr st) {
-    dv_bn_bwd_reduce(CP(dout), CP(out), CP(x), rows, C, CFP(mean), CFP(invstd), CFP(mscale), CFP(mshift), act, slope, FP(acc), ST(st));
+                            uptr mshift, int act, float slope, uptr acc, int mask_bits, uptr st) {
+    dv_bn_bwd_reduce(CP(dout), CP(out), CP(x), rows, C, CFP(mean), CFP(invstd), CFP(mscale), CFP(mshift), act, slope, FP(acc),
+                     mask_bits, ST(st));
     check_last("bn_bwd_reduce");
   });
   m.def("bn_bwd_finalize", [](uptr acc, int C, double count, uptr gamma, uptr mean, uptr invstd, uptr dgamma, uptr dbeta,
@@ -70,8 +72,9 @@ PYBIND11_MODULE(_C, m) {
     check_last("bn_bwd_finalize");
   });
   m.def("bn_bwd_apply", [](uptr dout, uptr out, uptr x, uptr dx, uptr dres, int64_t n, int C, uptr kA, uptr kB, uptr kC,
-                           uptr mscale, uptr mshift, int act, float slope, uptr st) {
-    dv_bn_bwd_apply(CP(dout), CP(out), CP(x), P(dx), P(dres), n, C, CFP(kA), CFP(kB), CFP(kC), CFP(mscale), CFP(mshift), act, slope, ST(st));
+                           uptr mscale, uptr mshift, int act, float slope, int mask_bits, uptr st) {
+    dv_bn_bwd_apply(CP(dout), CP(out), CP(x), P(dx), P(dres), n, C, CFP(kA), CFP(kB), CFP(kC), CFP(mscale), CFP(mshift), act, slope,
+                    mask_bits, ST(st));
     check_last("bn_bwd_apply");
   });
   m.def("bn_bwd_eval", [](uptr dout, uptr out, uptr dx, uptr dres, int64_t n, int C, uptr scale, int act, float slope, uptr st) {

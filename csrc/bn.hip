@@ -156,11 +156,11 @@ struct RowTile {
 };
 
 // ---- out = act(x*scale + shift (+res)) ----
-template <int VEC>
+template <int VEC, bool MB>
 __global__ __launch_bounds__(NT) void bn_apply_kernel(const u16* __restrict__ x, const u16* __restrict__ res,
                                                         u16* __restrict__ out, int64_t rows, int C, int64_t rows_per_block,
                                                         const float* __restrict__ scale, const float* __restrict__ shift,
-                                                        int act, float slope) {
+                                                        int act, float slope, uint8_t* __restrict__ mask) {
   RowTile t(C, VEC);
   if (t.lane_r >= t.rpi) return;
   const int64_t r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
@@ -174,13 +174,16 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const u16* __restrict__ x,
       float v[VEC], rv[VEC];
       VecIO<VEC>::load(x + o, v);
       if (res) VecIO<VEC>::load(res + o, rv);
+      uint32_t bits = 0;
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
         float z = fmaf(v[k], sc[k], sf[k]);
         if (res) z += rv[k];
+        if constexpr (MB) bits |= (z > 0.f ? 1u : 0u) << k;
         v[k] = act_fwd(z, act, slope);
       }
       VecIO<VEC>::store(out + o, v);
+      if constexpr (MB) mask[o >> 3] = (uint8_t)bits;  // activation mask, 1 bit per element (VEC == 8)
     }
   }
 }
@@ -188,7 +191,9 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const u16* __restrict__ x,
 // ---- backward reduce: sum dz, sum dz*xhat (xhat = (x-mean)*invstd) ----
 // The activation mask comes from the saved output `out` when present (residual blocks), else it
 // is recomputed from the BN input: z = x*mscale + mshift (one tensor read less per pass).
-enum { MM_NONE = 0, MM_OUT = 1, MM_X = 2 };  // activation-mask source (compile time: no branchy loads)
+enum { MM_NONE = 0, MM_OUT = 1, MM_X = 2, MM_BITS = 3 };  // activation-mask source (compile time: no branchy loads)
+// MM_BITS: the forward apply stored the mask as bits (VEC == 8: one byte per 8 channels), 1/16 of
+// the bytes of re-reading the bf16 output (residual blocks, where the mask cannot come from x)
 
 template <int VEC, int MM>
 __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(const u16* __restrict__ dout, const u16* __restrict__ out,
@@ -222,10 +227,13 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(const u16* __restrict
         VecIO<VEC>::load(dout + r * C + g * VEC, d);
         VecIO<VEC>::load(x + r * C + g * VEC, xv);
         if constexpr (MM == MM_OUT) VecIO<VEC>::load(out + r * C + g * VEC, o);
+        uint32_t mb = 0;
+        if constexpr (MM == MM_BITS) mb = reinterpret_cast<const uint8_t*>(out)[(r * C + g * VEC) >> 3];
 #pragma unroll
         for (int i = 0; i < VEC; ++i) {
           float dz = d[i];
           if constexpr (MM == MM_OUT) dz = act_bwd(d[i], o[i], act, slope);
+          if constexpr (MM == MM_BITS) dz = ((mb >> i) & 1u) ? d[i] : (act == 2 ? d[i] * slope : 0.f);
           if constexpr (MM == MM_X) dz = act_bwd(d[i], fmaf(xv[i], ms[i], mh[i]), act, slope);
           s[i] += dz; q[i] += dz * (xv[i] - mu[i]) * is[i];
         }
@@ -297,10 +305,13 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const u16* __restrict_
       VecIO<VEC>::load(dout + o, d);
       VecIO<VEC>::load(x + o, xv);
       if constexpr (MM == MM_OUT) VecIO<VEC>::load(out + o, ov);
+      uint32_t mb = 0;
+      if constexpr (MM == MM_BITS) mb = reinterpret_cast<const uint8_t*>(out)[o >> 3];
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
         float dz = d[k];
         if constexpr (MM == MM_OUT) dz = act_bwd(d[k], ov[k], act, slope);
+        if constexpr (MM == MM_BITS) dz = ((mb >> k) & 1u) ? d[k] : (act == 2 ? d[k] * slope : 0.f);
         if constexpr (MM == MM_X) dz = act_bwd(d[k], fmaf(xv[k], ms[k], mh[k]), act, slope);
         rr[k] = dz;
         d[k] = fmaf(a[k], dz, fmaf(b[k], xv[k], cc[k]));
@@ -382,12 +393,20 @@ void dv_bn_eval_prep(int C, float eps, const float* gamma, const float* beta, co
 }
 
 void dv_bn_apply(const void* x, const void* res, void* out, int64_t n, int C, const float* scale, const float* shift,
-                 int act, float slope, hipStream_t st) {
+                 int act, float slope, void* mask, hipStream_t st) {
   const int v = vec_for(C);
   const int64_t rows = n / C;
   const int64_t rpb = apply_rows_per_block(rows, C, v);
   const int g = (int)((rows + rpb - 1) / rpb);
-  DISPATCH_VEC(C, bn_apply_kernel, <<<g, NT, 0, st>>>((const u16*)x, (const u16*)res, (u16*)out, rows, C, rpb, scale, shift, act, slope))
+#define AP_ARGS <<<g, NT, 0, st>>>((const u16*)x, (const u16*)res, (u16*)out, rows, C, rpb, scale, shift, act, slope, (uint8_t*)mask)
+  if (mask && v == 8) { bn_apply_kernel<8, true> AP_ARGS; return; }
+  switch (v) {
+    case 8: bn_apply_kernel<8, false> AP_ARGS; break;
+    case 4: bn_apply_kernel<4, false> AP_ARGS; break;
+    case 2: bn_apply_kernel<2, false> AP_ARGS; break;
+    default: bn_apply_kernel<1, false> AP_ARGS; break;
+  }
+#undef AP_ARGS
 }
 
 template <int MM>
@@ -404,8 +423,13 @@ static void bwd_reduce_launch(int g, const void* dout, const void* out, const vo
 
 void dv_bn_bwd_reduce(const void* dout, const void* out, const void* x, int64_t rows, int C, const float* mean,
                       const float* invstd, const float* mscale, const float* mshift, int act, float slope, float* acc,
-                      hipStream_t st) {
+                      int mask_bits, hipStream_t st) {
   const int g = reduce_grid(rows);
+  if (act && mask_bits && vec_for(C) == 8) {
+    bn_bwd_reduce_kernel<8, MM_BITS><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, rows, C, mean,
+                                                         invstd, mscale, mshift, act, slope, acc);
+    return;
+  }
   if (!act) bwd_reduce_launch<MM_NONE>(g, dout, out, x, rows, C, mean, invstd, mscale, mshift, act, slope, acc, st);
   else if (out) bwd_reduce_launch<MM_OUT>(g, dout, out, x, rows, C, mean, invstd, mscale, mshift, act, slope, acc, st);
   else bwd_reduce_launch<MM_X>(g, dout, out, x, rows, C, mean, invstd, mscale, mshift, act, slope, acc, st);
@@ -433,11 +457,16 @@ static void bwd_apply_launch(int g, const void* dout, const void* out, const voi
 
 void dv_bn_bwd_apply(const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t n, int C,
                      const float* kA, const float* kB, const float* kC, const float* mscale, const float* mshift, int act,
-                     float slope, hipStream_t st) {
+                     float slope, int mask_bits, hipStream_t st) {
   const int v = vec_for(C);
   const int64_t rows = n / C;
   const int64_t rpb = apply_rows_per_block(rows, C, v);
   const int g = (int)((rows + rpb - 1) / rpb);
+  if (act && mask_bits && v == 8) {
+    bn_bwd_apply_kernel<8, MM_BITS><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, (u16*)dx,
+                                                        (u16*)dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope);
+    return;
+  }
   if (!act) bwd_apply_launch<MM_NONE>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, st);
   else if (out) bwd_apply_launch<MM_OUT>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, st);
   else bwd_apply_launch<MM_X>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, st);

@@ -45,15 +45,15 @@ void dv_bn_finalize(float* acc, int C, double count, float eps, float momentum, 
 void dv_bn_eval_prep(int C, float eps, const float* gamma, const float* beta, const float* rm, const float* rv,
                      float* scale, float* shift, hipStream_t st);
 void dv_bn_apply(const void* x, const void* res, void* out, int64_t n, int C, const float* scale, const float* shift,
-                 int act, float slope, hipStream_t st);
+                 int act, float slope, void* mask, hipStream_t st);
 void dv_bn_bwd_reduce(const void* dout, const void* out, const void* x, int64_t rows, int C, const float* mean,
                       const float* invstd, const float* mscale, const float* mshift, int act, float slope, float* acc,
-                      hipStream_t st);
+                      int mask_bits, hipStream_t st);
 void dv_bn_bwd_finalize(float* acc, int C, double count, const float* gamma, const float* mean, const float* invstd,
                         float* dgamma, float* dbeta, int accumulate, float* kA, float* kB, float* kC, hipStream_t st);
 void dv_bn_bwd_apply(const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t n, int C,
                      const float* kA, const float* kB, const float* kC, const float* mscale, const float* mshift, int act,
-                     float slope, hipStream_t st);
+                     float slope, int mask_bits, hipStream_t st);
 void dv_bn_bwd_eval(const void* dout, const void* out, void* dx, void* dres, int64_t n, int C, const float* scale,
                     int act, float slope, hipStream_t st);
 

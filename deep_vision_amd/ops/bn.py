@@ -56,11 +56,16 @@ class _BNActFn(torch.autograd.Function):
                 mean.copy_(running_mean)
                 torch.rsqrt(running_var + eps, out=invstd)
         out = torch.empty_like(x)
-        L.bn_apply(ptr(x), ptr(residual), ptr(out), x.numel(), C, ptr(scale), ptr(shift), act, float(slope), st)
-        # activation mask in backward: from the saved output when a residual was added, else
-        # recomputed from x (z = x*scale + shift) so the output is not kept alive / re-read
-        keep_out = bool(act) and residual is not None
-        ctx.save_for_backward(x, out if keep_out else None, weight, bias, prm)
+        # activation mask in backward: recomputed from x (z = x*scale + shift) when there is no
+        # residual; with a residual it is stored as bits by this pass (training, C % 8 == 0) or,
+        # failing that, read back from the saved output
+        bits = training and bool(act) and residual is not None and C % 8 == 0
+        mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=dev) if bits else None
+        L.bn_apply(ptr(x), ptr(residual), ptr(out), x.numel(), C, ptr(scale), ptr(shift), act, float(slope), ptr(mask),
+                   st)
+        keep_out = bool(act) and residual is not None and not bits
+        ctx.save_for_backward(x, mask if bits else (out if keep_out else None), weight, bias, prm)
+        ctx.bits = bits
         ctx.cfg = (training, act, slope, residual is not None)
         ctx.ws_bwd = ws_bwd
         ctx.join = join
@@ -88,7 +93,7 @@ class _BNActFn(torch.autograd.Function):
             rows = N * H * W
             acc = ctx.ws_bwd if ctx.ws_bwd is not None else torch.zeros((STAT_SHARDS, 2, C), dtype=F32, device=dev)
             L.bn_bwd_reduce(ptr(dout), ptr(out), ptr(x), rows, C, ptr(mean), ptr(invstd), ptr(scale), ptr(shift), act,
-                            float(slope), ptr(acc), st)
+                            float(slope), ptr(acc), int(ctx.bits), st)
             sg = grad_sink(weight) if ctx.needs_input_grad[2] else None
             sb = grad_sink(bias) if ctx.needs_input_grad[3] else None
             direct = sg is not None and sb is not None
@@ -101,11 +106,11 @@ class _BNActFn(torch.autograd.Function):
                               ptr(coef[0]), ptr(coef[1]), ptr(coef[2]), st)
         if training:
             L.bn_bwd_apply(ptr(dout), ptr(out), ptr(x), ptr(dx), ptr(dres), x.numel(), C, ptr(coef[0]), ptr(coef[1]),
-                           ptr(coef[2]), ptr(scale), ptr(shift), act, float(slope), st)
+                           ptr(coef[2]), ptr(scale), ptr(shift), act, float(slope), int(ctx.bits), st)
         else:
             if act and out is None:  # eval backward needs the mask: rebuild the output
                 out = torch.empty_like(x)
-                L.bn_apply(ptr(x), 0, ptr(out), x.numel(), C, ptr(scale), ptr(shift), act, float(slope), st)
+                L.bn_apply(ptr(x), 0, ptr(out), x.numel(), C, ptr(scale), ptr(shift), act, float(slope), 0, st)
             L.bn_bwd_eval(ptr(dout), ptr(out), ptr(dx), ptr(dres), x.numel(), C, ptr(scale), act, float(slope), st)
         if direct:
             notify_grad_ready(weight)
