@@ -36,11 +36,13 @@ PYBIND11_MODULE(_C, m) {
     if (r != 0) throw std::runtime_error("conv_fwd: unsupported geometry (channels must be a multiple of 8)");
     check_last("conv_fwd");
   });
+  m.def("conv_fwd_variant", [](int v) { dv_conv_fwd_variant(v); });
+  m.def("conv_wgrad_tuning", [](int v, int split_pct) { dv_conv_wgrad_tuning(v, split_pct); });
   m.def("conv_wgrad", [](uptr x, uptr dy, uptr dw, int Nb, int H, int W, int Cg, int ldx, int G, int Kout, int P_, int Q,
                          int ldy, int R, int S, int sh, int sw, int ph, int pw, int dh, int dwl, int splits, int accumulate,
-                         uptr st) {
+                         int oirs_ig, uptr st) {
     ConvWgradArgs a{CP(x), CP(dy), FP(dw), Nb, H, W, Cg, ldx, G, Kout, P_, Q, ldy, R, S, sh, sw, ph, pw, dh, dwl, splits,
-                    accumulate};
+                    accumulate, oirs_ig};
     int r = dv_conv_wgrad(a, ST(st));
     if (r < 0) throw std::runtime_error("conv_wgrad: unsupported geometry (channels must be a multiple of 8)");
     check_last("conv_wgrad");
@@ -107,8 +109,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("add", [](uptr a, uptr b, uptr y, int64_t n, float alpha, float beta, int act, float slope, uptr st) { dv_add(CP(a), CP(b), P(y), n, alpha, beta, act, slope, ST(st)); check_last("add"); });
   m.def("dropout", [](uptr x, uptr y, int64_t n, float p, uint64_t seed, uptr st) { dv_dropout(CP(x), P(y), n, p, seed, ST(st)); check_last("dropout"); });
   m.def("wprep", [](uptr w, uptr out, int G, int Og, int Ig, int R, int S, int Ipad, int mode, uptr st) { dv_wprep(CFP(w), P(out), G, Og, Ig, R, S, Ipad, mode, ST(st)); check_last("wprep"); });
-  m.def("wgrad_unprep", [](uptr src, uptr dst, int G, int Og, int Ig, int R, int S, int Ipad, float alpha, int accumulate, uptr st) {
-    dv_wgrad_unprep(CFP(src), FP(dst), G, Og, Ig, R, S, Ipad, alpha, accumulate, ST(st)); check_last("wgrad_unprep");
+  m.def("wgrad_unprep", [](uptr src, uptr dst, int G, int Og, int Ig, int R, int S, int Ipad, float alpha, int accumulate,
+                           int zero_src, uptr st) {
+    dv_wgrad_unprep(FP(src), FP(dst), G, Og, Ig, R, S, Ipad, alpha, accumulate, zero_src, ST(st)); check_last("wgrad_unprep");
   });
   m.def("to_nhwc", [](uptr x, int is_f32, uptr y, int N, int C, int H, int W, int Cp, uptr st) { dv_to_nhwc(CP(x), is_f32, P(y), N, C, H, W, Cp, ST(st)); check_last("to_nhwc"); });
   m.def("f32_to_bf16", [](uptr x, uptr y, int64_t n, uptr st) { dv_f32_to_bf16(CFP(x), P(y), n, ST(st)); check_last("f32_to_bf16"); });

@@ -105,20 +105,47 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(const u16* __restrict__ x,
   }
 }
 
+// Fold the SHARDS partial (a, b) pairs of channel blockIdx.x*64 + (tid & 63) and re-zero them
+// (the accumulator is persistent and self-cleaning: no memset launch). 256 threads = 64 channels
+// x 4 shard groups, so each thread issues 16 independent coalesced loads instead of a serial
+// 64-deep chain. Returns true on the thread that holds the channel's totals.
+DV_DEVICE bool fold_shards(float* __restrict__ acc, int C, double& s, double& q) {
+  __shared__ double red[2][4][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  constexpr int PER = SHARDS / 4;
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    float va[PER], vb[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const float* p = acc + (int64_t)(grp * PER + i) * 2 * C + c;
+      va[i] = p[0]; vb[i] = p[C];
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      float* p = acc + (int64_t)(grp * PER + i) * 2 * C + c;
+      p[0] = 0.f; p[C] = 0.f;
+      a += va[i]; b += vb[i];
+    }
+  }
+  red[0][grp][cl] = a; red[1][grp][cl] = b;
+  __syncthreads();
+  if (grp != 0 || c >= C) return false;
+  s = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
+  q = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+  return true;
+}
+
 // ---- fold shards -> mean/invstd/scale/shift, update running stats ----
 __global__ void bn_finalize_kernel(float* __restrict__ acc, int C, double count, float eps,
                                    float momentum, const float* __restrict__ gamma, const float* __restrict__ beta,
                                    float* __restrict__ running_mean, float* __restrict__ running_var,
                                    float* __restrict__ save_mean, float* __restrict__ save_invstd,
                                    float* __restrict__ scale, float* __restrict__ shift) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  // fold and re-zero the shards: the accumulator is persistent and self-cleaning (no memset launch)
-  for (int i = 0; i < SHARDS; ++i) {
-    float* a = acc + (int64_t)i * 2 * C + c;
-    s += a[0]; q += a[C]; a[0] = 0.f; a[C] = 0.f;
-  }
+  double s, q;
+  if (!fold_shards(acc, C, s, q)) return;
+  const int c = blockIdx.x * 64 + threadIdx.x;
   const double mean = s / count;
   double var = q / count - mean * mean;
   if (var < 0) var = 0;
@@ -263,13 +290,9 @@ __global__ void bn_bwd_finalize_kernel(float* __restrict__ acc, int C, double co
                                        const float* __restrict__ mean, const float* __restrict__ invstd,
                                        float* __restrict__ dgamma, float* __restrict__ dbeta, int accumulate,
                                        float* __restrict__ kA, float* __restrict__ kB, float* __restrict__ kC) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int i = 0; i < SHARDS; ++i) {
-    float* a = acc + (int64_t)i * 2 * C + c;
-    s += a[0]; q += a[C]; a[0] = 0.f; a[C] = 0.f;
-  }
+  double s, q;
+  if (!fold_shards(acc, C, s, q)) return;
+  const int c = blockIdx.x * 64 + threadIdx.x;
   if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)s : (float)s;
   if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)q : (float)q;
   const double mdz = s / count, mdzx = q / count;
@@ -383,7 +406,7 @@ void dv_bn_stats(const void* x, int64_t rows, int C, float* acc, hipStream_t st)
 void dv_bn_finalize(float* acc, int C, double count, float eps, float momentum, const float* gamma,
                     const float* beta, float* rm, float* rv, float* save_mean, float* save_invstd, float* scale,
                     float* shift, hipStream_t st) {
-  bn_finalize_kernel<<<(C + 255) / 256, 256, 0, st>>>(acc, C, count, eps, momentum, gamma, beta, rm, rv, save_mean,
+  bn_finalize_kernel<<<(C + 63) / 64, 256, 0, st>>>(acc, C, count, eps, momentum, gamma, beta, rm, rv, save_mean,
                                                       save_invstd, scale, shift);
 }
 
@@ -437,7 +460,7 @@ void dv_bn_bwd_reduce(const void* dout, const void* out, const void* x, int64_t 
 
 void dv_bn_bwd_finalize(float* acc, int C, double count, const float* gamma, const float* mean, const float* invstd,
                         float* dgamma, float* dbeta, int accumulate, float* kA, float* kB, float* kC, hipStream_t st) {
-  bn_bwd_finalize_kernel<<<(C + 255) / 256, 256, 0, st>>>(acc, C, count, gamma, mean, invstd, dgamma, dbeta, accumulate,
+  bn_bwd_finalize_kernel<<<(C + 63) / 64, 256, 0, st>>>(acc, C, count, gamma, mean, invstd, dgamma, dbeta, accumulate,
                                                           kA, kB, kC);
 }
 

@@ -70,7 +70,15 @@ DV_DEVICE bf16x8 read_kc(const char* img, int row, int chunk) {
 template <int BM_, int BN_, int BK_>
 constexpr int stage_bytes() { return (BM_ + BN_) * BK_ * 2; }
 
-template <int BM_, int BN_, int BK_, int KMODE, bool RES>
+// s_waitcnt vmcnt(N) with expcnt / lgkmcnt left at their maxima (gfx9 encoding: vmcnt bits
+// [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8]).
+template <int N>
+DV_DEVICE void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | (0x7 << 4) | (0xF << 8) | ((N >> 4) << 14));
+}
+
+template <int BM_, int BN_, int BK_, int KMODE, bool RES, int STAGES>
 __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
   constexpr int WN = BN_ / 64, WM = BM_ / 64;
   static_assert(WN * WM == 4, "4 waves of 64x64");
@@ -190,14 +198,8 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
     for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nt = (p.K + BK_ - 1) / BK_;
-  stage(0, 0);
-  advance();
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int t = 0; t < nt; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < nt) { stage(t + 1, cur ^ 1); advance(); }
-    const char* img_n = smem + cur * STAGE;
+  auto compute = [&](int buf) {
+    const char* img_n = smem + buf * STAGE;
     const char* img_m = img_n + BN_ * BK_ * 2;
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
@@ -213,8 +215,42 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
         for (int i = 0; i < 4; ++i)
           acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[j], fb[i], acc[j][i], 0, 0, 0);
     }
+  };
+  if constexpr (STAGES == 2) {
+    // double buffer, one barrier per K-tile: the DMA of tile t+1 overlaps the MFMAs of tile t
+    stage(0, 0);
+    advance();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    for (int t = 0; t < nt; ++t) {
+      const int cur = t & 1;
+      if (t + 1 < nt) { stage(t + 1, cur ^ 1); advance(); }
+      compute(cur);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
+    // STAGES-deep ring: STAGES-2 tiles stay in flight across each barrier. A counted vmcnt
+    // retires only tile t's DMAs (IPT per wave per tile, issued in order) and the raw s_barrier
+    // does not drain the younger ones (__syncthreads() would emit vmcnt(0)).
+    constexpr int IPT = MI + NI;
+#pragma unroll
+    for (int s = 0; s < STAGES - 1; ++s)
+      if (s < nt) { stage(s, s); advance(); }
+    int cur = 0, nxt = STAGES - 1;
+    for (int t = 0; t < nt; ++t) {
+      const int ahead = min(nt - 1, t + STAGES - 2) - t;  // tiles issued after t
+      if (ahead >= STAGES - 2) wait_vm<(STAGES - 2) * IPT>();
+      else if (STAGES > 3 && ahead == 1) wait_vm<IPT>();
+      else wait_vm<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (t + STAGES - 1 < nt) { stage(t + STAGES - 1, nxt); advance(); }
+      compute(cur);
+      cur = cur + 1 == STAGES ? 0 : cur + 1;
+      nxt = nxt + 1 == STAGES ? 0 : nxt + 1;
+    }
+    __syncthreads();  // every DMA retired (vmcnt(0) on the last tile): smem is free for the epilogue
   }
 
   // ---------------- epilogue ----------------
@@ -321,40 +357,75 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
   }
 }
 
+// the epilogue staging tile and the statistics scratch reuse the (drained) operand stages
 template <int BM_, int BN_, int BK_>
 constexpr int lds_bytes(int stages) {
-  return (stages * stage_bytes<BM_, BN_, BK_>() > EPI_BYTES ? stages * stage_bytes<BM_, BN_, BK_>() : EPI_BYTES) +
-         STAT_BYTES;
+  return stages * stage_bytes<BM_, BN_, BK_>() > EPI_BYTES + STAT_BYTES ? stages * stage_bytes<BM_, BN_, BK_>()
+                                                                       : EPI_BYTES + STAT_BYTES;
 }
 
-template <int BM_, int BN_, int BK_, int KMODE, bool RES>
+template <int BM_, int BN_, int BK_, int KMODE, bool RES, int STAGES>
 void launch_fwd(const FwdParams& p, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        lds_bytes<BM_, BN_, BK_>(2));
+    hipFuncSetAttribute((const void*)conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes<BM_, BN_, BK_>(STAGES));
     attr = true;
   }
   const int nt = (p.K + BK_ - 1) / BK_;
-  const size_t lds = lds_bytes<BM_, BN_, BK_>(nt > 1 ? 2 : 1);
+  const size_t lds = lds_bytes<BM_, BN_, BK_>(nt < STAGES ? nt : STAGES);
   const int blocks = ((p.M + BM_ - 1) / BM_) * ((p.N + BN_ - 1) / BN_) * p.G;
-  conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES><<<dim3(blocks), dim3(NT), lds, st>>>(p);
+  conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES><<<dim3(blocks), dim3(NT), lds, st>>>(p);
+}
+
+int g_fwd_variant = 0;  // benchmarking override of the tile / pipeline choice (0 = heuristic)
+
+template <int KMODE, bool RES>
+void dispatch_res(const FwdParams& p, hipStream_t st) {
+  if constexpr (KMODE == KM_FAST) {
+    switch (g_fwd_variant) {
+      case 1: return launch_fwd<128, 128, 64, KMODE, RES, 2>(p, st);
+      case 2: return launch_fwd<256, 64, 32, KMODE, RES, 2>(p, st);
+      case 3: return launch_fwd<256, 64, 64, KMODE, RES, 2>(p, st);
+      case 4: return launch_fwd<128, 128, 64, KMODE, RES, 3>(p, st);
+      case 5: return launch_fwd<256, 64, 32, KMODE, RES, 4>(p, st);
+      case 6: return launch_fwd<256, 64, 64, KMODE, RES, 3>(p, st);
+      case 7: return launch_fwd<128, 128, 32, KMODE, RES, 4>(p, st);
+      case 8: return launch_fwd<128, 128, 32, KMODE, RES, 2>(p, st);
+      case 9: return launch_fwd<256, 64, 32, KMODE, RES, 3>(p, st);
+      default: break;
+    }
+  }
+  // Tile choice measured on the ResNet-50 layer set (tools/bench_conv.py, profiles/convbench_*):
+  //  * N <= 64: a 256x64 tile keeps every MFMA useful; short K (<= 256, HBM-bound 1x1 layers)
+  //    runs best with a 3-deep ring, long K with the plain double buffer;
+  //  * N > 64: 128x128. K <= 64 is one K-tile (single stage, most blocks per CU); up to K < 2048
+  //    BK=32 (32 KB of LDS: up to 4 blocks per CU) beats BK=64 by 5-25 %; long-K layers (3x3 x
+  //    256+ channels, 2048-deep 1x1) keep BK=64.
+  if (KMODE == KM_FAST) {
+    if (p.N <= 64) {
+      if (p.K <= 256) launch_fwd<256, 64, 32, KMODE, RES, 3>(p, st);
+      else launch_fwd<256, 64, 32, KMODE, RES, 2>(p, st);
+    } else {
+      if (p.K > 64 && p.K < 2048) launch_fwd<128, 128, 32, KMODE, RES, 2>(p, st);
+      else launch_fwd<128, 128, 64, KMODE, RES, 2>(p, st);
+    }
+    return;
+  }
+  if (p.N <= 64) launch_fwd<256, 64, 32, KMODE, RES, 2>(p, st);
+  else launch_fwd<128, 128, 64, KMODE, RES, 2>(p, st);
 }
 
 template <int KMODE>
 void dispatch_tile(const FwdParams& p, hipStream_t st) {
-  // 64-channel outputs: a 256x64 tile keeps every MFMA useful; BK=32 keeps two stages at
-  // 40 KB so three blocks share a CU.
-  if (p.res) {  // in-place gradient accumulation epilogue (compile-time: no cost for the others)
-    if (p.N <= 64) launch_fwd<256, 64, 32, KMODE, true>(p, st);
-    else launch_fwd<128, 128, 64, KMODE, true>(p, st);
-  } else {
-    if (p.N <= 64) launch_fwd<256, 64, 32, KMODE, false>(p, st);
-    else launch_fwd<128, 128, 64, KMODE, false>(p, st);
-  }
+  // in-place gradient accumulation epilogue is compile-time: no cost for the others
+  if (p.res) dispatch_res<KMODE, true>(p, st);
+  else dispatch_res<KMODE, false>(p, st);
 }
 
 }  // namespace
+
+void dv_conv_fwd_variant(int v) { g_fwd_variant = v; }
 
 int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
   FwdParams p{};

@@ -20,7 +20,7 @@
 
 namespace {
 
-constexpr int BK = 64;  // pixels per K-tile
+constexpr int BK = 64;  // pixels per K-tile of the split bookkeeping (kernels may use BKW = 32)
 constexpr int NT = 256;
 constexpr int F32_PAD = 4;
 
@@ -33,6 +33,7 @@ struct WgParams {
   int P, Q;
   int R, S, sh, sw, ph, pw, dh, dw_;
   int splits, ktiles_per_split, atomic_out, accumulate;
+  int oirs_ig;  // > 0: write dW straight into the parameter layout [G*M][oirs_ig][R][S]
   FastDiv div_pq, div_q, div_cg, div_s;
 };
 
@@ -62,7 +63,13 @@ DV_DEVICE bf16x8 read_mn(const char* img, int col0, int kbase, int lane) {
   return __builtin_bit_cast(bf16x8, r);
 }
 
-template <int BM_, int BN_, bool PLAIN>
+template <int N>
+DV_DEVICE void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | (0x7 << 4) | (0xF << 8) | ((N >> 4) << 14));
+}
+
+template <int BM_, int BN_, bool PLAIN, int BK = 64, int STAGES = 2>
 __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgParams p) {
   constexpr int WN = BN_ / 64, WM = BM_ / 64;
   static_assert(WN * WM == 4, "4 waves of 64x64");
@@ -170,33 +177,58 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgParams p) {
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nt > 0) {
-    stage(kt0, 0);
-    advance();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int t = 0; t < nt; ++t) {
-      const int cur = t & 1;
-      if (t + 1 < nt) { stage(kt0 + t + 1, cur ^ 1); advance(); }
-      const char* img_m = smem + cur * STAGE;
-      const char* img_n = img_m + MBYTES;
+  auto compute = [&](int buf) {
+    const char* img_m = smem + buf * STAGE;
+    const char* img_n = img_m + MBYTES;
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        bf16x8 fa[4], fb[4];
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 fa[4], fb[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          fa[j] = read_mn<BN_>(img_n, wave_n * 64 + j * 16, kk * 32, lane);
-          fb[j] = read_mn<BM_>(img_m, wave_m * 64 + j * 16, kk * 32, lane);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[j], fb[i], acc[j][i], 0, 0, 0);
+      for (int j = 0; j < 4; ++j) {
+        fa[j] = read_mn<BN_>(img_n, wave_n * 64 + j * 16, kk * 32, lane);
+        fb[j] = read_mn<BM_>(img_m, wave_m * 64 + j * 16, kk * 32, lane);
       }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[j], fb[i], acc[j][i], 0, 0, 0);
+    }
+  };
+  if constexpr (STAGES == 2) {
+    if (nt > 0) {
+      stage(kt0, 0);
+      advance();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      for (int t = 0; t < nt; ++t) {
+        const int cur = t & 1;
+        if (t + 1 < nt) { stage(kt0 + t + 1, cur ^ 1); advance(); }
+        compute(cur);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
     }
+  } else {
+    // STAGES-deep ring (see conv_fwd.hip): counted vmcnt + raw barrier keep STAGES-2 tiles in flight
+    constexpr int IPT = MI + NI;
+#pragma unroll
+    for (int s = 0; s < STAGES - 1; ++s)
+      if (s < nt) { stage(kt0 + s, s); advance(); }
+    int cur = 0, nxt = STAGES - 1;
+    for (int t = 0; t < nt; ++t) {
+      const int ahead = min(nt - 1, t + STAGES - 2) - t;
+      if (ahead >= STAGES - 2) wait_vm<(STAGES - 2) * IPT>();
+      else if (STAGES > 3 && ahead == 1) wait_vm<IPT>();
+      else wait_vm<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (t + STAGES - 1 < nt) { stage(kt0 + t + STAGES - 1, nxt); advance(); }
+      compute(cur);
+      cur = cur + 1 == STAGES ? 0 : cur + 1;
+      nxt = nxt + 1 == STAGES ? 0 : nxt + 1;
+    }
+    __syncthreads();
   }
 
   // ---- epilogue: fp32 tile through LDS, then 256-B row segments (atomic or plain) ----
@@ -212,16 +244,28 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgParams p) {
       *reinterpret_cast<f32x4*>(&T[ml * LD + nl]) = acc[j][i];
     }
   __syncthreads();
-  float* dwp = p.dw + (int64_t)grp * p.M * p.N;
+  // destination of column n: packed [G][M][N] row offset n, or the parameter's OIRS position
+  // (n = (r, s, c) -> c*R*S + r*S + s; padded channels c >= oirs_ig are dropped)
+  const int64_t row_stride = p.oirs_ig > 0 ? (int64_t)p.oirs_ig * p.R * p.S : p.N;
+  float* dwp = p.dw + (int64_t)grp * p.M * row_stride;
+  int64_t coff[BN_ / 64];
+#pragma unroll
+  for (int h = 0; h < BN_ / 64; ++h) {
+    const int n = n0 + h * 64 + lane;
+    coff[h] = n < p.N ? n : -1;
+    if (p.oirs_ig > 0 && n < p.N) {
+      const int rs = (int)fdiv((uint32_t)n, p.div_cg), c = n - rs * p.Cg;
+      coff[h] = c < p.oirs_ig ? (int64_t)c * p.R * p.S + rs : -1;
+    }
+  }
   for (int rr = wid; rr < BM_; rr += 4) {
     const int m = m0 + rr;
     if (m >= p.M) break;
 #pragma unroll
     for (int h = 0; h < BN_ / 64; ++h) {
-      const int nl = h * 64 + lane, n = n0 + nl;
-      if (n < p.N) {
-        const float v = T[rr * LD + nl];
-        float* dst = dwp + (int64_t)m * p.N + n;
+      if (coff[h] >= 0) {
+        const float v = T[rr * LD + h * 64 + lane];
+        float* dst = dwp + (int64_t)m * row_stride + coff[h];
         if (p.atomic_out) atomicAdd(dst, v);
         else *dst = p.accumulate ? *dst + v : v;
       }
@@ -229,22 +273,46 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgParams p) {
   }
 }
 
-template <int BM_, int BN_>
+template <int BM_, int BN_, int BKW, int STAGES>
 constexpr int wg_lds_bytes() {
-  constexpr int st = 2 * BK * (BM_ + BN_) * 2, ep = BM_ * (BN_ + F32_PAD) * 4;
+  constexpr int st = STAGES * BKW * (BM_ + BN_) * 2, ep = BM_ * (BN_ + F32_PAD) * 4;
   return st > ep ? st : ep;
 }
 
-template <int BM_, int BN_, bool PLAIN>
-void launch_wg(const WgParams& p, int blocks, hipStream_t st) {
+// p.ktiles_per_split arrives in 64-pixel units; BKW = 32 kernels walk twice as many tiles
+template <int BM_, int BN_, bool PLAIN, int BKW = 64, int STAGES = 2>
+void launch_wg(WgParams p, int blocks, hipStream_t st) {
   static bool attr = false;
+  constexpr int lds = wg_lds_bytes<BM_, BN_, BKW, STAGES>();
   if (!attr) {
-    hipFuncSetAttribute((const void*)conv_wgrad_kernel<BM_, BN_, PLAIN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        wg_lds_bytes<BM_, BN_>());
+    hipFuncSetAttribute((const void*)conv_wgrad_kernel<BM_, BN_, PLAIN, BKW, STAGES>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  constexpr int lds = wg_lds_bytes<BM_, BN_>();
-  conv_wgrad_kernel<BM_, BN_, PLAIN><<<dim3(blocks), dim3(NT), lds, st>>>(p);
+  p.ktiles_per_split *= BK / BKW;
+  conv_wgrad_kernel<BM_, BN_, PLAIN, BKW, STAGES><<<dim3(blocks), dim3(NT), lds, st>>>(p);
+}
+
+// 64x256 tiles only when the weight gradient is 64 rows by >= 256 columns (else 3/4 of the tile idles)
+inline bool wg_narrow(int M, int N) { return M <= 64 && N >= 256; }
+
+int g_wg_variant = 0;       // benchmarking override of tile / K-depth / pipeline (0 = heuristic)
+int g_wg_split_pct = 100;   // benchmarking scale of the split-K heuristic
+
+template <bool PLAIN>
+void dispatch_wg(const WgParams& p, int blocks_narrow, int blocks_wide, hipStream_t st) {
+  switch (g_wg_variant) {
+    case 1: return launch_wg<128, 128, PLAIN, 64, 2>(p, blocks_wide, st);
+    case 2: return launch_wg<64, 256, PLAIN, 64, 2>(p, blocks_narrow, st);
+    case 3: return launch_wg<128, 128, PLAIN, 32, 2>(p, blocks_wide, st);
+    case 4: return launch_wg<64, 256, PLAIN, 32, 2>(p, blocks_narrow, st);
+    case 5: return launch_wg<128, 128, PLAIN, 32, 4>(p, blocks_wide, st);
+    case 6: return launch_wg<64, 256, PLAIN, 32, 4>(p, blocks_narrow, st);
+    case 7: return launch_wg<128, 128, PLAIN, 64, 3>(p, blocks_wide, st);
+    default: break;
+  }
+  if (wg_narrow(p.M, p.N)) launch_wg<64, 256, PLAIN>(p, blocks_narrow, st);
+  else launch_wg<128, 128, PLAIN>(p, blocks_wide, st);
 }
 
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
@@ -253,15 +321,23 @@ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 int dv_conv_wgrad_splits(const ConvWgradArgs& a) {
   const int M = a.Kout, N = a.R * a.S * a.Cg, K = a.Nb * a.P * a.Q;
-  const bool narrow = M <= 64;
+  const bool narrow = g_wg_variant == 2 || g_wg_variant == 4 || g_wg_variant == 6 ||
+                      (g_wg_variant == 0 && wg_narrow(M, N));
   const int tiles = cdiv(M, narrow ? 64 : 128) * cdiv(N, narrow ? 256 : 128) * a.G;
   const int ktiles = cdiv(K, BK);
-  int splits = cdiv(768, tiles);                        // ~3 blocks per CU
-  splits = std::min(splits, std::max(1, ktiles / 32));  // >= 2048 pixels per split (atomic budget)
+  // ~1.5 blocks per CU: measured 5-15 % faster than 3 per CU on the ResNet-50 3x3 / strided
+  // layers (half the atomic epilogues), equal on the rest (profiles/wgbench_variants.txt)
+  int splits = cdiv(384 * g_wg_split_pct / 100, tiles);
+  splits = std::min(splits, std::max(1, ktiles / 32));   // >= 2048 pixels per split (atomic budget)
   return std::max(1, std::min(splits, ktiles));
 }
 
 int dv_conv_stats_tiles(int Nb, int P, int Q) { return cdiv(Nb * P * Q, 128); }
+
+void dv_conv_wgrad_tuning(int variant, int split_pct) {
+  g_wg_variant = variant;
+  g_wg_split_pct = split_pct > 0 ? split_pct : 100;
+}
 
 int dv_conv_wgrad(const ConvWgradArgs& a, hipStream_t st) {
   WgParams p{};
@@ -281,16 +357,16 @@ int dv_conv_wgrad(const ConvWgradArgs& a, hipStream_t st) {
   p.splits = cdiv(ktiles, p.ktiles_per_split);
   p.atomic_out = p.splits > 1 ? 1 : 0;
   p.accumulate = a.accumulate;
-  if (p.atomic_out && !a.accumulate) (void)hipMemsetAsync(a.dw, 0, (size_t)p.G * p.M * p.N * sizeof(float), st);
+  p.oirs_ig = a.oirs_ig;
+  if (p.oirs_ig > p.Cg) return -1;
+  const size_t out_elems = (size_t)p.G * p.M * (p.oirs_ig > 0 ? (size_t)p.oirs_ig * p.R * p.S : (size_t)p.N);
+  if (p.atomic_out && !a.accumulate) (void)hipMemsetAsync(a.dw, 0, out_elems * sizeof(float), st);
   // plain rows: the im2col of a 1x1 / stride-1 / pad-0 conv is X itself (pixel grid == input grid)
   const bool plain = a.R == 1 && a.S == 1 && a.sh == 1 && a.sw == 1 && a.ph == 0 && a.pw == 0 && a.P == a.H &&
                      a.Q == a.W;
-  const bool narrow = p.M <= 64;
-  const int blocks = cdiv(p.M, narrow ? 64 : 128) * cdiv(p.N, narrow ? 256 : 128) * p.G * p.splits;
-  if (narrow) {
-    if (plain) launch_wg<64, 256, true>(p, blocks, st); else launch_wg<64, 256, false>(p, blocks, st);
-  } else {
-    if (plain) launch_wg<128, 128, true>(p, blocks, st); else launch_wg<128, 128, false>(p, blocks, st);
-  }
+  const int bn = cdiv(p.M, 64) * cdiv(p.N, 256) * p.G * p.splits;
+  const int bw = cdiv(p.M, 128) * cdiv(p.N, 128) * p.G * p.splits;
+  if (plain) dispatch_wg<true>(p, bn, bw, st);
+  else dispatch_wg<false>(p, bn, bw, st);
   return p.splits;
 }

@@ -180,16 +180,23 @@ __global__ __launch_bounds__(256) void wprep_batched_kernel(const WprepDesc* __r
 }
 
 // fp32 [G][O][R][S][Ipad] gradient (kernel layout) -> fp32 OIHW param-grad layout (drop padding)
-__global__ void wgrad_unprep_kernel(const float* __restrict__ src, float* __restrict__ dst, int G, int Og, int Ig,
-                                    int R, int S, int Ipad, float alpha, int accumulate) {
-  const int64_t total = (int64_t)G * Og * Ig * R * S;
+// [G][Og][R][S][Ipad] (GEMM layout) -> [G*Og][Ig][R][S]; walks the SOURCE (coalesced reads).
+// With zero_src the source is re-zeroed as it is consumed: the wgrad workspace is persistent and
+// self-cleaning, so the split-K atomics need no memset launch.
+__global__ void wgrad_unprep_kernel(float* __restrict__ src, float* __restrict__ dst, int G, int Og, int Ig,
+                                    int R, int S, int Ipad, float alpha, int accumulate, int zero_src) {
+  const int64_t total = (int64_t)G * Og * R * S * Ipad;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    int64_t u = t;  // dst index: [o][i][r][s]
-    const int s = (int)(u % S); u /= S;
-    const int r = (int)(u % R); u /= R;
-    const int i = (int)(u % Ig); const int64_t o = u / Ig;  // o includes group
-    const float v = alpha * src[((o * R + r) * S + s) * Ipad + i];
-    dst[t] = accumulate ? dst[t] + v : v;
+    const int i = (int)(t % Ipad);
+    const int64_t ors = t / Ipad;  // (o, r, s)
+    const int rs = (int)(ors % (R * S));
+    const int64_t o = ors / (R * S);  // o includes group
+    const float v = src[t];
+    if (zero_src) src[t] = 0.f;
+    if (i < Ig) {
+      const int64_t d = (o * Ig + i) * (R * S) + rs;
+      dst[d] = accumulate ? dst[d] + alpha * v : alpha * v;
+    }
   }
 }
 
@@ -253,10 +260,10 @@ void dv_wprep_batched(const void* descs, const void* chunks, int nchunks, hipStr
   if (nchunks > 0)
     wprep_batched_kernel<<<nchunks, 256, 0, st>>>((const WprepDesc*)descs, (const int2*)chunks);
 }
-void dv_wgrad_unprep(const float* src, float* dst, int G, int Og, int Ig, int R, int S, int Ipad, float alpha,
-                     int accumulate, hipStream_t st) {
-  const int64_t total = (int64_t)G * Og * Ig * R * S;
-  wgrad_unprep_kernel<<<grid_for(total), NT, 0, st>>>(src, dst, G, Og, Ig, R, S, Ipad, alpha, accumulate);
+void dv_wgrad_unprep(float* src, float* dst, int G, int Og, int Ig, int R, int S, int Ipad, float alpha,
+                     int accumulate, int zero_src, hipStream_t st) {
+  const int64_t total = (int64_t)G * Og * R * S * Ipad;
+  wgrad_unprep_kernel<<<grid_for(total), NT, 0, st>>>(src, dst, G, Og, Ig, R, S, Ipad, alpha, accumulate, zero_src);
 }
 void dv_to_nhwc(const void* x, int x_is_f32, void* y, int N, int C, int H, int W, int Cp, hipStream_t st) {
   const int64_t total = (int64_t)N * H * W * (Cp / 8);

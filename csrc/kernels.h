@@ -30,10 +30,13 @@ struct ConvWgradArgs {
   int R, S, sh, sw, ph, pw, dh, dw_;
   int splits;      // 0 = heuristic
   int accumulate;  // add into dw (live gradient buffer) instead of overwriting
+  int oirs_ig;     // > 0: dw is the parameter's own [G*Kout][oirs_ig][R][S] layout (padded channels dropped)
 };
 
 int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st);
+void dv_conv_fwd_variant(int v);  // 0 = heuristic tile choice; others: benchmarking override
 int dv_conv_wgrad(const ConvWgradArgs& a, hipStream_t st);
+void dv_conv_wgrad_tuning(int variant, int split_pct);  // benchmarking override (0, 100 = heuristic)
 int dv_conv_wgrad_splits(const ConvWgradArgs& a);
 int dv_conv_stats_tiles(int Nb, int P, int Q);
 
@@ -77,8 +80,8 @@ void dv_act_bwd(const void* dy, const void* y, void* dx, int64_t n, int act, flo
 void dv_add(const void* a, const void* b, void* y, int64_t n, float alpha, float beta, int act, float slope, hipStream_t st);
 void dv_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, hipStream_t st);
 void dv_wprep(const float* w, void* out, int G, int Og, int Ig, int R, int S, int Ipad, int mode, hipStream_t st);
-void dv_wgrad_unprep(const float* src, float* dst, int G, int Og, int Ig, int R, int S, int Ipad, float alpha,
-                     int accumulate, hipStream_t st);
+void dv_wgrad_unprep(float* src, float* dst, int G, int Og, int Ig, int R, int S, int Ipad, float alpha,
+                     int accumulate, int zero_src, hipStream_t st);
 void dv_to_nhwc(const void* x, int x_is_f32, void* y, int N, int C, int H, int W, int Cp, hipStream_t st);
 void dv_f32_to_bf16(const float* x, void* y, int64_t n, hipStream_t st);
 

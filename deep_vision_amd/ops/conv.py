@@ -184,20 +184,32 @@ def _wgrad(x, dy, weight, Cg_x, G, stride, padding, dilation, out=None):
     sh, sw = stride
     ph, pw = padding
     dh, dw = dilation
-    direct = R == 1 and S == 1 and Cg_x == Ig
-    if direct:
+    if R == 1 and S == 1 and Cg_x == Ig:  # GEMM layout == OIHW: accumulate straight into the grad
         buf = out if out is not None else torch.empty((O, Ig, 1, 1), dtype=F32, device=x.device)
-        acc = int(out is not None)
-    else:
-        buf = torch.empty(G * Og * R * S * Cg_x, dtype=F32, device=x.device)
-        acc = 0
-    lib().conv_wgrad(ptr(x), ptr(dy), ptr(buf), N, H, W, Cg_x, ld_of(x), G, Og, P, Q, ld_of(dy), R, S, sh, sw, ph, pw,
-                     dh, dw, 0, acc, stream_handle())
-    if direct:
+        lib().conv_wgrad(ptr(x), ptr(dy), ptr(buf), N, H, W, Cg_x, ld_of(x), G, Og, P, Q, ld_of(dy), R, S, sh, sw,
+                         ph, pw, dh, dw, 0, int(out is not None), 0, stream_handle())
         return buf
+    # [G][Og][R][S][Cg] into the persistent zeroed workspace (split-K atomics, no memset), then
+    # one pass to OIHW that re-zeroes the workspace as it reads it
+    ws = _wgrad_workspace(G * Og * R * S * Cg_x, x.device)
+    lib().conv_wgrad(ptr(x), ptr(dy), ptr(ws), N, H, W, Cg_x, ld_of(x), G, Og, P, Q, ld_of(dy), R, S, sh, sw, ph, pw,
+                     dh, dw, 0, 1, 0, stream_handle())
     dW = out if out is not None else torch.empty((O, Ig, R, S), dtype=F32, device=x.device)
-    lib().wgrad_unprep(ptr(buf), ptr(dW), G, Og, Ig, R, S, Cg_x, 1.0, int(out is not None), stream_handle())
+    lib().wgrad_unprep(ptr(ws), ptr(dW), G, Og, Ig, R, S, Cg_x, 1.0, int(out is not None), 1, stream_handle())
     return dW
+
+
+_WS = {}
+
+
+def _wgrad_workspace(numel, device):
+    """Zero-filled fp32 scratch per (device, stream), kept zero by its consumer (wgrad_unprep)."""
+    key = (device, stream_handle())
+    ws = _WS.get(key)
+    if ws is None or ws.numel() < numel:
+        ws = torch.zeros(max(numel, 1 << 20), dtype=F32, device=device)
+        _WS[key] = ws
+    return ws
 
 
 class _ConvFn(torch.autograd.Function):
@@ -457,15 +469,15 @@ class _LinearFn(torch.autograd.Function):
                          ldy=Kp)
             dx = dx_full if Kp == K else dx_full[:, :K]
         if ctx.needs_input_grad[1]:
-            sink = grad_sink(weight) if Kp == K else None
-            buf = sink if sink is not None else torch.empty(O * Kp, dtype=F32, device=dy.device)
+            sink = grad_sink(weight)
+            buf = sink if sink is not None else torch.empty((O, K), dtype=F32, device=dy.device)
             lib().conv_wgrad(ptr(x), ptr(dy), ptr(buf), N, 1, 1, Kp, Kp, 1, O, 1, 1, Op, 1, 1, 1, 1, 0, 0, 1, 1, 0,
-                             int(sink is not None), stream_handle())
+                             int(sink is not None), K if Kp != K else 0, stream_handle())
             if sink is not None:
                 dw = None
                 notify_grad_ready(weight)
             else:
-                dw = buf.view(O, Kp)[:, :K].contiguous() if Kp != K else buf.view(O, K)
+                dw = buf
         if has_bias and ctx.needs_input_grad[2]:
             db = dy.float().sum(0)
             sink = grad_sink(bias)
