@@ -1,12 +1,22 @@
 #!/usr/bin/env python3
-"""Flagship benchmark: ResNet-50 V1 bf16 training throughput (images/sec, whole job).
+"""Training-throughput benchmark (images/sec, whole job) for the BASELINE.json configs.
 
-Config named by BASELINE.json: ResNet-50 224x224 bf16, synthetic ImageNet-shaped data,
-random-init weights, SGD(lr .1, momentum .9, wd 1e-4) as R/ResNet/pytorch/train.py:166-184,
-per-GPU batch 256 (weak scaling), data parallel over RCCL with one process per GPU.
+Default / flagship: ResNet-50 V1 bf16 224x224, synthetic ImageNet-shaped data, random-init
+weights, SGD(lr .1, momentum .9, wd 1e-4) as R/ResNet/pytorch/train.py:166-184, per-GPU batch
+256 (weak scaling), data parallel over RCCL with one process per GPU.
 
-Every timed step is a full training step: forward, softmax-CE loss, backward, bucketed
-gradient all-reduce (N > 1), fused SGD update, gradient zeroing.
+Other BASELINE.json configs (``--model``):
+  mobilenet1  MobileNet V1 1.0, depthwise HIP path, RMSprop(.045, .9, eps 1) per-GPU batch 128
+              (R/ResNet/pytorch/train.py:185-214)
+  yolov3      YOLOv3-80 416x416, synthetic COCO-shaped boxes -> 3-scale labels, YoloLoss,
+              Adam(.01), 16 images per replica (R/YOLO/tensorflow/train.py:13-19,46-68)
+  hourglass   Stacked Hourglass-104 (4 stacks, 16 heatmaps) 256x256, synthetic MPII-shaped
+              heatmaps, weighted MSE, Adam(1e-3), 32 per replica (R/Hourglass/tensorflow/main.py:22-33)
+  lenet5      LeNet-5 1x32x32 on the CPU (plumbing config), Adam(1e-3), batch 64
+
+Every timed step is a full training step: forward, loss, backward, bucketed gradient
+all-reduce (N > 1), fused optimizer update, gradient zeroing. Inputs/labels are generated once
+on the device (synthetic, no host pipeline in the timed region).
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--model resnet50]
         (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
@@ -15,12 +25,85 @@ from __future__ import annotations
 
 import argparse
 import json
-import os
 import sys
 import time
 
-# Reference-derived comparator: ResNet-50-equivalent proxy ~376 img/s per node.
-BASELINE_IMG_S = 376.0
+# Reference-derived comparators, images/sec per node:
+#   ResNet-50-equivalent proxy ~376 (8 GPUs), YOLOv3 ~179 (8x V100), LeNet-5 PT ~906.
+BASELINES = {"resnet50": 376.0, "yolov3": 179.0, "lenet5": 906.0}
+RESNET_METRIC = "images/sec (whole node), ResNet-50 224x224 bf16 at 1/2/4/8 MI355X"
+
+# model -> (per-GPU batch, image size, optimizer name, optimizer kwargs, family)
+SPECS = {
+    "resnet50": (256, 224, "SGD", {"lr": 0.1, "momentum": 0.9, "weight_decay": 1e-4}, "cls"),
+    "resnet152": (256, 224, "SGD", {"lr": 0.1, "momentum": 0.9, "weight_decay": 1e-4}, "cls"),
+    "resnet34": (256, 224, "SGD", {"lr": 0.1, "momentum": 0.9, "weight_decay": 1e-4}, "cls"),
+    "mobilenet1": (128, 224, "RMSprop", {"lr": 0.045, "alpha": 0.9, "eps": 1.0}, "cls"),
+    "shufflenet1": (128, 224, "RMSprop", {"lr": 0.045, "alpha": 0.9, "eps": 1.0}, "cls"),
+    "vgg16": (128, 224, "SGD", {"lr": 0.01, "momentum": 0.9, "weight_decay": 5e-4}, "cls"),
+    "alexnet2": (128, 224, "SGD", {"lr": 0.01, "momentum": 0.9, "weight_decay": 5e-4}, "cls"),
+    "inception1": (128, 224, "SGD", {"lr": 0.01, "momentum": 0.9, "weight_decay": 2e-4}, "cls"),
+    "yolov3": (16, 416, "Adam", {"lr": 0.01}, "yolo"),
+    "hourglass": (32, 256, "Adam", {"lr": 1e-3}, "hourglass"),
+    "lenet5": (64, 32, "Adam", {"lr": 1e-3}, "cls"),
+}
+
+
+def build(args, device):
+    """-> (module, loss_fn(out) -> scalar, x, labels, optimizer)."""
+    import torch
+
+    from deep_vision_amd import ops as F
+    from deep_vision_amd.models import get_model
+    from deep_vision_amd.train.optim import OPTIMIZERS
+
+    B, size, opt_name, opt_kw, fam = SPECS[args.model]
+    B = args.batch or B
+    if fam == "cls":
+        model = get_model(args.model).to(device)
+        cin = 1 if args.model == "lenet5" else 3
+        x = torch.randn(B, cin, size, size, device=device)
+        y = torch.randint(0, 10 if args.model == "lenet5" else 1000, (B,), device=device)
+        if args.model == "inception1":
+            def loss_fn(out):  # main + 0.3 x aux heads (SURVEY A3)
+                if isinstance(out, tuple):
+                    return F.cross_entropy(out[0], y) + 0.3 * (F.cross_entropy(out[1], y) + F.cross_entropy(out[2], y))
+                return F.cross_entropy(out, y)
+        elif args.backend == "torch":
+            def loss_fn(out):
+                return torch.nn.functional.cross_entropy(out.float(), y)
+        else:
+            def loss_fn(out):
+                return F.cross_entropy(out, y)
+    elif fam == "yolo":
+        from deep_vision_amd.data import yolo as Y
+        from deep_vision_amd.train.detection import yolo_loss
+
+        model = get_model("yolov3", num_classes=80).to(device)
+        imgs, labels = Y.collate([Y.SyntheticYoloDataset(B, 80, size, 1)[i] for i in range(B)])
+        x = imgs.to(device)
+        lab = tuple(t.to(device) for t in labels)
+
+        def loss_fn(out):
+            return yolo_loss(out, lab, 80)[0] / B
+    elif fam == "hourglass":
+        from deep_vision_amd.data import pose as P
+        from deep_vision_amd.train.detection import hourglass_loss
+
+        model = get_model("hourglass104", num_stack=4, num_residual=1, num_heatmap=16).to(device)
+        ds = P.SyntheticPoseDataset(B, size, (size // 4, size // 4, 16), 1)
+        x = torch.stack([torch.from_numpy(ds[i][0]) for i in range(B)]).to(device)
+        hm = torch.stack([torch.from_numpy(ds[i][1]) for i in range(B)]).to(device)
+
+        def loss_fn(out):
+            return hourglass_loss(out, hm)[0] / B
+    else:
+        raise ValueError(fam)
+    if args.backend == "torch" and device.type == "cuda":
+        model = model.to(memory_format=torch.channels_last)
+        x = x.contiguous(memory_format=torch.channels_last)
+    opt = OPTIMIZERS[opt_name](model.parameters(), **opt_kw)
+    return model, loss_fn, x, opt, B, size
 
 
 def main():
@@ -28,52 +111,45 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
-    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (0 = the config's)")
+    ap.add_argument("--model", default="resnet50", choices=sorted(SPECS))
     ap.add_argument("--backend", default="native", choices=["native", "torch"],
                     help="torch = PyTorch/MIOpen reference path (for comparison only)")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
-    ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--device", default=None, help="cpu to force the CPU plumbing path")
     args = ap.parse_args()
 
     import torch
 
     from deep_vision_amd import ops as F
-    from deep_vision_amd.models import get_model
     from deep_vision_amd.parallel.ddp import DataParallel
     from deep_vision_amd.parallel.dist import barrier, init_distributed, is_dist
-    from deep_vision_amd.train.optim import FusedSGD
 
-    world, rank, local, device = init_distributed()
+    world, rank, local, device = init_distributed("gloo" if args.device == "cpu" else None)
+    if args.device == "cpu":
+        device = torch.device("cpu")
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     F.set_backend(args.backend)
     torch.manual_seed(1234 + rank)
     torch.backends.cudnn.benchmark = True
+    cuda = device.type == "cuda"
 
-    model = get_model(args.model).to(device)
-    if args.backend == "torch":
-        model = model.to(memory_format=torch.channels_last)
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
+
+    model, loss_fn, x, opt, B, size = build(args, device)
     ddp = DataParallel(model, bucket_mb=args.bucket_mb) if is_dist() else None
-    opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
     gscale = ddp.grad_scale if ddp else 1.0
     net = ddp if ddp else model
-
-    B = args.batch
-    x = torch.randn(B, 3, 224, 224, device=device)
-    if args.backend == "torch":
-        x = x.to(memory_format=torch.channels_last)
-    y = torch.randint(0, 1000, (B,), device=device)
+    amp = args.backend == "torch" and cuda
 
     def step():
         opt.zero_grad()
-        if args.backend == "torch":
-            with torch.autocast("cuda", dtype=torch.bfloat16):
-                out = net(x)
-                loss = torch.nn.functional.cross_entropy(out.float(), y)
-        else:
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
             out = net(x)
-            loss = F.cross_entropy(out, y)
+            loss = loss_fn(out)
         loss.backward()
         if ddp:
             ddp.finish()
@@ -82,17 +158,17 @@ def main():
 
     for _ in range(args.warmup):
         loss = step()
-    torch.cuda.synchronize()
+    sync()
     first_loss = float(loss.item()) if args.warmup else float("nan")
 
     barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
-    torch.cuda.synchronize()
+    sync()
     barrier()
-    torch.cuda.synchronize()
+    sync()
     dt = time.perf_counter() - t0
 
     if is_dist():
@@ -105,28 +181,34 @@ def main():
     ms = dt / args.steps * 1e3
     imgs = B * world * args.steps / dt
     if rank == 0:
+        base = BASELINES.get(args.model)
+        if args.model == "resnet50":
+            metric = RESNET_METRIC
+        else:
+            metric = f"images/sec (whole node), {args.model} {size}x{size} {'bf16' if cuda else 'fp32'}"
         rec = {
-            "metric": "images/sec (whole node), ResNet-50 224x224 bf16 at 1/2/4/8 MI355X",
+            "metric": metric,
             "value": round(imgs, 2),
             "unit": "images/sec",
-            "n_gpus": world,
+            "n_gpus": world if cuda else 0,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(imgs / BASELINE_IMG_S, 3),
-            "dtype": "bf16",
-            "data": "synthetic (random 224x224x3 images / labels, random-init weights)",
+            "vs_baseline": round(imgs / base, 3) if base else None,
+            "dtype": "bf16" if cuda else "fp32",
+            "data": "synthetic (random inputs / labels of the config's shapes, random-init weights)",
             "config": {
                 "model": args.model,
                 "global_batch": B * world,
                 "per_gpu_batch": B,
                 "seq_len": None,
-                "image_size": 224,
+                "image_size": size,
                 "parallelism": f"dp{world}",
-                "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4) fused",
+                "optimizer": f"{type(opt).__name__} {SPECS[args.model][3]}",
                 "backend": args.backend,
+                "device": str(device),
                 "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],
             },
         }

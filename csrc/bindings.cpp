@@ -29,14 +29,23 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_fwd", [](uptr x, uptr w, uptr y, uptr bias, uptr stats, int Nb, int H, int W, int Cg, int ldx, int G,
                        int Kout, int P_, int Q, int R, int S, int sh, int sw, int ph, int pw, int dh, int dw, int tgather,
                        int OH, int OW, int osh, int osw, int oph, int opw, int ldy, int act, float slope, uptr res,
-                       uptr st) {
+                       uptr st, uptr bnx, uptr bnbits, uptr bnprm, uptr bnacc, int bnmode, int bnact, float bnslope) {
     ConvFwdArgs a{CP(x), CP(w), P(y), CFP(bias), FP(stats), Nb, H, W, Cg, ldx, G, Kout, P_, Q, R, S, sh, sw, ph, pw,
-                  dh, dw, tgather, OH, OW, osh, osw, oph, opw, ldy, act, slope, CP(res)};
+                  dh, dw, tgather, OH, OW, osh, osw, oph, opw, ldy, act, slope, CP(res),
+                  CP(bnx), CP(bnbits), CFP(bnprm), FP(bnacc), bnmode, bnact, bnslope};
     int r = dv_conv_fwd(a, ST(st));
-    if (r != 0) throw std::runtime_error("conv_fwd: unsupported geometry (channels must be a multiple of 8)");
+    if (r < 0) throw std::runtime_error("conv_fwd: unsupported geometry (channels must be a multiple of 8)");
     check_last("conv_fwd");
-  });
+    return r;
+  }, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"), py::arg("stats"), py::arg("Nb"), py::arg("H"),
+     py::arg("W"), py::arg("Cg"), py::arg("ldx"), py::arg("G"), py::arg("Kout"), py::arg("P"), py::arg("Q"), py::arg("R"),
+     py::arg("S"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"),
+     py::arg("tgather"), py::arg("OH"), py::arg("OW"), py::arg("osh"), py::arg("osw"), py::arg("oph"), py::arg("opw"),
+     py::arg("ldy"), py::arg("act"), py::arg("slope"), py::arg("res"), py::arg("st"), py::arg("bnx") = 0,
+     py::arg("bnbits") = 0, py::arg("bnprm") = 0, py::arg("bnacc") = 0, py::arg("bnmode") = 0, py::arg("bnact") = 0,
+     py::arg("bnslope") = 0.f);
   m.def("conv_fwd_variant", [](int v) { dv_conv_fwd_variant(v); });
+  m.def("bn_tuning", [](int blocks, int unroll) { dv_bn_tuning(blocks, unroll); });
   m.def("conv_wgrad_tuning", [](int v, int split_pct) { dv_conv_wgrad_tuning(v, split_pct); });
   m.def("conv_wgrad", [](uptr x, uptr dy, uptr dw, int Nb, int H, int W, int Cg, int ldx, int G, int Kout, int P_, int Q,
                          int ldy, int R, int S, int sh, int sw, int ph, int pw, int dh, int dwl, int splits, int accumulate,
@@ -108,7 +117,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("act_bwd", [](uptr dy, uptr y, uptr dx, int64_t n, int act, float slope, uptr st) { dv_act_bwd(CP(dy), CP(y), P(dx), n, act, slope, ST(st)); check_last("act_bwd"); });
   m.def("add", [](uptr a, uptr b, uptr y, int64_t n, float alpha, float beta, int act, float slope, uptr st) { dv_add(CP(a), CP(b), P(y), n, alpha, beta, act, slope, ST(st)); check_last("add"); });
   m.def("dropout", [](uptr x, uptr y, int64_t n, float p, uint64_t seed, uptr st) { dv_dropout(CP(x), P(y), n, p, seed, ST(st)); check_last("dropout"); });
-  m.def("wprep", [](uptr w, uptr out, int G, int Og, int Ig, int R, int S, int Ipad, int mode, uptr st) { dv_wprep(CFP(w), P(out), G, Og, Ig, R, S, Ipad, mode, ST(st)); check_last("wprep"); });
+  m.def("wprep", [](uptr w, uptr out, int G, int Og, int Ig, int R, int S, int Ipad, int mode, int Sp, uptr st) { dv_wprep(CFP(w), P(out), G, Og, Ig, R, S, Ipad, mode, Sp, ST(st)); check_last("wprep"); });
+  m.def("stem_pack", [](uptr x, int is_f32, uptr y, int N, int C, int H, int W, int Hp, int Wp, int pt, int pl, uptr st) {
+    dv_stem_pack(CP(x), is_f32, P(y), N, C, H, W, Hp, Wp, pt, pl, ST(st)); check_last("stem_pack"); });
   m.def("wgrad_unprep", [](uptr src, uptr dst, int G, int Og, int Ig, int R, int S, int Ipad, float alpha, int accumulate,
                            int zero_src, uptr st) {
     dv_wgrad_unprep(FP(src), FP(dst), G, Og, Ig, R, S, Ipad, alpha, accumulate, zero_src, ST(st)); check_last("wgrad_unprep");

@@ -62,47 +62,64 @@ DV_DEVICE float act_bwd(float dout, float out, int act, float slope) {
 }
 
 // ---- statistics of an NHWC tensor: rows x C -> shard accumulators ----
-// Thread layout: TPR = C/VEC threads per row (capped at NT); each thread owns VEC channels.
+// 2-D grid: blockIdx.y = channel slab of up to 64 x VEC channels (one wave-width of 16-B vectors
+// per row), blockIdx.x = row range. TPR threads cover the slab of one row, RPI = NT/TPR rows per
+// iteration. Wide layers (C = 1024 / 2048 at 14x14 / 7x7) have few rows: slabs keep >= ~4
+// blocks per CU in flight there instead of a few hundred row blocks.
+constexpr int SLAB_TPR = 64;
+struct SlabTile {
+  int cg, tpr, rpi, lane_c, lane_r, g;
+  int64_t r0, r1;
+  DV_DEVICE SlabTile(int C, int VEC, int64_t rows) {
+    cg = C / VEC; tpr = cg < SLAB_TPR ? cg : SLAB_TPR; rpi = NT / tpr;
+    lane_c = threadIdx.x % tpr; lane_r = threadIdx.x / tpr;
+    g = blockIdx.y * tpr + lane_c;
+    const int64_t rpb = (rows + gridDim.x - 1) / gridDim.x;
+    r0 = blockIdx.x * rpb; r1 = min(rows, r0 + rpb);
+  }
+  DV_DEVICE bool active() const { return lane_r < rpi && g < cg; }
+};
+
+// per-block partial sums of the slab -> LDS -> per-channel totals over the RPI row lanes ->
+// shard atomics with consecutive lanes on consecutive channels (256-B coalesced atomic rows;
+// lane-strided atomics run ~8x slower, MI355X_MICROARCH.md "Global float atomics")
+template <int VEC>
+DV_DEVICE void slab_commit(const SlabTile& t, float* s, float* q, float* __restrict__ acc, int C) {
+  __shared__ float sh[2][NT * VEC];
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) { sh[0][tid * VEC + i] = s[i]; sh[1][tid * VEC + i] = q[i]; }
+  __syncthreads();
+  const int sw = t.tpr * VEC;  // slab width (channels); sh is [row lane][slab channel]
+  const int c0 = blockIdx.y * sw;
+  float* a = acc + (int64_t)(blockIdx.x % SHARDS) * 2 * C;
+  for (int ch = tid; ch < sw; ch += NT) {
+    if (c0 + ch < C) {
+      float ss = 0.f, qq = 0.f;
+      for (int rr = 0; rr < t.rpi; ++rr) { ss += sh[0][rr * sw + ch]; qq += sh[1][rr * sw + ch]; }
+      atomicAdd(a + c0 + ch, ss);
+      atomicAdd(a + C + c0 + ch, qq);
+    }
+  }
+}
+
 template <int VEC>
 __global__ __launch_bounds__(NT) void bn_stats_kernel(const u16* __restrict__ x, int64_t rows, int C,
                                                         float* __restrict__ acc) {
-  __shared__ float sh[2][NT * VEC];
-  const int cg = C / VEC;
-  const int tpr = cg < NT ? cg : NT;
-  const int rpi = NT / tpr;
-  const int tid = threadIdx.x;
-  const int lane_c = tid % tpr, lane_r = tid / tpr;
-  const int64_t rows_per_block = (rows + gridDim.x - 1) / gridDim.x;
-  const int64_t r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
-  for (int cb = 0; cb < cg; cb += tpr) {
-    const int g = cb + lane_c;
-    float s[VEC], q[VEC];
+  SlabTile t(C, VEC, rows);
+  float s[VEC], q[VEC];
 #pragma unroll
-    for (int i = 0; i < VEC; ++i) { s[i] = 0.f; q[i] = 0.f; }
-    if (lane_r < rpi && g < cg) {
+  for (int i = 0; i < VEC; ++i) { s[i] = 0.f; q[i] = 0.f; }
+  if (t.active()) {
 #pragma unroll 2
-      for (int64_t r = r0 + lane_r; r < r1; r += rpi) {
-        float v[VEC];
-        VecIO<VEC>::load(x + r * C + g * VEC, v);
+    for (int64_t r = t.r0 + t.lane_r; r < t.r1; r += t.rpi) {
+      float v[VEC];
+      VecIO<VEC>::load(x + r * C + t.g * VEC, v);
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) { s[i] += v[i]; q[i] += v[i] * v[i]; }
-      }
-    }
-    // reduce over lane_r through LDS
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) { sh[0][tid * VEC + i] = s[i]; sh[1][tid * VEC + i] = q[i]; }
-    __syncthreads();
-    if (lane_r == 0 && g < cg) {
-      for (int rr = 1; rr < rpi; ++rr) {
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) { s[i] += sh[0][(rr * tpr + lane_c) * VEC + i]; q[i] += sh[1][(rr * tpr + lane_c) * VEC + i]; }
-      }
-      float* a = acc + (int64_t)(blockIdx.x % SHARDS) * 2 * C;
-#pragma unroll
-      for (int i = 0; i < VEC; ++i) { atomicAdd(a + g * VEC + i, s[i]); atomicAdd(a + C + g * VEC + i, q[i]); }
+      for (int i = 0; i < VEC; ++i) { s[i] += v[i]; q[i] += v[i] * v[i]; }
     }
   }
+  slab_commit<VEC>(t, s, q, acc, C);
 }
 
 // Fold the SHARDS partial (a, b) pairs of channel blockIdx.x*64 + (tid & 63) and re-zero them
@@ -222,64 +239,43 @@ enum { MM_NONE = 0, MM_OUT = 1, MM_X = 2, MM_BITS = 3 };  // activation-mask sou
 // MM_BITS: the forward apply stored the mask as bits (VEC == 8: one byte per 8 channels), 1/16 of
 // the bytes of re-reading the bf16 output (residual blocks, where the mask cannot come from x)
 
-template <int VEC, int MM>
+template <int VEC, int MM, int UNR = 2>
 __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(const u16* __restrict__ dout, const u16* __restrict__ out,
                                                              const u16* __restrict__ x, int64_t rows, int C,
                                                              const float* __restrict__ mean, const float* __restrict__ invstd,
                                                              const float* __restrict__ mscale, const float* __restrict__ mshift,
                                                              int act, float slope, float* __restrict__ acc) {
-  __shared__ float sh[2][NT * VEC];
-  const int cg = C / VEC;
-  const int tpr = cg < NT ? cg : NT;
-  const int rpi = NT / tpr;
-  const int tid = threadIdx.x;
-  const int lane_c = tid % tpr, lane_r = tid / tpr;
-  const int64_t rows_per_block = (rows + gridDim.x - 1) / gridDim.x;
-  const int64_t r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
-  for (int cb = 0; cb < cg; cb += tpr) {
-    const int g = cb + lane_c;
-    float s[VEC], q[VEC], mu[VEC], is[VEC], ms[VEC], mh[VEC];
+  SlabTile t(C, VEC, rows);
+  const int g = t.g;
+  float s[VEC], q[VEC], mu[VEC], is[VEC], ms[VEC], mh[VEC];
 #pragma unroll
-    for (int i = 0; i < VEC; ++i) { s[i] = 0.f; q[i] = 0.f; }
-    if (lane_r < rpi && g < cg) {
+  for (int i = 0; i < VEC; ++i) { s[i] = 0.f; q[i] = 0.f; }
+  if (t.active()) {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      mu[i] = mean[g * VEC + i]; is[i] = invstd[g * VEC + i];
+      ms[i] = MM == MM_X ? mscale[g * VEC + i] : 0.f;
+      mh[i] = MM == MM_X ? mshift[g * VEC + i] : 0.f;
+    }
+#pragma unroll UNR
+    for (int64_t r = t.r0 + t.lane_r; r < t.r1; r += t.rpi) {
+      float d[VEC], o[VEC], xv[VEC];
+      VecIO<VEC>::load(dout + r * C + g * VEC, d);
+      VecIO<VEC>::load(x + r * C + g * VEC, xv);
+      if constexpr (MM == MM_OUT) VecIO<VEC>::load(out + r * C + g * VEC, o);
+      uint32_t mb = 0;
+      if constexpr (MM == MM_BITS) mb = reinterpret_cast<const uint8_t*>(out)[(r * C + g * VEC) >> 3];
 #pragma unroll
       for (int i = 0; i < VEC; ++i) {
-        mu[i] = mean[g * VEC + i]; is[i] = invstd[g * VEC + i];
-        ms[i] = MM == MM_X ? mscale[g * VEC + i] : 0.f;
-        mh[i] = MM == MM_X ? mshift[g * VEC + i] : 0.f;
+        float dz = d[i];
+        if constexpr (MM == MM_OUT) dz = act_bwd(d[i], o[i], act, slope);
+        if constexpr (MM == MM_BITS) dz = ((mb >> i) & 1u) ? d[i] : (act == 2 ? d[i] * slope : 0.f);
+        if constexpr (MM == MM_X) dz = act_bwd(d[i], fmaf(xv[i], ms[i], mh[i]), act, slope);
+        s[i] += dz; q[i] += dz * (xv[i] - mu[i]) * is[i];
       }
-#pragma unroll 2
-      for (int64_t r = r0 + lane_r; r < r1; r += rpi) {
-        float d[VEC], o[VEC], xv[VEC];
-        VecIO<VEC>::load(dout + r * C + g * VEC, d);
-        VecIO<VEC>::load(x + r * C + g * VEC, xv);
-        if constexpr (MM == MM_OUT) VecIO<VEC>::load(out + r * C + g * VEC, o);
-        uint32_t mb = 0;
-        if constexpr (MM == MM_BITS) mb = reinterpret_cast<const uint8_t*>(out)[(r * C + g * VEC) >> 3];
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) {
-          float dz = d[i];
-          if constexpr (MM == MM_OUT) dz = act_bwd(d[i], o[i], act, slope);
-          if constexpr (MM == MM_BITS) dz = ((mb >> i) & 1u) ? d[i] : (act == 2 ? d[i] * slope : 0.f);
-          if constexpr (MM == MM_X) dz = act_bwd(d[i], fmaf(xv[i], ms[i], mh[i]), act, slope);
-          s[i] += dz; q[i] += dz * (xv[i] - mu[i]) * is[i];
-        }
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) { sh[0][tid * VEC + i] = s[i]; sh[1][tid * VEC + i] = q[i]; }
-    __syncthreads();
-    if (lane_r == 0 && g < cg) {
-      for (int rr = 1; rr < rpi; ++rr) {
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) { s[i] += sh[0][(rr * tpr + lane_c) * VEC + i]; q[i] += sh[1][(rr * tpr + lane_c) * VEC + i]; }
-      }
-      float* a = acc + (int64_t)(blockIdx.x % SHARDS) * 2 * C;
-#pragma unroll
-      for (int i = 0; i < VEC; ++i) { atomicAdd(a + g * VEC + i, s[i]); atomicAdd(a + C + g * VEC + i, q[i]); }
     }
   }
+  slab_commit<VEC>(t, s, q, acc, C);
 }
 
 // fold backward shards (and re-zero them): dbeta = sum dz, dgamma = sum dz*xhat (written, or
@@ -376,10 +372,15 @@ __global__ __launch_bounds__(NT) void bn_bwd_eval_kernel(const u16* __restrict__
 }
 
 inline int vec_for(int C) { return (C % 8 == 0) ? 8 : (C % 4 == 0) ? 4 : (C % 2 == 0) ? 2 : 1; }
-inline int reduce_grid(int64_t rows) {
-  // >= 4 blocks/CU worth of parallelism but at least ~32 rows per block
-  int64_t g = std::min<int64_t>(1024, std::max<int64_t>(1, rows / 32));
-  return (int)g;
+int g_reduce_blocks = 1024;  // benchmarking override (dv_bn_tuning)
+int g_reduce_unroll = 2;
+// (row blocks, channel slabs): ~4 blocks per CU (8 with several slabs), >= 32 rows per block
+inline dim3 reduce_grid(int64_t rows, int C) {
+  const int v = vec_for(C), cg = C / v, tpr = cg < SLAB_TPR ? cg : SLAB_TPR;
+  const int slabs = (cg + tpr - 1) / tpr;
+  const int64_t target = (int64_t)g_reduce_blocks * (slabs > 1 ? 2 : 1) / slabs;
+  const int64_t g = std::min<int64_t>(std::max<int64_t>(target, 1), std::max<int64_t>(1, rows / 32));
+  return dim3((unsigned)g, (unsigned)slabs);
 }
 // rows per block for the row-tiled apply passes: ~4096 blocks, a multiple of rows/iteration
 inline int64_t apply_rows_per_block(int64_t rows, int C, int v) {
@@ -398,8 +399,13 @@ inline int64_t apply_rows_per_block(int64_t rows, int C, int v) {
     default: KERNEL<1> __VA_ARGS__; break;                                         \
   }
 
+void dv_bn_tuning(int reduce_blocks, int reduce_unroll) {
+  g_reduce_blocks = reduce_blocks > 0 ? reduce_blocks : 1024;
+  g_reduce_unroll = reduce_unroll == 4 ? 4 : 2;
+}
+
 void dv_bn_stats(const void* x, int64_t rows, int C, float* acc, hipStream_t st) {
-  const int g = reduce_grid(rows);
+  const dim3 g = reduce_grid(rows, C);
   DISPATCH_VEC(C, bn_stats_kernel, <<<g, NT, 0, st>>>((const u16*)x, rows, C, acc))
 }
 
@@ -433,7 +439,7 @@ void dv_bn_apply(const void* x, const void* res, void* out, int64_t n, int C, co
 }
 
 template <int MM>
-static void bwd_reduce_launch(int g, const void* dout, const void* out, const void* x, int64_t rows, int C, const float* mean,
+static void bwd_reduce_launch(dim3 g, const void* dout, const void* out, const void* x, int64_t rows, int C, const float* mean,
                               const float* invstd, const float* mscale, const float* mshift, int act, float slope, float* acc,
                               hipStream_t st) {
   switch (vec_for(C)) {
@@ -447,9 +453,18 @@ static void bwd_reduce_launch(int g, const void* dout, const void* out, const vo
 void dv_bn_bwd_reduce(const void* dout, const void* out, const void* x, int64_t rows, int C, const float* mean,
                       const float* invstd, const float* mscale, const float* mshift, int act, float slope, float* acc,
                       int mask_bits, hipStream_t st) {
-  const int g = reduce_grid(rows);
+  const dim3 g = reduce_grid(rows, C);
   if (act && mask_bits && vec_for(C) == 8) {
-    bn_bwd_reduce_kernel<8, MM_BITS><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, rows, C, mean,
+    if (g_reduce_unroll == 4)
+      bn_bwd_reduce_kernel<8, MM_BITS, 4><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, rows, C, mean,
+                                                              invstd, mscale, mshift, act, slope, acc);
+    else
+      bn_bwd_reduce_kernel<8, MM_BITS><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, rows, C, mean,
+                                                           invstd, mscale, mshift, act, slope, acc);
+    return;
+  }
+  if (act && !out && vec_for(C) == 8 && g_reduce_unroll == 4) {
+    bn_bwd_reduce_kernel<8, MM_X, 4><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, rows, C, mean,
                                                          invstd, mscale, mshift, act, slope, acc);
     return;
   }

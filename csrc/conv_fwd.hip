@@ -50,6 +50,12 @@ struct FwdParams {
   int act; float slope;
   int identity_map;
   FastDiv div_pq, div_q;
+  // fused BatchNorm-backward statistics of y (see kernels.h ConvFwdArgs)
+  const u16* bnx;
+  const uint8_t* bnbits;
+  const float* bnprm;
+  float* bnacc;
+  int bnmode, bnact; float bnslope;
 };
 
 DV_DEVICE void glds16(const void* src, char* lds_wave_base) {
@@ -70,6 +76,28 @@ DV_DEVICE bf16x8 read_kc(const char* img, int row, int chunk) {
 template <int BM_, int BN_, int BK_>
 constexpr int stage_bytes() { return (BM_ + BN_) * BK_ * 2; }
 
+// BatchNorm-backward reduction terms of 8 stored gradient values `o` (bf16, exactly what the
+// unfused bn_bwd_reduce pass would read back) at element offset `off` of the BN input / mask:
+// dz = act'(z) * dout, sum dz and sum dz * (x - mean) * invstd (csrc/bn.hip bn_bwd_reduce_kernel).
+DV_DEVICE void bn_bwd_accum(const FwdParams& p, const uint4& o, const uint4& xr, uint32_t mb, float* bs, float* bq,
+                            const float* bmu, const float* bis, const float* bms, const float* bmh) {
+  const uint32_t dw[4] = {o.x, o.y, o.z, o.w}, xw[4] = {xr.x, xr.y, xr.z, xr.w};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float d = bf2f((u16)(dw[e >> 1] >> ((e & 1) * 16)));
+    const float x = bf2f((u16)(xw[e >> 1] >> ((e & 1) * 16)));
+    float dz = d;
+    if (p.bnmode == 3) {
+      dz = ((mb >> e) & 1u) ? d : (p.bnact == 2 ? d * p.bnslope : 0.f);
+    } else if (p.bnmode == 2) {
+      const float z = fmaf(x, bms[e], bmh[e]);
+      dz = z > 0.f ? d : (p.bnact == 2 ? d * p.bnslope : 0.f);
+    }
+    bs[e] += dz;
+    bq[e] += dz * (x - bmu[e]) * bis[e];
+  }
+}
+
 // s_waitcnt vmcnt(N) with expcnt / lgkmcnt left at their maxima (gfx9 encoding: vmcnt bits
 // [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8]).
 template <int N>
@@ -78,7 +106,7 @@ DV_DEVICE void wait_vm() {
   __builtin_amdgcn_s_waitcnt((N & 0xF) | (0x7 << 4) | (0xF << 8) | ((N >> 4) << 14));
 }
 
-template <int BM_, int BN_, int BK_, int KMODE, bool RES, int STAGES>
+template <int BM_, int BN_, int BK_, int KMODE, bool RES, int STAGES, bool BNR = false>
 __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
   constexpr int WN = BN_ / 64, WM = BM_ / 64;
   static_assert(WN * WM == 4, "4 waves of 64x64");
@@ -284,6 +312,40 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
       *reinterpret_cast<uint2*>(st + ml * EPI_PITCH + j * 16 + (lane >> 4) * 4) = pk;
     }
   }
+  // Prefetch what the store loop reads besides the staged tile (the residual gradient, the BN
+  // input and mask) for all 8 row groups now: issued in the loop they would each wait behind the
+  // previous iteration's stores (one vmcnt queue for loads and stores), 8 serial round trips.
+  const int64_t goff_y = (int64_t)grp * p.N;
+  const bool vec = ((p.N & 7) == 0) && ((p.ldy & 7) == 0) && ((goff_y & 7) == 0);
+  constexpr bool PF = RES || BNR;
+  int64_t pf_off[PF ? 8 : 1];
+  uint4 pf_res[RES ? 8 : 1], pf_x[BNR ? 8 : 1];
+  uint32_t pf_mb[BNR ? 8 : 1];
+  if constexpr (PF) {
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int m = m0 + wave_m * 64 + it * 8 + (lane >> 3);
+      const int n = nw0 + (lane & 7) * 8;
+      int64_t off = -1;
+      if (m < p.M && n < p.N) {
+        int64_t opix;
+        if (p.identity_map) opix = m;
+        else {
+          const int img = (int)fdiv((uint32_t)m, p.div_pq), rem = m - img * (p.P * p.Q);
+          const int pp = (int)fdiv((uint32_t)rem, p.div_q), qq = rem - pp * p.Q;
+          opix = ((int64_t)img * p.OH + pp * p.osh + p.oph) * p.OW + qq * p.osw + p.opw;
+        }
+        off = opix * p.ldy + goff_y + n;
+      }
+      pf_off[it] = off;
+      const bool ld = off >= 0 && vec;
+      if constexpr (RES) pf_res[it] = ld ? *reinterpret_cast<const uint4*>(p.res + off) : uint4{0u, 0u, 0u, 0u};
+      if constexpr (BNR) {
+        pf_x[it] = ld ? *reinterpret_cast<const uint4*>(p.bnx + off) : uint4{0u, 0u, 0u, 0u};
+        pf_mb[it] = (ld && p.bnmode == 3) ? (uint32_t)p.bnbits[off >> 3] : 0u;
+      }
+    }
+  }
   if (p.stats) {
     float* sh = reinterpret_cast<float*>(smem + EPI_BYTES);  // [WM][BN_][2]
 #pragma unroll
@@ -314,27 +376,44 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
     }
   }
   // staged tile -> global: each wave writes its 64 rows x 64 channels as 16-B pieces
-  const int64_t goff_y = (int64_t)grp * p.N;
-  const bool vec = ((p.N & 7) == 0) && ((p.ldy & 7) == 0) && ((goff_y & 7) == 0);
+  // BNR: this lane's 8 channels are fixed over the store loop (rows it*8 + lane/8)
+  float bs[8], bq[8], bmu[8], bis[8], bms[8], bmh[8];
+  if constexpr (BNR) {
+    const int nb = nw0 + (lane & 7) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      bs[e] = 0.f; bq[e] = 0.f;
+      const bool ok = nb + e < p.N;
+      bms[e] = ok ? p.bnprm[nb + e] : 0.f;
+      bmh[e] = ok ? p.bnprm[p.N + nb + e] : 0.f;
+      bmu[e] = ok ? p.bnprm[2 * p.N + nb + e] : 0.f;
+      bis[e] = ok ? p.bnprm[3 * p.N + nb + e] : 0.f;
+    }
+  }
 #pragma unroll
   for (int it = 0; it < 8; ++it) {
     const int rl = it * 8 + (lane >> 3), ch = (lane & 7) * 8;
     const int m = m0 + wave_m * 64 + rl;
     const int n = nw0 + ch;
     if (m >= p.M || n >= p.N) continue;
-    int64_t opix;
-    if (p.identity_map) opix = m;
+    int64_t yoff;
+    if constexpr (PF) yoff = pf_off[it];
     else {
-      const int img = (int)fdiv((uint32_t)m, p.div_pq), rem = m - img * (p.P * p.Q);
-      const int pp = (int)fdiv((uint32_t)rem, p.div_q), qq = rem - pp * p.Q;
-      opix = ((int64_t)img * p.OH + pp * p.osh + p.oph) * p.OW + qq * p.osw + p.opw;
+      int64_t opix;
+      if (p.identity_map) opix = m;
+      else {
+        const int img = (int)fdiv((uint32_t)m, p.div_pq), rem = m - img * (p.P * p.Q);
+        const int pp = (int)fdiv((uint32_t)rem, p.div_q), qq = rem - pp * p.Q;
+        opix = ((int64_t)img * p.OH + pp * p.osh + p.oph) * p.OW + qq * p.osw + p.opw;
+      }
+      yoff = opix * p.ldy + goff_y + n;
     }
-    u16* dst = p.y + opix * p.ldy + goff_y + n;
+    u16* dst = p.y + yoff;
     const u16* src = st + rl * EPI_PITCH + ch;
     if constexpr (RES) {  // residual-gradient join: dX += stashed gradient (fused instead of an add pass)
-      const u16* rp = p.res + opix * p.ldy + goff_y + n;
+      const u16* rp = p.res + yoff;
       if (vec) {
-        uint4 a = *reinterpret_cast<const uint4*>(src), b = *reinterpret_cast<const uint4*>(rp);
+        uint4 a = *reinterpret_cast<const uint4*>(src), b = pf_res[it];
         const u16* av = reinterpret_cast<const u16*>(&a);
         const u16* bw = reinterpret_cast<const u16*>(&b);
         uint4 o;
@@ -343,16 +422,55 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
         for (int e = 0; e < 4; ++e)
           ov[e] = pack2bf(bf2f(av[2 * e]) + bf2f(bw[2 * e]), bf2f(av[2 * e + 1]) + bf2f(bw[2 * e + 1]));
         *reinterpret_cast<uint4*>(dst) = o;
+        if constexpr (BNR) bn_bwd_accum(p, o, pf_x[it], pf_mb[it], bs, bq, bmu, bis, bms, bmh);
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e)
           if (n + e < p.N) dst[e] = f2bf(bf2f(src[e]) + bf2f(rp[e]));
       }
     } else if (vec) {
-      *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+      const uint4 o = *reinterpret_cast<const uint4*>(src);
+      *reinterpret_cast<uint4*>(dst) = o;
+      if constexpr (BNR) bn_bwd_accum(p, o, pf_x[it], pf_mb[it], bs, bq, bmu, bis, bms, bmh);
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) if (n + e < p.N) dst[e] = src[e];
+    }
+  }
+  if constexpr (BNR) {
+    // lanes sharing (lane & 7) hold partials of the same 8 channels: butterfly over lane bits 3-5,
+    // then the WM waves of one channel column meet in LDS; one coalesced atomic row per block
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+#pragma unroll
+      for (int off = 8; off < 64; off <<= 1) {
+        bs[e] += __shfl_xor(bs[e], off, 64);
+        bq[e] += __shfl_xor(bq[e], off, 64);
+      }
+    }
+    float* sh = reinterpret_cast<float*>(smem + EPI_BYTES);  // [4 waves][64 channels][2]
+    if (lane < 8) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        sh[(wid * 64 + lane * 8 + e) * 2 + 0] = bs[e];
+        sh[(wid * 64 + lane * 8 + e) * 2 + 1] = bq[e];
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < BN_) {
+      const int nl = threadIdx.x, n = n0 + nl;
+      if (n < p.N) {
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int wm = 0; wm < WM; ++wm) {
+          const int w = wm * WN + nl / 64;
+          s1 += sh[(w * 64 + (nl & 63)) * 2];
+          s2 += sh[(w * 64 + (nl & 63)) * 2 + 1];
+        }
+        float* a = p.bnacc + (int64_t)(tm % DV_STAT_SHARDS) * 2 * p.N;
+        atomicAdd(a + n, s1);
+        atomicAdd(a + p.N + n, s2);
+      }
     }
   }
 }
@@ -364,24 +482,34 @@ constexpr int lds_bytes(int stages) {
                                                                        : EPI_BYTES + STAT_BYTES;
 }
 
-template <int BM_, int BN_, int BK_, int KMODE, bool RES, int STAGES>
+template <int BM_, int BN_, int BK_, int KMODE, bool RES, int STAGES, bool BNR = false>
 void launch_fwd(const FwdParams& p, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES>,
+    hipFuncSetAttribute((const void*)conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES, BNR>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes<BM_, BN_, BK_>(STAGES));
     attr = true;
   }
   const int nt = (p.K + BK_ - 1) / BK_;
   const size_t lds = lds_bytes<BM_, BN_, BK_>(nt < STAGES ? nt : STAGES);
   const int blocks = ((p.M + BM_ - 1) / BM_) * ((p.N + BN_ - 1) / BN_) * p.G;
-  conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES><<<dim3(blocks), dim3(NT), lds, st>>>(p);
+  conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES, BNR><<<dim3(blocks), dim3(NT), lds, st>>>(p);
 }
 
 int g_fwd_variant = 0;  // benchmarking override of the tile / pipeline choice (0 = heuristic)
 
-template <int KMODE, bool RES>
+template <int KMODE, bool RES, bool BNR = false>
 void dispatch_res(const FwdParams& p, hipStream_t st) {
+  if constexpr (BNR) {  // fused BN-backward statistics (dgrads, KM_FAST only): same tile choice
+    if (p.N <= 64) {
+      if (p.K <= 256) launch_fwd<256, 64, 32, KMODE, RES, 3, true>(p, st);
+      else launch_fwd<256, 64, 32, KMODE, RES, 2, true>(p, st);
+    } else {
+      if (p.K > 64 && p.K < 2048) launch_fwd<128, 128, 32, KMODE, RES, 2, true>(p, st);
+      else launch_fwd<128, 128, 64, KMODE, RES, 2, true>(p, st);
+    }
+    return;
+  }
   if constexpr (KMODE == KM_FAST) {
     switch (g_fwd_variant) {
       case 1: return launch_fwd<128, 128, 64, KMODE, RES, 2>(p, st);
@@ -418,7 +546,15 @@ void dispatch_res(const FwdParams& p, hipStream_t st) {
 
 template <int KMODE>
 void dispatch_tile(const FwdParams& p, hipStream_t st) {
-  // in-place gradient accumulation epilogue is compile-time: no cost for the others
+  // in-place gradient accumulation / fused BN statistics epilogues are compile-time: no cost
+  // for the others
+  if constexpr (KMODE == KM_FAST) {
+    if (p.bnmode) {
+      if (p.res) dispatch_res<KMODE, true, true>(p, st);
+      else dispatch_res<KMODE, false, true>(p, st);
+      return;
+    }
+  }
   if (p.res) dispatch_res<KMODE, true>(p, st);
   else dispatch_res<KMODE, false>(p, st);
 }
@@ -438,12 +574,38 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
   p.OH = a.OH; p.OW = a.OW; p.osh = a.osh; p.osw = a.osw; p.oph = a.oph; p.opw = a.opw; p.ldy = a.ldy;
   p.act = a.act; p.slope = a.slope;
   p.identity_map = (a.OH == a.P && a.OW == a.Q && a.osh == 1 && a.osw == 1 && a.oph == 0 && a.opw == 0);
-  if (p.Cg % 8 != 0 || p.ldx % 8 != 0) return -1;
+  p.bnx = (const u16*)a.bnx; p.bnbits = (const uint8_t*)a.bnbits; p.bnprm = a.bnprm; p.bnacc = a.bnacc;
+  p.bnmode = a.bnmode; p.bnact = a.bnact; p.bnslope = a.bnslope;
+  // fused BN statistics need every element of y written by this kernel as 16-B vectors of a dense
+  // single-group tensor on the fast loader (the dgrads of stride-1 convs)
+  int bn_status = 0;
+  if (p.bnmode) {
+    const bool ok = a.tgather == 0 && p.identity_map && p.G == 1 && (p.N & 7) == 0 && p.ldy == p.N &&
+                    p.Cg % 64 == 0 && p.ldx % 8 == 0 && p.R <= 16 && p.S <= 16 && p.bnx && p.bnprm && p.bnacc &&
+                    (p.bnmode != 3 || p.bnbits);
+    if (!ok) { p.bnmode = 0; bn_status = 1; }
+  }
   p.div_pq = make_fastdiv((uint32_t)(a.P * a.Q));
   p.div_q = make_fastdiv((uint32_t)a.Q);
+  if (a.tgather == 2) {
+    p.bnmode = 0;
+    // Tap-packed input (stem convs with <= 4 input channels, ops/conv.py _StemConvFn): a padded
+    // [N][Hp][Wp][4] image read as Cg = 32 "channels" at a pixel stride of 4, i.e. one 16-B
+    // chunk = 2 horizontally adjacent pixels = 2 filter taps; one K-tile (BK = 32) = one filter
+    // row of 8 taps. Needs: no padding (the image is pre-padded), 16-B aligned chunks (even
+    // horizontal stride: every chunk starts at an even pixel), and BK = 32 tiles.
+    if (p.Cg % 32 != 0 || p.ldx != 4 || p.S != 1 || (p.sw & 1) || p.ph || p.pw || p.dh != 1 || p.res) return -1;
+    if (g_fwd_variant == 5) launch_fwd<256, 64, 32, KM_FAST, false, 4>(p, st);
+    else if (g_fwd_variant == 7) launch_fwd<128, 128, 32, KM_FAST, false, 4>(p, st);
+    else if (g_fwd_variant == 8) launch_fwd<128, 128, 32, KM_FAST, false, 2>(p, st);
+    else if (p.N <= 64) launch_fwd<256, 64, 32, KM_FAST, false, 3>(p, st);
+    else launch_fwd<128, 128, 32, KM_FAST, false, 2>(p, st);
+    return bn_status;
+  }
+  if (p.Cg % 8 != 0 || p.ldx % 8 != 0) return -1;
   // the fast loader needs every K-tile inside one filter tap: Cg % 64 == 0 covers both BKs
   if (a.tgather) dispatch_tile<KM_TGATHER>(p, st);
   else if (p.Cg % 64 == 0 && p.R <= 16 && p.S <= 16) dispatch_tile<KM_FAST>(p, st);
   else dispatch_tile<KM_GENERIC>(p, st);
-  return 0;
+  return bn_status;
 }

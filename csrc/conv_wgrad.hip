@@ -294,7 +294,7 @@ void launch_wg(WgParams p, int blocks, hipStream_t st) {
 }
 
 // 64x256 tiles only when the weight gradient is 64 rows by >= 256 columns (else 3/4 of the tile idles)
-inline bool wg_narrow(int M, int N) { return M <= 64 && N >= 256; }
+inline bool wg_narrow(int M, int N) { return M <= 64 && N >= 192; }
 
 int g_wg_variant = 0;       // benchmarking override of tile / K-depth / pipeline (0 = heuristic)
 int g_wg_split_pct = 100;   // benchmarking scale of the split-K heuristic
@@ -346,7 +346,10 @@ int dv_conv_wgrad(const ConvWgradArgs& a, hipStream_t st) {
   p.Hin = a.H; p.Win = a.W; p.Cg = a.Cg; p.ldx = a.ldx; p.ldm = a.ldy;
   p.P = a.P; p.Q = a.Q; p.R = a.R; p.S = a.S;
   p.sh = a.sh; p.sw = a.sw; p.ph = a.ph; p.pw = a.pw; p.dh = a.dh; p.dw_ = a.dw_;
-  if (p.Cg % 8 != 0 || p.ldx % 8 != 0 || p.ldm % 8 != 0) return -1;
+  // ldx == 4: tap-packed stem image (see conv_fwd.hip): chunks of 2 pixels x 4 channels that
+  // start at even pixels (even horizontal stride, no padding) stay 16-B aligned
+  const bool packed = p.ldx == 4 && p.Cg % 32 == 0 && p.S == 1 && (p.sw & 1) == 0 && p.pw == 0 && p.ph == 0;
+  if (p.Cg % 8 != 0 || (p.ldx % 8 != 0 && !packed) || p.ldm % 8 != 0) return -1;
   p.div_pq = make_fastdiv((uint32_t)(a.P * a.Q));
   p.div_q = make_fastdiv((uint32_t)a.Q);
   p.div_cg = make_fastdiv((uint32_t)a.Cg);

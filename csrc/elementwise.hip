@@ -102,20 +102,22 @@ __global__ __launch_bounds__(NT) void dropout_kernel(const u16* __restrict__ x, 
 }
 
 __global__ void wprep_kernel(const float* __restrict__ w, u16* __restrict__ out, int G, int Og, int Ig, int R, int S,
-                             int pad, int mode) {
+                             int pad, int mode, int Sp) {
   // mode 0: out[g][o][r][s][i], i padded to `pad` (>= Ig)
   // mode 1: out[g][i][r][s][o], o padded to `pad` (>= Og)
-  const int64_t total = mode == 0 ? (int64_t)G * Og * pad * R * S : (int64_t)G * Ig * pad * R * S;
+  // mode 2: mode 0 with the filter width padded to Sp (>= S): the tap-packed stem operand
+  const int SS = mode == 2 ? Sp : S;
+  const int64_t total = mode != 1 ? (int64_t)G * Og * pad * R * SS : (int64_t)G * Ig * pad * R * S;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
     int64_t u = t;
     int g, o, i, r, s;
     bool ok;
-    if (mode == 0) {
+    if (mode != 1) {
       i = (int)(u % pad); u /= pad;
-      s = (int)(u % S); u /= S;
+      s = (int)(u % SS); u /= SS;
       r = (int)(u % R); u /= R;
       o = (int)(u % Og); g = (int)(u / Og);
-      ok = i < Ig;
+      ok = i < Ig && s < S;
     } else {
       o = (int)(u % pad); u /= pad;
       s = (int)(u % S); u /= S;
@@ -164,18 +166,20 @@ __global__ __launch_bounds__(256) void wprep_batched_kernel(const WprepDesc* __r
     }
     return;
   }
-  // forward layout: out[g][o][r][s][i] (i padded) -- reads stay inside one filter row (cached)
-  const FastDiv fpad = fastdiv_dev(d.pad), fs = fastdiv_dev(d.S), fr = fastdiv_dev(d.R);
+  // forward layout: out[g][o][r][s][i] (i padded; s padded to Sp in mode 2) -- reads stay inside
+  // one filter row (cached)
+  const int SS = d.mode == 2 ? d.Sp : d.S;
+  const FastDiv fpad = fastdiv_dev(d.pad), fs = fastdiv_dev(SS), fr = fastdiv_dev(d.R);
   const FastDiv fo = fastdiv_dev(d.Og);
   const uint32_t t0 = (uint32_t)ch.y * WPREP_CHUNK;
   const uint32_t t1 = (uint32_t)min(d.total, (int64_t)t0 + WPREP_CHUNK);
   for (uint32_t t = t0 + threadIdx.x; t < t1; t += 256) {
     uint32_t u = t, q;
     q = fdiv(u, fpad); const int i = (int)(u - q * d.pad); u = q;
-    q = fdiv(u, fs); const int s = (int)(u - q * d.S); u = q;
+    q = fdiv(u, fs); const int s = (int)(u - q * SS); u = q;
     q = fdiv(u, fr); const int r = (int)(u - q * d.R); u = q;
     q = fdiv(u, fo); const int o = (int)(u - q * d.Og); const int g = (int)q;
-    d.out[t] = i < d.Ig ? f2bf(d.w[((((int64_t)(g * d.Og + o)) * d.Ig + i) * d.R + r) * d.S + s]) : (u16)0;
+    d.out[t] = (i < d.Ig && s < d.S) ? f2bf(d.w[((((int64_t)(g * d.Og + o)) * d.Ig + i) * d.R + r) * d.S + s]) : (u16)0;
   }
 }
 
@@ -227,6 +231,36 @@ __global__ void to_nhwc_kernel(const T* __restrict__ x, u16* __restrict__ y, int
   }
 }
 
+// Stem input for tap-packed convolution (conv_fwd.hip "packed" mode): NCHW (C <= 4, fp32 or
+// bf16) -> bf16 [N][Hp][Wp][4], zero-padded by (pt, pl) at the top/left and to (Hp, Wp) at the
+// bottom/right, channel 3 (and up) zero. Each pixel is 8 bytes, so the 16 bytes a K-chunk reads
+// are two horizontally adjacent pixels = two filter taps of one row. One thread per pixel.
+template <typename T>
+__global__ void stem_pack_kernel(const T* __restrict__ x, u16* __restrict__ y, int N, int C, int H, int W, int Hp,
+                                 int Wp, int pt, int pl) {
+  const int64_t total = (int64_t)N * Hp * Wp;
+  const int64_t HW = (int64_t)H * W;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int wp = (int)(t % Wp);
+    const int64_t nh = t / Wp;
+    const int hp = (int)(nh % Hp);
+    const int64_t n = nh / Hp;
+    const int h = hp - pt, w = wp - pl;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (h >= 0 && h < H && w >= 0 && w < W) {
+      const int64_t src = n * C * HW + (int64_t)h * W + w;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (c < C) {
+          if constexpr (sizeof(T) == 4) v[c] = x[src + c * HW]; else v[c] = bf2f(x[src + c * HW]);
+        }
+    }
+    uint2 r;
+    r.x = pack2bf(v[0], v[1]); r.y = pack2bf(v[2], v[3]);
+    *reinterpret_cast<uint2*>(y + t * 4) = r;
+  }
+}
+
 __global__ void f32_to_bf16_kernel(const float* __restrict__ x, u16* __restrict__ y, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) y[i] = f2bf(x[i]);
 }
@@ -252,9 +286,15 @@ void dv_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, hipSt
   const float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
   dropout_kernel<<<grid_for(n), NT, 0, st>>>((const u16*)x, (u16*)y, n, t, scale, (uint32_t)seed, (uint32_t)(seed >> 32));
 }
-void dv_wprep(const float* w, void* out, int G, int Og, int Ig, int R, int S, int pad, int mode, hipStream_t st) {
-  const int64_t total = (int64_t)G * (mode == 0 ? Og : Ig) * pad * R * S;
-  wprep_kernel<<<grid_for(total), NT, 0, st>>>(w, (u16*)out, G, Og, Ig, R, S, pad, mode);
+void dv_wprep(const float* w, void* out, int G, int Og, int Ig, int R, int S, int pad, int mode, int Sp, hipStream_t st) {
+  const int64_t total = (int64_t)G * (mode != 1 ? Og : Ig) * pad * R * (mode == 2 ? Sp : S);
+  wprep_kernel<<<grid_for(total), NT, 0, st>>>(w, (u16*)out, G, Og, Ig, R, S, pad, mode, Sp);
+}
+void dv_stem_pack(const void* x, int x_is_f32, void* y, int N, int C, int H, int W, int Hp, int Wp, int pt, int pl,
+                  hipStream_t st) {
+  const int64_t total = (int64_t)N * Hp * Wp;
+  if (x_is_f32) stem_pack_kernel<float><<<grid_for(total), NT, 0, st>>>((const float*)x, (u16*)y, N, C, H, W, Hp, Wp, pt, pl);
+  else stem_pack_kernel<u16><<<grid_for(total), NT, 0, st>>>((const u16*)x, (u16*)y, N, C, H, W, Hp, Wp, pt, pl);
 }
 void dv_wprep_batched(const void* descs, const void* chunks, int nchunks, hipStream_t st) {
   if (nchunks > 0)

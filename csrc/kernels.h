@@ -15,10 +15,18 @@ struct ConvFwdArgs {
   int Nb, H, W, Cg, ldx, G;
   int Kout, P, Q;     // GEMM columns per group, pixel grid enumerated by m
   int R, S, sh, sw, ph, pw, dh, dw;
-  int tgather;        // transposed-conv gather (dgrad with stride > 1)
+  int tgather;        // 1: transposed-conv gather (dgrad with stride > 1); 2: tap-packed stem input
   int OH, OW, osh, osw, oph, opw, ldy;  // output pixel mapping
   int act; float slope;
   const void* res;    // optional residual added in the epilogue (layout of y, may alias y)
+  // optional fused BatchNorm-backward statistics of the produced tensor (a dgrad whose output is
+  // the incoming gradient of a BatchNorm): sum dz and sum dz*xhat per channel into bnacc
+  const void* bnx;        // the BN's input (same layout as y)
+  const void* bnbits;     // activation mask bits (bnmode 3) or nullptr
+  const float* bnprm;     // [4][C]: scale, shift, mean, invstd
+  float* bnacc;           // [SHARDS][2][C]
+  int bnmode;             // 0 off, 1 no activation, 2 mask recomputed from bnx, 3 mask bits
+  int bnact; float bnslope;
 };
 
 struct ConvWgradArgs {
@@ -33,7 +41,7 @@ struct ConvWgradArgs {
   int oirs_ig;     // > 0: dw is the parameter's own [G*Kout][oirs_ig][R][S] layout (padded channels dropped)
 };
 
-int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st);
+int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st);  // 0 ok, 1 ok but BN statistics not fused, -1 unsupported
 void dv_conv_fwd_variant(int v);  // 0 = heuristic tile choice; others: benchmarking override
 int dv_conv_wgrad(const ConvWgradArgs& a, hipStream_t st);
 void dv_conv_wgrad_tuning(int variant, int split_pct);  // benchmarking override (0, 100 = heuristic)
@@ -41,6 +49,7 @@ int dv_conv_wgrad_splits(const ConvWgradArgs& a);
 int dv_conv_stats_tiles(int Nb, int P, int Q);
 
 // ---- batchnorm (bn.hip) ----
+void dv_bn_tuning(int reduce_blocks, int reduce_unroll);  // benchmarking override (1024, 2 = default)
 void dv_bn_stats(const void* x, int64_t rows, int C, float* acc, hipStream_t st);
 void dv_bn_finalize(float* acc, int C, double count, float eps, float momentum, const float* gamma,
                     const float* beta, float* rm, float* rv, float* save_mean, float* save_invstd, float* scale,
@@ -79,7 +88,9 @@ void dv_act_fwd(const void* x, void* y, int64_t n, int act, float slope, hipStre
 void dv_act_bwd(const void* dy, const void* y, void* dx, int64_t n, int act, float slope, hipStream_t st);
 void dv_add(const void* a, const void* b, void* y, int64_t n, float alpha, float beta, int act, float slope, hipStream_t st);
 void dv_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, hipStream_t st);
-void dv_wprep(const float* w, void* out, int G, int Og, int Ig, int R, int S, int Ipad, int mode, hipStream_t st);
+void dv_wprep(const float* w, void* out, int G, int Og, int Ig, int R, int S, int Ipad, int mode, int Sp, hipStream_t st);
+void dv_stem_pack(const void* x, int x_is_f32, void* y, int N, int C, int H, int W, int Hp, int Wp, int pt, int pl,
+                  hipStream_t st);
 void dv_wgrad_unprep(float* src, float* dst, int G, int Og, int Ig, int R, int S, int Ipad, float alpha,
                      int accumulate, int zero_src, hipStream_t st);
 void dv_to_nhwc(const void* x, int x_is_f32, void* y, int N, int C, int H, int W, int Cp, hipStream_t st);
@@ -131,6 +142,6 @@ struct WprepDesc {  // 48 bytes, mirrored by deep_vision_amd/ops/wcache.py
   const float* w;
   unsigned short* out;
   int64_t total;
-  int G, Og, Ig, R, S, pad, mode, _unused;
+  int G, Og, Ig, R, S, pad, mode, Sp;  // Sp: padded filter width (mode 2)
 };
 void dv_wprep_batched(const void* descs, const void* chunks, int nchunks, hipStream_t st);

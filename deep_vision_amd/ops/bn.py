@@ -22,6 +22,39 @@ from .common import (ACT_IDS, BF16, F32, grad_nhwc, grad_sink, is_nhwc, ld_of, l
                      stream_handle, workspace)
 
 STAT_SHARDS = 64
+FUSE_BWD_STATS = True  # fold the backward reduction into the consumer conv's dgrad epilogue
+COUNTERS = {"bwd_reduce_fused": 0, "bwd_reduce_pass": 0}
+
+
+class BNRef:
+    """What a consumer conv's dgrad needs to fold this BatchNorm's backward reduction (sum dz,
+    sum dz*xhat) into its epilogue (csrc/conv_fwd.hip BNR): the BN input, mask source and
+    statistics. Attached to the BN output tensor (``_dv_bnref``); the conv records the gradient
+    tensor it produced, and the BN backward uses the fused sums only if the gradient it receives
+    IS that tensor (same storage, untouched version, a single fusion) -- otherwise it zeroes the
+    accumulator and runs its own reduce pass."""
+
+    __slots__ = ("x", "bits", "prm", "mode", "act", "slope", "acc", "fused", "nfused")
+
+    def __init__(self, x, bits, prm, mode, act, slope, acc):
+        self.x, self.bits, self.prm, self.mode, self.act, self.slope, self.acc = x, bits, prm, mode, act, slope, acc
+        self.fused = None
+        self.nfused = 0
+
+    def mark_fused(self, g):
+        self.fused = (g.data_ptr(), g._version, tuple(g.shape), g.stride())
+        self.nfused += 1
+
+    def take(self, dout):
+        """True when ``acc`` already holds the reduction of exactly ``dout``."""
+        if self.fused is None:
+            return False
+        ok = self.nfused == 1 and self.fused == (dout.data_ptr(), dout._version, tuple(dout.shape), dout.stride())
+        if not ok:
+            self.acc.zero_()  # partial / foreign sums
+        self.fused = None
+        self.nfused = 0
+        return ok
 
 
 def _nrows(x):
@@ -32,7 +65,7 @@ def _nrows(x):
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, stats, weight, bias, running_mean, running_var, residual, training, momentum, eps, act,
-                slope, ws_fwd, ws_bwd, join=None):
+                slope, ws_fwd, ws_bwd, join=None, refbox=None):
         N, C, H, W = x.shape
         if ld_of(x) != C:
             raise NotImplementedError("BatchNorm on a padded channel view")
@@ -69,6 +102,11 @@ class _BNActFn(torch.autograd.Function):
         ctx.cfg = (training, act, slope, residual is not None)
         ctx.ws_bwd = ws_bwd
         ctx.join = join
+        ctx.bnref = None
+        if refbox is not None and training and ws_bwd is not None and C % 8 == 0 and (not act or bits or residual is None):
+            mode = 3 if bits else (2 if act else 1)
+            ctx.bnref = BNRef(x, mask if bits else None, prm, mode, act, slope, ws_bwd)
+            refbox.append(ctx.bnref)
         return out
 
     @staticmethod
@@ -77,6 +115,7 @@ class _BNActFn(torch.autograd.Function):
         training, act, slope, has_res = ctx.cfg
         scale, shift, mean, invstd = prm[0], prm[1], prm[2], prm[3]
         N, C, H, W = x.shape
+        fused = ctx.bnref is not None and ctx.bnref.take(dout)
         dout = grad_nhwc(dout)
         if ld_of(dout) != C:
             dout = dout.contiguous(memory_format=torch.channels_last)
@@ -92,8 +131,10 @@ class _BNActFn(torch.autograd.Function):
             # sum dz and sum dz*xhat (xhat from the batch statistics, or the running ones in eval)
             rows = N * H * W
             acc = ctx.ws_bwd if ctx.ws_bwd is not None else torch.zeros((STAT_SHARDS, 2, C), dtype=F32, device=dev)
-            L.bn_bwd_reduce(ptr(dout), ptr(out), ptr(x), rows, C, ptr(mean), ptr(invstd), ptr(scale), ptr(shift), act,
-                            float(slope), ptr(acc), int(ctx.bits), st)
+            COUNTERS["bwd_reduce_fused" if fused else "bwd_reduce_pass"] += 1
+            if not fused:  # else the producing dgrad's epilogue already reduced into acc
+                L.bn_bwd_reduce(ptr(dout), ptr(out), ptr(x), rows, C, ptr(mean), ptr(invstd), ptr(scale), ptr(shift),
+                                act, float(slope), ptr(acc), int(ctx.bits), st)
             sg = grad_sink(weight) if ctx.needs_input_grad[2] else None
             sb = grad_sink(bias) if ctx.needs_input_grad[3] else None
             direct = sg is not None and sb is not None
@@ -117,7 +158,7 @@ class _BNActFn(torch.autograd.Function):
             notify_grad_ready(bias)
         if ctx.join is not None and dres is not None:
             dres = ctx.join.produce(dres)  # folded into the shortcut consumer's dgrad epilogue
-        return dx, None, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None, None
+        return dx, None, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None, None, None
 
 
 def _torch_bn_act(x, bn, act, slope, residual):
@@ -174,8 +215,12 @@ def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None, residu
     C = x.shape[1]
     ws_fwd = workspace(bn, "bn_fwd", (STAT_SHARDS, 2, C), x.device) if training else None
     ws_bwd = workspace(bn, "bn_bwd", (STAT_SHARDS, 2, C), x.device) if training else None
-    return _BNActFn.apply(x, stats, bn.weight, bn.bias, rm, rv, residual, training, mom,
-                          bn.eps, ACT_IDS[act], float(slope), ws_fwd, ws_bwd, residual_join)
+    refbox = [] if FUSE_BWD_STATS and torch.is_grad_enabled() else None
+    y = _BNActFn.apply(x, stats, bn.weight, bn.bias, rm, rv, residual, training, mom,
+                       bn.eps, ACT_IDS[act], float(slope), ws_fwd, ws_bwd, residual_join, refbox)
+    if refbox:
+        y._dv_bnref = refbox[0]  # read by the consumer conv (ops.conv._ConvFn)
+    return y
 
 
 def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None, join=None, join_role=None, residual_join=None):

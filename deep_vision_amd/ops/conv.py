@@ -67,7 +67,7 @@ def _prep_weight(weight: torch.Tensor, G: int, pad: int, mode: int, param=None) 
             w = w.float().contiguous()
         if out is None:
             out = torch.empty(n, dtype=BF16, device=w.device)
-        lib().wprep(ptr(w), ptr(out), G, Og, Ig, R, S, pad, mode, stream_handle())
+        lib().wprep(ptr(w), ptr(out), G, Og, Ig, R, S, pad, mode, 0, stream_handle())
         return out
 
     key = param if param is not None else weight
@@ -86,14 +86,21 @@ def _channel_sum(dy: torch.Tensor) -> torch.Tensor:
 
 
 def conv_fwd_raw(x, wk, y, bias, stats, N, H, W, Cg, ldx, G, Kout, P, Q, R, S, stride, padding, dilation,
-                 act=0, slope=0.0, tgather=0, omap=None, ldy=None, res=None):
+                 act=0, slope=0.0, tgather=0, omap=None, ldy=None, res=None, bnref=None):
+    """Launch the implicit-GEMM kernel. ``bnref`` (ops.bn.BNRef): also reduce that BatchNorm's
+    backward statistics over ``y`` in the epilogue; returns True when that was done."""
     sh, sw = stride
     ph, pw = padding
     dh, dw = dilation
     OH, OW, osh, osw, oph, opw = omap if omap is not None else (P, Q, 1, 1, 0, 0)
-    lib().conv_fwd(ptr(x), ptr(wk), ptr(y), ptr(bias), ptr(stats), N, H, W, Cg, ldx, G, Kout, P, Q, R, S, sh, sw, ph,
-                   pw, dh, dw, tgather, OH, OW, osh, osw, oph, opw, ldy if ldy is not None else ld_of(y), act, float(slope),
-                   ptr(res), stream_handle())
+    bn = {}
+    if bnref is not None:
+        bn = dict(bnx=ptr(bnref.x), bnbits=ptr(bnref.bits), bnprm=ptr(bnref.prm), bnacc=ptr(bnref.acc),
+                  bnmode=bnref.mode, bnact=bnref.act, bnslope=float(bnref.slope))
+    r = lib().conv_fwd(ptr(x), ptr(wk), ptr(y), ptr(bias), ptr(stats), N, H, W, Cg, ldx, G, Kout, P, Q, R, S, sh, sw,
+                       ph, pw, dh, dw, tgather, OH, OW, osh, osw, oph, opw, ldy if ldy is not None else ld_of(y), act,
+                       float(slope), ptr(res), stream_handle(), **bn)
+    return bnref is not None and r == 0
 
 
 def _gather_channels(t: torch.Tensor, per_group: int, G: int) -> int:
@@ -114,7 +121,7 @@ def _accumulable(t, shape):
             and t.is_contiguous(memory_format=CL))
 
 
-def _dgrad(dy, weight, x_shape, Cg_x, G, stride, padding, dilation, device, accum=None):
+def _dgrad(dy, weight, x_shape, Cg_x, G, stride, padding, dilation, device, accum=None, bnref=None):
     """dX (N, G*Cg_x, H, W) from dY; Cg_x may include zero-padding channels.
 
     ``accum``: a dense gradient of the same input from another consumer (residual shortcut /
@@ -136,8 +143,10 @@ def _dgrad(dy, weight, x_shape, Cg_x, G, stride, padding, dilation, device, accu
     else:
         dX, res = alloc_cl((N, G * Cg_x, H, W), zero=(scatter or Cg_x != Ig), device=device), None
     if (sh, sw) == (1, 1):
-        conv_fwd_raw(dy, wd, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, H, W, R, S, (1, 1), (-ph, -pw),
-                     (-dh, -dw), ldy=G * Cg_x, res=res)
+        fuse = bnref if (bnref is not None and G == 1 and Cg_x == Ig and (res is not None or accum is None)) else None
+        if conv_fwd_raw(dy, wd, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, H, W, R, S, (1, 1), (-ph, -pw),
+                        (-dh, -dw), ldy=G * Cg_x, res=res, bnref=fuse):
+            fuse.mark_fused(dX)
     elif scatter:
         conv_fwd_raw(dy, wd, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, P, Q, 1, 1, (1, 1), (0, 0), (1, 1),
                      omap=(H, W, sh, sw, 0, 0), ldy=G * Cg_x, res=res)
@@ -234,6 +243,8 @@ class _ConvFn(torch.autograd.Function):
         ctx.save_for_backward(x, weight, y if act else None)
         ctx.cfg = (stride, padding, dilation, G, act, slope, Cg_x, bias is not None)
         ctx.join = (join, join_role)
+        # the producing BatchNorm of x: its backward statistics can ride on this conv's dgrad
+        ctx.bnref = getattr(x, "_dv_bnref", None) if join_role != "producer" else None
         ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics output
         if want_stats:
             ctx.mark_non_differentiable(stats)
@@ -260,7 +271,8 @@ class _ConvFn(torch.autograd.Function):
         join, role = ctx.join
         if ctx.needs_input_grad[0]:
             accum = join.take() if (join is not None and role == "consumer") else None
-            dx = _dgrad(dy, weight, x.shape, Cg_x, G, stride, padding, dilation, x.device, accum=accum)
+            dx = _dgrad(dy, weight, x.shape, Cg_x, G, stride, padding, dilation, x.device, accum=accum,
+                        bnref=ctx.bnref)
             if dx.shape[1] != x.shape[1]:
                 dx = dx[:, : x.shape[1]]
             if join is not None and role == "producer":
@@ -274,6 +286,105 @@ class _ConvFn(torch.autograd.Function):
         if has_bias and ctx.needs_input_grad[2]:
             db = _channel_sum(dy)
         return dx, dw, db, None, None, None, None, None, None, None, None, None, None, None
+
+
+# ---------------------------------------------------------------------------------------
+# Tap-packed stem convolution: first layers with <= 4 input channels (ResNet/Inception 7x7 s2,
+# AlexNet 11x11 s4, Hourglass 7x7 s2, ...). The input is re-laid out ONCE as a zero-padded
+# [N][Hp][Wp][4] bf16 image; the kernel reads it as 8-tap x 4-channel rows (Cg = 4*Sp at a pixel
+# stride of 4), so K = R * Sp * 4 (7x7: 224) instead of R * S * 8 with channels padded to 8
+# (392): 1.75x fewer MFMA k-steps and no im2col bounds checks (csrc/conv_fwd.hip packed mode).
+# ---------------------------------------------------------------------------------------
+def _stem_geometry(x, weight, stride, padding, dilation, groups, extra):
+    """(Sp, Hp, Wp, P, Q) when the tap-packed path applies, else None."""
+    if groups != 1 or tuple(dilation) != (1, 1) or x.requires_grad or x.dim() != 4 or x.dtype not in (F32, BF16):
+        return None
+    N, C, H, W = x.shape
+    O, I, R, S = weight.shape
+    if C > 4 or I != C or stride[1] % 2 or not (5 <= S <= 16) or R > 16 or min(padding) < 0:
+        return None
+    Sp = 8 if S <= 8 else 16
+    P, Q = out_size(H + extra[0], W + extra[1], R, S, stride, padding, dilation)
+    Hp = (P - 1) * stride[0] + R
+    Wp = (Q - 1) * stride[1] + Sp  # even: every 16-B chunk starts at an even pixel
+    return Sp, Hp, Wp, P, Q
+
+
+def _prep_stem_weight(weight, Sp):
+    O, I, R, S = weight.shape
+    n = O * R * Sp * 4
+
+    def compute(out):
+        w = weight.detach()
+        if w.dtype != F32 or not w.is_contiguous():
+            w = w.float().contiguous()
+        if out is None:
+            out = torch.empty(n, dtype=BF16, device=w.device)
+        lib().wprep(ptr(w), ptr(out), 1, O, I, R, S, 4, 2, Sp, stream_handle())
+        return out
+
+    if isinstance(weight, torch.nn.Parameter) and weight.dtype == F32 and weight.is_contiguous():
+        return wcache.get(weight, 1, 4, 2, compute, Sp=Sp)
+    return compute(None)
+
+
+class _StemConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, padding, act, slope, want_stats, stats_buf, geo):
+        Sp, Hp, Wp, P, Q = geo
+        N, C, H, W = x.shape
+        O, I, R, S = weight.shape
+        xc = x if x.is_contiguous() else x.contiguous()
+        xp = torch.empty((N, Hp, Wp, 4), dtype=BF16, device=x.device)
+        lib().stem_pack(ptr(xc), int(xc.dtype == F32), ptr(xp), N, C, H, W, Hp, Wp, padding[0], padding[1],
+                        stream_handle())
+        wk = _prep_stem_weight(weight, Sp)
+        y = empty_nhwc(N, O, P, Q, x.device)
+        stats = None
+        if want_stats:
+            stats = stats_buf if stats_buf is not None else torch.zeros((STAT_SHARDS, 2, O), dtype=F32, device=x.device)
+        b = bias.detach().float().contiguous() if bias is not None else None
+        conv_fwd_raw(xp, wk, y, b, stats, N, Hp, Wp, 4 * Sp, 4, 1, O, P, Q, R, 1, stride, (0, 0), (1, 1), act=act,
+                     slope=slope, tgather=2)
+        ctx.save_for_backward(xp, weight, y if act else None)
+        ctx.cfg = (stride, act, slope, geo, bias is not None)
+        ctx.set_materialize_grads(False)
+        if want_stats:
+            ctx.mark_non_differentiable(stats)
+            return y, stats
+        return y
+
+    @staticmethod
+    def backward(ctx, dy, *unused):
+        xp, weight, y = ctx.saved_tensors
+        stride, act, slope, geo, has_bias = ctx.cfg
+        if dy is None:
+            return (None,) * 10
+        Sp, Hp, Wp, P, Q = geo
+        O, I, R, S = weight.shape
+        N = xp.shape[0]
+        dy = grad_nhwc(dy)
+        if act:
+            dy = like_layout(dy, y)
+            g = empty_layout(y)
+            lib().act_bwd(ptr(dy), ptr(y), ptr(g), nhwc_numel(y), act, float(slope), stream_handle())
+            dy = g
+        dw = db = None
+        if ctx.needs_input_grad[1]:
+            ws = _wgrad_workspace(O * R * Sp * 4, xp.device)  # [O][R][Sp][4], zero on entry and exit
+            lib().conv_wgrad(ptr(xp), ptr(dy), ptr(ws), N, Hp, Wp, 4 * Sp, 4, 1, O, P, Q, ld_of(dy), R, 1, stride[0],
+                             stride[1], 0, 0, 1, 1, 0, 1, 0, stream_handle())
+            full = torch.empty((O, I, R, Sp), dtype=F32, device=xp.device)
+            lib().wgrad_unprep(ptr(ws), ptr(full), 1, O, I, R, Sp, 4, 1.0, 0, 1, stream_handle())
+            sink = grad_sink(weight)
+            if sink is not None:
+                sink.add_(full[..., :S])
+                notify_grad_ready(weight)
+            else:
+                dw = full[..., :S].contiguous()
+        if has_bias and ctx.needs_input_grad[2]:
+            db = _channel_sum(dy)
+        return None, dw, db, None, None, None, None, None, None, None
 
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=None, slope=0.0,
@@ -307,6 +418,12 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=
         if extra != (0, 0):
             raise NotImplementedError("asymmetric padding on a channel-padded grouped conv")
         return _grouped_padded_conv(x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats)
+    geo = _stem_geometry(x, weight, stride, padding, dilation, groups, extra)
+    if geo is not None:  # network input: no gradient, no join
+        if join is not None and join_role == "consumer":
+            join.consumer_done = True
+        return _StemConvFn.apply(x, weight, bias, stride, padding, ACT_IDS[act], float(slope), want_stats, stats_buf,
+                                 geo)
     xn = as_nhwc(x, pad_to8=(groups == 1))
     if xn is not x and join is not None:
         if join_role == "consumer":  # the gradient reaches x through the layout copy: no join

@@ -25,15 +25,16 @@ _tables = {}  # device -> (n_entries_snapshot, descs, chunks, nchunks)
 ENABLED = True
 
 
-def _key(param, G, pad, mode):
-    return (id(param), G, pad, mode)
+def _key(param, G, pad, mode, Sp=0):
+    return (id(param), G, pad, mode, Sp)
 
 
-def get(param, G, pad, mode, compute):
-    """bf16 operand of ``param`` in layout (G, pad, mode); ``compute(out)`` fills a buffer."""
+def get(param, G, pad, mode, compute, Sp=0):
+    """bf16 operand of ``param`` in layout (G, pad, mode[, Sp]); ``compute(out)`` fills a buffer.
+    mode 2 = the forward layout with the filter width padded to ``Sp`` (tap-packed stem)."""
     if not ENABLED:
         return compute(None)
-    k = _key(param, G, pad, mode)
+    k = _key(param, G, pad, mode, Sp)
     e = _entries.get(k)
     if e is not None and e[0]() is param:
         if e[2] == _epoch and e[3] == param._version and e[4] == param.data_ptr():
@@ -42,7 +43,7 @@ def get(param, G, pad, mode, compute):
     else:
         buf = compute(None)
         _tables.pop(buf.device, None)
-    _entries[k] = [weakref.ref(param), buf, _epoch, param._version, param.data_ptr(), (G, pad, mode)]
+    _entries[k] = [weakref.ref(param), buf, _epoch, param._version, param.data_ptr(), (G, pad, mode, Sp)]
     return buf
 
 
@@ -57,13 +58,13 @@ def _build_table(device):
             continue
         if e[1].device != device or p.dtype != torch.float32 or not p.is_contiguous():
             continue
-        G, pad, mode = e[5]
+        G, pad, mode, Sp = e[5]
         shp = p.shape if p.dim() == 4 else (p.shape[0], p.shape[1], 1, 1)
         O, Ig, R, S = shp
         Og = O // G
-        total = G * (Og if mode == 0 else Ig) * R * S * pad
+        total = G * (Ig if mode == 1 else Og) * R * (Sp if mode == 2 else S) * pad
         di = len(descs)
-        descs.append(struct.pack("<qqqiiiiiiii", p.data_ptr(), e[1].data_ptr(), total, G, Og, Ig, R, S, pad, mode, 0))
+        descs.append(struct.pack("<qqqiiiiiiii", p.data_ptr(), e[1].data_ptr(), total, G, Og, Ig, R, S, pad, mode, Sp))
         if mode == 1:  # 64x64 transpose tiles per group (wprep_batched_kernel)
             K = Ig * R * S
             ntiles = G * ((K + 63) // 64) * ((pad + 63) // 64)

@@ -382,3 +382,36 @@ def test_resnet_grad_join_and_weight_cache():
                              zip(runs[v][0].parameters(), base.parameters())]) for v in runs}
         cn, cb = _cos(upd["native"], upd["fp32"]), _cos(upd["bf16"], upd["fp32"])
         assert cn > cb - 0.05, (name, cn, cb)
+
+
+def test_bn_backward_stats_fused_in_dgrad():
+    """BatchNorm backward reductions folded into the consumer conv's dgrad epilogue (ops.bn.BNRef,
+    csrc/conv_fwd.hip BNR) give the same gradients as the separate bn_bwd_reduce pass."""
+    from deep_vision_amd import models as M
+    from deep_vision_amd import ops as F
+    from deep_vision_amd.ops import bn as B
+
+    torch.manual_seed(0)
+    base = M.get_model("resnet50").to(DEV)
+    x = torch.randn(8, 3, 96, 96, device=DEV)
+    y = torch.randint(0, 1000, (8,), device=DEV)
+    grads = {}
+    try:
+        # two unfused runs measure the run-to-run noise (atomic-order fp32 sums -> bf16 rounding
+        # flips that propagate through 50 layers); the fused run must sit inside that noise
+        for key, fuse in (("a", False), ("b", False), ("fused", True)):
+            B.FUSE_BWD_STATS = fuse
+            m = copy.deepcopy(base)
+            c0 = dict(B.COUNTERS)
+            F.cross_entropy(m(x), y).backward()
+            torch.cuda.synchronize()
+            grads[key] = torch.cat([p.grad.flatten() for p in m.parameters()])
+            n_fused = B.COUNTERS["bwd_reduce_fused"] - c0["bwd_reduce_fused"]
+            if fuse:
+                assert n_fused >= 40, n_fused  # 53 BNs; the stem / stride-2-consumer / last ones run the pass
+            else:
+                assert n_fused == 0
+    finally:
+        B.FUSE_BWD_STATS = True
+    noise = _cos(grads["a"], grads["b"])
+    assert _cos(grads["fused"], grads["a"]) > min(noise, 0.99999) - 5e-4, (noise, _cos(grads["fused"], grads["a"]))

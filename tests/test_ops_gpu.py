@@ -404,7 +404,64 @@ def test_batched_weight_prep_matches_per_layer():
     for p, G, pad, mode in params:
         O, Ig, R, S = p.shape
         ref = torch.empty(G * (O // G if mode == 0 else Ig) * R * S * pad, dtype=torch.bfloat16, device=DEV)
-        lib().wprep(ptr(p.detach()), ptr(ref), G, O // G, Ig, R, S, pad, mode, stream_handle())
+        lib().wprep(ptr(p.detach()), ptr(ref), G, O // G, Ig, R, S, pad, mode, 0, stream_handle())
         got = _prep_weight(p, G, pad, mode)  # cache hit
         assert torch.equal(got, ref), (p.shape, G, pad, mode)
     wcache.clear()
+
+
+STEM_CASES = [
+    # N, C, H, W, K, R, S, stride, padding (int | (top, bottom, left, right)), bias, act
+    (2, 3, 32, 32, 64, 7, 7, 2, 3, False, None),         # ResNet / Inception stem
+    (2, 3, 36, 36, 96, 11, 11, 4, 2, True, "relu"),      # AlexNet V1 conv1 (Sp = 16)
+    (2, 3, 30, 30, 32, 5, 5, 2, 2, True, None),          # 5x5 s2
+    (3, 3, 32, 32, 128, 7, 7, 2, (2, 3, 2, 3), False, None),  # Keras 'same' 7x7 s2 (Hourglass stem)
+    (2, 1, 28, 28, 40, 5, 5, 2, 2, False, "relu"),       # 1 input channel
+]
+
+
+@pytest.mark.parametrize("case", STEM_CASES)
+def test_stem_packed_conv(case):
+    """Tap-packed stem path (ops.conv._StemConvFn, csrc conv_fwd packed mode + wgrad ldx=4) vs torch."""
+    from deep_vision_amd import ops as F
+    from deep_vision_amd.ops import conv as C
+
+    N, Cin, H, W, K, R, S, s, p, has_b, act = case
+    x = torch.randn(N, Cin, H, W, device=DEV).bfloat16().float()
+    w = (torch.randn(K, Cin, R, S, device=DEV) * 0.1).requires_grad_(True)
+    b = torch.randn(K, device=DEV).requires_grad_(True) if has_b else None
+    pad, extra = C.norm_padding(p)
+    assert C._stem_geometry(x, w, (s, s), pad, (1, 1), 1, extra) is not None
+    y = F.conv2d(x, w, b, s, p, act=act)
+    wr = w.detach().bfloat16().float().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True) if has_b else None
+    xr = TF.pad(x, (p[2], p[3], p[0], p[1])) if isinstance(p, tuple) else x
+    yr = TF.conv2d(xr, wr, br, s, 0 if isinstance(p, tuple) else p)
+    if act == "relu":
+        yr = TF.relu(yr)
+    assert y.shape == yr.shape
+    assert _rel(y, yr) < 2e-2
+    dy = torch.randn_like(yr).bfloat16().float()
+    y.backward(_nhwc(dy))
+    yr.backward(dy)
+    assert _rel(w.grad, wr.grad) < 3e-2
+    if has_b:
+        assert _rel(b.grad, br.grad) < 3e-2
+
+
+def test_stem_conv_bn_stats():
+    """Stem conv with BatchNorm statistics from the packed kernel's epilogue (ResNet stem)."""
+    from deep_vision_amd import nn
+    from deep_vision_amd import ops as F
+
+    conv = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False).to(DEV)
+    bn = nn.BatchNorm2d(64).to(DEV)
+    x = torch.randn(4, 3, 64, 64, device=DEV).bfloat16().float()
+    y = F.conv_bn_act(x, conv, bn, "relu")
+    ref_conv = torch.nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False).to(DEV)
+    ref_conv.weight.data.copy_(conv.weight.data.bfloat16().float())
+    ref_bn = torch.nn.BatchNorm2d(64).to(DEV)
+    yr = TF.relu(ref_bn(ref_conv(x)))
+    assert _rel(y, yr) < 3e-2
+    assert _rel(bn.running_mean, ref_bn.running_mean) < 2e-2
+    assert _rel(bn.running_var, ref_bn.running_var) < 2e-2

@@ -1,0 +1,15 @@
+# stem packed-conv tests + BN reduce variants + full GPU tests + bench + profile
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+cd $R && mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_ops_gpu.py -x -q -k "stem" --timeout 120 --timeout-method thread > gpurun_out/t_stem.log 2>&1 && \
+timeout -k 10 300 python tools/bn_bench.py > gpurun_out/bn_bench.log 2>&1 && \
+timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/tests.log 2>&1 && \
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1 && \
+cd /tmp && export TMPDIR=/tmp && \
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_r50 -o run --output-format csv -- python3 $R/bench.py --steps 5 --warmup 2 > $R/gpurun_out/prof_r50.log 2>&1
+rc=$?
+cd $R
+tail -3 gpurun_out/t_stem.log; cat gpurun_out/bn_bench.log; tail -2 gpurun_out/tests.log; tail -1 gpurun_out/bench.log
+echo rc=$rc
+exit $rc
