@@ -106,7 +106,13 @@ DV_DEVICE void wait_vm() {
   __builtin_amdgcn_s_waitcnt((N & 0xF) | (0x7 << 4) | (0xF << 8) | ((N >> 4) << 14));
 }
 
-template <int BM_, int BN_, int BK_, int KMODE, bool RES, int STAGES, bool BNR = false>
+// EPI (compile-time epilogue): EPI_PLAIN = store only (dgrad, ConvTranspose), EPI_STATS = + BN
+// partial statistics (the convs feeding a BatchNorm), EPI_FULL = runtime bias / activation /
+// statistics. The plain forms drop ~8 VALU per output element (profiled: on the short-K 1x1
+// layers the epilogue VALU outweighs the MFMA work).
+enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_FULL = 2 };
+
+template <int BM_, int BN_, int BK_, int KMODE, bool RES, int STAGES, bool BNR = false, int EPI = EPI_FULL>
 __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
   constexpr int WN = BN_ / 64, WM = BM_ / 64;
   static_assert(WN * WM == 4, "4 waves of 64x64");
@@ -292,7 +298,8 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int n = nw0 + j * 16 + (lane >> 4) * 4 + r;
-      bv[r] = (p.bias && n < p.N) ? p.bias[grp * p.N + n] : 0.f;
+      bv[r] = 0.f;
+      if constexpr (EPI == EPI_FULL) bv[r] = (p.bias && n < p.N) ? p.bias[grp * p.N + n] : 0.f;
       bsum[j][r] = 0.f; bsq[j][r] = 0.f;
     }
 #pragma unroll
@@ -302,11 +309,16 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
       float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float t = acc[j][i][r] + bv[r];
-        if (p.act == ACT_RELU) t = fmaxf(t, 0.f);
-        else if (p.act == ACT_LEAKY) t = t > 0.f ? t : t * p.slope;
+        float t = acc[j][i][r];
+        if constexpr (EPI == EPI_FULL) {
+          t += bv[r];
+          if (p.act == ACT_RELU) t = fmaxf(t, 0.f);
+          else if (p.act == ACT_LEAKY) t = t > 0.f ? t : t * p.slope;
+        }
         v[r] = t;
-        if (mv) { bsum[j][r] += t; bsq[j][r] += t * t; }
+        if constexpr (EPI != EPI_PLAIN) {
+          if (mv) { bsum[j][r] += t; bsq[j][r] += t * t; }
+        }
       }
       uint2 pk; pk.x = pack2bf(v[0], v[1]); pk.y = pack2bf(v[2], v[3]);
       *reinterpret_cast<uint2*>(st + ml * EPI_PITCH + j * 16 + (lane >> 4) * 4) = pk;
@@ -346,7 +358,7 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
       }
     }
   }
-  if (p.stats) {
+  if (EPI != EPI_PLAIN && p.stats) {
     float* sh = reinterpret_cast<float*>(smem + EPI_BYTES);  // [WM][BN_][2]
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -362,7 +374,7 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
       }
   }
   __syncthreads();
-  if (p.stats && threadIdx.x < BN_) {
+  if (EPI != EPI_PLAIN && p.stats && threadIdx.x < BN_) {
     const float* sh = reinterpret_cast<const float*>(smem + EPI_BYTES);
     const int n = n0 + threadIdx.x;
     if (n < p.N) {
@@ -482,32 +494,48 @@ constexpr int lds_bytes(int stages) {
                                                                        : EPI_BYTES + STAT_BYTES;
 }
 
-template <int BM_, int BN_, int BK_, int KMODE, bool RES, int STAGES, bool BNR = false>
+template <int BM_, int BN_, int BK_, int KMODE, bool RES, int STAGES, bool BNR = false, int EPI = EPI_FULL>
 void launch_fwd(const FwdParams& p, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES, BNR>,
+    hipFuncSetAttribute((const void*)conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES, BNR, EPI>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes<BM_, BN_, BK_>(STAGES));
     attr = true;
   }
   const int nt = (p.K + BK_ - 1) / BK_;
   const size_t lds = lds_bytes<BM_, BN_, BK_>(nt < STAGES ? nt : STAGES);
   const int blocks = ((p.M + BM_ - 1) / BM_) * ((p.N + BN_ - 1) / BN_) * p.G;
-  conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES, BNR><<<dim3(blocks), dim3(NT), lds, st>>>(p);
+  conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES, BNR, EPI><<<dim3(blocks), dim3(NT), lds, st>>>(p);
 }
 
 int g_fwd_variant = 0;  // benchmarking override of the tile / pipeline choice (0 = heuristic)
 
+// Tile choice measured on the ResNet-50 layer set (tools/bench_conv.py, profiles/convbench_*):
+//  * N <= 64: a 256x64 tile keeps every MFMA useful; short K (<= 256, HBM-bound 1x1 layers)
+//    runs best with a 3-deep ring, long K with the plain double buffer;
+//  * N > 64: 128x128. K <= 64 is one K-tile (single stage, most blocks per CU); up to K < 2048
+//    BK=32 (32 KB of LDS: up to 4 blocks per CU) beats BK=64 by 5-25 %; long-K layers (3x3 x
+//    256+ channels, 2048-deep 1x1) keep BK=64.
+template <int KMODE, bool RES, bool BNR, int EPI>
+void launch_heuristic(const FwdParams& p, hipStream_t st) {
+  if (KMODE == KM_FAST) {
+    if (p.N <= 64) {
+      if (p.K <= 256) launch_fwd<256, 64, 32, KMODE, RES, 3, BNR, EPI>(p, st);
+      else launch_fwd<256, 64, 32, KMODE, RES, 2, BNR, EPI>(p, st);
+    } else {
+      if (p.K > 64 && p.K < 2048) launch_fwd<128, 128, 32, KMODE, RES, 2, BNR, EPI>(p, st);
+      else launch_fwd<128, 128, 64, KMODE, RES, 2, BNR, EPI>(p, st);
+    }
+    return;
+  }
+  if (p.N <= 64) launch_fwd<256, 64, 32, KMODE, RES, 2, BNR, EPI>(p, st);
+  else launch_fwd<128, 128, 64, KMODE, RES, 2, BNR, EPI>(p, st);
+}
+
 template <int KMODE, bool RES, bool BNR = false>
 void dispatch_res(const FwdParams& p, hipStream_t st) {
-  if constexpr (BNR) {  // fused BN-backward statistics (dgrads, KM_FAST only): same tile choice
-    if (p.N <= 64) {
-      if (p.K <= 256) launch_fwd<256, 64, 32, KMODE, RES, 3, true>(p, st);
-      else launch_fwd<256, 64, 32, KMODE, RES, 2, true>(p, st);
-    } else {
-      if (p.K > 64 && p.K < 2048) launch_fwd<128, 128, 32, KMODE, RES, 2, true>(p, st);
-      else launch_fwd<128, 128, 64, KMODE, RES, 2, true>(p, st);
-    }
+  if constexpr (BNR) {  // fused BN-backward statistics (dgrads, KM_FAST only): plain epilogue
+    launch_heuristic<KMODE, RES, true, EPI_PLAIN>(p, st);
     return;
   }
   if constexpr (KMODE == KM_FAST) {
@@ -523,25 +551,13 @@ void dispatch_res(const FwdParams& p, hipStream_t st) {
       case 9: return launch_fwd<256, 64, 32, KMODE, RES, 3>(p, st);
       default: break;
     }
-  }
-  // Tile choice measured on the ResNet-50 layer set (tools/bench_conv.py, profiles/convbench_*):
-  //  * N <= 64: a 256x64 tile keeps every MFMA useful; short K (<= 256, HBM-bound 1x1 layers)
-  //    runs best with a 3-deep ring, long K with the plain double buffer;
-  //  * N > 64: 128x128. K <= 64 is one K-tile (single stage, most blocks per CU); up to K < 2048
-  //    BK=32 (32 KB of LDS: up to 4 blocks per CU) beats BK=64 by 5-25 %; long-K layers (3x3 x
-  //    256+ channels, 2048-deep 1x1) keep BK=64.
-  if (KMODE == KM_FAST) {
-    if (p.N <= 64) {
-      if (p.K <= 256) launch_fwd<256, 64, 32, KMODE, RES, 3>(p, st);
-      else launch_fwd<256, 64, 32, KMODE, RES, 2>(p, st);
-    } else {
-      if (p.K > 64 && p.K < 2048) launch_fwd<128, 128, 32, KMODE, RES, 2>(p, st);
-      else launch_fwd<128, 128, 64, KMODE, RES, 2>(p, st);
-    }
+    const bool full = p.bias || p.act;
+    if (!full && !p.stats) launch_heuristic<KMODE, RES, false, EPI_PLAIN>(p, st);
+    else if (!full) launch_heuristic<KMODE, RES, false, EPI_STATS>(p, st);
+    else launch_heuristic<KMODE, RES, false, EPI_FULL>(p, st);
     return;
   }
-  if (p.N <= 64) launch_fwd<256, 64, 32, KMODE, RES, 2>(p, st);
-  else launch_fwd<128, 128, 64, KMODE, RES, 2>(p, st);
+  launch_heuristic<KMODE, RES, false, EPI_FULL>(p, st);
 }
 
 template <int KMODE>

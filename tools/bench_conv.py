@@ -7,8 +7,12 @@ csrc/conv_fwd.hip dispatch_res (0 = heuristic).
 """
 import argparse
 import json
+import os
+import sys
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from deep_vision_amd._ext import lib
 from deep_vision_amd.ops.conv import conv_fwd_raw
@@ -112,10 +116,14 @@ def main():
     ap.add_argument("--out")
     ap.add_argument("--wgrad", action="store_true")
     ap.add_argument("--splits", default="100")
+    ap.add_argument("--layers", default="", help="comma-separated layer names (default: all)")
     a = ap.parse_args()
+    keep = set(a.layers.split(",")) if a.layers else None
     vs = [int(v) for v in a.variants.split(",")]
     out = {}
     for L in LAYERS:
+        if keep is not None and L[0] not in keep:
+            continue
         if a.wgrad:
             if not L[0].startswith("dg_"):
                 out[L[0]] = run_wgrad(*L, a.batch, vs, a.iters, [int(x) for x in a.splits.split(",")])
