@@ -1,0 +1,13 @@
+"""Top-5 classification from a training checkpoint (replaces the ResNet notebooks, e.g.
+R/ResNet/pytorch/notebooks/ResNet50.ipynb cells 3-9; inputs ARE normalised like training, A18).
+
+usage: python inference.py -m <model key> -c ./saved_models/<name>-<ts>-epoch-<e>.pt [--names synsets.txt] images...
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+from deep_vision_amd.inference import main  # noqa: E402
+
+if __name__ == "__main__":
+    main(["classify"] + sys.argv[1:])

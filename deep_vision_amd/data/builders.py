@@ -10,7 +10,10 @@
   labels 1..1000 (0 = background); 1024 / 128 shards
 * CycleGAN image folders (R/CycleGAN/tensorflow/tfrecords.py:9-70): trainA/B, testA/B
   (unreadable files are skipped instead of crashing, A19)
-* ``flatten_imagenet``: the train_flatten / val_flatten layout of flatten-script.sh (T1c)
+* ``flatten_imagenet`` / ``flatten_imagenet_val``: the train_flatten / val_flatten layout of
+  flatten-script.sh / flatten-val-script.sh (T1c)
+* ``process_bounding_boxes``: ImageNet bbox XML -> normalised, clipped CSV (T1b)
+* ``celeba_split``: CelebA -> CycleGAN trainA / trainB by attribute (T5)
 
 Shards are written by a process pool (the reference fans out with ray / threads).
 """
@@ -199,6 +202,99 @@ def flatten_imagenet(train_dir, out_dir):
     return n
 
 
+def flatten_imagenet_val(val_dir, labels_file, out_dir):
+    """val/ILSVRC2012_val_*.JPEG + one synset per line (imagenet_2012_validation_synset_labels.txt,
+    in file-name order) -> out_dir/nXXXX_ILSVRC2012_val_*.JPEG (flatten-val-script.sh, T1c)."""
+    labels = [l.strip() for l in open(labels_file) if l.strip()]
+    files = sorted(f for f in os.listdir(val_dir) if f.upper().endswith((".JPEG", ".JPG")))
+    if len(files) != len(labels):
+        raise ValueError(f"{len(files)} validation images but {len(labels)} labels")
+    os.makedirs(out_dir, exist_ok=True)
+    for f, syn in zip(files, labels):
+        dst = os.path.join(out_dir, f"{syn}_{f}")
+        try:
+            os.link(os.path.join(val_dir, f), dst)
+        except OSError:
+            shutil.copy(os.path.join(val_dir, f), dst)
+    return len(files)
+
+
+def parse_bbox_xml(path, synsets=None):
+    """One ImageNet bounding-box XML (R/Datasets/ILSVRC2012/process_bounding_boxes.py:119-169):
+    every box normalised by the image size, clipped to [0, 1], min/max ordered. Returns
+    (filename, [(xmin, ymin, xmax, ymax, synset)]) or None when the file does not parse."""
+    try:
+        root = ET.parse(path).getroot()
+    except ET.ParseError:
+        return None
+    fname = root.findtext("filename") or os.path.splitext(os.path.basename(path))[0]
+    size = root.find("size")
+    width = float(size.findtext("width")) if size is not None else 0.0
+    height = float(size.findtext("height")) if size is not None else 0.0
+    boxes = []
+    for obj in root.iter("object"):
+        syn = obj.findtext("name") or ""
+        if synsets is not None and syn not in synsets:
+            continue
+        bb = obj.find("bndbox")
+        if bb is None or width <= 0 or height <= 0:
+            continue
+        x0, y0 = float(bb.findtext("xmin")) / width, float(bb.findtext("ymin")) / height
+        x1, y1 = float(bb.findtext("xmax")) / width, float(bb.findtext("ymax")) / height
+        x0, x1 = sorted((min(max(x0, 0.0), 1.0), min(max(x1, 0.0), 1.0)))
+        y0, y1 = sorted((min(max(y0, 0.0), 1.0), min(max(y1, 0.0), 1.0)))
+        boxes.append((x0, y0, x1, y1, syn))
+    return fname, boxes
+
+
+def process_bounding_boxes(xml_dir, out_csv, synsets_file=None):
+    """Directory tree of bbox XMLs -> CSV lines ``<image>.JPEG,xmin,ymin,xmax,ymax`` (the
+    reference's output format; the TFRecord builder looks boxes up by file name)."""
+    synsets = set(l.split()[0] for l in open(synsets_file) if l.strip()) if synsets_file else None
+    n_files = n_boxes = skipped = 0
+    with open(out_csv, "w") as out:
+        for dirpath, _, files in sorted(os.walk(xml_dir)):
+            for f in sorted(files):
+                if not f.endswith(".xml"):
+                    continue
+                r = parse_bbox_xml(os.path.join(dirpath, f), synsets)
+                if r is None:
+                    skipped += 1
+                    continue
+                fname, boxes = r
+                if not fname.upper().endswith(".JPEG"):
+                    fname += ".JPEG"
+                for x0, y0, x1, y1, _ in boxes:
+                    out.write(f"{fname},{x0:.4f},{y0:.4f},{x1:.4f},{y1:.4f}\n")
+                    n_boxes += 1
+                n_files += 1
+    return n_files, n_boxes, skipped
+
+
+def celeba_split(attr_file, image_dir, out_root, attribute="Male"):
+    """CelebA -> CycleGAN folders by one binary attribute (R/CycleGAN/tensorflow/celeba.py:1-24:
+    Male -> trainA, the rest -> trainB). ``list_attr_celeba.txt`` format: count line, header
+    line of attribute names, then ``<file> <+1|-1> ...``."""
+    lines = [l.split() for l in open(attr_file) if l.strip()]
+    header = lines[1]
+    col = header.index(attribute)
+    counts = {"trainA": 0, "trainB": 0}
+    for d in counts:
+        os.makedirs(os.path.join(out_root, d), exist_ok=True)
+    for row in lines[2:]:
+        f, vals = row[0], row[1:]
+        dst = "trainA" if int(vals[col]) > 0 else "trainB"
+        src = os.path.join(image_dir, f)
+        if not os.path.exists(src):
+            continue
+        try:
+            os.link(src, os.path.join(out_root, dst, f))
+        except OSError:
+            shutil.copy(src, os.path.join(out_root, dst, f))
+        counts[dst] += 1
+    return counts
+
+
 # ------------------------------------------------------------------ CycleGAN
 def image_example(path):
     try:
@@ -256,7 +352,33 @@ def main(argv=None):
     g.add_argument("--dataset", required=True)
     g.add_argument("--datasets-dir", default="datasets")
     g.add_argument("--out", default="tfrecords")
+    f = sub.add_parser("flatten")
+    f.add_argument("--train-dir")
+    f.add_argument("--val-dir")
+    f.add_argument("--val-labels", help="imagenet_2012_validation_synset_labels.txt")
+    f.add_argument("--out", required=True)
+    b = sub.add_parser("bboxes")
+    b.add_argument("--xml-dir", required=True)
+    b.add_argument("--out", required=True)
+    b.add_argument("--synsets")
+    e = sub.add_parser("celeba")
+    e.add_argument("--attr", required=True)
+    e.add_argument("--images", required=True)
+    e.add_argument("--out", default="datasets/celeba")
+    e.add_argument("--attribute", default="Male")
     a = ap.parse_args(argv)
+    if a.cmd == "flatten":
+        if a.train_dir:
+            print("flattened", flatten_imagenet(a.train_dir, a.out), "training images")
+        if a.val_dir:
+            print("flattened", flatten_imagenet_val(a.val_dir, a.val_labels, a.out), "validation images")
+        return
+    if a.cmd == "bboxes":
+        print("files %d boxes %d skipped %d" % process_bounding_boxes(a.xml_dir, a.out, a.synsets))
+        return
+    if a.cmd == "celeba":
+        print(celeba_split(a.attr, a.images, a.out, a.attribute))
+        return
     if a.cmd == "coco":
         build_coco(a.annotations, a.images, a.out, a.split, a.shards)
     elif a.cmd == "voc":

@@ -191,3 +191,49 @@ def test_inference_classify_and_export(tmp_path):
     assert len(r[0]) == 5 and sum(p for _, _, p in r[0]) <= 1.0 + 1e-5
     st, ts = I.export("lenet5", None, str(tmp_path / "lenet"), (1, 1, 32, 32))
     assert os.path.getsize(st) > 0 and torch.jit.load(ts)(torch.randn(1, 1, 32, 32)).shape == (1, 10)
+
+
+def test_imagenet_bbox_xml_to_csv(tmp_path):
+    """ImageNet bounding-box XML -> normalised, clipped, ordered CSV (process_bounding_boxes, T1b)."""
+    from deep_vision_amd.data.builders import parse_bbox_xml, process_bounding_boxes
+
+    d = tmp_path / "n01440764"
+    d.mkdir()
+    (d / "n01440764_10.xml").write_text(
+        "<annotation><filename>n01440764_10</filename><size><width>200</width><height>100</height></size>"
+        "<object><name>n01440764</name><bndbox><xmin>20</xmin><ymin>10</ymin><xmax>220</xmax><ymax>50</ymax></bndbox></object>"
+        "<object><name>n09999999</name><bndbox><xmin>0</xmin><ymin>0</ymin><xmax>10</xmax><ymax>10</ymax></bndbox></object>"
+        "</annotation>")
+    (d / "broken.xml").write_text("<annotation><filename>")
+    fname, boxes = parse_bbox_xml(str(d / "n01440764_10.xml"))
+    assert fname == "n01440764_10" and len(boxes) == 2
+    assert boxes[0][:4] == (0.1, 0.1, 1.0, 0.5)  # xmax 220/200 clipped to 1
+    syn = tmp_path / "synsets.txt"
+    syn.write_text("n01440764 tench\n")
+    out = tmp_path / "boxes.csv"
+    n_files, n_boxes, skipped = process_bounding_boxes(str(tmp_path), str(out), str(syn))
+    assert (n_files, n_boxes, skipped) == (1, 1, 1)
+    assert out.read_text().strip() == "n01440764_10.JPEG,0.1000,0.1000,1.0000,0.5000"
+
+
+def test_celeba_split_and_val_flatten(tmp_path):
+    from deep_vision_amd.data.builders import celeba_split, flatten_imagenet_val
+
+    img = tmp_path / "img"
+    img.mkdir()
+    for f in ("000001.jpg", "000002.jpg", "000003.jpg"):
+        (img / f).write_bytes(b"x")
+    attr = tmp_path / "list_attr_celeba.txt"
+    attr.write_text("3\nBald Male Young\n000001.jpg -1 1 1\n000002.jpg -1 -1 1\n000003.jpg 1 1 -1\n")
+    counts = celeba_split(str(attr), str(img), str(tmp_path / "celeba"))
+    assert counts == {"trainA": 2, "trainB": 1}
+    assert sorted(os.listdir(tmp_path / "celeba" / "trainA")) == ["000001.jpg", "000003.jpg"]
+    val = tmp_path / "val"
+    val.mkdir()
+    for i in (2, 1):
+        (val / f"ILSVRC2012_val_0000000{i}.JPEG").write_bytes(b"y")
+    labels = tmp_path / "labels.txt"
+    labels.write_text("n01751748\nn09193705\n")
+    assert flatten_imagenet_val(str(val), str(labels), str(tmp_path / "vf")) == 2
+    assert sorted(os.listdir(tmp_path / "vf")) == ["n01751748_ILSVRC2012_val_00000001.JPEG",
+                                                   "n09193705_ILSVRC2012_val_00000002.JPEG"]
