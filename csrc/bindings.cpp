@@ -4,6 +4,7 @@
 #include <pybind11/pybind11.h>
 #include <hip/hip_runtime.h>
 #include <pybind11/stl.h>
+#include <cstdlib>
 #include <string>
 #include <vector>
 #include "kernels.h"
@@ -17,8 +18,20 @@ using uptr = uintptr_t;
 #define CFP(x) reinterpret_cast<const float*>(x)
 #define ST(x) reinterpret_cast<hipStream_t>(x)
 
+// DV_SYNC_CHECK=1 (or set_sync_check(True)): synchronise after every native launch so an
+// asynchronous fault is reported by the op that caused it (the HIP_LAUNCH_BLOCKING /
+// AMD_SERIALIZE_KERNEL debugging idiom, per op and without serialising other libraries).
+static bool g_sync_check = [] {
+  const char* v = std::getenv("DV_SYNC_CHECK");
+  return v && v[0] && v[0] != '0';
+}();
+
 static void check_last(const char* what) {
   hipError_t e = hipGetLastError();
+  if (e == hipSuccess && g_sync_check) {
+    e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipGetLastError();
+  }
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
@@ -46,6 +59,10 @@ PYBIND11_MODULE(_C, m) {
      py::arg("bnslope") = 0.f);
   m.def("conv_fwd_variant", [](int v) { dv_conv_fwd_variant(v); });
   m.def("bn_tuning", [](int blocks, int unroll) { dv_bn_tuning(blocks, unroll); });
+  m.def("set_sync_check", [](bool on) { g_sync_check = on; });
+  m.def("sync_check", []() { return g_sync_check; });
+  m.def("set_deterministic", [](bool on) { dv_set_deterministic(on ? 1 : 0); });
+  m.def("deterministic", []() { return dv_deterministic() != 0; });
   m.def("conv_wgrad_tuning", [](int v, int split_pct) { dv_conv_wgrad_tuning(v, split_pct); });
   m.def("conv_wgrad", [](uptr x, uptr dy, uptr dw, int Nb, int H, int W, int Cg, int ldx, int G, int Kout, int P_, int Q,
                          int ldy, int R, int S, int sh, int sw, int ph, int pw, int dh, int dwl, int splits, int accumulate,

@@ -15,6 +15,8 @@
 //
 // Tile variants (4 waves of 64x64): 128x128, and 64x256 for 64-output-channel layers.
 // A plain-row fast path serves 1x1 / stride-1 / pad-0 convs and Linear (no spatial decode).
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -34,6 +36,7 @@ struct WgParams {
   int R, S, sh, sw, ph, pw, dh, dw_;
   int splits, ktiles_per_split, atomic_out, accumulate;
   int oirs_ig;  // > 0: write dW straight into the parameter layout [G*M][oirs_ig][R][S]
+  int64_t slab;  // > 0: deterministic mode, split s writes its partial tile at dw + s * slab
   FastDiv div_pq, div_q, div_cg, div_s;
 };
 
@@ -247,7 +250,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgParams p) {
   // destination of column n: packed [G][M][N] row offset n, or the parameter's OIRS position
   // (n = (r, s, c) -> c*R*S + r*S + s; padded channels c >= oirs_ig are dropped)
   const int64_t row_stride = p.oirs_ig > 0 ? (int64_t)p.oirs_ig * p.R * p.S : p.N;
-  float* dwp = p.dw + (int64_t)grp * p.M * row_stride;
+  float* dwp = p.dw + (int64_t)grp * p.M * row_stride + (int64_t)split * p.slab;
   int64_t coff[BN_ / 64];
 #pragma unroll
   for (int h = 0; h < BN_ / 64; ++h) {
@@ -317,7 +320,27 @@ void dispatch_wg(const WgParams& p, int blocks_narrow, int blocks_wide, hipStrea
 
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
+// deterministic split-K: dst[i] (+)= sum over s of slab[s][i], in split order
+__global__ void slab_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dst, int64_t n, int splits,
+                                   int accumulate) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float v = accumulate ? dst[i] : 0.f;
+    for (int s = 0; s < splits; ++s) v += ws[(int64_t)s * n + i];
+    dst[i] = v;
+  }
+}
+
+int g_deterministic = [] {
+  const char* v = std::getenv("DV_DETERMINISTIC");
+  return (v && v[0] && v[0] != '0') ? 1 : 0;
+}();
+float* g_slab_ws = nullptr;
+size_t g_slab_elems = 0;
+
 }  // namespace
+
+void dv_set_deterministic(int on) { g_deterministic = on; }
+int dv_deterministic() { return g_deterministic; }
 
 int dv_conv_wgrad_splits(const ConvWgradArgs& a) {
   const int M = a.Kout, N = a.R * a.S * a.Cg, K = a.Nb * a.P * a.Q;
@@ -361,9 +384,28 @@ int dv_conv_wgrad(const ConvWgradArgs& a, hipStream_t st) {
   p.atomic_out = p.splits > 1 ? 1 : 0;
   p.accumulate = a.accumulate;
   p.oirs_ig = a.oirs_ig;
+  p.slab = 0;
   if (p.oirs_ig > p.Cg) return -1;
   const size_t out_elems = (size_t)p.G * p.M * (p.oirs_ig > 0 ? (size_t)p.oirs_ig * p.R * p.S : (size_t)p.N);
-  if (p.atomic_out && !a.accumulate) (void)hipMemsetAsync(a.dw, 0, out_elems * sizeof(float), st);
+  const bool det = g_deterministic && p.splits > 1;
+  if (det) {
+    // every split stores its partial tile (all tile elements, masked rows included) into its own
+    // slab; the slabs are summed in split order afterwards: no atomics, reproducible bits
+    const size_t need = (size_t)p.splits * out_elems;
+    if (need > g_slab_elems) {
+      (void)hipStreamSynchronize(st);
+      if (g_slab_ws) (void)hipFree(g_slab_ws);
+      if (hipMalloc(&g_slab_ws, need * sizeof(float)) != hipSuccess) { g_slab_ws = nullptr; g_slab_elems = 0; return -1; }
+      g_slab_elems = need;
+    }
+    (void)hipMemsetAsync(g_slab_ws, 0, need * sizeof(float), st);
+    p.dw = g_slab_ws;
+    p.slab = (int64_t)out_elems;
+    p.atomic_out = 0;
+    p.accumulate = 0;
+  } else if (p.atomic_out && !a.accumulate) {
+    (void)hipMemsetAsync(a.dw, 0, out_elems * sizeof(float), st);
+  }
   // plain rows: the im2col of a 1x1 / stride-1 / pad-0 conv is X itself (pixel grid == input grid)
   const bool plain = a.R == 1 && a.S == 1 && a.sh == 1 && a.sw == 1 && a.ph == 0 && a.pw == 0 && a.P == a.H &&
                      a.Q == a.W;
@@ -371,5 +413,10 @@ int dv_conv_wgrad(const ConvWgradArgs& a, hipStream_t st) {
   const int bw = cdiv(p.M, 128) * cdiv(p.N, 128) * p.G * p.splits;
   if (plain) dispatch_wg<true>(p, bn, bw, st);
   else dispatch_wg<false>(p, bn, bw, st);
+  if (det) {
+    const int64_t n = (int64_t)out_elems;
+    const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
+    slab_reduce_kernel<<<grid, 256, 0, st>>>(g_slab_ws, a.dw, n, p.splits, a.accumulate);
+  }
   return p.splits;
 }

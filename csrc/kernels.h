@@ -46,6 +46,10 @@ void dv_conv_fwd_variant(int v);  // 0 = heuristic tile choice; others: benchmar
 int dv_conv_wgrad(const ConvWgradArgs& a, hipStream_t st);
 void dv_conv_wgrad_tuning(int variant, int split_pct);  // benchmarking override (0, 100 = heuristic)
 int dv_conv_wgrad_splits(const ConvWgradArgs& a);
+// deterministic mode: split-K weight gradients go through per-split fp32 slabs reduced in a
+// fixed order instead of atomics (bitwise-reproducible dW)
+void dv_set_deterministic(int on);
+int dv_deterministic();
 int dv_conv_stats_tiles(int Nb, int P, int Q);
 
 // ---- batchnorm (bn.hip) ----

@@ -465,3 +465,41 @@ def test_stem_conv_bn_stats():
     assert _rel(y, yr) < 3e-2
     assert _rel(bn.running_mean, ref_bn.running_mean) < 2e-2
     assert _rel(bn.running_var, ref_bn.running_var) < 2e-2
+
+
+def test_deterministic_wgrad_bitwise():
+    """set_deterministic(): split-K weight gradients are bitwise reproducible (slab reduction in a
+    fixed order), and equal to the atomic path up to fp32 summation order."""
+    import deep_vision_amd as dv
+    from deep_vision_amd import ops as F
+
+    x = _nhwc(torch.randn(16, 64, 28, 28, device=DEV)).requires_grad_(False)
+    w = (torch.randn(128, 64, 3, 3, device=DEV) * 0.05).requires_grad_(True)
+    dy = _nhwc(torch.randn(16, 128, 28, 28, device=DEV))
+    grads = []
+    try:
+        dv.set_deterministic(True)
+        for _ in range(3):
+            w.grad = None
+            F.conv2d(x, w, None, 1, 1).backward(dy)
+            grads.append(w.grad.clone())
+    finally:
+        dv.set_deterministic(False)
+    assert torch.equal(grads[0], grads[1]) and torch.equal(grads[1], grads[2])
+    w.grad = None
+    F.conv2d(x, w, None, 1, 1).backward(dy)
+    assert _rel(w.grad, grads[0]) < 1e-5
+
+
+def test_sync_check_mode_runs():
+    import deep_vision_amd as dv
+    from deep_vision_amd import ops as F
+    from deep_vision_amd._ext import lib
+
+    try:
+        dv.set_sync_check(True)
+        assert lib().sync_check()
+        y = F.conv2d(_nhwc(torch.randn(2, 64, 8, 8, device=DEV)), torch.randn(64, 64, 3, 3, device=DEV), None, 1, 1)
+        assert torch.isfinite(y).all()
+    finally:
+        dv.set_sync_check(False)
