@@ -59,6 +59,7 @@ PYBIND11_MODULE(_C, m) {
      py::arg("bnslope") = 0.f);
   m.def("conv_fwd_variant", [](int v) { dv_conv_fwd_variant(v); });
   m.def("bn_tuning", [](int blocks, int unroll) { dv_bn_tuning(blocks, unroll); });
+  m.def("dw_variant", [](int v) { dv_dw_variant(v); });
   m.def("set_sync_check", [](bool on) { g_sync_check = on; });
   m.def("sync_check", []() { return g_sync_check; });
   m.def("set_deterministic", [](bool on) { dv_set_deterministic(on ? 1 : 0); });

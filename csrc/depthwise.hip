@@ -3,25 +3,27 @@
 // R/MobileNet/tensorflow/models/mobilenet_v1.py:7-25).
 //
 // Depthwise conv has no reduction over channels, so there is nothing for MFMA to do: it is a
-// bandwidth-bound stencil. Design:
-//   * one thread = 8 consecutive channels (16-B loads/stores) x a strip of QT output pixels
-//     along W; the weights of its 8 channels live in registers (read once, fp32 master
-//     weights directly — no bf16 weight-prep launch);
-//   * the input row segment shared by the strip is loaded once per filter row and reused
-//     from registers for all QT outputs (stride 1 reuses (QT+S-1)/ (QT*S) of the loads);
-//   * forward epilogue: optional bias, ReLU, and per-channel BatchNorm partial statistics
-//     (thread partials -> LDS reduction over the block's pixel rows -> sharded atomics),
-//     so the following BN needs no statistics pass;
-//   * dgrad: the transposed stencil (divisibility gather for stride 2);
-//   * wgrad: per-thread 8ch x R x S partials over a pixel range, LDS tree over the block,
-//     one fp32 atomic per (channel, tap) per block into dW (plain accumulate into the live
-//     gradient when requested).
+// bandwidth-bound stencil and every kernel here is built to touch each byte of HBM once:
+//   * one thread = 8 consecutive channels (16-B vectors) x a strip of QT output pixels along W;
+//     per filter row the strip's input columns ((QT-1)*SW + KS of them) are loaded ONCE and
+//     feed every (output, tap) pair that uses them (compile-time stride SW: no divisions);
+//   * the filter taps of the thread's 8 channels live in registers (fp32 master weights read
+//     directly: no bf16 weight-prep launch);
+//   * 2-D grid: blockIdx.y = a slab of up to 64 x 8 channels (one wave-width of vectors per
+//     pixel), blockIdx.x = a range of pixel strips, so every layer (32 channels @112 to 1024
+//     channels @7) launches a few thousand blocks;
+//   * forward epilogue: bias, ReLU / LeakyReLU and per-channel BatchNorm partial statistics
+//     (LDS reduction over the block's strips, channel-contiguous atomics into the shards);
+//   * dgrad: stride 1 = the forward stencil with the filter flipped; stride 2 = a gather whose
+//     output-parity pattern is uniform per launch (QT even), unrolled per parity;
+//   * wgrad: per-thread KS*KS x 8 partials over the strips, per-tap LDS reduction, one
+//     channel-contiguous atomic row per tap per block (256-B coalesced atomic rows).
 #include "common.h"
 #include "kernels.h"
 
 namespace {
 constexpr int NT = 256;
-constexpr int QT = 4;  // output pixels per thread along W (forward)
+constexpr int SLAB = 64;  // channel groups (of 8) per block slab
 
 DV_DEVICE void ld8(const u16* p, float* v) {
   uint4 r = *reinterpret_cast<const uint4*>(p); uint32_t w[4] = {r.x, r.y, r.z, r.w};
@@ -37,245 +39,388 @@ struct DwGeo {
   int N, H, W, C, ldx, P, Q, ldy, sh, sw, ph, pw;
 };
 
-// thread layout: TPR = C/8 channel groups per pixel strip (capped at NT), RPI strips per pass
-template <int KS>
-__global__ __launch_bounds__(NT) void dw_fwd_kernel(const u16* __restrict__ x, const float* __restrict__ w,
+// thread -> (channel group, strip lane) inside the block's slab
+struct DwTile {
+  int tpr, rpi, lane_c, lane_r, cg, c0;
+  DV_DEVICE DwTile(int C) {
+    const int cgn = C / 8, rem = cgn - (int)blockIdx.y * SLAB;
+    tpr = rem < SLAB ? rem : SLAB;
+    rpi = NT / tpr;
+    lane_c = threadIdx.x % tpr; lane_r = threadIdx.x / tpr;
+    cg = (int)blockIdx.y * SLAB + lane_c;
+    c0 = cg * 8;
+  }
+  DV_DEVICE bool active() const { return lane_r < rpi; }
+};
+
+// ---------------------------------------------------------------- forward (and stride-1 dgrad)
+// FLIP: correlate with the spatially flipped filter (dgrad of a stride-1 conv); then the caller
+// passes the flipped padding KS-1-p and the output grid is the input grid.
+template <int KS, int SW, int QT, bool FLIP, int OCC = 1>
+__global__ __launch_bounds__(NT, OCC) void dw_fwd_kernel(const u16* __restrict__ x, const float* __restrict__ w,
                                                       const float* __restrict__ bias, u16* __restrict__ y, DwGeo g,
-                                                      int act, float slope, float* __restrict__ stats, int strips_per_block) {
+                                                      int act, float slope, float* __restrict__ stats,
+                                                      int64_t strips_per_block) {
   __shared__ float sh[2][NT * 8];
-  const int cgn = g.C / 8;
-  const int tpr = cgn < NT ? cgn : NT, rpi = NT / tpr;
-  const int lane_c = threadIdx.x % tpr, lane_r = threadIdx.x / tpr;
+  DwTile t(g.C);
+  constexpr int NCOL = (QT - 1) * SW + KS;
+  float wr[KS * KS][8];
+#pragma unroll
+  for (int tp = 0; tp < KS * KS; ++tp)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) wr[tp][k] = w[(t.c0 + k) * KS * KS + (FLIP ? KS * KS - 1 - tp : tp)];
+  float bv[8], ssum[8], ssq[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { bv[k] = bias ? bias[t.c0 + k] : 0.f; ssum[k] = 0.f; ssq[k] = 0.f; }
   const int qstrips = (g.Q + QT - 1) / QT;
   const int64_t nstrips = (int64_t)g.N * g.P * qstrips;
-  const int64_t s0 = (int64_t)blockIdx.x * strips_per_block;
-  const int64_t s1 = min(nstrips, s0 + strips_per_block);
-  for (int cgi = lane_c; cgi < cgn; cgi += tpr) {
-    const int c0 = cgi * 8;
-    float wr[KS * KS][8];
+  const int64_t s0 = (int64_t)blockIdx.x * strips_per_block, s1 = min(nstrips, s0 + strips_per_block);
+  if (t.active()) {
+    for (int64_t s = s0 + t.lane_r; s < s1; s += t.rpi) {
+      const int qs = (int)(s % qstrips);
+      const int64_t np = s / qstrips;
+      const int p = (int)(np % g.P), n = (int)(np / g.P);
+      const int q0 = qs * QT;
+      float acc[QT][8];
 #pragma unroll
-    for (int t = 0; t < KS * KS; ++t)
+      for (int i = 0; i < QT; ++i)
 #pragma unroll
-      for (int k = 0; k < 8; ++k) wr[t][k] = w[(c0 + k) * KS * KS + t];
-    float bv[8];
+        for (int k = 0; k < 8; ++k) acc[i][k] = bv[k];
+      // every load is unconditional: out-of-image taps read the zero page (a branch around a
+      // load makes hipcc wait for it on the spot -- one serial HBM round trip per tap)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) bv[k] = bias ? bias[c0 + k] : 0.f;
-    float ssum[8], ssq[8];
+      for (int r = 0; r < KS; ++r) {
+        const int h = p * g.sh - g.ph + r;
+        const bool hv = h >= 0 && h < g.H;
+        const u16* xrow = x + ((int64_t)n * g.H + (hv ? h : 0)) * g.W * g.ldx + t.c0;
+        const int wbase = q0 * SW - g.pw;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { ssum[k] = 0.f; ssq[k] = 0.f; }
-    if (lane_r < rpi) {
-      for (int64_t s = s0 + lane_r; s < s1; s += rpi) {
-        const int qs = (int)(s % qstrips);
-        const int64_t np = s / qstrips;
-        const int p = (int)(np % g.P), n = (int)(np / g.P);
-        const int q0 = qs * QT;
-        float acc[QT][8];
-#pragma unroll
-        for (int i = 0; i < QT; ++i)
-#pragma unroll
-          for (int k = 0; k < 8; ++k) acc[i][k] = bv[k];
-#pragma unroll
-        for (int r = 0; r < KS; ++r) {
-          const int h = p * g.sh - g.ph + r;
-          if (h < 0 || h >= g.H) continue;
-          const u16* xrow = x + ((int64_t)n * g.H + h) * g.W * g.ldx + c0;
+        for (int j = 0; j < NCOL; ++j) {
+          const int ww = wbase + j;
+          const bool ok = hv && ww >= 0 && ww < g.W;
+          float v[8];
+          ld8(ok ? xrow + (int64_t)ww * g.ldx : reinterpret_cast<const u16*>(dv_zero_page), v);
 #pragma unroll
           for (int i = 0; i < QT; ++i) {
-            const int q = q0 + i;
-#pragma unroll
-            for (int sx = 0; sx < KS; ++sx) {
-              const int ww = q * g.sw - g.pw + sx;
-              if (q >= g.Q || ww < 0 || ww >= g.W) continue;
-              float v[8];
-              ld8(xrow + (int64_t)ww * g.ldx, v);
+            const int sx = j - i * SW;  // compile-time
+            if (sx >= 0 && sx < KS) {
 #pragma unroll
               for (int k = 0; k < 8; ++k) acc[i][k] = fmaf(v[k], wr[r * KS + sx][k], acc[i][k]);
             }
           }
         }
+      }
 #pragma unroll
-        for (int i = 0; i < QT; ++i) {
-          const int q = q0 + i;
-          if (q >= g.Q) continue;
+      for (int i = 0; i < QT; ++i) {
+        const int q = q0 + i;
+        if (q >= g.Q) continue;
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            float t = acc[i][k];
-            if (act == 1) t = fmaxf(t, 0.f);
-            else if (act == 2) t = t > 0.f ? t : t * slope;
-            acc[i][k] = t;
-            ssum[k] += t; ssq[k] += t * t;
-          }
-          st8(y + (((int64_t)n * g.P + p) * g.Q + q) * g.ldy + c0, acc[i]);
+        for (int k = 0; k < 8; ++k) {
+          float v = acc[i][k];
+          if (act == 1) v = fmaxf(v, 0.f);
+          else if (act == 2) v = v > 0.f ? v : v * slope;
+          acc[i][k] = v;
+          ssum[k] += v; ssq[k] += v * v;
         }
+        st8(y + (((int64_t)n * g.P + p) * g.Q + q) * g.ldy + t.c0, acc[i]);
       }
     }
-    if (stats) {
-      __syncthreads();
+  }
+  if (stats) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) { sh[0][threadIdx.x * 8 + k] = ssum[k]; sh[1][threadIdx.x * 8 + k] = ssq[k]; }
-      __syncthreads();
-      if (lane_r == 0) {
-        for (int rr = 1; rr < rpi; ++rr)
-#pragma unroll
-          for (int k = 0; k < 8; ++k) { ssum[k] += sh[0][(rr * tpr + lane_c) * 8 + k]; ssq[k] += sh[1][(rr * tpr + lane_c) * 8 + k]; }
-        float* a = stats + (int64_t)(blockIdx.x % DV_STAT_SHARDS) * 2 * g.C;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) { atomicAdd(a + c0 + k, ssum[k]); atomicAdd(a + g.C + c0 + k, ssq[k]); }
-      }
+    for (int k = 0; k < 8; ++k) { sh[0][threadIdx.x * 8 + k] = ssum[k]; sh[1][threadIdx.x * 8 + k] = ssq[k]; }
+    __syncthreads();
+    const int sw = t.tpr * 8;  // slab width in channels; sh is [strip lane][slab channel]
+    float* a = stats + (int64_t)(blockIdx.x % DV_STAT_SHARDS) * 2 * g.C;
+    const int cbase = (int)blockIdx.y * SLAB * 8;
+    for (int ch = threadIdx.x; ch < sw; ch += NT) {
+      float s1v = 0.f, s2v = 0.f;
+      for (int rr = 0; rr < t.rpi; ++rr) { s1v += sh[0][rr * sw + ch]; s2v += sh[1][rr * sw + ch]; }
+      atomicAdd(a + cbase + ch, s1v);
+      atomicAdd(a + g.C + cbase + ch, s2v);
     }
   }
 }
 
-// dx[n][h][w][c] = sum_{r,s} dy[n][(h+ph-r)/sh][(w+pw-s)/sw][c] * w[c][r][s]
-template <int KS>
-__global__ __launch_bounds__(NT) void dw_dgrad_kernel(const u16* __restrict__ dy, const float* __restrict__ w,
-                                                        u16* __restrict__ dx, DwGeo g) {
-  const int cgn = g.C / 8;
-  const int64_t total = (int64_t)g.N * g.H * g.W * cgn;
-  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < total; t += (int64_t)gridDim.x * NT) {
-    const int cgi = (int)(t % cgn);
-    int64_t pix = t / cgn;
-    const int ww = (int)(pix % g.W); pix /= g.W;
-    const int h = (int)(pix % g.H); const int n = (int)(pix / g.H);
-    const int c0 = cgi * 8;
-    float acc[8];
+// ---------------------------------------------------------------- stride-2 dgrad
+// dx[n][h][w][c] = sum over taps (r, s) with (h+ph-r), (w+pw-s) even of
+//                  dy[n][(h+ph-r)/2][(w+pw-s)/2][c] * w[c][r][s]
+// QT (even) consecutive w per thread: the parity of (w0 + pw) is the same for every thread, so
+// each parity is a fully unrolled body with compile-time register indices.
+// With B = w0 + pw = 2b + PAR, output i and tap s read q = (B + i - s) / 2 when B + i - s is
+// even; relative to qb = floor((B - (KS-1)) / 2) that column is
+//   j = ((PAR + i - s) >> 1) - ((PAR - KS + 1) >> 1)      (compile-time for a fixed PAR)
+template <int KS, int QT, int PAR>
+DV_DEVICE void dgrad2_row(const u16* __restrict__ dyrow, bool rv, int w0, const DwGeo& g, const float (*wr)[8],
+                          int r, float (*acc)[8]) {
+  const int qb = (w0 + g.pw - (KS - 1)) >> 1;  // arithmetic shift: floor for negatives too
+  constexpr int J0 = (PAR - KS + 1) >> 1;
+  constexpr int NQ = ((PAR + QT - 1) >> 1) - J0 + 1;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  for (int j = 0; j < NQ; ++j) {
+    const int q = qb + j;
+    float v[8];
+    ld8(rv && q >= 0 && q < g.Q ? dyrow + (int64_t)q * g.ldy : reinterpret_cast<const u16*>(dv_zero_page), v);
+#pragma unroll
+    for (int i = 0; i < QT; ++i)
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        if (((PAR + i - s) & 1) == 0 && ((PAR + i - s) >> 1) - J0 == j) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[i][k] = fmaf(v[k], wr[r * KS + s][k], acc[i][k]);
+        }
+      }
+  }
+}
+
+template <int KS, int QT, int OCC = 1>
+__global__ __launch_bounds__(NT, OCC) void dw_dgrad2_kernel(const u16* __restrict__ dy, const float* __restrict__ w,
+                                                         u16* __restrict__ dx, DwGeo g, int64_t strips_per_block) {
+  DwTile t(g.C);
+  if (!t.active()) return;
+  float wr[KS * KS][8];
+#pragma unroll
+  for (int tp = 0; tp < KS * KS; ++tp)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) wr[tp][k] = w[(t.c0 + k) * KS * KS + tp];
+  const int wstrips = (g.W + QT - 1) / QT;
+  const int64_t nstrips = (int64_t)g.N * g.H * wstrips;
+  const int64_t s0 = (int64_t)blockIdx.x * strips_per_block, s1 = min(nstrips, s0 + strips_per_block);
+  const int par = g.pw & 1;  // parity of w0 + pw (w0 is a multiple of the even QT)
+  for (int64_t s = s0 + t.lane_r; s < s1; s += t.rpi) {
+    const int ws = (int)(s % wstrips);
+    const int64_t nh = s / wstrips;
+    const int h = (int)(nh % g.H), n = (int)(nh / g.H);
+    const int w0 = ws * QT;
+    float acc[QT][8];
+#pragma unroll
+    for (int i = 0; i < QT; ++i)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[i][k] = 0.f;
 #pragma unroll
     for (int r = 0; r < KS; ++r) {
       const int hn = h + g.ph - r;
-      if (hn < 0 || hn % g.sh) continue;
-      const int p = hn / g.sh;
-      if (p >= g.P) continue;
-#pragma unroll
-      for (int sx = 0; sx < KS; ++sx) {
-        const int wn = ww + g.pw - sx;
-        if (wn < 0 || wn % g.sw) continue;
-        const int q = wn / g.sw;
-        if (q >= g.Q) continue;
-        float v[8];
-        ld8(dy + (((int64_t)n * g.P + p) * g.Q + q) * g.ldy + c0, v);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] = fmaf(v[k], w[(c0 + k) * KS * KS + r * KS + sx], acc[k]);
-      }
+      const int p = hn >> 1;
+      const bool rv = hn >= 0 && !(hn & 1) && p < g.P;  // invalid rows read the zero page
+      const u16* dyrow = dy + ((int64_t)n * g.P + (rv ? p : 0)) * g.Q * g.ldy + t.c0;
+      if (par == 0) dgrad2_row<KS, QT, 0>(dyrow, rv, w0, g, wr, r, acc);
+      else dgrad2_row<KS, QT, 1>(dyrow, rv, w0, g, wr, r, acc);
     }
-    st8(dx + (((int64_t)n * g.H + h) * g.W + ww) * g.ldx + c0, acc);
+#pragma unroll
+    for (int i = 0; i < QT; ++i)
+      if (w0 + i < g.W) st8(dx + (((int64_t)n * g.H + h) * g.W + w0 + i) * g.ldx + t.c0, acc[i]);
   }
 }
 
-// dw[c][r][s] += sum_{n,p,q} dy[n][p][q][c] * x[n][p*sh-ph+r][q*sw-pw+s][c]
-template <int KS>
-__global__ __launch_bounds__(NT) void dw_wgrad_kernel(const u16* __restrict__ x, const u16* __restrict__ dy,
-                                                        float* __restrict__ dw, DwGeo g, int64_t pix_per_block) {
+// ---------------------------------------------------------------- wgrad
+// dw[c][r][s] += sum_{n,p,q} dy[n][p][q][c] * x[n][p*sh-ph+r][q*SW-pw+s][c]
+template <int KS, int SW, int QT, int OCC = 1>
+__global__ __launch_bounds__(NT, OCC) void dw_wgrad_kernel(const u16* __restrict__ x, const u16* __restrict__ dy,
+                                                        float* __restrict__ dw, DwGeo g, int64_t strips_per_block) {
   __shared__ float sh[NT * 8];
-  const int cgn = g.C / 8;
-  const int tpr = cgn < NT ? cgn : NT, rpi = NT / tpr;
-  const int lane_c = threadIdx.x % tpr, lane_r = threadIdx.x / tpr;
-  const int64_t npix = (int64_t)g.N * g.P * g.Q;
-  const int64_t p0 = (int64_t)blockIdx.x * pix_per_block, p1 = min(npix, p0 + pix_per_block);
-  for (int cgi = lane_c; cgi < cgn; cgi += tpr) {
-    const int c0 = cgi * 8;
-    float acc[KS * KS][8];
+  __shared__ float red[SLAB * 8 * KS * KS];
+  DwTile t(g.C);
+  constexpr int NCOL = (QT - 1) * SW + KS;
+  float acc[KS * KS][8];
 #pragma unroll
-    for (int t = 0; t < KS * KS; ++t)
+  for (int tp = 0; tp < KS * KS; ++tp)
 #pragma unroll
-      for (int k = 0; k < 8; ++k) acc[t][k] = 0.f;
-    if (lane_r < rpi) {
-      for (int64_t pi = p0 + lane_r; pi < p1; pi += rpi) {
-        const int q = (int)(pi % g.Q);
-        const int64_t np = pi / g.Q;
-        const int p = (int)(np % g.P), n = (int)(np / g.P);
-        float d[8];
-        ld8(dy + pi * g.ldy + c0, d);
+    for (int k = 0; k < 8; ++k) acc[tp][k] = 0.f;
+  const int qstrips = (g.Q + QT - 1) / QT;
+  const int64_t nstrips = (int64_t)g.N * g.P * qstrips;
+  const int64_t s0 = (int64_t)blockIdx.x * strips_per_block, s1 = min(nstrips, s0 + strips_per_block);
+  if (t.active()) {
+    for (int64_t s = s0 + t.lane_r; s < s1; s += t.rpi) {
+      const int qs = (int)(s % qstrips);
+      const int64_t np = s / qstrips;
+      const int p = (int)(np % g.P), n = (int)(np / g.P);
+      const int q0 = qs * QT;
+      float d[QT][8];
 #pragma unroll
-        for (int r = 0; r < KS; ++r) {
-          const int h = p * g.sh - g.ph + r;
-          if (h < 0 || h >= g.H) continue;
+      for (int i = 0; i < QT; ++i)
+        ld8(q0 + i < g.Q ? dy + (((int64_t)n * g.P + p) * g.Q + q0 + i) * g.ldy + t.c0
+                         : reinterpret_cast<const u16*>(dv_zero_page), d[i]);
 #pragma unroll
-          for (int sx = 0; sx < KS; ++sx) {
-            const int ww = q * g.sw - g.pw + sx;
-            if (ww < 0 || ww >= g.W) continue;
-            float v[8];
-            ld8(x + (((int64_t)n * g.H + h) * g.W + ww) * g.ldx + c0, v);
+      for (int r = 0; r < KS; ++r) {
+        const int h = p * g.sh - g.ph + r;
+        const bool hv = h >= 0 && h < g.H;
+        const u16* xrow = x + ((int64_t)n * g.H + (hv ? h : 0)) * g.W * g.ldx + t.c0;
+        const int wbase = q0 * SW - g.pw;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) acc[r * KS + sx][k] = fmaf(d[k], v[k], acc[r * KS + sx][k]);
+        for (int j = 0; j < NCOL; ++j) {
+          const int ww = wbase + j;
+          const bool ok = hv && ww >= 0 && ww < g.W;
+          float v[8];
+          ld8(ok ? xrow + (int64_t)ww * g.ldx : reinterpret_cast<const u16*>(dv_zero_page), v);
+#pragma unroll
+          for (int i = 0; i < QT; ++i) {
+            const int sx = j - i * SW;
+            if (sx >= 0 && sx < KS) {
+#pragma unroll
+              for (int k = 0; k < 8; ++k) acc[r * KS + sx][k] = fmaf(d[i][k], v[k], acc[r * KS + sx][k]);
+            }
           }
         }
       }
     }
-    // block reduction per tap over the rpi pixel lanes sharing these channels
+  }
+  // per tap: strip lanes -> LDS -> per-channel sums into red[channel][tap]
+  const int sw = t.tpr * 8;
 #pragma unroll
-    for (int t = 0; t < KS * KS; ++t) {
-      __syncthreads();
+  for (int tp = 0; tp < KS * KS; ++tp) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) sh[threadIdx.x * 8 + k] = acc[t][k];
-      __syncthreads();
-      if (lane_r == 0) {
-        float s[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) s[k] = acc[t][k];
-        for (int rr = 1; rr < rpi; ++rr)
-#pragma unroll
-          for (int k = 0; k < 8; ++k) s[k] += sh[(rr * tpr + lane_c) * 8 + k];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) atomicAdd(dw + (c0 + k) * KS * KS + t, s[k]);
-      }
+    for (int k = 0; k < 8; ++k) sh[threadIdx.x * 8 + k] = acc[tp][k];
+    __syncthreads();
+    for (int ch = threadIdx.x; ch < sw; ch += NT) {
+      float sum = 0.f;
+      for (int rr = 0; rr < t.rpi; ++rr) sum += sh[rr * sw + ch];
+      red[ch * KS * KS + tp] = sum;
+    }
+    __syncthreads();
+  }
+  // dw is [C][KS*KS]: the slab's block of sw*KS*KS floats is contiguous -> coalesced atomics
+  float* dst = dw + (int64_t)blockIdx.y * SLAB * 8 * KS * KS;
+  for (int e = threadIdx.x; e < sw * KS * KS; e += NT) atomicAdd(dst + e, red[e]);
+}
+
+int64_t per_block(int64_t nstrips, int rpi, int slabs, int64_t target_blocks) {
+  // ~target blocks in total over the slabs, a whole number of strip passes per block
+  int64_t spb = std::max<int64_t>(rpi, (nstrips * slabs + target_blocks - 1) / target_blocks);
+  return (spb + rpi - 1) / rpi * rpi;
+}
+inline int slabs_of(int C) { return (C / 8 + SLAB - 1) / SLAB; }
+inline int rpi_of(int C) {
+  const int cgn = C / 8, tpr = cgn < SLAB ? cgn : SLAB;
+  return NT / tpr;
+}
+// Benchmark override of (strip length QT, minimum waves per SIMD) for the 3x3 kernels:
+// 0 = heuristic, 1 = (4, 4), 2 = (2, 4), 3 = (8, 2), 4 = (4, 2), 5 = (2, 2).
+int g_dw_variant = 0;
+
+template <int KS, int SW, bool FLIP, int QT, int OCC>
+void fwd_launch(const void* x, const float* w, const float* bias, void* y, const DwGeo& g, int act, float slope,
+                float* stats, int target, hipStream_t st) {
+  const int slabs = slabs_of(g.C), rpi = rpi_of(g.C);
+  const int64_t nstrips = (int64_t)g.N * g.P * ((g.Q + QT - 1) / QT);
+  const int64_t spb = per_block(nstrips, rpi, slabs, target);
+  const dim3 grid((unsigned)((nstrips + spb - 1) / spb), (unsigned)slabs);
+  dw_fwd_kernel<KS, SW, QT, FLIP, OCC><<<grid, NT, 0, st>>>((const u16*)x, w, bias, (u16*)y, g, act, slope, stats, spb);
+}
+template <int KS, int SW, bool FLIP>
+void fwd_variants(const void* x, const float* w, const float* bias, void* y, const DwGeo& g, int act, float slope,
+                  float* stats, hipStream_t st) {
+  if constexpr (KS == 3) {
+    switch (g_dw_variant) {
+      case 1: return fwd_launch<KS, SW, FLIP, 4, 4>(x, w, bias, y, g, act, slope, stats, 8192, st);
+      case 2: return fwd_launch<KS, SW, FLIP, 2, 4>(x, w, bias, y, g, act, slope, stats, 8192, st);
+      case 3: return fwd_launch<KS, SW, FLIP, 8, 2>(x, w, bias, y, g, act, slope, stats, 4096, st);
+      case 4: return fwd_launch<KS, SW, FLIP, 4, 2>(x, w, bias, y, g, act, slope, stats, 8192, st);
+      case 5: return fwd_launch<KS, SW, FLIP, 2, 2>(x, w, bias, y, g, act, slope, stats, 8192, st);
+      default: break;
     }
   }
+  fwd_launch<KS, SW, FLIP, 4, 1>(x, w, bias, y, g, act, slope, stats, 4096, st);
+}
+template <int KS, int SW, int QT, int OCC>
+void wgrad_launch(const void* x, const void* dy, float* dw, const DwGeo& g, int target, hipStream_t st) {
+  const int slabs = slabs_of(g.C), rpi = rpi_of(g.C);
+  const int64_t nstrips = (int64_t)g.N * g.P * ((g.Q + QT - 1) / QT);
+  // >= 4 strips per thread: every block ends in KS*KS reductions + C*KS*KS atomics (on the
+  // 1024-channel 7x7 layer those dominated a one-strip-per-thread grid)
+  const int64_t spb = std::max<int64_t>(per_block(nstrips, rpi, slabs, target), 4 * rpi);
+  const dim3 grid((unsigned)((nstrips + spb - 1) / spb), (unsigned)slabs);
+  dw_wgrad_kernel<KS, SW, QT, OCC><<<grid, NT, 0, st>>>((const u16*)x, (const u16*)dy, dw, g, spb);
+}
+template <int KS, int SW>
+void wgrad_variants(const void* x, const void* dy, float* dw, const DwGeo& g, hipStream_t st) {
+  if constexpr (KS == 3) {
+    switch (g_dw_variant) {
+      case 1: return wgrad_launch<KS, SW, 4, 4>(x, dy, dw, g, 2048, st);
+      case 2: return wgrad_launch<KS, SW, 2, 4>(x, dy, dw, g, 2048, st);
+      case 3: return wgrad_launch<KS, SW, 8, 2>(x, dy, dw, g, 1024, st);
+      case 4: return wgrad_launch<KS, SW, 4, 2>(x, dy, dw, g, 2048, st);
+      case 5: return wgrad_launch<KS, SW, 2, 2>(x, dy, dw, g, 2048, st);
+      default: break;
+    }
+  }
+  wgrad_launch<KS, SW, 4, 1>(x, dy, dw, g, 512, st);
+}
+template <int KS, int QT, int OCC>
+void dgrad2_launch(const void* dy, const float* w, void* dx, const DwGeo& g, int target, hipStream_t st) {
+  const int slabs = slabs_of(g.C), rpi = rpi_of(g.C);
+  const int64_t nstrips = (int64_t)g.N * g.H * ((g.W + QT - 1) / QT);
+  const int64_t spb = per_block(nstrips, rpi, slabs, target);
+  const dim3 grid((unsigned)((nstrips + spb - 1) / spb), (unsigned)slabs);
+  dw_dgrad2_kernel<KS, QT, OCC><<<grid, NT, 0, st>>>((const u16*)dy, w, (u16*)dx, g, spb);
+}
+template <int KS>
+void dgrad2_variants(const void* dy, const float* w, void* dx, const DwGeo& g, hipStream_t st) {
+  if constexpr (KS == 3) {
+    switch (g_dw_variant) {
+      case 1: return dgrad2_launch<KS, 4, 4>(dy, w, dx, g, 8192, st);
+      case 2: return dgrad2_launch<KS, 2, 4>(dy, w, dx, g, 8192, st);
+      case 3: return dgrad2_launch<KS, 8, 2>(dy, w, dx, g, 4096, st);
+      case 4: return dgrad2_launch<KS, 4, 2>(dy, w, dx, g, 8192, st);
+      case 5: return dgrad2_launch<KS, 2, 2>(dy, w, dx, g, 8192, st);
+      default: break;
+    }
+  }
+  // 8-pixel strips: measured 15-27 % faster than 4 on every MobileNet stride-2 layer (tools/dw_bench.py)
+  dgrad2_launch<KS, 8, 1>(dy, w, dx, g, 4096, st);
 }
 
-inline int grid_for(int64_t total) {
-  int64_t gsz = (total + NT - 1) / NT;
-  return (int)std::min<int64_t>(std::max<int64_t>(gsz, 1), 256 * 16);
-}
 }  // namespace
 
-#define DW_KS_DISPATCH(K, KERNEL, ...)                                  \
-  switch (K) {                                                          \
-    case 3: KERNEL<3> __VA_ARGS__; break;                               \
-    case 5: KERNEL<5> __VA_ARGS__; break;                               \
-    case 1: KERNEL<1> __VA_ARGS__; break;                               \
-    case 7: KERNEL<7> __VA_ARGS__; break;                               \
-    default: return -1;                                                 \
+#define DW_KS(K, BODY)                        \
+  switch (K) {                                \
+    case 3: { constexpr int KS = 3; BODY; } break; \
+    case 5: { constexpr int KS = 5; BODY; } break; \
+    case 1: { constexpr int KS = 1; BODY; } break; \
+    case 7: { constexpr int KS = 7; BODY; } break; \
+    default: return -1;                       \
   }
 
-// the block-wide barriers inside the channel-group loop need a uniform trip count
-static inline bool dw_shape_ok(int C, int ldx, int ldy) {
-  const int cgn = C / 8;
-  return C % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 && (cgn <= NT || cgn % NT == 0);
-}
+// every block's slab must be a whole number of 8-channel groups; partial last slabs are fine
+static inline bool dw_shape_ok(int C, int ldx, int ldy) { return C % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0; }
+
+void dv_dw_variant(int v) { g_dw_variant = v; }
 
 int dv_dw_fwd(const void* x, const float* w, const float* bias, void* y, int N, int H, int W, int C, int ldx, int P,
               int Q, int ldy, int K, int sh, int sw, int ph, int pw, int act, float slope, float* stats, hipStream_t st) {
-  if (!dw_shape_ok(C, ldx, ldy)) return -1;
+  if (!dw_shape_ok(C, ldx, ldy) || (sw != 1 && sw != 2)) return -1;
   DwGeo g{N, H, W, C, ldx, P, Q, ldy, sh, sw, ph, pw};
-  const int cgn = C / 8, tpr = cgn < NT ? cgn : NT, rpi = NT / tpr;
-  const int64_t nstrips = (int64_t)N * P * ((Q + QT - 1) / QT);
-  // channel groups beyond NT threads are looped inside the block
-  int64_t spb = std::max<int64_t>(rpi, (nstrips + 2047) / 2048);
-  spb = (spb + rpi - 1) / rpi * rpi;
-  const int blocks = (int)((nstrips + spb - 1) / spb);
-  DW_KS_DISPATCH(K, dw_fwd_kernel, <<<blocks, NT, 0, st>>>((const u16*)x, w, bias, (u16*)y, g, act, slope, stats, (int)spb))
+  if (sw == 1) {
+    DW_KS(K, (fwd_variants<KS, 1, false>(x, w, bias, y, g, act, slope, stats, st)))
+  } else {
+    DW_KS(K, (fwd_variants<KS, 2, false>(x, w, bias, y, g, act, slope, stats, st)))
+  }
   return 0;
 }
 
 int dv_dw_dgrad(const void* dy, const float* w, void* dx, int N, int H, int W, int C, int ldx, int P, int Q, int ldy,
                 int K, int sh, int sw, int ph, int pw, hipStream_t st) {
-  if (C % 8 || ldx % 8 || ldy % 8) return -1;
+  if (!dw_shape_ok(C, ldx, ldy)) return -1;
+  if (sh == 1 && sw == 1) {
+    // correlation of dY with the flipped filter, padding K-1-p, output grid = input grid
+    DwGeo g{N, P, Q, C, ldy, H, W, ldx, 1, 1, K - 1 - ph, K - 1 - pw};
+    DW_KS(K, (fwd_variants<KS, 1, true>(dy, w, nullptr, dx, g, 0, 0.f, nullptr, st)))
+    return 0;
+  }
+  if (sh != 2 || sw != 2) return -1;
   DwGeo g{N, H, W, C, ldx, P, Q, ldy, sh, sw, ph, pw};
-  const int64_t total = (int64_t)N * H * W * (C / 8);
-  DW_KS_DISPATCH(K, dw_dgrad_kernel, <<<grid_for(total), NT, 0, st>>>((const u16*)dy, w, (u16*)dx, g))
+  DW_KS(K, (dgrad2_variants<KS>(dy, w, dx, g, st)))
   return 0;
 }
 
 int dv_dw_wgrad(const void* x, const void* dy, float* dw, int N, int H, int W, int C, int ldx, int P, int Q, int ldy,
                 int K, int sh, int sw, int ph, int pw, int accumulate, hipStream_t st) {
-  if (!dw_shape_ok(C, ldx, ldy)) return -1;
+  if (!dw_shape_ok(C, ldx, ldy) || (sw != 1 && sw != 2)) return -1;
   DwGeo g{N, H, W, C, ldx, P, Q, ldy, sh, sw, ph, pw};
   if (!accumulate) (void)hipMemsetAsync(dw, 0, (size_t)C * K * K * sizeof(float), st);
-  const int64_t npix = (int64_t)N * P * Q;
-  int64_t ppb = std::max<int64_t>(256, (npix + 1023) / 1024);
-  const int blocks = (int)((npix + ppb - 1) / ppb);
-  DW_KS_DISPATCH(K, dw_wgrad_kernel, <<<blocks, NT, 0, st>>>((const u16*)x, (const u16*)dy, dw, g, ppb))
+  if (sw == 1) {
+    DW_KS(K, (wgrad_variants<KS, 1>(x, dy, dw, g, st)))
+  } else {
+    DW_KS(K, (wgrad_variants<KS, 2>(x, dy, dw, g, st)))
+  }
   return 0;
 }

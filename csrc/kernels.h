@@ -112,6 +112,7 @@ void dv_rmsprop(float* p, const float* g, float* sq, float* mom, float* gavg, in
 void dv_sumsq(const float* x, int64_t n, float* out, hipStream_t st);
 
 // ---- depthwise conv (depthwise.hip) ----
+void dv_dw_variant(int v);  // benchmarking override of strip length / occupancy (0 = heuristic)
 int dv_dw_fwd(const void* x, const float* w, const float* bias, void* y, int N, int H, int W, int C, int ldx, int P,
               int Q, int ldy, int K, int sh, int sw, int ph, int pw, int act, float slope, float* stats, hipStream_t st);
 int dv_dw_dgrad(const void* dy, const float* w, void* dx, int N, int H, int W, int C, int ldx, int P, int Q, int ldy,

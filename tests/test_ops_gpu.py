@@ -287,7 +287,8 @@ def test_optimizers_match_torch():
             assert torch.allclose(a, b, atol=1e-5, rtol=1e-4), cls.__name__
 
 
-@pytest.mark.parametrize("cfg", [(32, 3, 1, 1), (64, 3, 2, 1), (128, 3, 1, 1), (1024, 3, 1, 1), (48, 5, 2, 2)])
+@pytest.mark.parametrize("cfg", [(32, 3, 1, 1), (64, 3, 2, 1), (128, 3, 1, 1), (1024, 3, 1, 1), (48, 5, 2, 2),
+                                 (1040, 3, 2, 1), (64, 3, 2, 0), (16, 3, 1, 1), (24, 7, 1, 3), (40, 1, 2, 0)])
 def test_depthwise(cfg):
     from deep_vision_amd import ops as F
 

@@ -24,7 +24,7 @@ def main():
                          int(r["Workgroup_Size_X"])))
     rows.sort()
     which = int(sys.argv[2]) if len(sys.argv) > 2 else 1
-    ends = [i for i, r in enumerate(rows) if "sgd_kernel" in r[2]]
+    ends = [i for i, r in enumerate(rows) if re.search(r"(sgd|adam|rmsprop)_kernel", r[2])]
     if len(ends) < which + 1:
         sys.exit("not enough steps in the trace")
     a, b = ends[-which - 1] + 1, ends[-which] + 1
