@@ -19,7 +19,17 @@ all-reduce (N > 1), fused optimizer update, gradient zeroing. Inputs/labels are 
 on the device (synthetic, no host pipeline in the timed region).
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--model resnet50]
-        (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+  N > 1: either launched by the driver as ``torch.distributed.run --nproc-per-node N bench.py
+  --gpus N`` (one rank per GPU, RCCL), or run directly: ``bench.py --gpus N`` then spawns the N
+  ranks itself (deep_vision_amd.launch, a child ``torch.distributed.run`` on 127.0.0.1) BEFORE
+  touching the GPU and exits with the children's status -- it never measures 1 GPU while
+  claiming N.
+
+Reported besides the contract fields: ``per_gpu`` images/s, ``comm_exposed_ms`` (compute-stream
+time blocked on the gradient all-reduces per step, HIP events around DataParallel.finish) and
+``vs_same_box_miopen`` (ratio to the PyTorch/MIOpen eager run on the same MI355X,
+profiles/bench_resnet50_1gpu_torch_miopen.json, scaled by N). ``vs_baseline`` divides by the
+BASELINE.md proxy (~376 img/s per 8-GPU node, fp32 K80-era); it is NOT a like-for-like ratio.
 """
 from __future__ import annotations
 
@@ -31,6 +41,8 @@ import time
 # Reference-derived comparators, images/sec per node:
 #   ResNet-50-equivalent proxy ~376 (8 GPUs), YOLOv3 ~179 (8x V100), LeNet-5 PT ~906.
 BASELINES = {"resnet50": 376.0, "yolov3": 179.0, "lenet5": 906.0}
+# same-box PyTorch-ROCm eager (MIOpen) images/s per GPU, profiles/bench_resnet50_1gpu_torch_miopen.json
+SAME_BOX_MIOPEN = {"resnet50": 6753.44}
 RESNET_METRIC = "images/sec (whole node), ResNet-50 224x224 bf16 at 1/2/4/8 MI355X"
 
 # model -> (per-GPU batch, image size, optimizer name, optimizer kwargs, family)
@@ -116,10 +128,21 @@ def main():
     ap.add_argument("--backend", default="native", choices=["native", "torch"],
                     help="torch = PyTorch/MIOpen reference path (for comparison only)")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="gradient all-reduce wire format (fp32 master gradients either way)")
     ap.add_argument("--device", default=None, help="cpu to force the CPU plumbing path")
     args = ap.parse_args()
 
+    import os
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and args.device != "cpu":
+        # self-launch N ranks; this parent never initialises the GPU
+        from deep_vision_amd.launch import spawn
+
+        sys.exit(spawn(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
+
     import torch
+    import torch.distributed as dist
 
     from deep_vision_amd import ops as F
     from deep_vision_amd.parallel.ddp import DataParallel
@@ -128,8 +151,8 @@ def main():
     world, rank, local, device = init_distributed("gloo" if args.device == "cpu" else None)
     if args.device == "cpu":
         device = torch.device("cpu")
-    if world != args.gpus and rank == 0:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    if world != args.gpus and args.device != "cpu":
+        raise SystemExit(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a mismatched run")
     F.set_backend(args.backend)
     torch.manual_seed(1234 + rank)
     torch.backends.cudnn.benchmark = True
@@ -140,7 +163,9 @@ def main():
             torch.cuda.synchronize()
 
     model, loss_fn, x, opt, B, size = build(args, device)
-    ddp = DataParallel(model, bucket_mb=args.bucket_mb) if is_dist() else None
+    ddp = (DataParallel(model, bucket_mb=args.bucket_mb, timing=cuda,
+                        comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32)
+           if is_dist() else None)
     gscale = ddp.grad_scale if ddp else 1.0
     net = ddp if ddp else model
     amp = args.backend == "torch" and cuda
@@ -172,14 +197,17 @@ def main():
     dt = time.perf_counter() - t0
 
     if is_dist():
-        import torch.distributed as dist
-
         t = torch.tensor([dt], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     last_loss = float(loss.item())
     ms = dt / args.steps * 1e3
     imgs = B * world * args.steps / dt
+    comm_ms = ddp.exposed_comm_ms(last=args.steps) if (ddp is not None and cuda) else 0.0
+    if is_dist():
+        t = torch.tensor([comm_ms], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        comm_ms = float(t.item())
     if rank == 0:
         base = BASELINES.get(args.model)
         if args.model == "resnet50":
@@ -197,6 +225,10 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(imgs / base, 3) if base else None,
+            "vs_same_box_miopen": (round(imgs / (SAME_BOX_MIOPEN[args.model] * world), 3)
+                                   if args.model in SAME_BOX_MIOPEN and cuda and args.backend == "native" else None),
+            "per_gpu": round(imgs / max(1, world), 2),
+            "comm_exposed_ms": round(comm_ms, 3),
             "dtype": "bf16" if cuda else "fp32",
             "data": "synthetic (random inputs / labels of the config's shapes, random-init weights)",
             "config": {
@@ -206,6 +238,8 @@ def main():
                 "seq_len": None,
                 "image_size": size,
                 "parallelism": f"dp{world}",
+                "comm_dtype": args.comm_dtype,
+                "bucket_mb": args.bucket_mb,
                 "optimizer": f"{type(opt).__name__} {SPECS[args.model][3]}",
                 "backend": args.backend,
                 "device": str(device),
@@ -214,8 +248,6 @@ def main():
         }
         print(json.dumps(rec), flush=True)
     if is_dist():
-        import torch.distributed as dist
-
         dist.destroy_process_group()
 
 

@@ -342,6 +342,21 @@ size_t g_slab_elems = 0;
 void dv_set_deterministic(int on) { g_deterministic = on; }
 int dv_deterministic() { return g_deterministic; }
 
+float* dv_slab_workspace(size_t elems, hipStream_t st) {
+  if (elems > g_slab_elems) {
+    (void)hipStreamSynchronize(st);
+    if (g_slab_ws) (void)hipFree(g_slab_ws);
+    if (hipMalloc(&g_slab_ws, elems * sizeof(float)) != hipSuccess) { g_slab_ws = nullptr; g_slab_elems = 0; return nullptr; }
+    g_slab_elems = elems;
+  }
+  return g_slab_ws;
+}
+
+void dv_slab_reduce(const float* ws, float* dst, int64_t n, int splits, int accumulate, hipStream_t st) {
+  const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  slab_reduce_kernel<<<grid, 256, 0, st>>>(ws, dst, n, splits, accumulate);
+}
+
 int dv_conv_wgrad_splits(const ConvWgradArgs& a) {
   const int M = a.Kout, N = a.R * a.S * a.Cg, K = a.Nb * a.P * a.Q;
   const bool narrow = g_wg_variant == 2 || g_wg_variant == 4 || g_wg_variant == 6 ||
@@ -392,12 +407,7 @@ int dv_conv_wgrad(const ConvWgradArgs& a, hipStream_t st) {
     // every split stores its partial tile (all tile elements, masked rows included) into its own
     // slab; the slabs are summed in split order afterwards: no atomics, reproducible bits
     const size_t need = (size_t)p.splits * out_elems;
-    if (need > g_slab_elems) {
-      (void)hipStreamSynchronize(st);
-      if (g_slab_ws) (void)hipFree(g_slab_ws);
-      if (hipMalloc(&g_slab_ws, need * sizeof(float)) != hipSuccess) { g_slab_ws = nullptr; g_slab_elems = 0; return -1; }
-      g_slab_elems = need;
-    }
+    if (!dv_slab_workspace(need, st)) return -1;
     (void)hipMemsetAsync(g_slab_ws, 0, need * sizeof(float), st);
     p.dw = g_slab_ws;
     p.slab = (int64_t)out_elems;
@@ -414,9 +424,7 @@ int dv_conv_wgrad(const ConvWgradArgs& a, hipStream_t st) {
   if (plain) dispatch_wg<true>(p, bn, bw, st);
   else dispatch_wg<false>(p, bn, bw, st);
   if (det) {
-    const int64_t n = (int64_t)out_elems;
-    const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
-    slab_reduce_kernel<<<grid, 256, 0, st>>>(g_slab_ws, a.dw, n, p.splits, a.accumulate);
+    dv_slab_reduce(g_slab_ws, a.dw, (int64_t)out_elems, p.splits, a.accumulate, st);
   }
   return p.splits;
 }

@@ -216,7 +216,8 @@ __global__ __launch_bounds__(NT, OCC) void dw_dgrad2_kernel(const u16* __restric
 // dw[c][r][s] += sum_{n,p,q} dy[n][p][q][c] * x[n][p*sh-ph+r][q*SW-pw+s][c]
 template <int KS, int SW, int QT, int OCC = 1>
 __global__ __launch_bounds__(NT, OCC) void dw_wgrad_kernel(const u16* __restrict__ x, const u16* __restrict__ dy,
-                                                        float* __restrict__ dw, DwGeo g, int64_t strips_per_block) {
+                                                        float* __restrict__ dw, DwGeo g, int64_t strips_per_block,
+                                                        float* __restrict__ slabs) {
   __shared__ float sh[NT * 8];
   __shared__ float red[SLAB * 8 * KS * KS];
   DwTile t(g.C);
@@ -278,8 +279,16 @@ __global__ __launch_bounds__(NT, OCC) void dw_wgrad_kernel(const u16* __restrict
     }
     __syncthreads();
   }
-  // dw is [C][KS*KS]: the slab's block of sw*KS*KS floats is contiguous -> coalesced atomics
-  float* dst = dw + (int64_t)blockIdx.y * SLAB * 8 * KS * KS;
+  // dw is [C][KS*KS]: the slab's block of sw*KS*KS floats is contiguous -> coalesced atomics.
+  // Deterministic mode: this block's partial goes to its own [C][KS*KS] slab (row blockIdx.x),
+  // summed in block order by dv_slab_reduce -- reproducible bits, no atomics.
+  const int64_t coff = (int64_t)blockIdx.y * SLAB * 8 * KS * KS;
+  if (slabs) {
+    float* dst = slabs + (int64_t)blockIdx.x * g.C * KS * KS + coff;
+    for (int e = threadIdx.x; e < sw * KS * KS; e += NT) dst[e] = red[e];
+    return;
+  }
+  float* dst = dw + coff;
   for (int e = threadIdx.x; e < sw * KS * KS; e += NT) atomicAdd(dst + e, red[e]);
 }
 
@@ -329,7 +338,11 @@ void wgrad_launch(const void* x, const void* dy, float* dw, const DwGeo& g, int 
   // 1024-channel 7x7 layer those dominated a one-strip-per-thread grid)
   const int64_t spb = std::max<int64_t>(per_block(nstrips, rpi, slabs, target), 4 * rpi);
   const dim3 grid((unsigned)((nstrips + spb - 1) / spb), (unsigned)slabs);
-  dw_wgrad_kernel<KS, SW, QT, OCC><<<grid, NT, 0, st>>>((const u16*)x, (const u16*)dy, dw, g, spb);
+  float* ws = nullptr;
+  const int64_t n = (int64_t)g.C * KS * KS;
+  if (dv_deterministic()) ws = dv_slab_workspace((size_t)grid.x * n, st);
+  dw_wgrad_kernel<KS, SW, QT, OCC><<<grid, NT, 0, st>>>((const u16*)x, (const u16*)dy, dw, g, spb, ws);
+  if (ws) dv_slab_reduce(ws, dw, n, (int)grid.x, 1, st);
 }
 template <int KS, int SW>
 void wgrad_variants(const void* x, const void* dy, float* dw, const DwGeo& g, hipStream_t st) {

@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <sys/stat.h>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -57,7 +58,13 @@ inline bool read_record(FILE* f, std::string& out, bool check, const std::string
   std::memcpy(&len, hdr, 8);
   std::memcpy(&lc, hdr + 8, 4);
   if (check && masked_crc(hdr, 8) != lc) throw std::runtime_error("corrupt record length (crc) in " + path);
-  if (len > (uint64_t(1) << 40)) throw std::runtime_error("implausible record length in " + path);
+  // bound the allocation by what the file can still hold (a corrupt length must not make
+  // resize() ask for terabytes before the truncation check runs)
+  const off_t here = ftello(f);
+  struct stat sb;
+  if (here < 0 || fstat(fileno(f), &sb) != 0) throw std::runtime_error("cannot stat " + path);
+  const uint64_t remaining = sb.st_size > here ? uint64_t(sb.st_size - here) : 0;
+  if (len > remaining || remaining - len < 4) throw std::runtime_error("truncated record in " + path);
   out.resize(len);
   if (len && std::fread(&out[0], 1, len, f) != len) throw std::runtime_error("truncated record in " + path);
   uint32_t dc;

@@ -50,6 +50,10 @@ int dv_conv_wgrad_splits(const ConvWgradArgs& a);
 // fixed order instead of atomics (bitwise-reproducible dW)
 void dv_set_deterministic(int on);
 int dv_deterministic();
+// shared fp32 slab workspace (grown on demand) and the fixed-order slab sum
+// dst[i] (+)= sum_{s < splits} ws[s * n + i] used by every deterministic weight gradient
+float* dv_slab_workspace(size_t elems, hipStream_t st);
+void dv_slab_reduce(const float* ws, float* dst, int64_t n, int splits, int accumulate, hipStream_t st);
 int dv_conv_stats_tiles(int Nb, int P, int Q);
 
 // ---- batchnorm (bn.hip) ----

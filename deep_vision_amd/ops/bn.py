@@ -18,7 +18,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as TF
 
-from .common import (ACT_IDS, BF16, F32, grad_nhwc, grad_sink, is_nhwc, ld_of, lib, native, notify_grad_ready, ptr,
+from .common import (ACT_IDS, BF16, F32, grad_nhwc, grad_sink, is_nhwc, ld_of, lib, native, ptr,
                      stream_handle, workspace)
 
 STAT_SHARDS = 64
@@ -153,9 +153,6 @@ class _BNActFn(torch.autograd.Function):
                 out = torch.empty_like(x)
                 L.bn_apply(ptr(x), 0, ptr(out), x.numel(), C, ptr(scale), ptr(shift), act, float(slope), 0, st)
             L.bn_bwd_eval(ptr(dout), ptr(out), ptr(dx), ptr(dres), x.numel(), C, ptr(scale), act, float(slope), st)
-        if direct:
-            notify_grad_ready(weight)
-            notify_grad_ready(bias)
         if ctx.join is not None and dres is not None:
             dres = ctx.join.produce(dres)  # folded into the shortcut consumer's dgrad epilogue
         return dx, None, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None, None, None

@@ -135,11 +135,16 @@ def nhwc_numel(t: torch.Tensor) -> int:
 # Gradient sinks: native backward kernels write parameter gradients straight into the live
 # ``param.grad`` buffer (a view into the flat gradient buffer of parallel.flat / train.optim)
 # with accumulate semantics — exactly AccumulateGrad's in-place ``grad += g`` without the
-# extra pass — and then signal readiness to the data-parallel bucketing layer.
+# extra pass — and return None to autograd. Readiness for the data-parallel layer is NOT
+# signalled here: every use of a parameter still has its autograd edge to the parameter's
+# AccumulateGrad node, so the post-accumulate hook (parallel.ddp) fires once, after the LAST
+# use's backward (sink or not), which is the only per-step-complete signal.
 # ---------------------------------------------------------------------------------------------
 def grad_sink(param):
-    """The tensor to accumulate ``param``'s gradient into, or None (fall back to autograd)."""
-    if param is None or not param.requires_grad:
+    """The tensor to accumulate ``param``'s gradient into, or None (fall back to autograd).
+    Only leaf parameters sink: a non-leaf (e.g. a padded view of a weight) has no live
+    ``.grad`` and its gradient must flow back through autograd."""
+    if param is None or not param.requires_grad or not param.is_leaf:
         return None
     g = param.grad
     if g is None or g.dtype != F32 or not g.is_contiguous() or g.shape != param.shape or g.device != param.device:
@@ -147,12 +152,6 @@ def grad_sink(param):
     if torch.is_grad_enabled():  # double-backward: keep autograd semantics
         return None
     return g
-
-
-def notify_grad_ready(param):
-    hook = getattr(param, "_dv_ready_hook", None)
-    if hook is not None:
-        hook(param)
 
 
 def workspace(owner, key, shape, device, dtype=F32):

@@ -16,7 +16,7 @@ import torch.nn.functional as TF
 
 from . import wcache
 from .common import (ACT_IDS, BF16, CL, F32, alloc_cl, as_nhwc, empty_nhwc, grad_nhwc, grad_sink, ld_of, lib,
-                     like_layout, empty_layout, native, nhwc_numel, notify_grad_ready, ptr, round8, stream_handle)
+                     like_layout, empty_layout, native, nhwc_numel, ptr, round8, stream_handle)
 
 STAT_SHARDS = 64
 
@@ -282,7 +282,6 @@ class _ConvFn(torch.autograd.Function):
             dw = _wgrad(x, dy, weight, Cg_x, G, stride, padding, dilation, out=sink)
             if sink is not None:
                 dw = None
-                notify_grad_ready(weight)
         if has_bias and ctx.needs_input_grad[2]:
             db = _channel_sum(dy)
         return dx, dw, db, None, None, None, None, None, None, None, None, None, None, None
@@ -379,7 +378,6 @@ class _StemConvFn(torch.autograd.Function):
             sink = grad_sink(weight)
             if sink is not None:
                 sink.add_(full[..., :S])
-                notify_grad_ready(weight)
             else:
                 dw = full[..., :S].contiguous()
         if has_bias and ctx.needs_input_grad[2]:
@@ -592,7 +590,6 @@ class _LinearFn(torch.autograd.Function):
                              int(sink is not None), K if Kp != K else 0, stream_handle())
             if sink is not None:
                 dw = None
-                notify_grad_ready(weight)
             else:
                 dw = buf
         if has_bias and ctx.needs_input_grad[2]:
@@ -601,7 +598,6 @@ class _LinearFn(torch.autograd.Function):
             if sink is not None:
                 sink.add_(db)
                 db = None
-                notify_grad_ready(bias)
         return dx, dw, db, None, None
 
 
@@ -679,9 +675,7 @@ class _DWConvFn(torch.autograd.Function):
             buf = sink if sink is not None else torch.empty_like(w)
             lib().dw_wgrad(ptr(x), ptr(dy), ptr(buf), N, H, W, C, ld_of(x), P, Q, ld_of(dy), K, stride[0], stride[1],
                            padding[0], padding[1], int(sink is not None), stream_handle())
-            if sink is not None:
-                notify_grad_ready(weight)
-            else:
+            if sink is None:
                 dw = buf
         if has_bias and ctx.needs_input_grad[2]:
             db = _channel_sum(dy)
@@ -690,8 +684,10 @@ class _DWConvFn(torch.autograd.Function):
 
 def _is_depthwise(x, weight, groups, stride, dilation):
     O, Ig, R, S = weight.shape
+    # the dgrad kernels cover strides (1, 1) and (2, 2) only (csrc/depthwise.hip dv_dw_dgrad):
+    # anything else takes the grouped path instead of failing in backward
     return (groups > 1 and groups == x.shape[1] and O == groups and Ig == 1 and R == S and R in (1, 3, 5, 7)
-            and dilation == (1, 1) and x.shape[1] % 8 == 0)
+            and dilation == (1, 1) and tuple(stride) in ((1, 1), (2, 2)) and x.shape[1] % 8 == 0)
 
 
 def depthwise_conv2d(x, weight, bias=None, stride=1, padding=0, act=None, slope=0.0, want_stats=False,

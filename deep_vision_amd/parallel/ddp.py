@@ -1,16 +1,31 @@
 """Data parallelism: bucketed gradient all-reduce overlapped with backward.
 
+Replaces the reference's ``nn.DataParallel`` (R/ResNet/pytorch/train.py:353-355) and
+``MirroredStrategy`` gradient all-reduce (R/YOLO/tensorflow/train.py:99-100, 281).
+
 Design (MI355X-first, not a translation of DataParallel / MirroredStrategy):
   * one process per GPU; parameters live in one flat fp32 buffer laid out in reverse
     registration order (parallel.flat), gradients in a matching flat buffer;
-  * buckets are contiguous slices of that gradient buffer (default 64 MB — a ring all-reduce
+  * buckets are contiguous slices of that gradient buffer (default 32 MB — a ring all-reduce
     over xGMI is per-link bound at ~153 GB/s, so a few large messages beat many small ones);
-  * a post-accumulate-grad hook counts arrivals per bucket; the moment a bucket is complete its
-    all-reduce is issued (``async_op=True``): RCCL runs it on its own stream ordered after the
-    compute stream's current position, so it overlaps the rest of backward;
+  * a parameter is *complete* when autograd's post-accumulate-grad hook fires for it. The
+    engine runs a parameter's AccumulateGrad node once per backward, after EVERY node with an
+    edge to it -- i.e. after the last use's backward -- even when all uses are native ops that
+    accumulated straight into ``.grad`` (ops.common.grad_sink) and returned None. So a weight
+    used several times in one step (CycleGAN's generators run 3x, GAN discriminators 2x)
+    completes only after its last wgrad, and a bucket never starts reducing while a wgrad still
+    adds into it. (Round 1 also counted a per-use native notification: every native parameter
+    was reported twice and buckets were issued early.) A second report of one parameter in
+    one backward raises ``DoubleReadyError`` instead of silently corrupting the bucket.
+  * the moment a bucket is complete its all-reduce is issued (``async_op=True``): RCCL runs it
+    on its own stream ordered after the compute stream's current position, so it overlaps the
+    rest of backward. Optional bf16 wire format (``comm_dtype=torch.bfloat16``): the bucket is
+    cast into a persistent bf16 staging slice, reduced, and cast back into the fp32 master
+    gradient in ``finish`` (half the xGMI bytes; summation of ``world`` bf16 addends);
   * ``finish()`` (called before the optimizer) issues buckets that never completed (unused
     parameters: Inception aux heads in eval, Hourglass dead convs) and makes the compute stream
-    wait on every outstanding all-reduce;
+    wait on every outstanding all-reduce; with ``timing=True`` a HIP event pair around that wait
+    measures the *exposed* communication time (``comm_stats['exposed_ms']``);
   * the 1/world averaging is fused into the optimizer kernel (``grad_scale``) — no extra pass;
   * BatchNorm statistics stay per replica (reference semantics, no SyncBN); initial parameters
     and buffers are broadcast from rank 0.
@@ -26,8 +41,13 @@ from .dist import is_dist, world_size
 from .flat import flatten_parameters
 
 
+class DoubleReadyError(RuntimeError):
+    """A parameter reported a complete gradient twice in one backward (its bucket may already be
+    in flight), e.g. a second ``backward(retain_graph=True)`` without a new forward / prepare."""
+
+
 class _Bucket:
-    __slots__ = ("start", "end", "params", "pending", "work", "issued")
+    __slots__ = ("start", "end", "params", "pending", "work", "issued", "wire")
 
     def __init__(self, start):
         self.start = start
@@ -36,16 +56,18 @@ class _Bucket:
         self.pending = 0
         self.work = None
         self.issued = False
+        self.wire = None  # bf16 staging slice (comm_dtype != fp32)
 
 
 class DataParallel(torch.nn.Module):
-    def __init__(self, module: torch.nn.Module, bucket_mb: float = 64.0, broadcast: bool = True,
-                 process_group=None, comm=None):
+    def __init__(self, module: torch.nn.Module, bucket_mb: float = 32.0, broadcast: bool = True,
+                 process_group=None, comm=None, comm_dtype: torch.dtype = torch.float32, timing: bool = False):
         super().__init__()
         self.module = module
         self.pg = process_group
         self.comm = comm  # optional injected communicator (tests): callable(tensor) -> None (sum in place)
         self.world = world_size() if comm is None else getattr(comm, "world", 1)
+        self.comm_dtype = comm_dtype
         self.pflat, self.gflat, layout = flatten_parameters(module, reverse=True)
         self._sync_enabled = True
         if broadcast and is_dist():
@@ -55,7 +77,7 @@ class DataParallel(torch.nn.Module):
                     if b.numel():
                         dist.broadcast(b, 0, group=self.pg)
         # build buckets over the flat layout (params never split across buckets)
-        cap = int(bucket_mb * 1024 * 1024 / 4)
+        cap = max(1, int(bucket_mb * 1024 * 1024 / 4))
         self.buckets = []
         cur = _Bucket(0)
         for p, off, n in layout:
@@ -65,49 +87,65 @@ class DataParallel(torch.nn.Module):
             cur.params.append(p)
             cur.end = off + n
         self.buckets.append(cur)
+        if comm_dtype != torch.float32:
+            self._wire = torch.empty(self.gflat.numel(), dtype=comm_dtype, device=self.gflat.device)
+            for b in self.buckets:
+                b.wire = self._wire[b.start:b.end]
         self._bucket_of = {}
+        self.params = [p for p, _, _ in layout]
         for bi, b in enumerate(self.buckets):
             for p in b.params:
                 self._bucket_of[id(p)] = bi
         self._hooks = []
-        for p, _, _ in layout:
-            h = self._make_hook(p)
-            self._hooks.append(p.register_post_accumulate_grad_hook(h))
-            # native backward kernels write gradients straight into the flat buffer and signal
-            # readiness through this attribute instead of autograd's AccumulateGrad
-            p._dv_ready_hook = h
-        self.comm_stats = {"allreduce_calls": 0, "allreduce_bytes": 0}
+        for p in self.params:
+            self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(p)))
+        self.timing = timing and self.gflat.is_cuda
+        self.comm_stats = {"allreduce_calls": 0, "allreduce_bytes": 0, "exposed_ms": [], "steps": 0}
         self._reset()
 
-    # ------------------------------------------------------------------
+    # ------------------------------------------------------------------ readiness
     def _reset(self):
         for b in self.buckets:
             b.pending = len(b.params)
             b.work = None
             b.issued = False
+        self._done = set()
 
     def _make_hook(self, p):
         pid = id(p)
+        bi = self._bucket_of[pid]
 
         def hook(param):
             if not self._sync_enabled or self.world <= 1:
                 return
-            b = self.buckets[self._bucket_of[pid]]
+            if pid in self._done:
+                raise DoubleReadyError(f"parameter {tuple(param.shape)} reported ready twice in one backward "
+                                       "(retain_graph double backward without a new forward/prepare?)")
+            self._done.add(pid)
+            b = self.buckets[bi]
             b.pending -= 1
             if b.pending == 0 and not b.issued:
                 self._issue(b)
 
         return hook
 
+    # ------------------------------------------------------------------ communication
     def _issue(self, b: _Bucket):
         t = self.gflat[b.start:b.end]
         b.issued = True
         self.comm_stats["allreduce_calls"] += 1
-        self.comm_stats["allreduce_bytes"] += t.numel() * 4
         if self.comm is not None:
+            self.comm_stats["allreduce_bytes"] += t.numel() * 4
             self.comm(t)
             return
-        b.work = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+        from ..profiling import range as prange
+
+        with prange(f"dv_allreduce[{b.start}:{b.end}]"):
+            if b.wire is not None:
+                b.wire.copy_(t)
+                t = b.wire
+            self.comm_stats["allreduce_bytes"] += t.numel() * t.element_size()
+            b.work = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
 
     def forward(self, *args, **kw):
         self._reset()
@@ -135,10 +173,30 @@ class DataParallel(torch.nn.Module):
         for b in self.buckets:
             if not b.issued:
                 self._issue(b)
+        ev = None
+        if self.timing:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         for b in self.buckets:
             if b.work is not None:
                 b.work.wait()
                 b.work = None
+                if b.wire is not None:
+                    self.gflat[b.start:b.end].copy_(b.wire)
+        self.comm_stats["steps"] += 1
+        if ev is not None:
+            ev[1].record()
+            self.comm_stats["exposed_ms"].append(ev)
+
+    def exposed_comm_ms(self, last: int | None = None) -> float:
+        """Mean compute-stream time spent waiting on gradient all-reduces (synchronises)."""
+        evs = self.comm_stats["exposed_ms"]
+        if last:
+            evs = evs[-last:]
+        if not evs:
+            return 0.0
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in evs) / len(evs)
 
     @property
     def grad_scale(self) -> float:

@@ -1,0 +1,108 @@
+"""Collective watchdog: turn a hung or failed collective into a prompt, whole-job exit.
+
+The reference has no failure handling beyond Hourglass's NaN-skip
+(R/Hourglass/tensorflow/train.py:126-130). In a one-process-per-GPU job a dead or wedged rank
+leaves its peers blocked inside an RCCL all-reduce forever; this module bounds that:
+
+* ``CommWatchdog.guard(name)`` brackets a region that issues / waits on collectives. A
+  background thread checks the oldest open region; if it has been open longer than
+  ``timeout`` seconds (``DV_COMM_TIMEOUT``), it dumps every thread's Python stack and ends the
+  process with ``os._exit(EXIT_COMM_TIMEOUT)`` -- no Python cleanup that could block on the
+  wedged communicator. The launcher (torch.distributed.run / deep_vision_amd.launch) sees a
+  non-zero exit and tears the remaining ranks down. A restart is a fresh child process from
+  the launcher; a GPU-initialised process is never re-exec'ed.
+* Exceptions raised inside a guard by the backend (RCCL async errors surfaced by
+  ``TORCH_NCCL_ASYNC_ERROR_HANDLING``, gloo "connection closed by peer") are reported and turned
+  into ``os._exit(EXIT_COMM_ERROR)`` for the same reason.
+* ``install_backend_error_handling()`` sets the RCCL env knobs that make the process group
+  surface async errors and abort the communicator instead of hanging (must run before the
+  process group is created).
+"""
+from __future__ import annotations
+
+import contextlib
+import faulthandler
+import os
+import sys
+import threading
+import time
+
+EXIT_COMM_TIMEOUT = 75
+EXIT_COMM_ERROR = 76
+
+
+def install_backend_error_handling(timeout_s: int | None = None) -> None:
+    """RCCL (ProcessGroupNCCL) settings: async error handling tears the communicator down on a
+    failed / timed-out collective; the desync debug report names the rank that fell behind."""
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    os.environ.setdefault("TORCH_NCCL_DUMP_ON_TIMEOUT", "0")
+    if timeout_s:
+        os.environ.setdefault("DV_COMM_TIMEOUT", str(int(timeout_s)))
+
+
+class CommWatchdog:
+    def __init__(self, timeout: float | None = None, on_timeout=None, poll: float | None = None):
+        self.timeout = float(timeout if timeout is not None else os.environ.get("DV_COMM_TIMEOUT", "600"))
+        self.on_timeout = on_timeout
+        self.poll = poll if poll is not None else max(0.05, min(2.0, self.timeout / 10))
+        self._open = {}  # token -> (name, start)
+        self._lock = threading.Lock()
+        self._next = 0
+        self._stop = threading.Event()
+        self._t = None
+        self.fired = None
+
+    def start(self):
+        if self.timeout > 0 and self._t is None:
+            self._t = threading.Thread(target=self._run, name="dv-comm-watchdog", daemon=True)
+            self._t.start()
+        return self
+
+    def stop(self):
+        self._stop.set()
+
+    @contextlib.contextmanager
+    def guard(self, name: str):
+        with self._lock:
+            tok = self._next
+            self._next += 1
+            self._open[tok] = (name, time.monotonic())
+        try:
+            yield
+        except Exception as e:  # backend error inside a collective region
+            if self._is_comm_error(e):
+                self._abort(EXIT_COMM_ERROR, f"collective '{name}' failed: {type(e).__name__}: {e}")
+            raise
+        finally:
+            with self._lock:
+                self._open.pop(tok, None)
+
+    @staticmethod
+    def _is_comm_error(e: BaseException) -> bool:
+        msg = f"{type(e).__name__} {e}".lower()
+        return any(k in msg for k in ("nccl", "rccl", "gloo", "distbackenderror", "connection", "timed out",
+                                      "peer", "collective"))
+
+    def _abort(self, code: int, why: str):
+        self.fired = why
+        sys.stderr.write(f"[dv-comm-watchdog] {why}; aborting rank {os.environ.get('RANK', '0')}\n")
+        try:
+            faulthandler.dump_traceback(all_threads=True)
+        except Exception:
+            pass
+        sys.stderr.flush()
+        if self.on_timeout is not None:
+            self.on_timeout(code, why)
+            return
+        os._exit(code)
+
+    def _run(self):
+        while not self._stop.wait(self.poll):
+            now = time.monotonic()
+            with self._lock:
+                stale = [(n, t0) for n, t0 in self._open.values() if now - t0 > self.timeout]
+            if stale:
+                name, t0 = min(stale, key=lambda v: v[1])
+                self._abort(EXIT_COMM_TIMEOUT, f"collective region '{name}' open for {now - t0:.1f}s "
+                                               f"(> {self.timeout:.0f}s)")
+                return

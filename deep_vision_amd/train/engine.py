@@ -13,6 +13,7 @@ divide by the *global* batch (MirroredStrategy) -- ``Engine.w
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import random
 
@@ -22,6 +23,7 @@ import torch
 from .. import models as M
 from ..parallel import dist as D
 from ..parallel.ddp import DataParallel
+from ..parallel.watchdog import CommWatchdog, install_backend_error_handling
 from ..profiling import StepTimer
 from ..utils.fault import FaultInjector, NonFiniteGuard, Watchdog
 from .optim import FusedAdam, FusedRMSprop, FusedSGD
@@ -47,6 +49,7 @@ class Engine:
                  log_every: int = 10, watchdog_s: float | None = None, profile: bool = False):
         if device == "cpu":
             backend = backend or "gloo"
+        install_backend_error_handling()  # RCCL async errors abort the communicator (before init)
         self.world, self.rank, self.local_rank, dev = D.init_distributed(backend)
         self.device = torch.device(device) if device and device != "cuda" else dev
         self.bucket_mb = bucket_mb
@@ -56,6 +59,9 @@ class Engine:
         self.timer = StepTimer(enabled=profile)
         wd = float(os.environ.get("DV_WATCHDOG_S", watchdog_s or 0))
         self.watchdog = Watchdog(wd).start() if wd > 0 else None
+        # a hung / failed gradient all-reduce ends this rank with a non-zero exit (the launcher
+        # then tears the job down) instead of blocking the whole job forever
+        self.comm_watchdog = CommWatchdog().start() if self.world > 1 else None
         self.step_count = 0
 
     def log(self, *a, **kw):
@@ -89,16 +95,18 @@ class Engine:
         loss = self.faults.loss(loss, s)
         if zero_grad:
             optimizer.zero_grad()
-        with self.timer.phase("bwd"):
-            loss.backward()
-        flat = optimizer.flat_grads() if hasattr(optimizer, "flat_grads") else None
-        self.faults.grads(flat[0] if flat else None, s)
-        with self.timer.phase("comm"):
-            if isinstance(model, DataParallel):
-                model.finish()
-        ok = True
-        if self.guard.should_check(s):
-            ok = self.guard.ok(loss, flat[0] if flat else None)
+        guard = self.comm_watchdog.guard("backward+allreduce") if self.comm_watchdog else contextlib.nullcontext()
+        with guard:
+            with self.timer.phase("bwd"):
+                loss.backward()
+            flat = optimizer.flat_grads() if hasattr(optimizer, "flat_grads") else None
+            self.faults.grads(flat[0] if flat else None, s)
+            with self.timer.phase("comm"):
+                if isinstance(model, DataParallel):
+                    model.finish()
+            ok = True
+            if self.guard.should_check(s):  # same cadence on every rank: the verdict is all-reduced
+                ok = self.guard.ok(loss, flat[0] if flat else None, distributed=self.world > 1)
         if ok:
             with self.timer.phase("opt"):
                 gs = model.grad_scale if isinstance(model, DataParallel) else 1.0
@@ -119,4 +127,6 @@ class Engine:
     def close(self):
         if self.watchdog is not None:
             self.watchdog.stop()
+        if self.comm_watchdog is not None:
+            self.comm_watchdog.stop()
         D.destroy()

@@ -35,12 +35,22 @@ class NonFiniteGuard:
     def should_check(self, step: int) -> bool:
         return self.every > 0 and step % self.every == 0
 
-    def ok(self, loss: torch.Tensor, grads: torch.Tensor | None = None) -> bool:
-        """True if finite. ``grads`` may be the flat gradient buffer (one fused reduction)."""
-        vals = [loss.detach().float().reshape(1)]
+    def ok(self, loss: torch.Tensor, grads: torch.Tensor | None = None, distributed: bool = False) -> bool:
+        """True if finite. ``grads`` may be the flat gradient buffer (one fused reduction).
+        ``distributed``: the verdict is all-reduced (MAX of the non-finite flag) so every rank
+        skips or steps together -- a NaN loss seen by one rank only must not fork the replicas."""
+        vals = [loss.detach().float().reshape(1).to(grads.device if grads is not None else loss.device)]
         if grads is not None:
             vals.append(grads.detach().float().abs().sum().reshape(1))
-        finite = bool(torch.isfinite(torch.cat(vals)).all().item())
+        bad = (~torch.isfinite(torch.cat(vals))).any().to(torch.float32).reshape(1)
+        if distributed:
+            from ..parallel.dist import is_dist
+
+            if is_dist():
+                import torch.distributed as dist
+
+                dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+        finite = not bool(bad.item())
         if finite:
             self.consecutive = 0
             return True

@@ -1,0 +1,128 @@
+"""Data parallelism through the NATIVE kernels on the GPU.
+
+* two gloo ranks sharing one MI355X: a conv weight used twice per step (native wgrad sinks into
+  the flat gradient buffer twice) -> the all-reduced gradient equals the single-process
+  full-batch gradient (the bucket must not start before the second use);
+* RCCL (``nccl`` backend) DP-2 on two GPUs (skipped on a 1-GPU box): same check + initial
+  parameter broadcast + every bucket issued exactly once + a never-used parameter.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _make_net():
+    from deep_vision_amd import nn
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.stem = nn.Conv2d(16, 64, 3, padding=1, bias=False)
+            self.shared = nn.Conv2d(64, 64, 3, padding=1, bias=False)  # applied twice
+            self.unused = nn.Conv2d(64, 64, 1, bias=False)  # never used: finish() must issue it
+            self.fc = nn.Linear(64, 10)
+
+        def forward(self, x):
+            from deep_vision_amd import ops as F
+
+            x = F.relu(self.stem(x))
+            x = F.relu(self.shared(x))
+            x = F.relu(self.shared(x))
+            return self.fc(x.float().mean((2, 3)))
+
+    return Net()
+
+
+def _data(world, rank, dev):
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(8 * world, 16, 16, 16, generator=g)
+    y = torch.randint(0, 10, (8 * world,), generator=g)
+    if rank is None:
+        return x.to(dev), y.to(dev)
+    return x[rank * 8:(rank + 1) * 8].to(dev), y[rank * 8:(rank + 1) * 8].to(dev)
+
+
+def _worker(rank, world, port, backend, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), DV_DIST_BACKEND=backend)
+    import torch.distributed as dist
+
+    from deep_vision_amd import ops as F
+    from deep_vision_amd.parallel.ddp import DataParallel
+    from deep_vision_amd.parallel.dist import init_distributed
+    from deep_vision_amd.train.optim import FusedSGD
+
+    _, _, _, dev = init_distributed(backend)
+    torch.manual_seed(5 + rank)  # different init per rank: the broadcast must fix it
+    net = _make_net().to(dev)
+    ddp = DataParallel(net, bucket_mb=0.05)
+    opt = FusedSGD(net.parameters(), lr=0.01)
+    x, y = _data(world, rank, dev)
+    opt.zero_grad()
+    F.cross_entropy(ddp(x), y).backward()
+    ddp.finish()
+    g = (ddp.gflat * ddp.grad_scale).cpu().numpy().copy()
+    p0 = ddp.pflat.cpu().numpy().copy()
+    q.put((rank, g, p0, ddp.comm_stats["allreduce_calls"], len(ddp.buckets)))
+    dist.destroy_process_group()
+
+
+def _run(backend, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, backend, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=180) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def _reference(p0):
+    """Single process, full batch, the broadcast (rank-0) parameters."""
+    from deep_vision_amd import ops as F
+    from deep_vision_amd.parallel.flat import flatten_parameters
+
+    dev = torch.device("cuda:0")
+    net = _make_net().to(dev)
+    pflat, gflat, _ = flatten_parameters(net, reverse=True)
+    with torch.no_grad():
+        pflat.copy_(torch.from_numpy(p0))
+    x, y = _data(2, None, dev)
+    F.cross_entropy(net(x), y).backward()
+    return gflat.cpu()
+
+
+def _check(res, world):
+    g0, p0, calls, nb = res[0]
+    for r in range(1, world):
+        assert (res[r][1] == p0).all(), "initial parameters were not broadcast"
+        assert (res[r][0] == g0).all(), "replicas hold different reduced gradients"
+    assert nb >= 3 and calls == nb, (calls, nb)  # every bucket issued exactly once (incl. the unused one)
+    ref = _reference(p0)
+    g = torch.from_numpy(g0)
+    err = (g - ref).norm() / ref.norm()
+    assert err < 3e-2, float(err)
+
+
+def test_gloo_ranks_share_gpu_multi_use_weight():
+    _check(_run("gloo", 2), 2)
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="RCCL DP needs >= 2 GPUs")
+def test_rccl_dp2_matches_single_process():
+    _check(_run("nccl", 2), 2)

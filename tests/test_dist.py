@@ -137,3 +137,213 @@ def test_classification_trainer_two_ranks(tmp_path):
         assert p.exitcode == 0
     assert res[0][0] is not None and res[1][0] is None  # rank 0 writes the checkpoint
     assert res[0][1] == pytest.approx(res[1][1])  # validation metrics are all-reduced
+
+
+# ---------------------------------------------------------------------------------------------
+# Use accounting for native gradient sinks: a weight used several times in one
+# step must complete only after its LAST use. On CPU the native sink path is emulated by an
+# autograd.Function that accumulates into .grad exactly like ops/conv.py's wgrad kernels.
+# ---------------------------------------------------------------------------------------------
+_FORCE_FALLBACK = [False]
+
+
+class _SinkLinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return x @ w.t()
+
+    @staticmethod
+    def backward(ctx, dy):
+        from deep_vision_amd.ops.common import grad_sink
+
+        x, w = ctx.saved_tensors
+        dw = dy.t() @ x
+        sink = None if _FORCE_FALLBACK[0] else grad_sink(w)
+        if sink is not None:
+            sink.add_(dw)
+            dw = None
+        return dy @ w, dw
+
+
+def _sink_linear(x, w):
+    return _SinkLinearFn.apply(x, w)
+
+
+class _SharedNet(torch.nn.Module):
+    """One weight applied three times (CycleGAN-style reuse) plus a plain torch layer."""
+
+    def __init__(self):
+        super().__init__()
+        self.shared = torch.nn.Parameter(torch.randn(16, 16) * 0.2)
+        self.head = torch.nn.Linear(16, 4)
+
+    def forward(self, x):
+        for _ in range(3):
+            x = torch.tanh(_sink_linear(x, self.shared))
+        return self.head(x)
+
+
+class _RecordingComm:
+    world = 2
+
+    def __init__(self):
+        self.snaps = []
+
+    def __call__(self, t):
+        self.snaps.append((t.data_ptr(), t.clone()))
+
+
+def test_ddp_multi_use_completes_after_last_use():
+    from deep_vision_amd.parallel.ddp import DataParallel
+
+    torch.manual_seed(0)
+    net = _SharedNet()
+    comm = _RecordingComm()
+    ddp = DataParallel(net, bucket_mb=16 * 16 * 4 / 2**20, comm=comm)  # the shared weight gets its own bucket
+    x = torch.randn(8, 16)
+    for _ in range(2):
+        for p in net.parameters():
+            p.grad.zero_()
+        comm.snaps.clear()
+        ddp(x).sum().backward()
+        ddp.finish()
+        # every bucket issued exactly once, and what was on the wire is the FINAL gradient
+        assert len(comm.snaps) == len(ddp.buckets)
+        for b in ddp.buckets:
+            t = ddp.gflat[b.start:b.end]
+            snap = [s for ptr, s in comm.snaps if ptr == t.data_ptr()]
+            assert len(snap) == 1 and torch.equal(snap[0], t)
+    # reference gradient (plain autograd, no sinks)
+    ref = _SharedNet()
+    ref.load_state_dict(net.state_dict())
+    y = x
+    for _ in range(3):
+        y = torch.tanh(y @ ref.shared.t())
+    ref.head(y).sum().backward()
+    assert torch.allclose(net.shared.grad, ref.shared.grad, atol=1e-5)
+
+
+def test_ddp_double_report_raises():
+    """A second backward through the same graph without a new forward reports every parameter
+    again: the guard refuses instead of re-issuing buckets into live gradients."""
+    from deep_vision_amd.parallel.ddp import DataParallel, DoubleReadyError
+
+    net = _SharedNet()
+    ddp = DataParallel(net, comm=_RecordingComm())
+    loss = ddp(torch.randn(4, 16)).sum()
+    loss.backward(retain_graph=True)
+    with pytest.raises(DoubleReadyError):
+        loss.backward()
+
+
+def test_ddp_fallback_use_waits_for_autograd():
+    """A native use whose gradient goes back through autograd (no sink) completes only when
+    AccumulateGrad has run."""
+    from deep_vision_amd.parallel.ddp import DataParallel
+
+    net = _SharedNet()
+    comm = _RecordingComm()
+    ddp = DataParallel(net, bucket_mb=16 * 16 * 4 / 2**20, comm=comm)
+    x = torch.randn(4, 16)
+    _FORCE_FALLBACK[0] = True  # every native use hands its gradient back to autograd
+    try:
+        ddp(x).sum().backward()
+    finally:
+        _FORCE_FALLBACK[0] = False
+    ddp.finish()
+    b = ddp.buckets[ddp._bucket_of[id(net.shared)]]
+    t = ddp.gflat[b.start:b.end]
+    assert t.abs().sum() > 0
+    snap = [s for ptr, s in comm.snaps if ptr == t.data_ptr()]
+    assert len(snap) == 1 and torch.equal(snap[0], t)
+
+
+def _fault_worker(rank, world, port, spec):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), DV_FAULT=spec, DV_COMM_TIMEOUT="20")
+    from deep_vision_amd.parallel.ddp import DataParallel
+    from deep_vision_amd.parallel.dist import init_distributed
+    from deep_vision_amd.parallel.watchdog import CommWatchdog
+    from deep_vision_amd.utils.fault import FaultInjector
+
+    init_distributed("gloo", timeout_s=30)
+    wd = CommWatchdog(timeout=20).start()
+    net = Net()
+    ddp = DataParallel(net, bucket_mb=0.01)
+    inj = FaultInjector(rank=rank)
+    for step in range(1, 6):
+        inj.process(step)
+        with wd.guard("allreduce"):
+            ddp(torch.randn(4, 16)).sum().backward()
+            ddp.finish()
+    os._exit(0)
+
+
+def test_kill_rank_tears_down_every_rank():
+    """DV_FAULT=kill_rank@3:1 -> rank 1 dies at step 3; rank 0 must not hang: its collective
+    fails (or the comm watchdog fires) and it exits non-zero within the timeout."""
+    import time
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    port = _port()
+    procs = [ctx.Process(target=_fault_worker, args=(r, world, port, "kill_rank@3:1")) for r in range(world)]
+    t0 = time.time()
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert all(c is not None and c != 0 for c in codes), codes
+    assert time.time() - t0 < 120
+
+
+def _nan_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+
+    from deep_vision_amd.parallel.ddp import DataParallel
+    from deep_vision_amd.parallel.dist import init_distributed
+    from deep_vision_amd.train.optim import FusedSGD
+    from deep_vision_amd.utils.fault import FaultInjector, NonFiniteGuard
+
+    init_distributed("gloo")
+    torch.manual_seed(0)
+    net = Net()
+    ddp = DataParallel(net, bucket_mb=0.01)
+    opt = FusedSGD(ddp.parameters(), lr=0.1)
+    guard = NonFiniteGuard(every=1)
+    inj = FaultInjector("inf_grad@2:1", rank=rank)  # only rank 1 sees a bad gradient
+    decisions = []
+    for step in range(1, 5):
+        opt.zero_grad()
+        ddp(torch.randn(4, 16)).sum().backward()
+        inj.grads(ddp.gflat, step)
+        ddp.finish()
+        ok = guard.ok(torch.zeros(()), ddp.gflat, distributed=True)
+        decisions.append(ok)
+        if ok:
+            opt.step(grad_scale=ddp.grad_scale)
+    q.put((rank, decisions, net.a.weight.detach().numpy().copy()))
+    dist.destroy_process_group()
+
+
+def test_nan_skip_decision_identical_across_ranks():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_nan_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=240) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][0] == res[1][0] == [True, False, True, True]
+    assert (res[0][1] == res[1][1]).all()  # replicas still identical after the skipped step

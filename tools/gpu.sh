@@ -1,0 +1,56 @@
+#!/bin/bash
+# One entry point for every GPU-box job (run through gpurun from the repo root):
+#   tools/gpu.sh check           GPU tests, smoke, 1-GPU ResNet-50 bench
+#   tools/gpu.sh bench [args]    bench.py with the given args (default ResNet-50, 1 GPU)
+#   tools/gpu.sh prof MODEL      rocprofv3 kernel trace + stats of bench.py --model MODEL
+#   tools/gpu.sh pmc  LAYERS     PMC counter passes (one run per counter group) over tools/bench_conv.py layers
+#   tools/gpu.sh models          bench every BASELINE.json GPU config (native and torch/MIOpen reference)
+#   tools/gpu.sh tests [-k EXPR] GPU tests only
+# Every GPU step has its own time limit and the steps are chained with &&: after a fault,
+# abort or timeout nothing else runs on the GPU in that call.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R" && mkdir -p gpurun_out
+mode=${1:-check}; shift || true
+PYT="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
+case "$mode" in
+  check)
+    timeout -k 10 900 $PYT tests -m gpu > gpurun_out/tests.log 2>&1 && \
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
+    timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1
+    rc=$?; tail -3 gpurun_out/tests.log; tail -1 gpurun_out/bench.log | cut -c1-300 ;;
+  tests)
+    timeout -k 10 900 $PYT tests -m gpu "$@" > gpurun_out/tests.log 2>&1
+    rc=$?; grep -E "PASSED|FAILED|ERROR" gpurun_out/tests.log | tail -40; tail -3 gpurun_out/tests.log ;;
+  bench)
+    timeout -k 10 400 python bench.py "$@" > gpurun_out/bench.log 2>&1
+    rc=$?; tail -1 gpurun_out/bench.log | cut -c1-400 ;;
+  prof)
+    m=${1:-resnet50}
+    cd /tmp && export TMPDIR=/tmp && \
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$m" -o run --output-format csv -- \
+      python3 "$R/bench.py" --model "$m" --steps 5 --warmup 2 > "$R/gpurun_out/prof_$m.log" 2>&1
+    rc=$?; cd "$R"
+    f=$(find gpurun_out/prof_$m -name '*kernel_stats.csv' -print -quit)
+    [ -n "$f" ] && python tools/prof_summary.py "$f" 7 "$m bench.py --steps 5 --warmup 2" > gpurun_out/prof_$m.txt 2>&1
+    cat gpurun_out/prof_$m.txt | cut -c1-160 | sed -n '1,45p' ;;
+  pmc)
+    L=${1:-s2_1x1_128_512,s4_3x3_512,s1_1x1_64_256,s2_3x3_128}
+    mkdir -p gpurun_out/pmc && cd /tmp && export TMPDIR=/tmp && \
+    timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VMEM SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE -d "$R/gpurun_out/pmc/p1" -o run --output-format csv -- python3 "$R/tools/bench_conv.py" --layers "$L" --variants 0 --iters 3 > "$R/gpurun_out/pmc/p1.log" 2>&1 && \
+    timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INST_LEVEL_VMEM SQ_LEVEL_WAVES SQ_INSTS_VMEM TCC_HIT TCC_MISS -d "$R/gpurun_out/pmc/p2" -o run --output-format csv -- python3 "$R/tools/bench_conv.py" --layers "$L" --variants 0 --iters 3 > "$R/gpurun_out/pmc/p2.log" 2>&1 && \
+    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE TA_BUSY_avr -d "$R/gpurun_out/pmc/p3" -o run --output-format csv -- python3 "$R/tools/bench_conv.py" --layers "$L" --variants 0 --iters 3 > "$R/gpurun_out/pmc/p3.log" 2>&1
+    rc=$?; cd "$R"
+    python tools/pmc_summary.py "${2:-conv_}" $(find gpurun_out/pmc -name '*counter_collection.csv') > gpurun_out/pmc/summary.txt 2>&1
+    sed -n '1,80p' gpurun_out/pmc/summary.txt ;;
+  models)
+    rc=0
+    for m in mobilenet1 yolov3 hourglass; do
+      timeout -k 10 300 python bench.py --model $m --steps 10 --warmup 3 > gpurun_out/bench_$m.log 2>&1 || { rc=$?; break; }
+      timeout -k 10 300 python bench.py --model $m --steps 10 --warmup 3 --backend torch > gpurun_out/bench_${m}_torch.log 2>&1 || { rc=$?; break; }
+    done
+    for f in gpurun_out/bench_*.log; do echo "$f: $(tail -1 $f | cut -c1-200)"; done ;;
+  *) echo "unknown mode $mode"; exit 2 ;;
+esac
+echo "rc=$rc"
+exit $rc
