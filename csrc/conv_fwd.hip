@@ -56,7 +56,14 @@ struct FwdParams {
   const float* bnprm;
   float* bnacc;
   int bnmode, bnact; float bnslope;
+  const uint8_t* resbits;  // RES only: res is masked by act'() bits before the add
+  int resact; float resslope;
 };
+
+// act'(z)*g for one element of a masked residual gradient (bit set: z > 0)
+DV_DEVICE float masked_res(float g, uint32_t mb, int e, int act, float slope) {
+  return ((mb >> e) & 1u) ? g : (act == 2 ? g * slope : 0.f);
+}
 
 DV_DEVICE void glds16(const void* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(GLB_PTR(src), LDS_PTR(lds_wave_base), 16, 0, 0);
@@ -332,7 +339,7 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
   constexpr bool PF = RES || BNR;
   int64_t pf_off[PF ? 8 : 1];
   uint4 pf_res[RES ? 8 : 1], pf_x[BNR ? 8 : 1];
-  uint32_t pf_mb[BNR ? 8 : 1];
+  uint32_t pf_mb[BNR ? 8 : 1], pf_rmb[RES ? 8 : 1];
   if constexpr (PF) {
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
@@ -351,7 +358,10 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
       }
       pf_off[it] = off;
       const bool ld = off >= 0 && vec;
-      if constexpr (RES) pf_res[it] = ld ? *reinterpret_cast<const uint4*>(p.res + off) : uint4{0u, 0u, 0u, 0u};
+      if constexpr (RES) {
+        pf_res[it] = ld ? *reinterpret_cast<const uint4*>(p.res + off) : uint4{0u, 0u, 0u, 0u};
+        pf_rmb[it] = (off >= 0 && p.resbits) ? (uint32_t)p.resbits[off >> 3] : 0xffu;
+      }
       if constexpr (BNR) {
         pf_x[it] = ld ? *reinterpret_cast<const uint4*>(p.bnx + off) : uint4{0u, 0u, 0u, 0u};
         pf_mb[it] = (ld && p.bnmode == 3) ? (uint32_t)p.bnbits[off >> 3] : 0u;
@@ -430,15 +440,18 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
         const u16* bw = reinterpret_cast<const u16*>(&b);
         uint4 o;
         uint32_t* ov = reinterpret_cast<uint32_t*>(&o);
+        const uint32_t rmb = pf_rmb[it];
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          ov[e] = pack2bf(bf2f(av[2 * e]) + bf2f(bw[2 * e]), bf2f(av[2 * e + 1]) + bf2f(bw[2 * e + 1]));
+          ov[e] = pack2bf(bf2f(av[2 * e]) + masked_res(bf2f(bw[2 * e]), rmb, 2 * e, p.resact, p.resslope),
+                          bf2f(av[2 * e + 1]) + masked_res(bf2f(bw[2 * e + 1]), rmb, 2 * e + 1, p.resact, p.resslope));
         *reinterpret_cast<uint4*>(dst) = o;
         if constexpr (BNR) bn_bwd_accum(p, o, pf_x[it], pf_mb[it], bs, bq, bmu, bis, bms, bmh);
       } else {
+        const uint32_t rmb = pf_rmb[it];
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          if (n + e < p.N) dst[e] = f2bf(bf2f(src[e]) + bf2f(rp[e]));
+          if (n + e < p.N) dst[e] = f2bf(bf2f(src[e]) + masked_res(bf2f(rp[e]), rmb, e, p.resact, p.resslope));
       }
     } else if (vec) {
       const uint4 o = *reinterpret_cast<const uint4*>(src);
@@ -592,6 +605,12 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
   p.identity_map = (a.OH == a.P && a.OW == a.Q && a.osh == 1 && a.osw == 1 && a.oph == 0 && a.opw == 0);
   p.bnx = (const u16*)a.bnx; p.bnbits = (const uint8_t*)a.bnbits; p.bnprm = a.bnprm; p.bnacc = a.bnacc;
   p.bnmode = a.bnmode; p.bnact = a.bnact; p.bnslope = a.bnslope;
+  p.resbits = (const uint8_t*)a.resbits; p.resact = a.resact; p.resslope = a.resslope;
+  // the mask bits are indexed by the dense element offset of y: a single-group tensor whose
+  // pixel stride is its channel count, written by the identity-mapped (stride-1) epilogue
+  if (p.resbits && (!p.res || (p.N & 7) || p.ldy != p.N || p.G != 1 || a.tgather ||
+                    !(a.OH == a.P && a.OW == a.Q && a.osh == 1 && a.osw == 1 && a.oph == 0 && a.opw == 0)))
+    return -1;
   // fused BN statistics need every element of y written by this kernel as 16-B vectors of a dense
   // single-group tensor on the fast loader (the dgrads of stride-1 convs)
   int bn_status = 0;

@@ -27,6 +27,11 @@ struct ConvFwdArgs {
   float* bnacc;           // [SHARDS][2][C]
   int bnmode;             // 0 off, 1 no activation, 2 mask recomputed from bnx, 3 mask bits
   int bnact; float bnslope;
+  // optional activation mask of `res` (1 bit per element, dense [rows][C/8] bytes): the epilogue
+  // adds act'(res) -- res is the raw incoming gradient of a residual block's fused BN+add+ReLU
+  // and the mask turns it into that block's shortcut gradient (no materialised dres tensor)
+  const void* resbits;
+  int resact; float resslope;
 };
 
 struct ConvWgradArgs {

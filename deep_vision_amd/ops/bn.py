@@ -23,7 +23,8 @@ from .common import (ACT_IDS, BF16, F32, grad_nhwc, grad_sink, is_nhwc, ld_of, l
 
 STAT_SHARDS = 64
 FUSE_BWD_STATS = True  # fold the backward reduction into the consumer conv's dgrad epilogue
-COUNTERS = {"bwd_reduce_fused": 0, "bwd_reduce_pass": 0}
+LAZY_SHORTCUT = True   # identity-shortcut gradient masked inside the consumer's dgrad epilogue
+COUNTERS = {"bwd_reduce_fused": 0, "bwd_reduce_pass": 0, "shortcut_lazy": 0}
 
 
 class BNRef:
@@ -123,7 +124,11 @@ class _BNActFn(torch.autograd.Function):
         st = stream_handle()
         L = lib()
         dx = torch.empty_like(x)
-        dres = torch.empty_like(x) if (has_res and ctx.needs_input_grad[6]) else None
+        # identity shortcut of a residual block: hand the shortcut consumer's dgrad the raw dout +
+        # mask bits instead of writing dres = act'(z)*dout (csrc/conv_fwd.hip resbits epilogue)
+        lazy = (LAZY_SHORTCUT and training and has_res and ctx.needs_input_grad[6] and ctx.bits and ctx.join is not None
+                and ctx.join.can_stash() and dout.is_contiguous(memory_format=torch.channels_last))
+        dres = torch.empty_like(x) if (has_res and ctx.needs_input_grad[6] and not lazy) else None
         dgamma = dbeta = None
         want_affine = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
         direct = False
@@ -153,9 +158,27 @@ class _BNActFn(torch.autograd.Function):
                 out = torch.empty_like(x)
                 L.bn_apply(ptr(x), 0, ptr(out), x.numel(), C, ptr(scale), ptr(shift), act, float(slope), 0, st)
             L.bn_bwd_eval(ptr(dout), ptr(out), ptr(dx), ptr(dres), x.numel(), C, ptr(scale), act, float(slope), st)
-        if ctx.join is not None and dres is not None:
+        if lazy:
+            from .conv import MaskedGrad
+
+            COUNTERS["shortcut_lazy"] += 1
+            dres = ctx.join.produce(MaskedGrad(dout, out, act, slope))  # `out` holds the mask bits
+        elif ctx.join is not None and dres is not None:
             dres = ctx.join.produce(dres)  # folded into the shortcut consumer's dgrad epilogue
         return dx, None, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None, None, None
+
+
+def masked_grad(grad, bits, act, slope):
+    """act'(z) * grad with the mask stored as bits (1 per element, dense NHWC): the materialised
+    form of a MaskedGrad, via the BN backward apply pass with unit coefficients."""
+    C = grad.shape[1]
+    g = grad if grad.is_contiguous(memory_format=torch.channels_last) else grad.contiguous(memory_format=torch.channels_last)
+    out = torch.empty_like(g)
+    one = torch.ones(C, dtype=F32, device=g.device)
+    zero = torch.zeros(C, dtype=F32, device=g.device)
+    lib().bn_bwd_apply(ptr(g), ptr(bits), ptr(g), ptr(out), 0, g.numel(), C, ptr(one), ptr(zero), ptr(zero), ptr(one),
+                       ptr(zero), act, float(slope), 1, stream_handle())
+    return out
 
 
 def _torch_bn_act(x, bn, act, slope, residual):

@@ -86,9 +86,10 @@ def _channel_sum(dy: torch.Tensor) -> torch.Tensor:
 
 
 def conv_fwd_raw(x, wk, y, bias, stats, N, H, W, Cg, ldx, G, Kout, P, Q, R, S, stride, padding, dilation,
-                 act=0, slope=0.0, tgather=0, omap=None, ldy=None, res=None, bnref=None):
+                 act=0, slope=0.0, tgather=0, omap=None, ldy=None, res=None, bnref=None, resmask=None):
     """Launch the implicit-GEMM kernel. ``bnref`` (ops.bn.BNRef): also reduce that BatchNorm's
-    backward statistics over ``y`` in the epilogue; returns True when that was done."""
+    backward statistics over ``y`` in the epilogue; returns True when that was done.
+    ``resmask`` (bits, act, slope): ``res`` is a raw gradient masked by act'() before the add."""
     sh, sw = stride
     ph, pw = padding
     dh, dw = dilation
@@ -97,6 +98,8 @@ def conv_fwd_raw(x, wk, y, bias, stats, N, H, W, Cg, ldx, G, Kout, P, Q, R, S, s
     if bnref is not None:
         bn = dict(bnx=ptr(bnref.x), bnbits=ptr(bnref.bits), bnprm=ptr(bnref.prm), bnacc=ptr(bnref.acc),
                   bnmode=bnref.mode, bnact=bnref.act, bnslope=float(bnref.slope))
+    if resmask is not None:
+        bn.update(resbits=ptr(resmask[0]), resact=int(resmask[1]), resslope=float(resmask[2]))
     r = lib().conv_fwd(ptr(x), ptr(wk), ptr(y), ptr(bias), ptr(stats), N, H, W, Cg, ldx, G, Kout, P, Q, R, S, sh, sw,
                        ph, pw, dh, dw, tgather, OH, OW, osh, osw, oph, opw, ldy if ldy is not None else ld_of(y), act,
                        float(slope), ptr(res), stream_handle(), **bn)
@@ -126,7 +129,9 @@ def _dgrad(dy, weight, x_shape, Cg_x, G, stride, padding, dilation, device, accu
 
     ``accum``: a dense gradient of the same input from another consumer (residual shortcut /
     projection); the dgrad kernel adds into it in place (epilogue ``res`` aliasing ``y``),
-    replacing autograd's separate gradient-sum pass."""
+    replacing autograd's separate gradient-sum pass. A ``MaskedGrad`` accum (a residual block's
+    raw output gradient + its ReLU mask bits) is masked inside the same epilogue: the shortcut
+    gradient is never materialised."""
     N, _, H, W = x_shape
     O, Ig, R, S = weight.shape
     Og = O // G
@@ -138,6 +143,13 @@ def _dgrad(dy, weight, x_shape, Cg_x, G, stride, padding, dilation, device, accu
     wd = _prep_weight(weight, G, Cg_dy, mode=1)  # [G][Ig][R][S][Cg_dy]
     ldy_in = ld_of(dy)
     scatter = (sh, sw) != (1, 1) and R == 1 and S == 1 and (ph, pw) == (0, 0)
+    resmask = None
+    if isinstance(accum, MaskedGrad):
+        if ((sh, sw) == (1, 1) and G == 1 and Cg_x == Ig and _accumulable(accum.grad, (N, G * Cg_x, H, W))):
+            resmask = (accum.bits, accum.act, accum.slope)
+            accum = accum.grad
+        else:
+            accum = accum.materialize()
     if accum is not None and Cg_x == Ig and _accumulable(accum, (N, G * Cg_x, H, W)):
         dX, res = accum, accum  # scattered positions get res + val, the others keep res
     else:
@@ -145,7 +157,7 @@ def _dgrad(dy, weight, x_shape, Cg_x, G, stride, padding, dilation, device, accu
     if (sh, sw) == (1, 1):
         fuse = bnref if (bnref is not None and G == 1 and Cg_x == Ig and (res is not None or accum is None)) else None
         if conv_fwd_raw(dy, wd, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, H, W, R, S, (1, 1), (-ph, -pw),
-                        (-dh, -dw), ldy=G * Cg_x, res=res, bnref=fuse):
+                        (-dh, -dw), ldy=G * Cg_x, res=res, bnref=fuse, resmask=resmask):
             fuse.mark_fused(dX)
     elif scatter:
         conv_fwd_raw(dy, wd, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, P, Q, 1, 1, (1, 1), (0, 0), (1, 1),
@@ -156,6 +168,28 @@ def _dgrad(dy, weight, x_shape, Cg_x, G, stride, padding, dilation, device, accu
     if accum is not None and res is None:  # layout mismatch: plain add
         dX = dX[:, : accum.shape[1]] + accum if dX.shape[1] != accum.shape[1] else dX + accum
     return dX
+
+
+class MaskedGrad:
+    """A residual block's shortcut gradient in factored form: ``act'(z) * grad`` with the
+    activation mask stored as bits by the forward BN+add+ReLU pass (ops.bn). The consumer conv's
+    dgrad epilogue applies the mask while adding (csrc/conv_fwd.hip ``resbits``), so the masked
+    tensor is never written. ``grad`` is owned by this object and may be overwritten in place."""
+
+    __slots__ = ("grad", "bits", "act", "slope", "coef")
+
+    def __init__(self, grad, bits, act, slope):
+        self.grad, self.bits, self.act, self.slope = grad, bits, act, slope
+
+    def materialize(self):
+        from .bn import masked_grad
+
+        return masked_grad(self.grad, self.bits, self.act, self.slope)
+
+    def __add__(self, other):
+        return self.materialize() + (other.materialize() if isinstance(other, MaskedGrad) else other)
+
+    __radd__ = __add__
 
 
 class GradJoin:
@@ -173,9 +207,13 @@ class GradJoin:
     def produce(self, g):
         """Producer side: returns the gradient to hand to autograd (None when stashed)."""
         if g is None or self.consumer_done:
-            return g
+            return g.materialize() if isinstance(g, MaskedGrad) else g
         self.grad = g if self.grad is None else self.grad + g
         return None
+
+    def can_stash(self):
+        """True when a produced gradient would be stashed (not handed to autograd)."""
+        return not self.consumer_done and self.grad is None
 
     def take(self):
         """Consumer side: the stashed gradient (or None), marking the consumer as done."""
@@ -259,6 +297,8 @@ class _ConvFn(torch.autograd.Function):
             join, role = ctx.join
             if join is not None and role == "consumer":
                 g = join.take()  # nothing to add to: hand a stashed shortcut gradient through
+                if isinstance(g, MaskedGrad):
+                    g = g.materialize()
                 return (g, None, None) + (None,) * 11
             return (None,) * 14
         dy = grad_nhwc(dy)

@@ -415,3 +415,32 @@ def test_bn_backward_stats_fused_in_dgrad():
         B.FUSE_BWD_STATS = True
     noise = _cos(grads["a"], grads["b"])
     assert _cos(grads["fused"], grads["a"]) > min(noise, 0.99999) - 5e-4, (noise, _cos(grads["fused"], grads["a"]))
+
+
+def test_masked_shortcut_grad_in_dgrad_epilogue():
+    """Identity-shortcut gradients of the bottleneck blocks travel as (dout, ReLU mask bits) and are
+    masked inside conv1's dgrad epilogue (ops.conv.MaskedGrad, csrc/conv_fwd.hip resbits) instead
+    of a materialised dres tensor: gradients equal the materialised path within run-to-run noise."""
+    from deep_vision_amd import models as M
+    from deep_vision_amd import ops as F
+    from deep_vision_amd.ops import bn as B
+
+    torch.manual_seed(0)
+    base = M.get_model("resnet50").to(DEV)
+    x = torch.randn(8, 3, 96, 96, device=DEV)
+    y = torch.randint(0, 1000, (8,), device=DEV)
+    grads = {}
+    try:
+        for key, lazy in (("a", False), ("b", False), ("lazy", True)):
+            B.LAZY_SHORTCUT = lazy
+            m = copy.deepcopy(base)
+            c0 = B.COUNTERS["shortcut_lazy"]
+            F.cross_entropy(m(x), y).backward()
+            torch.cuda.synchronize()
+            grads[key] = torch.cat([p.grad.flatten() for p in m.parameters()])
+            n = B.COUNTERS["shortcut_lazy"] - c0
+            assert n == (12 if lazy else 0), n  # 16 blocks minus the 4 projection blocks
+    finally:
+        B.LAZY_SHORTCUT = True
+    noise = _cos(grads["a"], grads["b"])
+    assert _cos(grads["lazy"], grads["a"]) > min(noise, 0.99999) - 5e-4, (noise, _cos(grads["lazy"], grads["a"]))
