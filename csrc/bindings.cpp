@@ -87,9 +87,11 @@ PYBIND11_MODULE(_C, m) {
     dv_bn_eval_prep(C, eps, CFP(gamma), CFP(beta), CFP(rm), CFP(rv), FP(scale), FP(shift), ST(st)); check_last("bn_eval_prep");
   });
   m.def("bn_apply", [](uptr x, uptr res, uptr out, int64_t n, int C, uptr scale, uptr shift, int act, float slope,
-                       uptr mask, uptr st) {
-    dv_bn_apply(CP(x), CP(res), P(out), n, C, CFP(scale), CFP(shift), act, slope, P(mask), ST(st)); check_last("bn_apply");
-  });
+                       uptr mask, uptr st, uptr rscale, uptr rshift) {
+    dv_bn_apply(CP(x), CP(res), P(out), n, C, CFP(scale), CFP(shift), act, slope, P(mask), CFP(rscale), CFP(rshift), ST(st));
+    check_last("bn_apply");
+  }, py::arg("x"), py::arg("res"), py::arg("out"), py::arg("n"), py::arg("C"), py::arg("scale"), py::arg("shift"),
+     py::arg("act"), py::arg("slope"), py::arg("mask"), py::arg("st"), py::arg("rscale") = 0, py::arg("rshift") = 0);
   m.def("bn_bwd_reduce", [](uptr dout, uptr out, uptr x, int64_t rows, int C, uptr mean, uptr invstd, uptr mscale,
                             uptr mshift, int act, float slope, uptr acc, int mask_bits, uptr st) {
     dv_bn_bwd_reduce(CP(dout), CP(out), CP(x), rows, C, CFP(mean), CFP(invstd), CFP(mscale), CFP(mshift), act, slope, FP(acc),

@@ -200,18 +200,23 @@ struct RowTile {
 };
 
 // ---- out = act(x*scale + shift (+res)) ----
-template <int VEC, bool MB>
+template <int VEC, bool MB, bool RBN = false>
 __global__ __launch_bounds__(NT) void bn_apply_kernel(const u16* __restrict__ x, const u16* __restrict__ res,
                                                         u16* __restrict__ out, int64_t rows, int C, int64_t rows_per_block,
                                                         const float* __restrict__ scale, const float* __restrict__ shift,
-                                                        int act, float slope, uint8_t* __restrict__ mask) {
+                                                        int act, float slope, uint8_t* __restrict__ mask,
+                                                        const float* __restrict__ rscale, const float* __restrict__ rshift) {
   RowTile t(C, VEC);
   if (t.lane_r >= t.rpi) return;
   const int64_t r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
   for (int g = t.lane_c; g < t.cg; g += t.tpr) {
-    float sc[VEC], sf[VEC];
+    float sc[VEC], sf[VEC], rs[VEC];
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) { sc[k] = scale[g * VEC + k]; sf[k] = shift[g * VEC + k]; }
+    for (int k = 0; k < VEC; ++k) {
+      sc[k] = scale[g * VEC + k]; sf[k] = shift[g * VEC + k];
+      // residual BN: z = x*sc + res*rs + (sf + rshift): one shift per channel
+      if constexpr (RBN) { rs[k] = rscale[g * VEC + k]; sf[k] += rshift[g * VEC + k]; }
+    }
 #pragma unroll 2
     for (int64_t r = r0 + t.lane_r; r < r1; r += t.rpi) {
       const int64_t o = r * C + g * VEC;
@@ -222,7 +227,8 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const u16* __restrict__ x,
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
         float z = fmaf(v[k], sc[k], sf[k]);
-        if (res) z += rv[k];
+        if constexpr (RBN) z = fmaf(rv[k], rs[k], z);
+        else if (res) z += rv[k];
         if constexpr (MB) bits |= (z > 0.f ? 1u : 0u) << k;
         v[k] = act_fwd(z, act, slope);
       }
@@ -422,12 +428,20 @@ void dv_bn_eval_prep(int C, float eps, const float* gamma, const float* beta, co
 }
 
 void dv_bn_apply(const void* x, const void* res, void* out, int64_t n, int C, const float* scale, const float* shift,
-                 int act, float slope, void* mask, hipStream_t st) {
+                 int act, float slope, void* mask, const float* rscale, const float* rshift, hipStream_t st) {
   const int v = vec_for(C);
   const int64_t rows = n / C;
   const int64_t rpb = apply_rows_per_block(rows, C, v);
   const int g = (int)((rows + rpb - 1) / rpb);
-#define AP_ARGS <<<g, NT, 0, st>>>((const u16*)x, (const u16*)res, (u16*)out, rows, C, rpb, scale, shift, act, slope, (uint8_t*)mask)
+#define AP_ARGS <<<g, NT, 0, st>>>((const u16*)x, (const u16*)res, (u16*)out, rows, C, rpb, scale, shift, act, slope, (uint8_t*)mask, rscale, rshift)
+  if (res && rscale && rshift) {
+    if (mask && v == 8) bn_apply_kernel<8, true, true> AP_ARGS;
+    else if (v == 8) bn_apply_kernel<8, false, true> AP_ARGS;
+    else if (v == 4) bn_apply_kernel<4, false, true> AP_ARGS;
+    else if (v == 2) bn_apply_kernel<2, false, true> AP_ARGS;
+    else bn_apply_kernel<1, false, true> AP_ARGS;
+    return;
+  }
   if (mask && v == 8) { bn_apply_kernel<8, true> AP_ARGS; return; }
   switch (v) {
     case 8: bn_apply_kernel<8, false> AP_ARGS; break;

@@ -69,8 +69,10 @@ void dv_bn_finalize(float* acc, int C, double count, float eps, float momentum, 
                     float* shift, hipStream_t st);
 void dv_bn_eval_prep(int C, float eps, const float* gamma, const float* beta, const float* rm, const float* rv,
                      float* scale, float* shift, hipStream_t st);
+// out = act(x*scale + shift (+ res [* rscale + rshift])): rscale/rshift fold a second BatchNorm
+// (a residual block's projection BN) into the same pass instead of materialising its output
 void dv_bn_apply(const void* x, const void* res, void* out, int64_t n, int C, const float* scale, const float* shift,
-                 int act, float slope, void* mask, hipStream_t st);
+                 int act, float slope, void* mask, const float* rscale, const float* rshift, hipStream_t st);
 void dv_bn_bwd_reduce(const void* dout, const void* out, const void* x, int64_t rows, int C, const float* mean,
                       const float* invstd, const float* mscale, const float* mshift, int act, float slope, float* acc,
                       int mask_bits, hipStream_t st);

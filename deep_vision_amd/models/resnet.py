@@ -48,11 +48,13 @@ class BasicBlock(tnn.Module):
         # conv1's dgrad epilogue instead of a separate autograd add (ops.conv.GradJoin)
         j = GradJoin() if F.native(x) else None
         out = F.conv_bn_act(x, self.conv1, self.bn1, "relu", join=j, join_role="consumer")
-        if self.downsample:
-            identity, rj = F.conv_bn_act(x, self.projection[0], self.projection[1], join=j, join_role="producer"), None
+        rbn = None
+        if self.downsample:  # projection BN folded into the block's last BN+add+ReLU pass
+            identity, rbn = F.conv_bn_deferred(x, self.projection[0], self.projection[1], join=j, join_role="producer")
+            rj = None
         else:
             identity, rj = x, j
-        return F.conv_bn_act(out, self.conv2, self.bn2, "relu", residual=identity, residual_join=rj)
+        return F.conv_bn_act(out, self.conv2, self.bn2, "relu", residual=identity, residual_join=rj, residual_bn=rbn)
 
 
 class BottleneckBlock(tnn.Module):
@@ -75,12 +77,15 @@ class BottleneckBlock(tnn.Module):
         j = GradJoin() if F.native(x) else None
         out = F.conv_bn_act(x, self.conv1, self.bn1, "relu", join=j, join_role="consumer")
         out = F.conv_bn_act(out, self.conv2, self.bn2, "relu")
-        # projection created after the main path: its backward runs first and stashes its dx
+        # projection created after the main path: its backward runs first and stashes its dx;
+        # its BatchNorm is applied inside bn3's BN+add+ReLU pass (ops.bn.conv_bn_deferred)
+        rbn = None
         if self.downsample:
-            identity, rj = F.conv_bn_act(x, self.projection[0], self.projection[1], join=j, join_role="producer"), None
+            identity, rbn = F.conv_bn_deferred(x, self.projection[0], self.projection[1], join=j, join_role="producer")
+            rj = None
         else:
             identity, rj = x, j
-        return F.conv_bn_act(out, self.conv3, self.bn3, "relu", residual=identity, residual_join=rj)
+        return F.conv_bn_act(out, self.conv3, self.bn3, "relu", residual=identity, residual_join=rj, residual_bn=rbn)
 
 
 class _ResNetBase(tnn.Module):

@@ -24,6 +24,7 @@ from .common import (ACT_IDS, BF16, F32, grad_nhwc, grad_sink, is_nhwc, ld_of, l
 STAT_SHARDS = 64
 FUSE_BWD_STATS = True  # fold the backward reduction into the consumer conv's dgrad epilogue
 LAZY_SHORTCUT = True   # identity-shortcut gradient masked inside the consumer's dgrad epilogue
+FOLD_RESIDUAL_BN = True  # projection-shortcut BN applied inside the block's last BN pass
 COUNTERS = {"bwd_reduce_fused": 0, "bwd_reduce_pass": 0, "shortcut_lazy": 0}
 
 
@@ -66,7 +67,11 @@ def _nrows(x):
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, stats, weight, bias, running_mean, running_var, residual, training, momentum, eps, act,
-                slope, ws_fwd, ws_bwd, join=None, refbox=None):
+                slope, ws_fwd, ws_bwd, join=None, refbox=None, r_stats=None, r_weight=None, r_bias=None, r_rm=None,
+                r_rv=None, r_cfg=None):
+        # r_*: a second, training-mode BatchNorm applied to ``residual`` inside the same pass
+        # (a residual block's projection BN): out = act(bn(x) + bn_r(residual)); bn_r's output is
+        # never materialised and its backward reads (dout, mask bits, residual) directly
         N, C, H, W = x.shape
         if ld_of(x) != C:
             raise NotImplementedError("BatchNorm on a padded channel view")
@@ -89,6 +94,13 @@ class _BNActFn(torch.autograd.Function):
             if weight is not None and weight.requires_grad:  # dgamma needs xhat of the running stats
                 mean.copy_(running_mean)
                 torch.rsqrt(running_var + eps, out=invstd)
+        rprm = None
+        if r_cfg is not None:
+            r_mom, r_eps, r_ws_fwd, r_ws_bwd = r_cfg
+            rprm = torch.empty((4, C), dtype=F32, device=dev)
+            L.bn_finalize(ptr(r_stats), C, float(rows), float(r_eps), float(r_mom), ptr(r_weight.detach()),
+                          ptr(r_bias.detach()), ptr(r_rm), ptr(r_rv), ptr(rprm[2]), ptr(rprm[3]), ptr(rprm[0]),
+                          ptr(rprm[1]), st)
         out = torch.empty_like(x)
         # activation mask in backward: recomputed from x (z = x*scale + shift) when there is no
         # residual; with a residual it is stored as bits by this pass (training, C % 8 == 0) or,
@@ -96,9 +108,11 @@ class _BNActFn(torch.autograd.Function):
         bits = training and bool(act) and residual is not None and C % 8 == 0
         mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=dev) if bits else None
         L.bn_apply(ptr(x), ptr(residual), ptr(out), x.numel(), C, ptr(scale), ptr(shift), act, float(slope), ptr(mask),
-                   st)
+                   st, rscale=ptr(rprm[0]) if rprm is not None else 0, rshift=ptr(rprm[1]) if rprm is not None else 0)
         keep_out = bool(act) and residual is not None and not bits
-        ctx.save_for_backward(x, mask if bits else (out if keep_out else None), weight, bias, prm)
+        ctx.save_for_backward(x, mask if bits else (out if keep_out else None), weight, bias, prm,
+                              residual if rprm is not None else None, rprm, r_weight, r_bias)
+        ctx.r_ws_bwd = r_cfg[3] if r_cfg is not None else None
         ctx.bits = bits
         ctx.cfg = (training, act, slope, residual is not None)
         ctx.ws_bwd = ws_bwd
@@ -112,7 +126,7 @@ class _BNActFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        x, out, weight, bias, prm = ctx.saved_tensors
+        x, out, weight, bias, prm, r_x, rprm, r_weight, r_bias = ctx.saved_tensors
         training, act, slope, has_res = ctx.cfg
         scale, shift, mean, invstd = prm[0], prm[1], prm[2], prm[3]
         N, C, H, W = x.shape
@@ -127,8 +141,9 @@ class _BNActFn(torch.autograd.Function):
         # identity shortcut of a residual block: hand the shortcut consumer's dgrad the raw dout +
         # mask bits instead of writing dres = act'(z)*dout (csrc/conv_fwd.hip resbits epilogue)
         lazy = (LAZY_SHORTCUT and training and has_res and ctx.needs_input_grad[6] and ctx.bits and ctx.join is not None
-                and ctx.join.can_stash() and dout.is_contiguous(memory_format=torch.channels_last))
-        dres = torch.empty_like(x) if (has_res and ctx.needs_input_grad[6] and not lazy) else None
+                and ctx.join.can_stash() and dout.is_contiguous(memory_format=torch.channels_last) and rprm is None)
+        dres = (torch.empty_like(x) if (has_res and ctx.needs_input_grad[6] and not lazy and rprm is None)
+                else None)
         dgamma = dbeta = None
         want_affine = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
         direct = False
@@ -158,6 +173,9 @@ class _BNActFn(torch.autograd.Function):
                 out = torch.empty_like(x)
                 L.bn_apply(ptr(x), 0, ptr(out), x.numel(), C, ptr(scale), ptr(shift), act, float(slope), 0, st)
             L.bn_bwd_eval(ptr(dout), ptr(out), ptr(dx), ptr(dres), x.numel(), C, ptr(scale), act, float(slope), st)
+        r_dgamma = r_dbeta = None
+        if rprm is not None:
+            dres, r_dgamma, r_dbeta = _residual_bn_backward(ctx, dout, out, r_x, rprm, r_weight, r_bias, act, slope)
         if lazy:
             from .conv import MaskedGrad
 
@@ -165,7 +183,36 @@ class _BNActFn(torch.autograd.Function):
             dres = ctx.join.produce(MaskedGrad(dout, out, act, slope))  # `out` holds the mask bits
         elif ctx.join is not None and dres is not None:
             dres = ctx.join.produce(dres)  # folded into the shortcut consumer's dgrad epilogue
-        return dx, None, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None, None, None
+        return (dx, None, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None, None, None,
+                None, r_dgamma, r_dbeta, None, None, None)
+
+
+def _residual_bn_backward(ctx, dout, bits, r_x, rprm, r_weight, r_bias, act, slope):
+    """Backward of the folded residual BatchNorm: dz = act'(z)*dout from the mask bits (never
+    materialised), its reduction against xhat_r, then d(r_x) = kA*dz + kB*r_x + kC."""
+    L = lib()
+    st = stream_handle()
+    N, C, H, W = r_x.shape
+    rows = N * H * W
+    mbits = int(bits is not None and ctx.bits)
+    acc = ctx.r_ws_bwd
+    L.bn_bwd_reduce(ptr(dout), ptr(bits), ptr(r_x), rows, C, ptr(rprm[2]), ptr(rprm[3]), 0, 0, act, float(slope), ptr(acc),
+                    mbits, st)
+    sg = grad_sink(r_weight) if ctx.needs_input_grad[17] else None
+    sb = grad_sink(r_bias) if ctx.needs_input_grad[18] else None
+    direct = sg is not None and sb is not None
+    dgamma = dbeta = None
+    if not direct:
+        dgamma = torch.empty(C, dtype=F32, device=r_x.device)
+        dbeta = torch.empty(C, dtype=F32, device=r_x.device)
+    coef = torch.empty((3, C), dtype=F32, device=r_x.device)
+    L.bn_bwd_finalize(ptr(acc), C, float(rows), ptr(r_weight.detach()), ptr(rprm[2]), ptr(rprm[3]),
+                      ptr(sg if direct else dgamma), ptr(sb if direct else dbeta), int(direct), ptr(coef[0]), ptr(coef[1]),
+                      ptr(coef[2]), st)
+    dr = torch.empty_like(r_x)
+    L.bn_bwd_apply(ptr(dout), ptr(bits), ptr(r_x), ptr(dr), 0, r_x.numel(), C, ptr(coef[0]), ptr(coef[1]), ptr(coef[2]),
+                   0, 0, act, float(slope), mbits, st)
+    return (dr if ctx.needs_input_grad[6] else None), dgamma, dbeta
 
 
 def masked_grad(grad, bits, act, slope):
@@ -219,8 +266,20 @@ def bn_momentum(bn) -> float:
     return bn.momentum
 
 
-def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None, residual_join=None):
-    """act(BN(x) (+ residual)) with ``bn`` an nn.BatchNorm2d (parameters, buffers, mode)."""
+def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None, residual_join=None, residual_bn=None):
+    """act(BN(x) (+ residual)) with ``bn`` an nn.BatchNorm2d (parameters, buffers, mode).
+    ``residual_bn=(bn_r, stats_r)``: ``residual`` is a raw conv output still to be normalised by
+    ``bn_r`` (training mode, batch statistics ``stats_r`` from its conv epilogue); the two BNs,
+    the add and the activation run as one pass (see conv_bn_deferred)."""
+    if residual_bn is not None:
+        rbn, rstats = residual_bn
+        C = x.shape[1]
+        fold = (native(x) and bn.training and rbn.training and rbn.track_running_stats and rstats is not None
+                and rbn.affine and C % 8 == 0 and (act is None or act in ("relu", "leaky", "leaky_relu"))
+                and is_nhwc(residual) and ld_of(residual) == C and ld_of(x) == C)
+        if not fold:
+            residual = batch_norm_act(residual, rbn, None, 0.0, None, rstats)
+            residual_bn = None
     if not native(x):
         return _torch_bn_act(x, bn, act, slope, residual)
     training = bn.training or not bn.track_running_stats
@@ -236,14 +295,41 @@ def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None, residu
     ws_fwd = workspace(bn, "bn_fwd", (STAT_SHARDS, 2, C), x.device) if training else None
     ws_bwd = workspace(bn, "bn_bwd", (STAT_SHARDS, 2, C), x.device) if training else None
     refbox = [] if FUSE_BWD_STATS and torch.is_grad_enabled() else None
+    rargs = ()
+    if residual_bn is not None:
+        rbn, rstats = residual_bn
+        if rbn.num_batches_tracked is not None:
+            _count_batch(rbn)
+        rargs = (rstats, rbn.weight, rbn.bias, rbn.running_mean, rbn.running_var,
+                 (bn_momentum(rbn), rbn.eps, workspace(rbn, "bn_fwd", (STAT_SHARDS, 2, C), x.device),
+                  workspace(rbn, "bn_bwd", (STAT_SHARDS, 2, C), x.device)))
     y = _BNActFn.apply(x, stats, bn.weight, bn.bias, rm, rv, residual, training, mom,
-                       bn.eps, ACT_IDS[act], float(slope), ws_fwd, ws_bwd, residual_join, refbox)
+                       bn.eps, ACT_IDS[act], float(slope), ws_fwd, ws_bwd, residual_join, refbox, *rargs)
     if refbox:
         y._dv_bnref = refbox[0]  # read by the consumer conv (ops.conv._ConvFn)
     return y
 
 
-def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None, join=None, join_role=None, residual_join=None):
+def conv_bn_deferred(x, conv, bn, join=None, join_role=None):
+    """conv -> BatchNorm whose apply pass is deferred into its consumer's BN pass (a residual
+    block's projection shortcut, folded into the block's last BN+add+ReLU by
+    ``conv_bn_act(..., residual=y, residual_bn=rbn)``). Returns ``(y, rbn)``: the raw conv output
+    and ``(bn, stats)``, or the normal BN output and None when the fold does not apply."""
+    from .conv import conv2d
+
+    ok = (FOLD_RESIDUAL_BN and native(x) and bn.training and bn.track_running_stats and bn.affine
+          and conv.out_channels % 8 == 0 and torch.is_grad_enabled())
+    if not ok:
+        return conv_bn_act(x, conv, bn, join=join, join_role=join_role), None
+    sbuf = workspace(bn, "bn_fwd", (STAT_SHARDS, 2, conv.out_channels), x.device)
+    pad = conv.native_padding(x.shape[2], x.shape[3]) if hasattr(conv, "native_padding") else conv.padding
+    y, stats = conv2d(x, conv.weight, conv.bias, conv.stride, pad, conv.dilation, conv.groups, want_stats=True,
+                      stats_buf=sbuf, join=join, join_role=join_role)
+    return y, (bn, stats)
+
+
+def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None, join=None, join_role=None, residual_join=None,
+                residual_bn=None):
     """Fused conv -> BN (batch stats from the conv epilogue) -> (+residual) -> activation.
 
     ``join`` / ``join_role`` ('consumer' | 'producer') and ``residual_join``: a conv.GradJoin
@@ -252,6 +338,8 @@ def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None, join=None, join
     from .conv import conv2d
 
     if not native(x):
+        if residual_bn is not None:
+            residual = _torch_bn_act(residual, residual_bn[0], None, 0.0, None)
         return _torch_bn_act(conv(x), bn, act, slope, residual)
     # BN kernels need dense channels: a channel count that is not a multiple of 8 comes back as a
     # padded view, which is compacted below and gets its statistics from a separate pass
@@ -264,4 +352,4 @@ def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None, join=None, join
     if y.shape[1] % 8 != 0:  # padded view: BN kernels require dense channels
         y = y.contiguous(memory_format=torch.channels_last)
         stats = None
-    return batch_norm_act(y, bn, act, slope, residual, stats, residual_join=residual_join)
+    return batch_norm_act(y, bn, act, slope, residual, stats, residual_join=residual_join, residual_bn=residual_bn)

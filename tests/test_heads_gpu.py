@@ -444,3 +444,49 @@ def test_masked_shortcut_grad_in_dgrad_epilogue():
         B.LAZY_SHORTCUT = True
     noise = _cos(grads["a"], grads["b"])
     assert _cos(grads["lazy"], grads["a"]) > min(noise, 0.99999) - 5e-4, (noise, _cos(grads["lazy"], grads["a"]))
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_projection_bn_folded_into_block_apply(stride):
+    """A projection bottleneck block: the shortcut BatchNorm is applied inside bn3's BN+add+ReLU
+    pass (ops.bn.conv_bn_deferred). Output, both BNs' running statistics and every gradient
+    equal the unfolded native path within its run-to-run noise, and track a torch fp32 run of the
+    same block (reference semantics R/ResNet/pytorch/models/resnet50.py:68-75,147-165)."""
+    from deep_vision_amd.models.resnet import BottleneckBlock
+    from deep_vision_amd.ops import bn as B
+    from deep_vision_amd.ops.common import set_backend
+
+    torch.manual_seed(0)
+    base = BottleneckBlock(64, 64, 256, stride=stride, downsample=True).to(DEV)
+    x32 = torch.randn(8, 64, 28, 28, device=DEV).bfloat16().float()
+    g = torch.randn(8, 256, 28 // stride, 28 // stride, device=DEV)
+    runs = {}
+    for key in ("a", "b", "fold", "torch"):
+        blk = copy.deepcopy(base)
+        B.FOLD_RESIDUAL_BN = key == "fold"
+        set_backend("torch" if key == "torch" else "native")
+        try:
+            if key == "torch":
+                x = x32.clone().requires_grad_(True)
+                y = blk(x)
+                y.backward(g)
+            else:
+                x = x32.to(torch.bfloat16).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+                y = blk(x)
+                y.backward(g.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+        finally:
+            B.FOLD_RESIDUAL_BN = True
+            set_backend("native")
+        blk.state_dict()  # flushes the lazily counted num_batches_tracked
+        vec = torch.cat([x.grad.float().flatten()] + [p.grad.flatten() for p in blk.parameters()])
+        runs[key] = (y.detach().float(), vec, blk)
+    noise = _cos(runs["a"][1], runs["b"][1])
+    assert _cos(runs["fold"][1], runs["a"][1]) > min(noise, 0.99999) - 5e-4, (noise, _cos(runs["fold"][1], runs["a"][1]))
+    assert _cos(runs["fold"][0], runs["a"][0]) > 0.9999
+    assert _cos(runs["fold"][0], runs["torch"][0]) > 0.999
+    assert _cos(runs["fold"][1], runs["torch"][1]) > 0.99
+    bf, bt = runs["fold"][2], runs["torch"][2]
+    for bn_n, bn_r in ((bf.bn3, bt.bn3), (bf.projection[1], bt.projection[1])):
+        assert torch.allclose(bn_n.running_mean, bn_r.running_mean, atol=2e-3, rtol=2e-2)
+        assert torch.allclose(bn_n.running_var, bn_r.running_var, atol=2e-3, rtol=2e-2)
+        assert int(bn_n.num_batches_tracked) == int(bn_r.num_batches_tracked) == 1
