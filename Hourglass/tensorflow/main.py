@@ -38,7 +38,7 @@ def main(epochs, start_epoch, learning_rate, tensorboard_dir, checkpoint, num_he
                       model_params={**cfg.model_params, "num_heatmap": num_heatmap},
                       extras={**cfg.extras, "version": version})
     model_path = train(cfg, checkpoint, train_glob=train_tfrecords, val_glob=val_tfrecords, synthetic=synthetic,
-                       device=device)
+                       device=device, tensorboard_dir=tensorboard_dir)
     print("Received model " + str(model_path))
     if output_bucket is None or output_dir is None or model_path is None:
         return

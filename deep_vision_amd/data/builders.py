@@ -163,24 +163,71 @@ def build_mpii(annotation_json, image_dir, out_dir, split="train", num_shards=16
 
 
 # ------------------------------------------------------------------ ImageNet
-def imagenet_example(filepath, label, synset, human=""):
+def imagenet_example(filepath, label, synset, human="", bboxes=()):
+    """The reference's 15-feature Example (R/Datasets/ILSVRC2012/build_imagenet_tfrecord.py:
+    184-232): image geometry / colorspace, label (1..1000), synset, human text, the image's
+    bounding boxes as four parallel float lists + one label per box, format, filename, JPEG."""
     content, width, height = read_jpeg(filepath)
+    xmin = [b[0] for b in bboxes]
+    ymin = [b[1] for b in bboxes]
+    xmax = [b[2] for b in bboxes]
+    ymax = [b[3] for b in bboxes]
     return encode_example({
         "image/height": int64_feature(height), "image/width": int64_feature(width),
         "image/colorspace": bytes_feature(b"RGB"), "image/channels": int64_feature(3),
         "image/class/label": int64_feature(label), "image/class/synset": bytes_feature(synset),
-        "image/class/text": bytes_feature(human), "image/format": bytes_feature(b"JPEG"),
+        "image/class/text": bytes_feature(human),
+        "image/object/bbox/xmin": float_list_feature(xmin), "image/object/bbox/xmax": float_list_feature(xmax),
+        "image/object/bbox/ymin": float_list_feature(ymin), "image/object/bbox/ymax": float_list_feature(ymax),
+        "image/object/bbox/label": int64_list_feature([label] * len(xmin)),
+        "image/format": bytes_feature(b"JPEG"),
         "image/filename": bytes_feature(os.path.basename(filepath)), "image/encoded": bytes_feature(content),
     })
 
 
-def build_imagenet(flat_dir, synsets_file, out_dir, split="train", num_shards=1024, workers=8):
+def build_bounding_box_lookup(bbox_csv):
+    """``<file>.JPEG,xmin,ymin,xmax,ymax`` lines (process_bounding_boxes output) -> {file: [box]}
+    (build_imagenet_tfrecord.py:643-688)."""
+    out = {}
+    n = 0
+    with open(bbox_csv) as f:
+        for line in f:
+            parts = line.strip().split(",")
+            if len(parts) != 5:
+                continue
+            out.setdefault(parts[0], []).append(tuple(float(v) for v in parts[1:]))
+            n += 1
+    return out
+
+
+def build_synset_lookup(metadata_file):
+    """``nXXXXXXXX<TAB>human label`` lines (imagenet_metadata.txt) -> {synset: human}."""
+    out = {}
+    with open(metadata_file) as f:
+        for line in f:
+            parts = line.rstrip("\n").split("\t")
+            if len(parts) == 2:
+                out[parts[0]] = parts[1]
+    return out
+
+
+def build_imagenet(flat_dir, synsets_file, out_dir, split="train", num_shards=1024, workers=8, bbox_csv=None,
+                   metadata_file=None):
     """From a flattened directory (``nXXXXXXXX_*.JPEG``); labels start at 1 (TF-models convention,
-    the reader subtracts 1)."""
+    ``data.imagenet_tf.ImageNetTFRecordDataset`` subtracts 1). ``bbox_csv`` /
+    ``metadata_file`` fill the bounding-box and human-text features by file name / synset."""
     syn = [l.split()[0] for l in open(synsets_file) if l.strip()]
     idx = {s: i + 1 for i, s in enumerate(syn)}
-    items = [(os.path.join(flat_dir, f), idx[f.split("_")[0]], f.split("_")[0]) for f in sorted(os.listdir(flat_dir))
-             if f.split("_")[0] in idx]
+    boxes = build_bounding_box_lookup(bbox_csv) if bbox_csv else {}
+    human = build_synset_lookup(metadata_file) if metadata_file else {}
+    items = []
+    for f in sorted(os.listdir(flat_dir)):
+        s0 = f.split("_")[0]
+        if s0 in idx:
+            # the bbox CSV is keyed by the original file name (flattened val files carry a synset prefix)
+            key = f if f in boxes else f[len(s0) + 1:]
+            items.append((os.path.join(flat_dir, f), idx[s0], s0, human.get(s0, ""), tuple(boxes.get(key, ()))))
+    print("Found %d images with bboxes out of %d images" % (sum(1 for it in items if it[4]), len(items)))
     return write_sharded(items, imagenet_example, out_dir, split, num_shards, workers)
 
 
@@ -348,6 +395,8 @@ def main(argv=None):
     i.add_argument("--out", required=True)
     i.add_argument("--split", default="train")
     i.add_argument("--shards", type=int, default=1024)
+    i.add_argument("--bounding-box-file", default=None, help="CSV from the 'bboxes' command")
+    i.add_argument("--imagenet-metadata-file", default=None, help="synset<TAB>human label per line")
     g = sub.add_parser("cyclegan")
     g.add_argument("--dataset", required=True)
     g.add_argument("--datasets-dir", default="datasets")
@@ -386,7 +435,8 @@ def main(argv=None):
     elif a.cmd == "mpii":
         build_mpii(a.annotations, a.images, a.out, a.split, a.shards)
     elif a.cmd == "imagenet":
-        build_imagenet(a.flat_dir, a.synsets, a.out, a.split, a.shards)
+        build_imagenet(a.flat_dir, a.synsets, a.out, a.split, a.shards, bbox_csv=a.bounding_box_file,
+                       metadata_file=a.imagenet_metadata_file)
     else:
         build_cyclegan(a.datasets_dir, a.dataset, a.out)
 

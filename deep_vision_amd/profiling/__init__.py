@@ -5,8 +5,12 @@
   node aggregate comes from one packed all-reduce.
 * ``range(name)``: roctx ranges (torch.cuda.nvtx maps to roctx on ROCm) visible in rocprofv3
   ``--marker-trace`` / sys traces; a no-op on CPU.
-* ``rocprof_command``: the rocprofv3 invocation used by ``--profile`` / tools/gpu_prof.sh
-  (kernel trace + stats; counter collection in a separate run, never mixed with traces).
+* ``rocprof_command``: the rocprofv3 invocations used by ``--profile rocprof`` / tools/gpu.sh:
+  kernel trace + stats, or (a separate run per counter group) ``--pmc`` counters with nothing
+  but the counter collection -- never combined with traces.
+* ``run_under_rocprof``: ``--profile rocprof`` on any entry point re-runs the same command as a
+  child of ``rocprofv3 --kernel-trace --stats`` (the program itself directly after ``--``, no
+  shell or env hop) before anything touches the GPU, and exits with the child's status.
 """
 from __future__ import annotations
 
@@ -113,8 +117,37 @@ def node_throughput(samples_per_s: float) -> float:
 
 
 def rocprof_command(out_dir: str, argv: List[str], counters: List[str] | None = None) -> List[str]:
-    """rocprofv3 invocation: kernel trace + stats, or (separately) PMC counters with stats."""
-    cmd = ["rocprofv3", "--kernel-trace", "--stats", "-d", out_dir, "-o", "run"]
+    """rocprofv3 invocation: kernel trace + stats (per-kernel times), or -- in its own run --
+    PMC counters alone (``--pmc`` is never combined with a trace domain)."""
     if counters:
-        cmd = ["rocprofv3", "--pmc", *counters, "--kernel-trace", "--stats", "-d", out_dir, "-o", "pmc"]
-    return cmd + ["--", *argv]
+        return ["rocprofv3", "--pmc", *counters, "-d", out_dir, "-o", "pmc", "--output-format", "csv", "--", *argv]
+    return ["rocprofv3", "--kernel-trace", "--stats", "-d", out_dir, "-o", "run", "--output-format", "csv", "--",
+            *argv]
+
+
+def run_under_rocprof(argv: List[str] | None = None, out_dir: str | None = None) -> None:
+    """Re-run this program (``sys.argv`` without the ``--profile rocprof`` flag) under rocprofv3
+    kernel tracing as a child process and exit with its status. Must be called before any GPU
+    work in this process (nothing is exec'ed from a GPU-initialised process)."""
+    import os
+    import subprocess
+    import sys
+
+    args = list(sys.argv if argv is None else [sys.argv[0]] + list(argv))
+    clean, skip = [], False
+    for a in args:
+        if skip:
+            skip = False
+            if a in ("timer", "rocprof"):
+                continue
+        if a == "--profile":
+            skip = True
+            continue
+        if a.startswith("--profile="):
+            continue
+        clean.append(a)
+    out_dir = out_dir or os.environ.get("DV_ROCPROF_DIR", os.path.abspath("rocprof_out"))
+    script = os.path.abspath(clean[0])
+    cmd = rocprof_command(out_dir, [sys.executable, script] + clean[1:])
+    print("[dv-profile] " + " ".join(cmd), flush=True)
+    sys.exit(subprocess.call(cmd))

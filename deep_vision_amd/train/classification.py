@@ -16,7 +16,9 @@ collective, Inception's auxiliary heads are trained with the GoogLeNet 0.3 weigh
 from __future__ import annotations
 
 import argparse
+import glob
 import os
+import pickle
 import time
 
 import torch
@@ -26,6 +28,7 @@ from ..config import TrainConfig, get_config
 from ..data import transforms as T
 from ..data.datasets import ImageNet2012Dataset, MnistDataset, SyntheticClassification
 from ..data.loader import DevicePrefetcher, make_loader, set_epoch
+from ..utils.tensorboard import SummaryWriter
 from . import checkpoint as C
 from .engine import Engine, seed_everything
 from .schedulers import make_scheduler, plateau_metric
@@ -70,6 +73,14 @@ def build_datasets(cfg: TrainConfig, data_dir=None, synthetic=False, synthetic_s
             return (SyntheticClassification(synthetic_size, cfg.input_shape, nc, key, seed=1),
                     SyntheticClassification(max(64, synthetic_size // 4), cfg.input_shape, nc, key, seed=2))
         return mk("train"), mk("t10k")
+    if cfg.dataset == "imagenet" and not synthetic and cfg.extras.get("keras"):
+        # TF1-Keras configs read the TFRecord shards (R/ResNet/tensorflow/train.py:226-235)
+        root = data_dir or "../dataset"
+        tr, va = os.path.join(root, "tfrecord", "tfrecord_train", "*"), os.path.join(root, "tfrecord", "tfrecord_val", "*")
+        if glob.glob(tr) and glob.glob(va):
+            from ..data.imagenet_tf import ImageNetTFRecordDataset
+
+            return ImageNetTFRecordDataset(tr, True), ImageNetTFRecordDataset(va, False)
     if cfg.dataset == "imagenet" and not synthetic:
         root = data_dir or "../dataset"
         labels = os.path.join(root, "synsets.txt")
@@ -91,12 +102,16 @@ def _criterion(output, target, aux_weight):
     return F.cross_entropy(output, target), output
 
 
-def train(loader, net, optimizer, epoch, loggers, eng: Engine, cfg: TrainConfig, max_steps=None, scheduler=None):
+def train(loader, net, optimizer, epoch, loggers, eng: Engine, cfg: TrainConfig, max_steps=None, scheduler=None,
+          epoch_stats=None):
+    """``epoch_stats`` (Keras configs): a dict receiving the epoch's mean loss / top-1 / top-5 as
+    fractions (the Keras History ``loss`` / ``acc`` / ``top_5_accuracy``)."""
     net.train()
     key = _label_key(cfg)
     aux_w = cfg.extras.get("aux_weight", 0.3)
     eng.log("Start training epoch {}".format(epoch))
     acc = torch.zeros((), device=eng.device)
+    ep = torch.zeros(4, dtype=torch.float64, device=eng.device)  # loss sum, correct1, correct5, samples
     seen = 0
     for batch_i, data in enumerate(loader):
         if max_steps is not None and batch_i >= max_steps:
@@ -105,9 +120,14 @@ def train(loader, net, optimizer, epoch, loggers, eng: Engine, cfg: TrainConfig,
         target = data[key].to(eng.device, dtype=torch.long, non_blocking=True)
         with eng.timer.step(samples=image.shape[0]):
             with eng.timer.phase("fwd"):
-                loss, _ = _criterion(net(image), target, aux_w)
+                loss, main = _criterion(net(image), target, aux_w)
             lr = C.get_lr(optimizer)
             eng.backward_step(loss, net, optimizer)
+        if epoch_stats is not None:
+            a1, a5 = accuracy(main.detach(), target, topk=(1, min(5, main.shape[1])))
+            n = target.numel()
+            ep += torch.stack([loss.detach().double() * n, a1[0].double() * n / 100, a5[0].double() * n / 100,
+                               torch.tensor(float(n), dtype=torch.float64, device=eng.device)])
         acc += loss.detach().float()
         seen += 1
         if batch_i % 10 == 9:
@@ -116,7 +136,52 @@ def train(loader, net, optimizer, epoch, loggers, eng: Engine, cfg: TrainConfig,
                 C.timestamp(), epoch, batch_i + 1, avg, lr))
             C.log_metrics(loggers, "train_loss", avg, epoch)
             acc.zero_()
+    if epoch_stats is not None:
+        v = eng.reduce_sum(ep.tolist())
+        n = max(1.0, v[3])
+        epoch_stats.update(loss=v[0] / n, acc=v[1] / n, top_5_accuracy=v[2] / n)
     return seen
+
+
+def keras_model_filename(cfg: TrainConfig, model_id: str) -> str:
+    """``{name}-tf-{ts}`` (R/ResNet/tensorflow/train.py:258-260); the registry's ``_tf`` suffix is
+    not part of the reference name."""
+    name = cfg.name[:-3] if cfg.name.endswith("_tf") else cfg.name
+    return "{}-tf-{}".format(name, model_id)
+
+
+KERAS_LOGGER_KEYS = ("train_loss", "train_top1_acc", "train_top5_acc", "val_loss", "val_top1_acc", "val_top5_acc", "lr")
+
+
+def keras_epoch_end(eng: Engine, model_dir: str, model_filename: str, loggers: dict, epoch: int, train_stats: dict,
+                    val: tuple, lr: float, tb: SummaryWriter):
+    """The reference's three Keras callbacks at ``on_epoch_end``: LoggersCallback (7 series, printed
+    and pickled to ``{model_dir}{name}-tf-{ts}-loggers-epoch-{e}.pkl``, :81-144) and the
+    TensorBoard callback's epoch scalars (:268-269, step = epoch index). Accuracies are fractions
+    as in Keras; the checkpoint itself is written by the caller."""
+    val_loss, top1, top5 = val
+    vals = {"train_loss": train_stats.get("loss", float("nan")), "train_top1_acc": train_stats.get("acc", float("nan")),
+            "train_top5_acc": train_stats.get("top_5_accuracy", float("nan")), "val_loss": val_loss,
+            "val_top1_acc": top1 / 100.0, "val_top5_acc": top5 / 100.0, "lr": lr}
+    for k in KERAS_LOGGER_KEYS:
+        loggers.setdefault(k, {"epochs": [], "value": []})
+        loggers[k]["epochs"].append(epoch)
+        loggers[k]["value"].append(vals[k])
+        eng.log("Epoch: {}, {}: {}".format(epoch, k, vals[k]))
+    eng.log("Time: {}".format(C.timestamp()))
+    for tag, k in (("loss", "train_loss"), ("acc", "train_top1_acc"), ("top_5_accuracy", "train_top5_acc"),
+                   ("val_loss", "val_loss"), ("val_acc", "val_top1_acc"), ("val_top_5_accuracy", "val_top5_acc"),
+                   ("lr", "lr")):
+        tb.add_scalar(tag, vals[k], epoch - 1)
+    if eng.is_main:
+        os.makedirs(model_dir or ".", exist_ok=True)
+        path = os.path.join(model_dir, "{}-loggers-epoch-{}.pkl".format(model_filename, epoch))
+        tmp = path + ".tmp"
+        with open(tmp, "wb") as f:
+            pickle.dump({k: loggers[k] for k in KERAS_LOGGER_KEYS}, f, pickle.HIGHEST_PROTOCOL)
+        os.replace(tmp, path)
+        return path
+    return None
 
 
 def validate(loader, net, epoch, loggers, eng: Engine, cfg: TrainConfig, max_steps=None):
@@ -155,7 +220,7 @@ def validate(loader, net, epoch, loggers, eng: Engine, cfg: TrainConfig, max_ste
 
 def run_epochs(config: TrainConfig, checkpoint_path=None, *, device=None, data_dir=None, synthetic=False,
                epochs=None, max_steps=None, val_steps=None, synthetic_size=512, num_workers=None, seed=0,
-               checkpoint_dir=None, profile=False, batch_size=None):
+               checkpoint_dir=None, profile=False, batch_size=None, tensorboard_dir=None):
     eng = Engine(device=device, profile=profile)
     seed_everything(seed, eng.rank)
     eng.log("CUDA is available: {}".format(torch.cuda.is_available()))
@@ -182,22 +247,38 @@ def run_epochs(config: TrainConfig, checkpoint_path=None, *, device=None, data_d
         net, optimizer, scheduler, loggers, start_epoch = C.load_checkpoint(checkpoint_path, net, optimizer, scheduler,
                                                                             loggers)
     device_loader = DevicePrefetcher(train_loader, eng.device)
-    validate(val_loader, net, 0, loggers, eng, cfg, val_steps)
+    keras = bool(cfg.extras.get("keras"))
+    tb = None
+    if keras:  # TF1-Keras configs: hdf5-style checkpoint names, pickled loggers, TensorBoard callback
+        model_filename = keras_model_filename(cfg, model_id)
+        kloggers = {}  # the LoggersCallback's own 7 series (pickled per epoch)
+        tb = SummaryWriter(os.path.join(tensorboard_dir or "./tensorboard", model_filename), enabled=eng.is_main)
+    else:
+        validate(val_loader, net, 0, loggers, eng, cfg, val_steps)  # Keras fit() has no epoch-0 validation
     total = epochs if epochs is not None else cfg.total_epochs
     last = None
     for epoch in range(start_epoch, total + 1):
         set_epoch(train_loader, epoch)
-        train(device_loader, net, optimizer, epoch, loggers, eng, cfg, max_steps)
+        stats = {} if keras else None
+        lr_epoch = C.get_lr(optimizer)
+        train(device_loader, net, optimizer, epoch, loggers, eng, cfg, max_steps, epoch_stats=stats)
         val_loss, top1, top5 = validate(val_loader, net, epoch, loggers, eng, cfg, val_steps)
+        if keras:
+            keras_epoch_end(eng, model_dir, model_filename, kloggers, epoch, stats, (val_loss, top1, top5), lr_epoch, tb)
         if isinstance(scheduler, torch.optim.lr_scheduler.ReduceLROnPlateau):
             scheduler.step(val_loss if plateau_metric(cfg.scheduler_params) == "val_loss" else top1)
         elif scheduler is not None:
             scheduler.step()
-        path = os.path.join(model_dir, C.classifier_checkpoint_name(cfg.name, model_id, epoch))
+        if keras:
+            path = os.path.join(model_dir, "{}-checkpoint-epoch-{}.pt".format(model_filename, epoch))
+        else:
+            path = os.path.join(model_dir, C.classifier_checkpoint_name(cfg.name, model_id, epoch))
         last = C.atomic_save(C.training_state(epoch, net, optimizer, scheduler, loggers, config=cfg.name), path)
         if eng.timer.enabled:
             eng.log("[dv-profile] epoch {}: {}".format(epoch, eng.timer.summary()))
             eng.timer.reset()
+    if tb is not None:
+        tb.close()
     eng.barrier()
     eng.close()
     return last, loggers
@@ -216,13 +297,19 @@ def add_common_args(ap: argparse.ArgumentParser):
     ap.add_argument("--device", default=None, help="cuda | cpu (default: cuda when available)")
     ap.add_argument("--checkpoint-dir", default=None)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--profile", action="store_true", help="per-phase HIP-event step timing")
+    ap.add_argument("--profile", nargs="?", const="timer", default=None, choices=["timer", "rocprof"],
+                    help="timer: per-phase HIP-event step timing; rocprof: re-run this command under "
+                         "rocprofv3 --kernel-trace --stats (counters are collected in separate runs)")
+    ap.add_argument("--tensorboard-dir", default=None, help="TensorBoard root (Keras configs: ./tensorboard)")
     ap.add_argument("--nproc", type=int, default=None, help="spawn N ranks (one per GPU) via torch.distributed.run")
     return ap
 
 
 def resolve_checkpoint(arg, cfg, checkpoint_dir=None):
     if arg == "latest":
+        if cfg.extras.get("keras"):
+            base = cfg.name[:-3] if cfg.name.endswith("_tf") else cfg.name
+            return C.latest(checkpoint_dir or cfg.checkpoint_dir, f"{base}-tf-*-checkpoint-epoch-*.pt")
         return C.latest(checkpoint_dir or cfg.checkpoint_dir, f"{cfg.name}-*.pt")
     return arg
 
@@ -235,9 +322,14 @@ def main(argv=None, choices=None, default=None):
     ap.add_argument("-m", "--model", choices=choices, default=default, required=default is None)
     add_common_args(ap)
     a = ap.parse_args(argv)
+    if a.profile == "rocprof":
+        from ..profiling import run_under_rocprof
+
+        run_under_rocprof(argv)  # exits with the profiled child's status
     maybe_spawn(a.nproc)
     cfg = get_config(a.model)
     ck = resolve_checkpoint(a.checkpoint, cfg, a.checkpoint_dir)
     run_epochs(cfg, ck, device=a.device, data_dir=a.data_dir, synthetic=a.synthetic, epochs=a.epochs,
                max_steps=a.max_steps, val_steps=a.val_steps, synthetic_size=a.synthetic_size, num_workers=a.workers,
-               seed=a.seed, checkpoint_dir=a.checkpoint_dir, profile=a.profile, batch_size=a.batch_size)
+               seed=a.seed, checkpoint_dir=a.checkpoint_dir, profile=a.profile == "timer", batch_size=a.batch_size,
+               tensorboard_dir=a.tensorboard_dir)

@@ -31,6 +31,7 @@ from ..data.loader import DevicePrefetcher, make_loader, set_epoch
 from ..models.yolov3 import ANCHOR_MASKS, ANCHORS_WH
 from ..ops import detection as Det
 from ..ops import loss as L
+from ..utils.tensorboard import SummaryWriter
 from . import checkpoint as C
 from .engine import Engine, seed_everything
 from .schedulers import ManualPlateau
@@ -116,7 +117,7 @@ def _to_device(batch, device):
 
 class Trainer:
     def __init__(self, cfg: TrainConfig, eng: Engine, model, initial_epoch=1, epochs=None, log_every=10,
-                 checkpoint_dir=None):
+                 checkpoint_dir=None, tensorboard_dir=None):
         self.cfg = cfg
         self.eng = eng
         self.model = model
@@ -130,6 +131,17 @@ class Trainer:
         self.model_dir = checkpoint_dir or cfg.checkpoint_dir
         self.best_model = None
         self.nc = cfg.model_params.get("num_classes", 80)
+        # TensorBoard streams with the reference's tags and directories (rank 0 only):
+        # YOLO / CenterNet logs/gradient_tape/{ts}/{train,val} (R/YOLO/tensorflow/train.py:196-199),
+        # Hourglass one writer in ./logs (R/Hourglass/tensorflow/train.py:134-157)
+        ts = C.timestamp("%Y%m%d-%H%M%S")
+        if cfg.family == "hourglass":
+            self.tb_train = self.tb_val = SummaryWriter(tensorboard_dir or "./logs", enabled=eng.is_main)
+        else:
+            root = os.path.join(tensorboard_dir or "logs/gradient_tape", ts)
+            self.tb_train = SummaryWriter(os.path.join(root, "train"), enabled=eng.is_main)
+            self.tb_val = SummaryWriter(os.path.join(root, "val"), enabled=eng.is_main)
+        self.total_steps = 0
 
     # ---- loss of one local batch, normalised for gradient averaging across ranks ----
     def compute_loss(self, outputs, labels, local_batch):
@@ -167,9 +179,15 @@ class Trainer:
                 v = eng.reduce_sum((acc / self.log_every).tolist())
                 v = [x / eng.world for x in v]
                 msg = "Trained batch: {} batch loss: {}".format(nb, v[0])
+                step = self.total_steps + nb
+                if self.cfg.family != "hourglass":
+                    self.tb_train.add_scalar("batch train loss", v[0], step)
                 if comps is not None:
                     msg += " batch xy loss {} batch wh loss {} batch obj loss {} batch_class_loss {}".format(
                         v[1], v[2], v[4], v[3])
+                    for tag, val in (("batch xy loss", v[1]), ("batch wh loss", v[2]), ("batch obj loss", v[4]),
+                                     ("batch class loss", v[3])):
+                        self.tb_train.add_scalar(tag, val, step)
                 eng.log(msg + " epoch total loss: {}".format(eng.reduce_sum([total.item()])[0] / eng.world))
                 acc.zero_()
         return total, nb
@@ -210,26 +228,33 @@ class Trainer:
                     "Last lowest val loss is {}.".format(C.timestamp("%Y%m%d-%H%M%S"), epoch,
                                                          self.plateau.current_learning_rate,
                                                          self.plateau.patience_count, self.plateau.lowest_val_loss))
+            if self.cfg.family == "hourglass":
+                self.tb_train.add_scalar("epoch learning rate", self.plateau.current_learning_rate, epoch)
             total, nb = self.train_epoch(DevicePrefetcher(train_loader, eng.device), epoch, max_steps)
             t1 = time.time()
             train_loss = eng.reduce_sum([total.item()])[0] / eng.world / max(nb, 1)
+            self.total_steps += nb
+            self.tb_train.add_scalar("epoch train loss", train_loss, epoch)
             eng.log("{} Epoch {} train loss {}, total train batches {}, {} examples per second".format(
                 C.timestamp("%Y%m%d-%H%M%S"), epoch, train_loss, nb, nb * self.global_batch_size / (t1 - t0)))
             vt, vn = self.val_epoch(val_loader, val_steps)
             t2 = time.time()
             val_loss = vt / vn if vn else float("nan")
+            self.tb_val.add_scalar("epoch val loss", val_loss, epoch)
             eng.log("{} Epoch {} val loss {}, total val batches {}, {} examples per second".format(
                 C.timestamp("%Y%m%d-%H%M%S"), epoch, val_loss, vn, vn * self.global_batch_size / max(t2 - t1, 1e-9)))
             if self.plateau.update(val_loss):
                 self.save_model(epoch, val_loss)
         self.save_model(self.epochs, self.plateau.last_val_loss)
         eng.log("{} Finished.".format(C.timestamp("%Y%m%d-%H%M%S")))
+        self.tb_train.close()
+        self.tb_val.close()
         return self.best_model
 
 
 def train(cfg: TrainConfig, checkpoint=None, *, train_glob=None, val_glob=None, synthetic=False, synthetic_size=64,
           epochs=None, max_steps=None, val_steps=None, device=None, workers=2, log_every=10, checkpoint_dir=None,
-          seed=None, batch_size=None, profile=False):
+          seed=None, batch_size=None, profile=False, tensorboard_dir=None):
     eng = Engine(device=device, log_every=log_every, profile=profile)
     seed_everything(cfg.extras.get("seed", 0) if seed is None else seed, eng.rank)
     if batch_size:
@@ -246,7 +271,7 @@ def train(cfg: TrainConfig, checkpoint=None, *, train_glob=None, val_glob=None, 
         initial_epoch = C.epoch_from_name(checkpoint) + 1
         eng.log("Resume training from checkpoint {} and epoch {}".format(checkpoint, initial_epoch))
     net = eng.wrap(model)
-    trainer = Trainer(cfg, eng, net, initial_epoch, epochs, log_every, checkpoint_dir)
+    trainer = Trainer(cfg, eng, net, initial_epoch, epochs, log_every, checkpoint_dir, tensorboard_dir)
     best = trainer.run(train_loader, val_loader, max_steps, val_steps)
     eng.barrier()
     eng.close()
@@ -264,7 +289,8 @@ def add_args(ap):
     ap.add_argument("--log-every", type=int, default=10)
     ap.add_argument("--checkpoint-dir", default=None)
     ap.add_argument("--batch-size", type=int, default=None, help="per-replica batch")
-    ap.add_argument("--profile", action="store_true")
+    ap.add_argument("--profile", nargs="?", const="timer", default=None, choices=["timer", "rocprof"])
+    ap.add_argument("--tensorboard-dir", default=None)
     ap.add_argument("--nproc", type=int, default=None)
     return ap
 
@@ -278,9 +304,14 @@ def main(family_config: str, argv=None, tfrecords_default="./dataset/tfrecords")
     ap.add_argument("--tfrecords", default=tfrecords_default, help="directory with train* / val* TFRecord shards")
     add_args(ap)
     a = ap.parse_args(argv)
+    if a.profile == "rocprof":
+        from ..profiling import run_under_rocprof
+
+        run_under_rocprof(argv)
     maybe_spawn(a.nproc)
     cfg = get_config(family_config)
     return train(cfg, a.checkpoint, train_glob=os.path.join(a.tfrecords, "train*"),
                  val_glob=os.path.join(a.tfrecords, "val*"), synthetic=a.synthetic, synthetic_size=a.synthetic_size,
                  epochs=a.epochs, max_steps=a.max_steps, val_steps=a.val_steps, device=a.device, workers=a.workers,
-                 log_every=a.log_every, checkpoint_dir=a.checkpoint_dir, batch_size=a.batch_size, profile=a.profile)
+                 log_every=a.log_every, checkpoint_dir=a.checkpoint_dir, batch_size=a.batch_size,
+                 profile=a.profile == "timer", tensorboard_dir=a.tensorboard_dir)

@@ -29,6 +29,7 @@ from .. import models as M
 from ..config import get_config
 from ..data.loader import make_loader
 from ..ops import loss as L
+from ..utils.tensorboard import SummaryWriter
 from . import checkpoint as C
 from .engine import Engine, seed_everything
 from .schedulers import LinearDecay
@@ -196,7 +197,7 @@ class SyntheticPairs(torch.utils.data.Dataset):
 
 def train_cyclegan(dataset="horse2zebra", batch_size=4, epochs=None, synthetic=False, synthetic_size=8, size=256,
                    n_blocks=9, device=None, checkpoint_dir=None, max_steps=None, workers=0, tfrecord_dir="tfrecords",
-                   seed=0):
+                   seed=0, tensorboard_dir=None):
     cfg = get_config("cyclegan")
     ex = cfg.extras
     eng = Engine(device=device)
@@ -234,7 +235,16 @@ def train_cyclegan(dataset="horse2zebra", batch_size=4, epochs=None, synthetic=F
         eng.log("Initializing from scratch.")
     pool_b2a, pool_a2b = ImagePool(ex["pool_size"]), ImagePool(ex["pool_size"])
     lc, li = ex["lambda_cycle"], ex["lambda_identity"]
+    # tf.keras.metrics.Mean x 10 + both learning rates -> TensorBoard once per epoch
+    # (R/CycleGAN/tensorflow/train.py:267-312, logs/{dataset}/{ts}/train); the means accumulate on
+    # the device (no per-step host sync)
+    tb = SummaryWriter(os.path.join(tensorboard_dir or "logs", dataset, C.timestamp("%Y%m%d-%H%M%S"), "train"),
+                       enabled=eng.is_main)
+    metric_names = ("loss_gen_a2b", "loss_gen_b2a", "loss_dis_b", "loss_dis_a", "loss_id_a2b", "loss_id_b2a",
+                    "loss_gen_total", "loss_dis_total", "loss_cycle_a2b2a", "loss_cycle_b2a2b")
     for epoch in range(start_epoch, total_epochs + 1):
+        msum = torch.zeros(len(metric_names), dtype=torch.float64, device=eng.device)
+        mcount = 0
         start = time.time()
         eng.log("Epoch {} starts. Learning rate: {}, {}".format(epoch, gen_lr.current_learning_rate,
                                                                 dis_lr.current_learning_rate))
@@ -271,12 +281,22 @@ def train_cyclegan(dataset="horse2zebra", batch_size=4, epochs=None, synthetic=F
             l_dis = l_dis_a + l_dis_b
             eng.backward_step(l_dis, diss, opt_dis)
             dis_lr.step()
+            cur = dict(loss_gen_a2b=l_gen_a2b, loss_gen_b2a=l_gen_b2a, loss_dis_b=l_dis_b, loss_dis_a=l_dis_a,
+                       loss_id_a2b=l_id_a2b, loss_id_b2a=l_id_b2a, loss_gen_total=l_gen, loss_dis_total=l_dis,
+                       loss_cycle_a2b2a=l_cyc_a, loss_cycle_b2a2b=l_cyc_b)
+            msum += torch.stack([cur[k].detach().double() for k in metric_names])
+            mcount += 1
             if step % 10 == 0:
                 vals = dict(loss_gen_a2b=l_gen_a2b, loss_gen_b2a=l_gen_b2a, loss_id_a2b=l_id_a2b, loss_id_b2a=l_id_b2a,
                             loss_cycle_a2b2a=l_cyc_a, loss_cycle_b2a2b=l_cyc_b, loss_gen_total=l_gen,
                             loss_dis_b=l_dis_b, loss_dis_a=l_dis_a, loss_dis_total=l_dis)
                 eng.log("Epoch {} Step {} ".format(epoch, step),
                         " ".join("{}:{} ".format(k, float(v.detach())) for k, v in vals.items()))
+        means = eng.reduce_sum((msum / max(1, mcount)).tolist())
+        for k, v in zip(metric_names, means):
+            tb.add_scalar(k, v / eng.world, epoch)
+        tb.add_scalar("gen_learning_rate", gen_lr.current_learning_rate, epoch)
+        tb.add_scalar("dis_learning_rate", dis_lr.current_learning_rate, epoch)
         if epoch % ex["save_every"] == 0:
             st = {"generator_a2b": C.strip_module_prefix(g_a2b.state_dict()),
                   "generator_b2a": C.strip_module_prefix(g_b2a.state_dict()),
@@ -288,6 +308,7 @@ def train_cyclegan(dataset="horse2zebra", batch_size=4, epochs=None, synthetic=F
             eng.log("Saved checkpoint for epoch {}: {}".format(epoch, path))
         eng.log("Time for epoch {} is {} sec".format(epoch, time.time() - start))
     eng.log("Finished training.")
+    tb.close()
     eng.close()
     return mgr.latest_checkpoint
 
@@ -303,6 +324,8 @@ def cyclegan_main(argv=None):
     ap.add_argument("--device", default=None)
     ap.add_argument("--checkpoint-dir", default=None)
     ap.add_argument("--tfrecord-dir", default="tfrecords")
+    ap.add_argument("--tensorboard-dir", default=None, help="TensorBoard root (default ./logs)")
     a = ap.parse_args(argv)
     return train_cyclegan(a.dataset, int(a.batch_size), a.epochs, a.synthetic, size=a.size, device=a.device,
-                          checkpoint_dir=a.checkpoint_dir, max_steps=a.max_steps, tfrecord_dir=a.tfrecord_dir)
+                          checkpoint_dir=a.checkpoint_dir, max_steps=a.max_steps, tfrecord_dir=a.tfrecord_dir,
+                          tensorboard_dir=a.tensorboard_dir)

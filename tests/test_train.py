@@ -1,6 +1,7 @@
 """CPU tests of the orchestration layer: config registry (Appendix C), checkpoints (Appendix B),
 schedulers, fault handling, trainer smoke runs of every family, entry-point CLIs."""
 import math
+import glob
 import os
 import subprocess
 import sys
@@ -148,8 +149,19 @@ def test_family_trainers_smoke(tmp_path, name, size, extra):
     cfg = get_config(name, input_shape=(3, size, size), batch_size=2)
     cfg = cfg.replace(model_params={**cfg.model_params, **extra})
     best = train(cfg, synthetic=True, synthetic_size=4, epochs=1, device="cpu", workers=0, log_every=1,
-                 checkpoint_dir=str(tmp_path))
+                 checkpoint_dir=str(tmp_path), tensorboard_dir=str(tmp_path / "tb"))
     assert best and os.path.basename(best).startswith("model-v") and C.epoch_from_name(best) == 1
+    # TensorBoard streams with the reference tags (YOLO/CenterNet: train + val writers)
+    from deep_vision_amd.utils.tensorboard import read_scalars
+
+    tags = {}
+    for f in glob.glob(str(tmp_path / "tb" / "**" / "events.out.tfevents.*"), recursive=True):
+        tags.update(read_scalars(f))
+    assert {"epoch train loss", "epoch val loss"} <= set(tags)
+    if name == "yolov3":
+        assert {"batch train loss", "batch xy loss", "batch class loss"} <= set(tags)
+    if name == "hourglass":
+        assert "epoch learning rate" in tags
 
 
 def test_gan_trainers_smoke(tmp_path):
@@ -158,7 +170,13 @@ def test_gan_trainers_smoke(tmp_path):
     assert train_dcgan(epochs=2, batch_size=8, synthetic=True, synthetic_size=16, device="cpu",
                        checkpoint_dir=str(tmp_path / "dc"), max_steps=2).endswith("ckpt-1.pt")
     assert train_cyclegan("toy", 1, 2, True, synthetic_size=1, size=32, n_blocks=1, device="cpu",
-                          checkpoint_dir=str(tmp_path / "cg-{dataset}")).endswith("ckpt-1.pt")
+                          checkpoint_dir=str(tmp_path / "cg-{dataset}"),
+                          tensorboard_dir=str(tmp_path / "tb")).endswith("ckpt-1.pt")
+    from deep_vision_amd.utils.tensorboard import read_scalars
+
+    ev = glob.glob(str(tmp_path / "tb" / "toy" / "*" / "train" / "events.out.tfevents.*"))
+    sc = read_scalars(ev[0])
+    assert len(sc) == 12 and [s for s, _, _ in sc["loss_gen_total"]] == [1, 2]
     pool = ImagePool(2)
     a = torch.randn(3, 1, 2, 2)
     out = pool.query(a)
