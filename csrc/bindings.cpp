@@ -43,10 +43,11 @@ PYBIND11_MODULE(_C, m) {
                        int Kout, int P_, int Q, int R, int S, int sh, int sw, int ph, int pw, int dh, int dw, int tgather,
                        int OH, int OW, int osh, int osw, int oph, int opw, int ldy, int act, float slope, uptr res,
                        uptr st, uptr bnx, uptr bnbits, uptr bnprm, uptr bnacc, int bnmode, int bnact, float bnslope,
-                       uptr resbits, int resact, float resslope) {
+                       uptr resbits, int resact, float resslope, int reflect) {
     ConvFwdArgs a{CP(x), CP(w), P(y), CFP(bias), FP(stats), Nb, H, W, Cg, ldx, G, Kout, P_, Q, R, S, sh, sw, ph, pw,
                   dh, dw, tgather, OH, OW, osh, osw, oph, opw, ldy, act, slope, CP(res),
-                  CP(bnx), CP(bnbits), CFP(bnprm), FP(bnacc), bnmode, bnact, bnslope, CP(resbits), resact, resslope};
+                  CP(bnx), CP(bnbits), CFP(bnprm), FP(bnacc), bnmode, bnact, bnslope, CP(resbits), resact, resslope,
+                  reflect};
     int r = dv_conv_fwd(a, ST(st));
     if (r < 0) throw std::runtime_error("conv_fwd: unsupported geometry (channels must be a multiple of 8)");
     check_last("conv_fwd");
@@ -57,7 +58,8 @@ PYBIND11_MODULE(_C, m) {
      py::arg("tgather"), py::arg("OH"), py::arg("OW"), py::arg("osh"), py::arg("osw"), py::arg("oph"), py::arg("opw"),
      py::arg("ldy"), py::arg("act"), py::arg("slope"), py::arg("res"), py::arg("st"), py::arg("bnx") = 0,
      py::arg("bnbits") = 0, py::arg("bnprm") = 0, py::arg("bnacc") = 0, py::arg("bnmode") = 0, py::arg("bnact") = 0,
-     py::arg("bnslope") = 0.f, py::arg("resbits") = 0, py::arg("resact") = 0, py::arg("resslope") = 0.f);
+     py::arg("bnslope") = 0.f, py::arg("resbits") = 0, py::arg("resact") = 0, py::arg("resslope") = 0.f,
+     py::arg("reflect") = 0);
   m.def("conv_fwd_variant", [](int v) { dv_conv_fwd_variant(v); });
   m.def("bn_tuning", [](int blocks, int unroll) { dv_bn_tuning(blocks, unroll); });
   m.def("dw_variant", [](int v) { dv_dw_variant(v); });
@@ -68,14 +70,17 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_wgrad_tuning", [](int v, int split_pct) { dv_conv_wgrad_tuning(v, split_pct); });
   m.def("conv_wgrad", [](uptr x, uptr dy, uptr dw, int Nb, int H, int W, int Cg, int ldx, int G, int Kout, int P_, int Q,
                          int ldy, int R, int S, int sh, int sw, int ph, int pw, int dh, int dwl, int splits, int accumulate,
-                         int oirs_ig, uptr st) {
+                         int oirs_ig, uptr st, int reflect) {
     ConvWgradArgs a{CP(x), CP(dy), FP(dw), Nb, H, W, Cg, ldx, G, Kout, P_, Q, ldy, R, S, sh, sw, ph, pw, dh, dwl, splits,
-                    accumulate, oirs_ig};
+                    accumulate, oirs_ig, reflect};
     int r = dv_conv_wgrad(a, ST(st));
     if (r < 0) throw std::runtime_error("conv_wgrad: unsupported geometry (channels must be a multiple of 8)");
     check_last("conv_wgrad");
     return r;
-  });
+  }, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("Nb"), py::arg("H"), py::arg("W"), py::arg("Cg"), py::arg("ldx"),
+     py::arg("G"), py::arg("Kout"), py::arg("P"), py::arg("Q"), py::arg("ldy"), py::arg("R"), py::arg("S"), py::arg("sh"),
+     py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw_"), py::arg("splits"), py::arg("accumulate"),
+     py::arg("oirs_ig"), py::arg("st"), py::arg("reflect") = 0);
 
   m.def("bn_stats", [](uptr x, int64_t rows, int C, uptr acc, uptr st) { dv_bn_stats(CP(x), rows, C, FP(acc), ST(st)); check_last("bn_stats"); });
   m.def("bn_finalize", [](uptr acc, int C, double count, float eps, float mom, uptr gamma, uptr beta, uptr rm, uptr rv,
@@ -139,8 +144,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("add", [](uptr a, uptr b, uptr y, int64_t n, float alpha, float beta, int act, float slope, uptr st) { dv_add(CP(a), CP(b), P(y), n, alpha, beta, act, slope, ST(st)); check_last("add"); });
   m.def("dropout", [](uptr x, uptr y, int64_t n, float p, uint64_t seed, uptr st) { dv_dropout(CP(x), P(y), n, p, seed, ST(st)); check_last("dropout"); });
   m.def("wprep", [](uptr w, uptr out, int G, int Og, int Ig, int R, int S, int Ipad, int mode, int Sp, uptr st) { dv_wprep(CFP(w), P(out), G, Og, Ig, R, S, Ipad, mode, Sp, ST(st)); check_last("wprep"); });
-  m.def("stem_pack", [](uptr x, int is_f32, uptr y, int N, int C, int H, int W, int Hp, int Wp, int pt, int pl, uptr st) {
-    dv_stem_pack(CP(x), is_f32, P(y), N, C, H, W, Hp, Wp, pt, pl, ST(st)); check_last("stem_pack"); });
+  m.def("stem_pack", [](uptr x, int is_f32, uptr y, int N, int C, int H, int W, int Hp, int Wp, int pt, int pl, uptr st,
+                        int reflect) {
+    dv_stem_pack(CP(x), is_f32, P(y), N, C, H, W, Hp, Wp, pt, pl, reflect, ST(st)); check_last("stem_pack");
+  }, py::arg("x"), py::arg("is_f32"), py::arg("y"), py::arg("N"), py::arg("C"), py::arg("H"), py::arg("W"),
+     py::arg("Hp"), py::arg("Wp"), py::arg("pt"), py::arg("pl"), py::arg("st"), py::arg("reflect") = 0);
+  m.def("reflect_pad_bwd", [](uptr dxp, uptr dx, int N, int H, int W, int C, int ldp, int ld, int ph, int pw, uptr st) {
+    dv_reflect_pad_bwd(CP(dxp), P(dx), N, H, W, C, ldp, ld, ph, pw, ST(st)); check_last("reflect_pad_bwd");
+  });
   m.def("wgrad_unprep", [](uptr src, uptr dst, int G, int Og, int Ig, int R, int S, int Ipad, float alpha, int accumulate,
                            int zero_src, uptr st) {
     dv_wgrad_unprep(FP(src), FP(dst), G, Og, Ig, R, S, Ipad, alpha, accumulate, zero_src, ST(st)); check_last("wgrad_unprep");

@@ -58,7 +58,14 @@ struct FwdParams {
   int bnmode, bnact; float bnslope;
   const uint8_t* resbits;  // RES only: res is masked by act'() bits before the add
   int resact; float resslope;
+  int reflect;             // generic loader: reflected instead of zero-filled out-of-image taps
 };
+
+// ReflectionPad2d index map (pad < n): -1 -> 1, n -> n - 2
+DV_DEVICE int reflect_idx(int i, int n) {
+  i = i < 0 ? -i : i;
+  return i >= n ? 2 * n - 2 - i : i;
+}
 
 // act'(z)*g for one element of a masked residual gradient (bit set: z > 0)
 DV_DEVICE float masked_res(float g, uint32_t mb, int e, int act, float slope) {
@@ -217,6 +224,7 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
           h = hn / p.sh; w = wn / p.sw;
         } else {
           h = hb[j] + r * p.dh; w = wb[j] + s * p.dw;
+          if (p.reflect) { h = reflect_idx(h, p.Hin); w = reflect_idx(w, p.Win); }
         }
         ok = ok && h >= 0 && h < p.Hin && w >= 0 && w < p.Win;
         const void* src = zero;
@@ -606,6 +614,8 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
   p.bnx = (const u16*)a.bnx; p.bnbits = (const uint8_t*)a.bnbits; p.bnprm = a.bnprm; p.bnacc = a.bnacc;
   p.bnmode = a.bnmode; p.bnact = a.bnact; p.bnslope = a.bnslope;
   p.resbits = (const uint8_t*)a.resbits; p.resact = a.resact; p.resslope = a.resslope;
+  p.reflect = a.reflect;
+  if (p.reflect && (a.tgather || p.ph >= p.Hin || p.pw >= p.Win || p.ph < 0 || p.pw < 0 || p.bnmode)) return -1;
   // the mask bits are indexed by the dense element offset of y: a single-group tensor whose
   // pixel stride is its channel count, written by the identity-mapped (stride-1) epilogue
   if (p.resbits && (!p.res || (p.N & 7) || p.ldy != p.N || p.G != 1 || a.tgather ||
@@ -640,7 +650,7 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
   if (p.Cg % 8 != 0 || p.ldx % 8 != 0) return -1;
   // the fast loader needs every K-tile inside one filter tap: Cg % 64 == 0 covers both BKs
   if (a.tgather) dispatch_tile<KM_TGATHER>(p, st);
-  else if (p.Cg % 64 == 0 && p.R <= 16 && p.S <= 16) dispatch_tile<KM_FAST>(p, st);
+  else if (p.Cg % 64 == 0 && p.R <= 16 && p.S <= 16 && !p.reflect) dispatch_tile<KM_FAST>(p, st);
   else dispatch_tile<KM_GENERIC>(p, st);
   return bn_status;
 }

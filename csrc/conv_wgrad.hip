@@ -37,6 +37,7 @@ struct WgParams {
   int splits, ktiles_per_split, atomic_out, accumulate;
   int oirs_ig;  // > 0: write dW straight into the parameter layout [G*M][oirs_ig][R][S]
   int64_t slab;  // > 0: deterministic mode, split s writes its partial tile at dw + s * slab
+  int reflect;   // reflected (ReflectionPad2d) instead of zero-filled out-of-image taps
   FastDiv div_pq, div_q, div_cg, div_s;
 };
 
@@ -154,8 +155,12 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgParams p) {
       if (PLAIN) {
         if (nok[j] && k0 + row < p.K) src = nrow[j] + (int64_t)k0 * p.ldx;
       } else {
-        const int h = w_p[j] * p.sh - p.ph + n_r[j] * p.dh;
-        const int w = w_q[j] * p.sw - p.pw + n_s[j] * p.dw_;
+        int h = w_p[j] * p.sh - p.ph + n_r[j] * p.dh;
+        int w = w_q[j] * p.sw - p.pw + n_s[j] * p.dw_;
+        if (p.reflect) {
+          h = h < 0 ? -h : (h >= p.Hin ? 2 * p.Hin - 2 - h : h);
+          w = w < 0 ? -w : (w >= p.Win ? 2 * p.Win - 2 - w : w);
+        }
         if (nok[j] && k0 + row < p.K && (unsigned)h < (unsigned)p.Hin && (unsigned)w < (unsigned)p.Win)
           src = p.x + (((int64_t)w_img[j] * p.Hin + h) * p.Win + w) * p.ldx + goff_x + n_c[j];
       }
@@ -400,6 +405,8 @@ int dv_conv_wgrad(const ConvWgradArgs& a, hipStream_t st) {
   p.accumulate = a.accumulate;
   p.oirs_ig = a.oirs_ig;
   p.slab = 0;
+  p.reflect = a.reflect;
+  if (p.reflect && (p.ph >= p.Hin || p.pw >= p.Win || p.ph < 0 || p.pw < 0)) return -1;
   if (p.oirs_ig > p.Cg) return -1;
   const size_t out_elems = (size_t)p.G * p.M * (p.oirs_ig > 0 ? (size_t)p.oirs_ig * p.R * p.S : (size_t)p.N);
   const bool det = g_deterministic && p.splits > 1;
@@ -418,7 +425,7 @@ int dv_conv_wgrad(const ConvWgradArgs& a, hipStream_t st) {
   }
   // plain rows: the im2col of a 1x1 / stride-1 / pad-0 conv is X itself (pixel grid == input grid)
   const bool plain = a.R == 1 && a.S == 1 && a.sh == 1 && a.sw == 1 && a.ph == 0 && a.pw == 0 && a.P == a.H &&
-                     a.Q == a.W;
+                     a.Q == a.W && !a.reflect;
   const int bn = cdiv(p.M, 64) * cdiv(p.N, 256) * p.G * p.splits;
   const int bw = cdiv(p.M, 128) * cdiv(p.N, 128) * p.G * p.splits;
   if (plain) dispatch_wg<true>(p, bn, bw, st);

@@ -237,7 +237,7 @@ __global__ void to_nhwc_kernel(const T* __restrict__ x, u16* __restrict__ y, int
 // are two horizontally adjacent pixels = two filter taps of one row. One thread per pixel.
 template <typename T>
 __global__ void stem_pack_kernel(const T* __restrict__ x, u16* __restrict__ y, int N, int C, int H, int W, int Hp,
-                                 int Wp, int pt, int pl) {
+                                 int Wp, int pt, int pl, int reflect) {
   const int64_t total = (int64_t)N * Hp * Wp;
   const int64_t HW = (int64_t)H * W;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
@@ -245,7 +245,14 @@ __global__ void stem_pack_kernel(const T* __restrict__ x, u16* __restrict__ y, i
     const int64_t nh = t / Wp;
     const int hp = (int)(nh % Hp);
     const int64_t n = nh / Hp;
-    const int h = hp - pt, w = wp - pl;
+    int h = hp - pt, w = wp - pl;
+    if (reflect) {  // ReflectionPad2d; positions past the reflected border (tap-packing slack,
+                    // multiplied by zero weights) are clamped so they stay finite
+      h = h < 0 ? -h : (h >= H ? 2 * H - 2 - h : h);
+      w = w < 0 ? -w : (w >= W ? 2 * W - 2 - w : w);
+      h = h < 0 ? 0 : (h >= H ? H - 1 : h);
+      w = w < 0 ? 0 : (w >= W ? W - 1 : w);
+    }
     float v[4] = {0.f, 0.f, 0.f, 0.f};
     if (h >= 0 && h < H && w >= 0 && w < W) {
       const int64_t src = n * C * HW + (int64_t)h * W + w;
@@ -258,6 +265,38 @@ __global__ void stem_pack_kernel(const T* __restrict__ x, u16* __restrict__ y, i
     uint2 r;
     r.x = pack2bf(v[0], v[1]); r.y = pack2bf(v[2], v[3]);
     *reinterpret_cast<uint2*>(y + t * 4) = r;
+  }
+}
+
+// reflection-pad backward (NHWC bf16, 8 channels per thread): gather the interior position and
+// the mirrored border positions that reflect onto (h, w); fp32 sum, one bf16 store
+__global__ void reflect_pad_bwd_kernel(const u16* __restrict__ dxp, u16* __restrict__ dx, int N, int H, int W, int C,
+                                       int ldp, int ld, int ph, int pw) {
+  const int Hp = H + 2 * ph, Wp = W + 2 * pw, cg = C / 8;
+  const int64_t total = (int64_t)N * H * W * cg;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(t % cg) * 8;
+    int64_t r = t / cg;
+    const int w = (int)(r % W); r /= W;
+    const int h = (int)(r % H);
+    const int64_t n = r / H;
+    int hs[2], ws[2], nh = 1, nw = 1;
+    hs[0] = h + ph; ws[0] = w + pw;
+    if (h >= 1 && h <= ph) hs[nh++] = ph - h;                     // top border reflects onto h
+    else if (h >= H - 1 - ph && h <= H - 2) hs[nh++] = 2 * (H - 1) - h + ph;  // bottom border
+    if (w >= 1 && w <= pw) ws[nw++] = pw - w;
+    else if (w >= W - 1 - pw && w <= W - 2) ws[nw++] = 2 * (W - 1) - w + pw;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < nh; ++i)
+      for (int j = 0; j < nw; ++j) {
+        const uint4 v = *reinterpret_cast<const uint4*>(dxp + ((n * Hp + hs[i]) * (int64_t)Wp + ws[j]) * ldp + c);
+        const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { acc[2 * e] += bf2f((u16)(u[e] & 0xffff)); acc[2 * e + 1] += bf2f((u16)(u[e] >> 16)); }
+      }
+    uint4 o;
+    o.x = pack2bf(acc[0], acc[1]); o.y = pack2bf(acc[2], acc[3]); o.z = pack2bf(acc[4], acc[5]); o.w = pack2bf(acc[6], acc[7]);
+    *reinterpret_cast<uint4*>(dx + ((n * H + h) * (int64_t)W + w) * ld + c) = o;
   }
 }
 
@@ -291,10 +330,15 @@ void dv_wprep(const float* w, void* out, int G, int Og, int Ig, int R, int S, in
   wprep_kernel<<<grid_for(total), NT, 0, st>>>(w, (u16*)out, G, Og, Ig, R, S, pad, mode, Sp);
 }
 void dv_stem_pack(const void* x, int x_is_f32, void* y, int N, int C, int H, int W, int Hp, int Wp, int pt, int pl,
-                  hipStream_t st) {
+                  int reflect, hipStream_t st) {
   const int64_t total = (int64_t)N * Hp * Wp;
-  if (x_is_f32) stem_pack_kernel<float><<<grid_for(total), NT, 0, st>>>((const float*)x, (u16*)y, N, C, H, W, Hp, Wp, pt, pl);
-  else stem_pack_kernel<u16><<<grid_for(total), NT, 0, st>>>((const u16*)x, (u16*)y, N, C, H, W, Hp, Wp, pt, pl);
+  if (x_is_f32) stem_pack_kernel<float><<<grid_for(total), NT, 0, st>>>((const float*)x, (u16*)y, N, C, H, W, Hp, Wp, pt, pl, reflect);
+  else stem_pack_kernel<u16><<<grid_for(total), NT, 0, st>>>((const u16*)x, (u16*)y, N, C, H, W, Hp, Wp, pt, pl, reflect);
+}
+void dv_reflect_pad_bwd(const void* dxp, void* dx, int N, int H, int W, int C, int ldp, int ld, int ph, int pw,
+                        hipStream_t st) {
+  const int64_t total = (int64_t)N * H * W * (C / 8);
+  reflect_pad_bwd_kernel<<<grid_for(total), NT, 0, st>>>((const u16*)dxp, (u16*)dx, N, H, W, C, ldp, ld, ph, pw);
 }
 void dv_wprep_batched(const void* descs, const void* chunks, int nchunks, hipStream_t st) {
   if (nchunks > 0)

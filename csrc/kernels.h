@@ -32,6 +32,9 @@ struct ConvFwdArgs {
   // and the mask turns it into that block's shortcut gradient (no materialised dres tensor)
   const void* resbits;
   int resact; float resslope;
+  // 1: out-of-image taps read the reflected pixel (ReflectionPad2d fused into the gather;
+  // CycleGAN R/CycleGAN/tensorflow/models.py:8-14) instead of zeros
+  int reflect;
 };
 
 struct ConvWgradArgs {
@@ -44,6 +47,7 @@ struct ConvWgradArgs {
   int splits;      // 0 = heuristic
   int accumulate;  // add into dw (live gradient buffer) instead of overwriting
   int oirs_ig;     // > 0: dw is the parameter's own [G*Kout][oirs_ig][R][S] layout (padded channels dropped)
+  int reflect;     // im2col with reflected out-of-image taps (see ConvFwdArgs)
 };
 
 int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st);  // 0 ok, 1 ok but BN statistics not fused, -1 unsupported
@@ -104,8 +108,12 @@ void dv_act_bwd(const void* dy, const void* y, void* dx, int64_t n, int act, flo
 void dv_add(const void* a, const void* b, void* y, int64_t n, float alpha, float beta, int act, float slope, hipStream_t st);
 void dv_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, hipStream_t st);
 void dv_wprep(const float* w, void* out, int G, int Og, int Ig, int R, int S, int Ipad, int mode, int Sp, hipStream_t st);
+// reflection-pad backward: dx[h][w] = sum of the padded gradient at every padded position that
+// reflects onto (h, w) (the interior one plus up to three mirrored border positions)
+void dv_reflect_pad_bwd(const void* dxp, void* dx, int N, int H, int W, int C, int ldp, int ld, int ph, int pw,
+                        hipStream_t st);
 void dv_stem_pack(const void* x, int x_is_f32, void* y, int N, int C, int H, int W, int Hp, int Wp, int pt, int pl,
-                  hipStream_t st);
+                  int reflect, hipStream_t st);
 void dv_wgrad_unprep(float* src, float* dst, int G, int Og, int Ig, int R, int S, int Ipad, float alpha,
                      int accumulate, int zero_src, hipStream_t st);
 void dv_to_nhwc(const void* x, int x_is_f32, void* y, int N, int C, int H, int W, int Cp, hipStream_t st);

@@ -75,6 +75,12 @@ class DCGANDiscriminator(tnn.Module):
 
 
 # ---------------------------------------- CycleGAN ----------------------------------------
+def _rpad(pad_module):
+    """(top, left) of a symmetric nn.ReflectionPad2d (padding = (left, right, top, bottom))."""
+    l, r, t, b = pad_module.padding
+    assert l == r and t == b, "asymmetric reflection padding"
+    return (t, l)
+
 class ResNetBlock(tnn.Module):
     """reflect-pad 1 -> conv3x3 -> BN -> ReLU -> reflect-pad 1 -> conv3x3 -> BN, + input (models.py:17-38)."""
 
@@ -87,8 +93,10 @@ class ResNetBlock(tnn.Module):
         self.bn2 = _bn(dim)
 
     def forward(self, x):
-        y = F.conv_bn_act(self.pad(x), self.conv1, self.bn1, "relu")
-        return F.conv_bn_act(self.pad(y), self.conv2, self.bn2, None, residual=x)
+        # ReflectionPad2d(1) is fused into each conv's im2col gather (mirrored taps, no padded copy)
+        p = _rpad(self.pad)
+        y = F.conv_bn_act(x, self.conv1, self.bn1, "relu", reflect_pad=p)
+        return F.conv_bn_act(y, self.conv2, self.bn2, None, residual=x, reflect_pad=p)
 
 
 class CycleGANGenerator(tnn.Module):
@@ -110,13 +118,13 @@ class CycleGANGenerator(tnn.Module):
         self.conv_out = nn.Conv2d(64, channels, 7)
 
     def forward(self, x):
-        x = F.conv_bn_act(self.pad_in(x), self.conv_in, self.bn_in, "relu")
+        x = F.conv_bn_act(x, self.conv_in, self.bn_in, "relu", reflect_pad=_rpad(self.pad_in))
         x = F.conv_bn_act(x, self.down1, self.bn_d1, "relu")
         x = F.conv_bn_act(x, self.down2, self.bn_d2, "relu")
         x = self.blocks(x)
         x = F.batch_norm_act(self.up1(x), self.bn_u1, "relu")
         x = F.batch_norm_act(self.up2(x), self.bn_u2, "relu")
-        x = self.conv_out(self.pad_out(x))
+        x = F.conv2d(x, self.conv_out.weight, self.conv_out.bias, 1, _rpad(self.pad_out), pad_mode="reflect")
         return F.activation(x, "tanh")
 
 

@@ -329,7 +329,7 @@ def conv_bn_deferred(x, conv, bn, join=None, join_role=None):
 
 
 def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None, join=None, join_role=None, residual_join=None,
-                residual_bn=None):
+                residual_bn=None, reflect_pad=None):
     """Fused conv -> BN (batch stats from the conv epilogue) -> (+residual) -> activation.
 
     ``join`` / ``join_role`` ('consumer' | 'producer') and ``residual_join``: a conv.GradJoin
@@ -340,14 +340,20 @@ def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None, join=None, join
     if not native(x):
         if residual_bn is not None:
             residual = _torch_bn_act(residual, residual_bn[0], None, 0.0, None)
+        if reflect_pad is not None:
+            p = (reflect_pad, reflect_pad) if isinstance(reflect_pad, int) else tuple(reflect_pad)
+            x = TF.pad(x, (p[1], p[1], p[0], p[0]), mode="reflect")
         return _torch_bn_act(conv(x), bn, act, slope, residual)
     # BN kernels need dense channels: a channel count that is not a multiple of 8 comes back as a
     # padded view, which is compacted below and gets its statistics from a separate pass
     want = (bn.training or not bn.track_running_stats) and conv.out_channels % 8 == 0
     sbuf = workspace(bn, "bn_fwd", (STAT_SHARDS, 2, conv.out_channels), x.device) if want else None
     pad = conv.native_padding(x.shape[2], x.shape[3]) if hasattr(conv, "native_padding") else conv.padding
+    mode = "zeros"
+    if reflect_pad is not None:  # ReflectionPad2d in front of a pad-0 conv: fused into the gather
+        pad, mode = reflect_pad, "reflect"
     r = conv2d(x, conv.weight, conv.bias, conv.stride, pad, conv.dilation, conv.groups, want_stats=want,
-               stats_buf=sbuf, join=join, join_role=join_role)
+               stats_buf=sbuf, join=join, join_role=join_role, pad_mode=mode)
     y, stats = r if want else (r, None)
     if y.shape[1] % 8 != 0:  # padded view: BN kernels require dense channels
         y = y.contiguous(memory_format=torch.channels_last)

@@ -86,7 +86,7 @@ def _channel_sum(dy: torch.Tensor) -> torch.Tensor:
 
 
 def conv_fwd_raw(x, wk, y, bias, stats, N, H, W, Cg, ldx, G, Kout, P, Q, R, S, stride, padding, dilation,
-                 act=0, slope=0.0, tgather=0, omap=None, ldy=None, res=None, bnref=None, resmask=None):
+                 act=0, slope=0.0, tgather=0, omap=None, ldy=None, res=None, bnref=None, resmask=None, reflect=False):
     """Launch the implicit-GEMM kernel. ``bnref`` (ops.bn.BNRef): also reduce that BatchNorm's
     backward statistics over ``y`` in the epilogue; returns True when that was done.
     ``resmask`` (bits, act, slope): ``res`` is a raw gradient masked by act'() before the add."""
@@ -100,6 +100,8 @@ def conv_fwd_raw(x, wk, y, bias, stats, N, H, W, Cg, ldx, G, Kout, P, Q, R, S, s
                   bnmode=bnref.mode, bnact=bnref.act, bnslope=float(bnref.slope))
     if resmask is not None:
         bn.update(resbits=ptr(resmask[0]), resact=int(resmask[1]), resslope=float(resmask[2]))
+    if reflect:
+        bn["reflect"] = 1
     r = lib().conv_fwd(ptr(x), ptr(wk), ptr(y), ptr(bias), ptr(stats), N, H, W, Cg, ldx, G, Kout, P, Q, R, S, sh, sw,
                        ph, pw, dh, dw, tgather, OH, OW, osh, osw, oph, opw, ldy if ldy is not None else ld_of(y), act,
                        float(slope), ptr(res), stream_handle(), **bn)
@@ -192,6 +194,17 @@ class MaskedGrad:
     __radd__ = __add__
 
 
+def _reflect_dgrad(dy, weight, x, Cg_x, G, stride, padding, dilation):
+    """dX of a reflection-padded conv: the dgrad over the padded grid (a pad-0 conv of the padded
+    input), then the border folded back onto the pixels it mirrors (csrc reflect_pad_bwd)."""
+    N, _, H, W = x.shape
+    ph, pw = padding
+    dxp = _dgrad(dy, weight, (N, x.shape[1], H + 2 * ph, W + 2 * pw), Cg_x, G, stride, (0, 0), dilation, x.device)
+    dx = empty_layout(x) if ld_of(x) == G * Cg_x else alloc_cl((N, G * Cg_x, H, W), device=x.device)
+    lib().reflect_pad_bwd(ptr(dxp), ptr(dx), N, H, W, G * Cg_x, ld_of(dxp), ld_of(dx), ph, pw, stream_handle())
+    return dx
+
+
 class GradJoin:
     """Meeting point of two gradients of one tensor (a block input used by a conv and by a
     residual add / projection conv). Whichever backward runs first stashes or announces itself;
@@ -222,8 +235,9 @@ class GradJoin:
         return g
 
 
-def _wgrad(x, dy, weight, Cg_x, G, stride, padding, dilation, out=None):
-    """Weight gradient (OIHW fp32). With ``out`` the result is ADDED into ``out`` (live grad)."""
+def _wgrad(x, dy, weight, Cg_x, G, stride, padding, dilation, out=None, reflect=False):
+    """Weight gradient (OIHW fp32). With ``out`` the result is ADDED into ``out`` (live grad).
+    ``reflect``: the forward padded by reflection (im2col taps outside the image are mirrored)."""
     N, _, H, W = x.shape
     O, Ig, R, S = weight.shape
     Og = O // G
@@ -231,7 +245,7 @@ def _wgrad(x, dy, weight, Cg_x, G, stride, padding, dilation, out=None):
     sh, sw = stride
     ph, pw = padding
     dh, dw = dilation
-    if R == 1 and S == 1 and Cg_x == Ig:  # GEMM layout == OIHW: accumulate straight into the grad
+    if R == 1 and S == 1 and Cg_x == Ig and not reflect:  # GEMM layout == OIHW: accumulate straight into the grad
         buf = out if out is not None else torch.empty((O, Ig, 1, 1), dtype=F32, device=x.device)
         lib().conv_wgrad(ptr(x), ptr(dy), ptr(buf), N, H, W, Cg_x, ld_of(x), G, Og, P, Q, ld_of(dy), R, S, sh, sw,
                          ph, pw, dh, dw, 0, int(out is not None), 0, stream_handle())
@@ -240,7 +254,7 @@ def _wgrad(x, dy, weight, Cg_x, G, stride, padding, dilation, out=None):
     # one pass to OIHW that re-zeroes the workspace as it reads it
     ws = _wgrad_workspace(G * Og * R * S * Cg_x, x.device)
     lib().conv_wgrad(ptr(x), ptr(dy), ptr(ws), N, H, W, Cg_x, ld_of(x), G, Og, P, Q, ld_of(dy), R, S, sh, sw, ph, pw,
-                     dh, dw, 0, 1, 0, stream_handle())
+                     dh, dw, 0, 1, 0, stream_handle(), reflect=int(reflect))
     dW = out if out is not None else torch.empty((O, Ig, R, S), dtype=F32, device=x.device)
     lib().wgrad_unprep(ptr(ws), ptr(dW), G, Og, Ig, R, S, Cg_x, 1.0, int(out is not None), 1, stream_handle())
     return dW
@@ -262,7 +276,7 @@ def _wgrad_workspace(numel, device):
 class _ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats, stats_buf=None,
-                extra=(0, 0), join=None, join_role=None):
+                extra=(0, 0), join=None, join_role=None, reflect=False):
         N, Cx, H, W = x.shape
         O, Ig, R, S = weight.shape
         G = groups
@@ -277,9 +291,10 @@ class _ConvFn(torch.autograd.Function):
             stats = stats_buf if stats_buf is not None else torch.zeros((STAT_SHARDS, 2, O), dtype=F32, device=x.device)
         b = bias.detach().float().contiguous() if bias is not None else None
         conv_fwd_raw(x, wk, y, b, stats, N, H, W, Cg_x, ldx, G, Og, P, Q, R, S, stride, padding, dilation,
-                     act=act, slope=slope)
+                     act=act, slope=slope, reflect=reflect)
         ctx.save_for_backward(x, weight, y if act else None)
         ctx.cfg = (stride, padding, dilation, G, act, slope, Cg_x, bias is not None)
+        ctx.reflect = reflect
         ctx.join = (join, join_role)
         # the producing BatchNorm of x: its backward statistics can ride on this conv's dgrad
         ctx.bnref = getattr(x, "_dv_bnref", None) if join_role != "producer" else None
@@ -299,8 +314,8 @@ class _ConvFn(torch.autograd.Function):
                 g = join.take()  # nothing to add to: hand a stashed shortcut gradient through
                 if isinstance(g, MaskedGrad):
                     g = g.materialize()
-                return (g, None, None) + (None,) * 11
-            return (None,) * 14
+                return (g, None, None) + (None,) * 12
+            return (None,) * 15
         dy = grad_nhwc(dy)
         if act:
             dy = like_layout(dy, y)  # the saved output's exact layout (dy may be a concat slice)
@@ -311,20 +326,23 @@ class _ConvFn(torch.autograd.Function):
         join, role = ctx.join
         if ctx.needs_input_grad[0]:
             accum = join.take() if (join is not None and role == "consumer") else None
-            dx = _dgrad(dy, weight, x.shape, Cg_x, G, stride, padding, dilation, x.device, accum=accum,
-                        bnref=ctx.bnref)
+            if ctx.reflect:
+                dx = _reflect_dgrad(dy, weight, x, Cg_x, G, stride, padding, dilation)
+            else:
+                dx = _dgrad(dy, weight, x.shape, Cg_x, G, stride, padding, dilation, x.device, accum=accum,
+                            bnref=ctx.bnref)
             if dx.shape[1] != x.shape[1]:
                 dx = dx[:, : x.shape[1]]
             if join is not None and role == "producer":
                 dx = join.produce(dx)
         if ctx.needs_input_grad[1]:
             sink = grad_sink(weight)
-            dw = _wgrad(x, dy, weight, Cg_x, G, stride, padding, dilation, out=sink)
+            dw = _wgrad(x, dy, weight, Cg_x, G, stride, padding, dilation, out=sink, reflect=ctx.reflect)
             if sink is not None:
                 dw = None
         if has_bias and ctx.needs_input_grad[2]:
             db = _channel_sum(dy)
-        return dx, dw, db, None, None, None, None, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 # ---------------------------------------------------------------------------------------
@@ -369,14 +387,14 @@ def _prep_stem_weight(weight, Sp):
 
 class _StemConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, padding, act, slope, want_stats, stats_buf, geo):
+    def forward(ctx, x, weight, bias, stride, padding, act, slope, want_stats, stats_buf, geo, reflect=False):
         Sp, Hp, Wp, P, Q = geo
         N, C, H, W = x.shape
         O, I, R, S = weight.shape
         xc = x if x.is_contiguous() else x.contiguous()
         xp = torch.empty((N, Hp, Wp, 4), dtype=BF16, device=x.device)
         lib().stem_pack(ptr(xc), int(xc.dtype == F32), ptr(xp), N, C, H, W, Hp, Wp, padding[0], padding[1],
-                        stream_handle())
+                        stream_handle(), reflect=int(reflect))
         wk = _prep_stem_weight(weight, Sp)
         y = empty_nhwc(N, O, P, Q, x.device)
         stats = None
@@ -398,7 +416,7 @@ class _StemConvFn(torch.autograd.Function):
         xp, weight, y = ctx.saved_tensors
         stride, act, slope, geo, has_bias = ctx.cfg
         if dy is None:
-            return (None,) * 10
+            return (None,) * 11
         Sp, Hp, Wp, P, Q = geo
         O, I, R, S = weight.shape
         N = xp.shape[0]
@@ -422,21 +440,33 @@ class _StemConvFn(torch.autograd.Function):
                 dw = full[..., :S].contiguous()
         if has_bias and ctx.needs_input_grad[2]:
             db = _channel_sum(dy)
-        return None, dw, db, None, None, None, None, None, None, None
+        return None, dw, db, None, None, None, None, None, None, None, None
 
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=None, slope=0.0,
-           want_stats=False, stats_buf=None, join=None, join_role=None):
+           want_stats=False, stats_buf=None, join=None, join_role=None, pad_mode="zeros"):
     """Conv2d (+fused bias/activation). Returns y, or (y, stats) when want_stats (GPU only).
 
-    ``padding`` may be (top, bottom, left, right) for TF/Keras asymmetric 'same' padding."""
+    ``padding`` may be (top, bottom, left, right) for TF/Keras asymmetric 'same' padding.
+    ``pad_mode='reflect'``: ReflectionPad2d(padding) fused into the im2col gather (the taps
+    outside the image read the mirrored pixels; no padded copy of the input)."""
     if isinstance(padding, str):
         raise NotImplementedError("string padding: use nn.Conv2d(padding='same_keras')")
     stride, dilation = _pair(stride), _pair(dilation)
     padding, extra = norm_padding(padding)
-    if join is not None and join_role == "consumer" and not native(x):
+    reflect = pad_mode == "reflect"
+    if pad_mode not in ("zeros", "reflect"):
+        raise NotImplementedError(f"pad_mode {pad_mode!r}")
+    if reflect and (extra != (0, 0) or dilation != (1, 1)):
+        raise NotImplementedError("reflect padding with asymmetric pads / dilation")
+    if join is not None and join_role == "consumer" and (not native(x) or reflect):
         join.consumer_done = True
+    if reflect:
+        join = None
     if not native(x):
+        if reflect:
+            x = TF.pad(x, (padding[1], padding[1], padding[0], padding[0]), mode="reflect")
+            padding = (0, 0)
         if extra != (0, 0):
             x = TF.pad(x, (padding[1], padding[1] + extra[1], padding[0], padding[0] + extra[0]))
             padding = (0, 0)
@@ -450,6 +480,8 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=
     padded_groups = groups > 1 and ((x.shape[1] // groups) % 8 != 0 or (weight.shape[0] // groups) % 8 != 0)
     if join is not None and join_role == "consumer" and (dw or padded_groups):
         join.consumer_done = True  # these paths do not fold the join: producers hand grads to autograd
+    if reflect and (dw or padded_groups):
+        raise NotImplementedError("reflect padding on depthwise / channel-padded grouped convs")
     if dw:
         return depthwise_conv2d(x, weight, bias, stride, padding, act, slope, want_stats, stats_buf, extra)
     if padded_groups:
@@ -461,14 +493,14 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=
         if join is not None and join_role == "consumer":
             join.consumer_done = True
         return _StemConvFn.apply(x, weight, bias, stride, padding, ACT_IDS[act], float(slope), want_stats, stats_buf,
-                                 geo)
+                                 geo, reflect)
     xn = as_nhwc(x, pad_to8=(groups == 1))
     if xn is not x and join is not None:
         if join_role == "consumer":  # the gradient reaches x through the layout copy: no join
             join.consumer_done = True
         join = None
     return _ConvFn.apply(xn, weight, bias, stride, padding, dilation, groups, ACT_IDS[act], float(slope), want_stats,
-                         stats_buf, extra, join, join_role)
+                         stats_buf, extra, join, join_role, reflect)
 
 
 def _grouped_padded_conv(x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats):

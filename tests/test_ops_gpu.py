@@ -504,3 +504,37 @@ def test_sync_check_mode_runs():
         assert torch.isfinite(y).all()
     finally:
         dv.set_sync_check(False)
+
+
+@pytest.mark.parametrize("case", [
+    # N, C, H, W, K, R, pad, bias, input needs grad
+    (2, 256, 16, 16, 256, 3, 1, False, True),   # CycleGAN ResNet block conv
+    (2, 3, 32, 32, 64, 7, 3, False, False),     # generator stem on the network input (tap-packed)
+    (2, 3, 32, 32, 64, 7, 3, False, True),      # stem on a generated image (cycle loss: needs dX)
+    (2, 64, 20, 18, 3, 7, 3, True, True),       # output conv 64 -> 3 with bias
+])
+def test_reflect_pad_fused_conv(case):
+    """ReflectionPad2d fused into the im2col gather (pad_mode='reflect'): forward, dgrad (padded-grid
+    dgrad + border fold) and wgrad (mirrored taps) vs torch pad(reflect) + conv in fp32."""
+    from deep_vision_amd import ops as F
+
+    N, C, H, W, K, R, p, has_b, xg = case
+    x32 = torch.randn(N, C, H, W, device=DEV).bfloat16().float()
+    w = (torch.randn(K, C, R, R, device=DEV) * (2.0 / (C * R * R)) ** 0.5).requires_grad_(True)
+    b = torch.randn(K, device=DEV).requires_grad_(True) if has_b else None
+    x = (_nhwc(x32) if C % 8 == 0 else x32.clone()).requires_grad_(xg)
+    y = F.conv2d(x, w, b, 1, p, pad_mode="reflect")
+    xr = x32.clone().requires_grad_(xg)
+    wr = w.detach().bfloat16().float().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True) if has_b else None
+    yr = TF.conv2d(TF.pad(xr, (p, p, p, p), mode="reflect"), wr, br)
+    assert y.shape == yr.shape
+    assert _rel(y, yr) < 2e-2
+    dy32 = torch.randn_like(yr).bfloat16().float()
+    y.backward(_nhwc(dy32) if K % 8 == 0 else dy32)
+    yr.backward(dy32)
+    assert _rel(w.grad, wr.grad) < 3e-2
+    if xg:
+        assert _rel(x.grad, xr.grad) < 3e-2
+    if has_b:
+        assert _rel(b.grad, br.grad) < 3e-2
