@@ -149,6 +149,11 @@ PYBIND11_MODULE(_C, m) {
     dv_stem_pack(CP(x), is_f32, P(y), N, C, H, W, Hp, Wp, pt, pl, reflect, ST(st)); check_last("stem_pack");
   }, py::arg("x"), py::arg("is_f32"), py::arg("y"), py::arg("N"), py::arg("C"), py::arg("H"), py::arg("W"),
      py::arg("Hp"), py::arg("Wp"), py::arg("pt"), py::arg("pl"), py::arg("st"), py::arg("reflect") = 0);
+  m.def("nhwc_copy", [](uptr src, int lds, uptr dst, int ldd, int64_t rows, int C, uptr idx, uptr st) {
+    if (dv_nhwc_copy(CP(src), lds, P(dst), ldd, rows, C, (const int*)CP(idx), ST(st)))
+      throw std::runtime_error("nhwc_copy: channel count / strides must be multiples of 8 for a plain copy");
+    check_last("nhwc_copy");
+  });
   m.def("reflect_pad_bwd", [](uptr dxp, uptr dx, int N, int H, int W, int C, int ldp, int ld, int ph, int pw, uptr st) {
     dv_reflect_pad_bwd(CP(dxp), P(dx), N, H, W, C, ldp, ld, ph, pw, ST(st)); check_last("reflect_pad_bwd");
   });

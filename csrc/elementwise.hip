@@ -268,6 +268,29 @@ __global__ void stem_pack_kernel(const T* __restrict__ x, u16* __restrict__ y, i
   }
 }
 
+// NHWC channel-slice copy / gather: dst[row][c] = src[row][idx ? idx[c] : c] for c < C.
+// Contiguous copies (concat into a channel slice) move 16-B vectors; gathers (channel shuffle
+// and its inverse) read 2-B elements through the index table.
+__global__ void nhwc_copy_kernel(const u16* __restrict__ src, int lds, u16* __restrict__ dst, int ldd, int64_t rows,
+                                 int C) {
+  const int cg = C / 8;
+  const int64_t total = rows * cg;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = t / cg;
+    const int c = (int)(t - r * cg) * 8;
+    *reinterpret_cast<uint4*>(dst + r * ldd + c) = *reinterpret_cast<const uint4*>(src + r * lds + c);
+  }
+}
+__global__ void nhwc_gather_kernel(const u16* __restrict__ src, int lds, u16* __restrict__ dst, int ldd, int64_t rows,
+                                   int C, const int* __restrict__ idx) {
+  const int64_t total = rows * C;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = t / C;
+    const int c = (int)(t - r * C);
+    dst[r * ldd + c] = src[r * lds + idx[c]];
+  }
+}
+
 // reflection-pad backward (NHWC bf16, 8 channels per thread): gather the interior position and
 // the mirrored border positions that reflect onto (h, w); fp32 sum, one bf16 store
 __global__ void reflect_pad_bwd_kernel(const u16* __restrict__ dxp, u16* __restrict__ dx, int N, int H, int W, int C,
@@ -334,6 +357,15 @@ void dv_stem_pack(const void* x, int x_is_f32, void* y, int N, int C, int H, int
   const int64_t total = (int64_t)N * Hp * Wp;
   if (x_is_f32) stem_pack_kernel<float><<<grid_for(total), NT, 0, st>>>((const float*)x, (u16*)y, N, C, H, W, Hp, Wp, pt, pl, reflect);
   else stem_pack_kernel<u16><<<grid_for(total), NT, 0, st>>>((const u16*)x, (u16*)y, N, C, H, W, Hp, Wp, pt, pl, reflect);
+}
+int dv_nhwc_copy(const void* src, int lds, void* dst, int ldd, int64_t rows, int C, const int* idx, hipStream_t st) {
+  if (idx != nullptr) {
+    nhwc_gather_kernel<<<grid_for(rows * C), NT, 0, st>>>((const u16*)src, lds, (u16*)dst, ldd, rows, C, idx);
+    return 0;
+  }
+  if (C % 8 || lds % 8 || ldd % 8) return -1;  // plain copies move whole 16-B vectors
+  nhwc_copy_kernel<<<grid_for(rows * (C / 8)), NT, 0, st>>>((const u16*)src, lds, (u16*)dst, ldd, rows, C);
+  return 0;
 }
 void dv_reflect_pad_bwd(const void* dxp, void* dx, int N, int H, int W, int C, int ldp, int ld, int ph, int pw,
                         hipStream_t st) {

@@ -108,6 +108,9 @@ void dv_act_bwd(const void* dy, const void* y, void* dx, int64_t n, int act, flo
 void dv_add(const void* a, const void* b, void* y, int64_t n, float alpha, float beta, int act, float slope, hipStream_t st);
 void dv_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, hipStream_t st);
 void dv_wprep(const float* w, void* out, int G, int Og, int Ig, int R, int S, int Ipad, int mode, int Sp, hipStream_t st);
+// NHWC channel-slice copy (16-B vectors; concat into a slice of a wider buffer) or, with an index
+// table, a channel gather (ShuffleNet channel shuffle / its inverse). -1: unsupported geometry.
+int dv_nhwc_copy(const void* src, int lds, void* dst, int ldd, int64_t rows, int C, const int* idx, hipStream_t st);
 // reflection-pad backward: dx[h][w] = sum of the padded gradient at every padded position that
 // reflects onto (h, w) (the interior one plus up to three mirrored border positions)
 void dv_reflect_pad_bwd(const void* dxp, void* dx, int N, int H, int W, int C, int ldp, int ld, int ph, int pw,

@@ -22,9 +22,9 @@ class BasicConv2d(tnn.Module):
         super().__init__()
         self.conv = nn.Conv2d(in_channels, out_channels, kernel_size, **kw)
 
-    def forward(self, x):
+    def forward(self, x, out=None):
         c = self.conv
-        return F.conv2d(x, c.weight, c.bias, c.stride, c.padding, c.dilation, c.groups, act="relu")
+        return F.conv2d(x, c.weight, c.bias, c.stride, c.padding, c.dilation, c.groups, act="relu", out=out)
 
 
 class InceptionModule(tnn.Module):
@@ -39,14 +39,22 @@ class InceptionModule(tnn.Module):
         self.branch4_conv1x1 = BasicConv2d(in_channels, p6, 1, stride=1)
 
     def forward(self, x):
-        b1 = self.branch1_conv1x1(x)
-        b2 = self.branch2_conv3x3(self.branch2_conv1x1(x))
-        b3 = self.branch3_conv5x5(self.branch3_conv1x1(x))
-        b4 = self.branch4_conv1x1(self.branch4_maxpool(x))
-        y = torch.cat([b1, b2, b3, b4], 1)
+        outs = [None] * 4
         if F.native(x):
-            y = y.contiguous(memory_format=torch.channels_last)
-        return y
+            # write-into-slice concat: each branch's last conv epilogue stores straight into its
+            # channel slice of the module output (R/Inception/pytorch/models/inception_v1.py:156-158)
+            N, _, H, W = x.shape
+            outs = F.concat_slices(N, [m.conv.out_channels for m in self._last()], H, W, x.device)
+        b1 = self.branch1_conv1x1(x, out=outs[0])
+        b2 = self.branch2_conv3x3(self.branch2_conv1x1(x), out=outs[1])
+        b3 = self.branch3_conv5x5(self.branch3_conv1x1(x), out=outs[2])
+        b4 = self.branch4_conv1x1(self.branch4_maxpool(x), out=outs[3])
+        if F.native(x):
+            return F.slice_cat([b1, b2, b3, b4])
+        return torch.cat([b1, b2, b3, b4], 1)
+
+    def _last(self):
+        return (self.branch1_conv1x1, self.branch2_conv3x3, self.branch3_conv5x5, self.branch4_conv1x1)
 
 
 class AuxiliaryClassifier(tnn.Module):
@@ -136,8 +144,7 @@ class _CBR(tnn.Module):
 
 
 def _cat(xs, ref):
-    y = torch.cat(xs, 1)
-    return y.contiguous(memory_format=torch.channels_last) if F.native(ref) else y
+    return F.concat(xs)  # native slice copies on the GPU path
 
 
 class _InceptionA(tnn.Module):

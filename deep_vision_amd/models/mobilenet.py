@@ -134,10 +134,7 @@ class ShuffleUnit(tnn.Module):
             return F.conv_bn_act(y, self.gconv2, self.bn3, "relu", residual=x)
         y = F.conv_bn_act(y, self.gconv2, self.bn3, None)
         sc = F.avg_pool2d(x, 3, 2, 1)
-        out = torch.cat([sc, y], 1)
-        if F.native(x):
-            out = out.contiguous(memory_format=torch.channels_last)
-        return F.relu(out)
+        return F.relu(F.concat([sc, y]))
 
 
 class ShuffleNetV1(tnn.Module):

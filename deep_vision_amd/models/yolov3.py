@@ -114,9 +114,7 @@ class YoloV3(tnn.Module):
 
     @staticmethod
     def _up_cat(x, skip):
-        x = F.upsample_nearest(x, 2)
-        out = torch.cat([x, skip], 1)
-        return out.contiguous(memory_format=torch.channels_last) if F.native(x) else out
+        return F.concat([F.upsample_nearest(x, 2), skip])  # route (yolov3.py:151-152,180-181)
 
     def forward(self, x):
         """Raw head tensors (small, medium, large), each (N, g, g, 3, 5+C)."""

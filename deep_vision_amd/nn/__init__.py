@@ -12,7 +12,7 @@ import torch
 import torch.nn as tnn
 
 from .. import ops as F
-from ..ops.common import native
+from ..ops.common import native, unsupported
 
 __all__ = [
     "Conv2d", "ConvTranspose2d", "Linear", "BatchNorm2d", "ReLU", "LeakyReLU", "Tanh", "Sigmoid", "MaxPool2d",
@@ -52,9 +52,12 @@ class Conv2d(tnn.Conv2d):
             return F.conv2d(x, self.weight, self.bias, self.stride, self.native_padding(x.shape[2], x.shape[3]),
                             self.dilation, self.groups)
         if self.padding_mode != "zeros":
-            return super().forward(x) if not native(x) else F.conv2d(
-                tnn.functional.pad(x, self._reversed_padding_repeated_twice, mode=self.padding_mode), self.weight,
-                self.bias, self.stride, 0, self.dilation, self.groups)
+            if not native(x):
+                return super().forward(x)
+            if self.padding_mode != "reflect":
+                unsupported(f"Conv2d padding_mode={self.padding_mode!r}")
+            return F.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, self.groups,
+                            pad_mode="reflect")
         return F.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, self.groups)
 
 
@@ -82,10 +85,17 @@ class ConvTranspose2d(tnn.ConvTranspose2d):
             pad, out = keras_same_transpose(x.shape[2], x.shape[3], self.kernel_size, self.stride)
             return F.conv_transpose2d(x, self.weight, self.bias, self.stride, pad, 0, self.groups, self.dilation,
                                       output_size=out)
-        if output_size is not None or not native(x):
+        if not native(x):
             return super().forward(x, output_size)
-        return F.conv_transpose2d(x, self.weight, self.bias, self.stride, self.padding, self.output_padding,
-                                  self.groups, self.dilation)
+        op = self.output_padding
+        if output_size is not None:  # torch semantics: output_size picks the output_padding
+            osz = tuple(output_size)[-2:]
+            op = tuple(osz[i] - ((x.shape[2 + i] - 1) * self.stride[i] - 2 * self.padding[i]
+                                 + self.dilation[i] * (self.kernel_size[i] - 1) + 1) for i in range(2))
+            if any(v < 0 or v >= max(self.stride[i], self.dilation[i]) for i, v in enumerate(op)):
+                raise ValueError(f"requested output size {osz} is not reachable")
+        return F.conv_transpose2d(x, self.weight, self.bias, self.stride, self.padding, op, self.groups,
+                                  self.dilation)
 
 
 class Linear(tnn.Linear):
@@ -122,8 +132,10 @@ class Sigmoid(tnn.Sigmoid):
 
 class MaxPool2d(tnn.MaxPool2d):
     def forward(self, x):
-        if not native(x) or self.dilation not in (1, (1, 1)) or self.return_indices:
+        if not native(x):
             return super().forward(x)
+        if self.dilation not in (1, (1, 1)) or self.return_indices:
+            unsupported("MaxPool2d with dilation / return_indices")
         return F.max_pool2d(x, self.kernel_size, self.stride, self.padding, self.ceil_mode)
 
 
@@ -147,9 +159,11 @@ class Dropout(tnn.Dropout):
 
 class Upsample(tnn.Upsample):
     def forward(self, x):
-        if native(x) and self.mode == "nearest" and self.scale_factor is not None:
-            return F.upsample_nearest(x, self.scale_factor)
-        return super().forward(x)
+        if not native(x):
+            return super().forward(x)
+        if self.mode != "nearest" or self.scale_factor is None:
+            unsupported(f"Upsample mode={self.mode!r} / size=")
+        return F.upsample_nearest(x, self.scale_factor)
 
 
 class LocalResponseNorm(tnn.LocalResponseNorm):
@@ -175,19 +189,14 @@ class ReflectionPad2d(tnn.ReflectionPad2d):
 
 
 class ChannelShuffle(tnn.Module):
-    """ShuffleNet channel shuffle: (N, g*c, H, W) -> transpose groups."""
+    """ShuffleNet channel shuffle: (N, g*c, H, W) -> transpose groups (native channel gather)."""
 
     def __init__(self, groups):
         super().__init__()
         self.groups = groups
 
     def forward(self, x):
-        N, C, H, W = x.shape
-        g = self.groups
-        y = x.reshape(N, g, C // g, H, W).transpose(1, 2).reshape(N, C, H, W)
-        if native(x):
-            y = y.contiguous(memory_format=torch.channels_last)
-        return y
+        return F.channel_shuffle(x, self.groups)
 
 
 _ACTS = {tnn.ReLU: ("relu", None), tnn.LeakyReLU: ("leaky", "negative_slope")}
@@ -217,6 +226,19 @@ class FusedSequential(tnn.Sequential):
         while i < len(mods):
             m = mods[i]
             nxt = mods[i + 1] if i + 1 < len(mods) else None
+            if isinstance(m, (tnn.ZeroPad2d, tnn.ReflectionPad2d)) and isinstance(nxt, Conv2d) and \
+                    nxt.padding_mode == "zeros" and not nxt.keras_same and tuple(nxt.padding) == (0, 0):
+                # pad -> pad-0 conv: the pad becomes the conv's (asymmetric) padding / reflect gather
+                l, r, t, b = m.padding
+                act, slope = _act_of(mods[i + 2]) if i + 2 < len(mods) else (None, 0.0)
+                if isinstance(m, tnn.ReflectionPad2d):
+                    x = F.conv2d(x, nxt.weight, nxt.bias, nxt.stride, (t, l), nxt.dilation, nxt.groups, act=act,
+                                 slope=slope, pad_mode="reflect")
+                else:
+                    x = F.conv2d(x, nxt.weight, nxt.bias, nxt.stride, (t, b, l, r) if (t, l) != (b, r) else (t, l),
+                                 nxt.dilation, nxt.groups, act=act, slope=slope)
+                i += 3 if act else 2
+                continue
             if isinstance(m, Conv2d) and m.padding_mode == "zeros":
                 pad = m.native_padding(x.shape[2], x.shape[3])
                 if isinstance(nxt, tnn.BatchNorm2d):

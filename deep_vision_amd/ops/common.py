@@ -39,6 +39,13 @@ def native(x: torch.Tensor) -> bool:
     return x.is_cuda and not _FORCE_TORCH
 
 
+def unsupported(what: str):
+    """A GPU-path op the native kernels do not implement: raise instead of silently running a
+    PyTorch/MIOpen kernel (the torch path exists only as the ``--backend torch`` oracle)."""
+    raise NotImplementedError(f"no native gfx950 kernel for {what}; use the torch backend "
+                              "(set_backend('torch') / --backend torch) for it")
+
+
 def round8(c: int) -> int:
     return (c + 7) // 8 * 8
 

@@ -15,7 +15,7 @@ import torch
 import torch.nn.functional as TF
 
 from . import wcache
-from .common import (ACT_IDS, BF16, CL, F32, alloc_cl, as_nhwc, empty_nhwc, grad_nhwc, grad_sink, ld_of, lib,
+from .common import (ACT_IDS, BF16, CL, F32, alloc_cl, as_nhwc, empty_nhwc, grad_nhwc, grad_sink, is_nhwc, ld_of, lib,
                      like_layout, empty_layout, native, nhwc_numel, ptr, round8, stream_handle)
 
 STAT_SHARDS = 64
@@ -276,7 +276,7 @@ def _wgrad_workspace(numel, device):
 class _ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats, stats_buf=None,
-                extra=(0, 0), join=None, join_role=None, reflect=False):
+                extra=(0, 0), join=None, join_role=None, reflect=False, out_box=None):
         N, Cx, H, W = x.shape
         O, Ig, R, S = weight.shape
         G = groups
@@ -285,7 +285,12 @@ class _ConvFn(torch.autograd.Function):
         Cg_x = _gather_channels(x, Cx // G, G)  # padded channels (G == 1) are zeros
         P, Q = out_size(H + extra[0], W + extra[1], R, S, stride, padding, dilation)
         wk = _prep_weight(weight, G, Cg_x, mode=0)
-        y = empty_nhwc(N, O, P, Q, x.device)
+        if out_box:  # write-into-slice: the epilogue stores into a channel slice of a concat buffer
+            y = out_box[0]
+            if (tuple(y.shape) != (N, O, P, Q) or not is_nhwc(y) or ld_of(y) % 8 or y.data_ptr() % 16):
+                raise ValueError(f"conv2d out= must be an NHWC bf16 (slice) view of shape {(N, O, P, Q)}")
+        else:
+            y = empty_nhwc(N, O, P, Q, x.device)
         stats = None
         if want_stats:
             stats = stats_buf if stats_buf is not None else torch.zeros((STAT_SHARDS, 2, O), dtype=F32, device=x.device)
@@ -314,8 +319,8 @@ class _ConvFn(torch.autograd.Function):
                 g = join.take()  # nothing to add to: hand a stashed shortcut gradient through
                 if isinstance(g, MaskedGrad):
                     g = g.materialize()
-                return (g, None, None) + (None,) * 12
-            return (None,) * 15
+                return (g, None, None) + (None,) * 13
+            return (None,) * 16
         dy = grad_nhwc(dy)
         if act:
             dy = like_layout(dy, y)  # the saved output's exact layout (dy may be a concat slice)
@@ -444,12 +449,14 @@ class _StemConvFn(torch.autograd.Function):
 
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=None, slope=0.0,
-           want_stats=False, stats_buf=None, join=None, join_role=None, pad_mode="zeros"):
+           want_stats=False, stats_buf=None, join=None, join_role=None, pad_mode="zeros", out=None):
     """Conv2d (+fused bias/activation). Returns y, or (y, stats) when want_stats (GPU only).
 
     ``padding`` may be (top, bottom, left, right) for TF/Keras asymmetric 'same' padding.
     ``pad_mode='reflect'``: ReflectionPad2d(padding) fused into the im2col gather (the taps
-    outside the image read the mirrored pixels; no padded copy of the input)."""
+    outside the image read the mirrored pixels; no padded copy of the input).
+    ``out``: a preallocated NHWC (channel-slice) view the output is written into (write-into-slice
+    concat, ops.concat.slice_cat); native path only."""
     if isinstance(padding, str):
         raise NotImplementedError("string padding: use nn.Conv2d(padding='same_keras')")
     stride, dilation = _pair(stride), _pair(dilation)
@@ -478,16 +485,20 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=
         return (y, None) if want_stats else y
     dw = _is_depthwise(x, weight, groups, stride, dilation)
     padded_groups = groups > 1 and ((x.shape[1] // groups) % 8 != 0 or (weight.shape[0] // groups) % 8 != 0)
-    if join is not None and join_role == "consumer" and (dw or padded_groups):
-        join.consumer_done = True  # these paths do not fold the join: producers hand grads to autograd
-    if reflect and (dw or padded_groups):
-        raise NotImplementedError("reflect padding on depthwise / channel-padded grouped convs")
+    if join is not None and join_role == "consumer" and dw:
+        join.consumer_done = True  # the depthwise path does not fold the join: producers hand grads to autograd
+    if reflect and dw:
+        raise NotImplementedError("reflect padding on depthwise convs")
+    if out is not None and (dw or padded_groups):
+        raise NotImplementedError("conv2d out= on depthwise / channel-padded grouped convs")
     if dw:
         return depthwise_conv2d(x, weight, bias, stride, padding, act, slope, want_stats, stats_buf, extra)
     if padded_groups:
-        if extra != (0, 0):
-            raise NotImplementedError("asymmetric padding on a channel-padded grouped conv")
-        return _grouped_padded_conv(x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats)
+        # channels per group not a multiple of 8 (ShuffleNet V1 g=3: 20 / 40 / 80): run as a dense
+        # conv with a block-diagonal weight -- the activations are read and written once, in
+        # place, no channel-padding copies (the FLOPs x groups are negligible for these 1x1s)
+        weight = _block_diagonal(weight, groups, x.shape[1])
+        groups = 1
     geo = _stem_geometry(x, weight, stride, padding, dilation, groups, extra)
     if geo is not None:  # network input: no gradient, no join
         if join is not None and join_role == "consumer":
@@ -500,29 +511,25 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=
             join.consumer_done = True
         join = None
     return _ConvFn.apply(xn, weight, bias, stride, padding, dilation, groups, ACT_IDS[act], float(slope), want_stats,
-                         stats_buf, extra, join, join_role, reflect)
+                         stats_buf, extra, join, join_role, reflect, [out] if out is not None else None)
 
 
-def _grouped_padded_conv(x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats):
-    """Grouped conv whose channels per group are not multiples of 8 (ShuffleNet V1 g=3: 20/40/80
-    channels per group). Input channels and output channels of every group are zero-padded to a
-    multiple of 8 (differentiable copies), the MFMA kernel runs with the padded group strides,
-    and the padding channels are dropped from the output. Statistics are left to the BN pass."""
-    N, C, H, W = x.shape
-    G = groups
-    Cg, O = C // G, weight.shape[0]
-    Og = O // G
-    Cgp, Ogp = round8(Cg), round8(Og)
-    xg = x.to(BF16).reshape(N, G, Cg, H, W)
-    xg = TF.pad(xg, (0, 0, 0, 0, 0, Cgp - Cg)).reshape(N, G * Cgp, H, W).contiguous(memory_format=CL)
-    R, S = weight.shape[2], weight.shape[3]
-    wp = TF.pad(weight.view(G, Og, Cg, R, S), (0, 0, 0, 0, 0, Cgp - Cg, 0, Ogp - Og)).reshape(G * Ogp, Cgp, R, S)
-    bp = TF.pad(bias.view(G, Og), (0, Ogp - Og)).reshape(-1) if bias is not None else None
-    y = _ConvFn.apply(xg, wp, bp, stride, padding, dilation, groups, ACT_IDS[act], float(slope), False, None)
-    if Ogp != Og:
-        P, Q = y.shape[2], y.shape[3]
-        y = y.reshape(N, G, Ogp, P, Q)[:, :, :Og].reshape(N, O, P, Q).contiguous(memory_format=CL)
-    return (y, None) if want_stats else y
+def _block_diagonal(weight, groups, cin):
+    """Grouped OIHW weight (O, C/G, R, S) -> the equivalent dense weight (O, C, R, S) with zeros
+    outside each output channel's group (differentiable: gradients flow back to ``weight``)."""
+    O, Cg, R, S = weight.shape
+    Og = O // groups
+    key = (O, cin, groups, str(weight.device))
+    mask = _BD_MASK.get(key)
+    if mask is None:
+        o = torch.arange(O, device=weight.device) // Og
+        c = torch.arange(cin, device=weight.device) // Cg
+        mask = (o[:, None] == c[None, :]).to(weight.dtype)[:, :, None, None]
+        _BD_MASK[key] = mask
+    return weight.repeat(1, groups, 1, 1) * mask
+
+
+_BD_MASK = {}
 
 
 # ---------------------------------------------------------------------------------------
@@ -553,17 +560,16 @@ class _ConvTFn(torch.autograd.Function):
         Cpad = round8(Cog) if G == 1 else Cog
         Cg_in = _gather_channels(x, Ci // G, G)
         wd = _prep_weight(weight, G, Cg_in, mode=1)
-        y_full = alloc_cl((N, G * Cpad, OH, OW), zero=True, device=x.device)
+        y_full = alloc_cl((N, G * Cpad, OH, OW), zero=(Cpad != Cog), device=x.device)
         ldx = ld_of(x)
+        b = bias.detach().float().contiguous() if bias is not None else None  # bias in the epilogue
         if (sh, sw) == (1, 1):
-            conv_fwd_raw(x, wd, y_full, None, None, N, H, W, Cg_in, ldx, G, Cog, OH, OW, R, S, (1, 1), (-ph, -pw),
+            conv_fwd_raw(x, wd, y_full, b, None, N, H, W, Cg_in, ldx, G, Cog, OH, OW, R, S, (1, 1), (-ph, -pw),
                          (-dh, -dw), ldy=G * Cpad)
         else:
-            conv_fwd_raw(x, wd, y_full, None, None, N, H, W, Cg_in, ldx, G, Cog, OH, OW, R, S, stride, padding,
+            conv_fwd_raw(x, wd, y_full, b, None, N, H, W, Cg_in, ldx, G, Cog, OH, OW, R, S, stride, padding,
                          dilation, tgather=1, ldy=G * Cpad)
         y = y_full if Cpad == Cog else y_full[:, :Cout]
-        if bias is not None:
-            y.add_(bias.detach().to(BF16).view(1, -1, 1, 1))
         ctx.save_for_backward(x, weight)
         ctx.cfg = (stride, padding, dilation, G, bias is not None)
         return y

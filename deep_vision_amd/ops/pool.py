@@ -12,7 +12,7 @@ import math
 import torch
 import torch.nn.functional as TF
 
-from .common import BF16, CL, as_nhwc, grad_nhwc, ld_of, lib, native, ptr, stream_handle
+from .common import BF16, CL, as_nhwc, grad_nhwc, ld_of, lib, native, ptr, stream_handle, unsupported
 
 
 def _pair(v):
@@ -130,6 +130,7 @@ def adaptive_avg_pool2d(x, output_size):
             if H % os_[0] == 0 and W % os_[1] == 0:
                 kh, kw = H // os_[0], W // os_[1]
                 return avg_pool2d(x, (kh, kw), (kh, kw))
+            unsupported(f"adaptive_avg_pool2d {H}x{W} -> {os_} (non-divisible)")
         return TF.adaptive_avg_pool2d(x, os_)
     x = _dense(as_nhwc(x, pad_to8=False))
     return _GAPFn.apply(x)
@@ -155,7 +156,9 @@ class _UpsampleFn(torch.autograd.Function):
 
 def upsample_nearest(x, scale_factor=2):
     f = int(scale_factor)
-    if not native(x) or f != scale_factor:
+    if native(x) and f != scale_factor:
+        unsupported(f"nearest upsampling by a non-integer factor {scale_factor}")
+    if not native(x):
         return TF.interpolate(x, scale_factor=scale_factor, mode="nearest")
     x = _dense(as_nhwc(x, pad_to8=False))
     return _UpsampleFn.apply(x, f)

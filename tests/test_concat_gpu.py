@@ -1,0 +1,136 @@
+"""Native concat / shuffle / grouped / transposed-conv paths that replaced torch copies on the GPU
+path, each against a plain PyTorch fp32 reference."""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as TF
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _cos(a, b):
+    a, b = a.float().flatten(), b.float().flatten()
+    return (a @ b / (a.norm() * b.norm()).clamp_min(1e-12)).item()
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+
+
+def _nhwc(t):
+    return t.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+
+
+def _native_vs_torch(module, x32, g_shape=None):
+    from deep_vision_amd.ops.common import set_backend
+
+    ref = copy.deepcopy(module)
+    x = _nhwc(x32).requires_grad_(True)
+    y = module(x)
+    g = torch.randn(y.shape, device=DEV)
+    y.backward(_nhwc(g))
+    xr = x32.clone().requires_grad_(True)
+    set_backend("torch")
+    try:
+        yr = ref(xr)
+        yr.backward(g)
+    finally:
+        set_backend("native")
+    return (y, x.grad, module), (yr, xr.grad, ref)
+
+
+def test_inception_module_write_into_slice():
+    """Inception V1 module: each branch's last conv writes into its channel slice of the output
+    (no torch.cat); output and all gradients match torch."""
+    from deep_vision_amd.models.inception import InceptionModule
+
+    torch.manual_seed(0)
+    m = InceptionModule(192, 64, 96, 128, 16, 32, 32).to(DEV)
+    (y, gx, mn), (yr, gxr, mr) = _native_vs_torch(m, torch.randn(4, 192, 14, 14, device=DEV).bfloat16().float())
+    assert y.shape == yr.shape == (4, 256, 14, 14)
+    assert y._base is None and y.is_contiguous(memory_format=torch.channels_last)
+    assert _cos(y, yr) > 0.999 and _cos(gx, gxr) > 0.995
+    for (n, p), (_, q) in zip(mn.named_parameters(), mr.named_parameters()):
+        assert _cos(p.grad, q.grad) > 0.99, n
+
+
+def test_native_concat_and_shuffle():
+    from deep_vision_amd import ops as F
+
+    a32 = torch.randn(2, 16, 5, 7, device=DEV)
+    b32 = torch.randn(2, 40, 5, 7, device=DEV)
+    a, b = _nhwc(a32).requires_grad_(True), _nhwc(b32).requires_grad_(True)
+    y = F.concat([a, b])
+    assert torch.equal(y.float(), torch.cat([a32, b32], 1).bfloat16().float())
+    s = F.channel_shuffle(y, 4)
+    ref = torch.cat([a32, b32], 1).bfloat16().float()
+    ref = ref.reshape(2, 4, 14, 5, 7).transpose(1, 2).reshape(2, 56, 5, 7)
+    assert torch.equal(s.float(), ref)
+    g = torch.randn(2, 56, 5, 7, device=DEV).bfloat16().float()
+    s.backward(_nhwc(g))
+    gu = g.reshape(2, 14, 4, 5, 7).transpose(1, 2).reshape(2, 56, 5, 7)  # inverse shuffle
+    assert torch.equal(a.grad.float(), gu[:, :16]) and torch.equal(b.grad.float(), gu[:, 16:])
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_shufflenet_unit_block_diagonal_grouped(stride):
+    """ShuffleNet V1 unit (g=3, 20 channels per group): grouped 1x1 convs run as dense
+    block-diagonal convs (no channel-padding copies), native shuffle and concat."""
+    from deep_vision_amd.models.mobilenet import ShuffleUnit
+
+    torch.manual_seed(1)
+    cin = 240
+    m = ShuffleUnit(cin, 240 if stride == 1 else 480, 3, stride).to(DEV)
+    (y, gx, mn), (yr, gxr, mr) = _native_vs_torch(m, torch.randn(4, cin, 14, 14, device=DEV).bfloat16().float())
+    assert y.shape == yr.shape
+    assert _cos(y, yr) > 0.998 and _cos(gx, gxr) > 0.99
+    for (n, p), (_, q) in zip(mn.named_parameters(), mr.named_parameters()):
+        assert _cos(p.grad, q.grad) > 0.98, n
+
+
+def test_conv_transpose_bias_and_output_size():
+    from deep_vision_amd import nn
+
+    torch.manual_seed(2)
+    for ctor, osz in ((dict(in_channels=32, out_channels=24, kernel_size=3, stride=2, padding=1), (15, 17)),
+                      (dict(in_channels=16, out_channels=8, kernel_size=4, stride=2, padding=1), None)):
+        m = nn.ConvTranspose2d(**ctor).to(DEV)
+        x32 = torch.randn(2, ctor["in_channels"], 8, 9, device=DEV).bfloat16().float()
+        x = _nhwc(x32).requires_grad_(True)
+        y = m(x, output_size=osz)
+        mr = torch.nn.ConvTranspose2d(**ctor).to(DEV)
+        mr.weight.data.copy_(m.weight.data.bfloat16().float())
+        mr.bias.data.copy_(m.bias.data)
+        xr = x32.clone().requires_grad_(True)
+        yr = mr(xr, output_size=osz)
+        assert y.shape == yr.shape
+        assert _rel(y, yr) < 2e-2
+        g = torch.randn_like(yr).bfloat16().float()
+        y.backward(_nhwc(g))
+        yr.backward(g)
+        assert _rel(m.bias.grad, mr.bias.grad) < 2e-2 and _rel(x.grad, xr.grad) < 3e-2
+
+
+def test_unsupported_gpu_ops_raise():
+    from deep_vision_amd import nn
+
+    x = _nhwc(torch.randn(2, 8, 8, 8, device=DEV))
+    with pytest.raises(NotImplementedError):
+        nn.MaxPool2d(2, return_indices=True)(x)
+    with pytest.raises(NotImplementedError):
+        nn.Upsample(scale_factor=2, mode="bilinear")(x)
+
+
+def test_fused_zero_pad_conv_sequential():
+    """AlexNet V2 TF: ZeroPad2d(3) -> 11x11/4 conv folded into one conv with padding 3."""
+    from deep_vision_amd import nn
+
+    torch.manual_seed(3)
+    seq = nn.FusedSequential(nn.ZeroPad2d(3), nn.Conv2d(3, 64, 11, stride=4), nn.ReLU()).to(DEV)
+    x = torch.randn(2, 3, 64, 64, device=DEV)
+    y = seq(x)
+    yr = TF.relu(TF.conv2d(TF.pad(x, (3, 3, 3, 3)), seq[1].weight.bfloat16().float(), seq[1].bias, 4))
+    assert y.shape == yr.shape and _rel(y, yr) < 2e-2
