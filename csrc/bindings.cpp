@@ -141,6 +141,12 @@ PYBIND11_MODULE(_C, m) {
 
   m.def("act_fwd", [](uptr x, uptr y, int64_t n, int act, float slope, uptr st) { dv_act_fwd(CP(x), P(y), n, act, slope, ST(st)); check_last("act_fwd"); });
   m.def("act_bwd", [](uptr dy, uptr y, uptr dx, int64_t n, int act, float slope, uptr st) { dv_act_bwd(CP(dy), CP(y), P(dx), n, act, slope, ST(st)); check_last("act_bwd"); });
+  m.def("act_bwd_rows", [](uptr dy, int lddy, uptr y, int ldy, uptr dx, int lddx, int64_t rows, int C, int act, float slope,
+                           uptr st) {
+    if (dv_act_bwd_rows(CP(dy), lddy, CP(y), ldy, P(dx), lddx, rows, C, act, slope, ST(st)))
+      throw std::runtime_error("act_bwd_rows: channel count / strides must be multiples of 8 and >= C");
+    check_last("act_bwd_rows");
+  });
   m.def("add", [](uptr a, uptr b, uptr y, int64_t n, float alpha, float beta, int act, float slope, uptr st) { dv_add(CP(a), CP(b), P(y), n, alpha, beta, act, slope, ST(st)); check_last("add"); });
   m.def("dropout", [](uptr x, uptr y, int64_t n, float p, uint64_t seed, uptr st) { dv_dropout(CP(x), P(y), n, p, seed, ST(st)); check_last("dropout"); });
   m.def("wprep", [](uptr w, uptr out, int G, int Og, int Ig, int R, int S, int Ipad, int mode, int Sp, uptr st) { dv_wprep(CFP(w), P(out), G, Og, Ig, R, S, Ipad, mode, Sp, ST(st)); check_last("wprep"); });

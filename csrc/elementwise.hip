@@ -71,6 +71,26 @@ __global__ __launch_bounds__(NT) void act_bwd_kernel(const u16* __restrict__ dy,
   if (t < n && blockIdx.x * (int64_t)NT + threadIdx.x < 8) dx[t] = f2bf(actb(bf2f(dy[t]), bf2f(y[t]), a, s));
 }
 
+// activation backward over rows x C (C % 8 == 0) of three NHWC tensors with their own pixel
+// strides: a conv output written into a concat slice and its gradient (a slice of the concat
+// gradient) are strided views, the result is dense
+__global__ __launch_bounds__(NT) void act_bwd_rows_kernel(const u16* __restrict__ dy, int lddy, const u16* __restrict__ y,
+                                                            int ldy, u16* __restrict__ dx, int lddx, int64_t rows, int C,
+                                                            int a, float s) {
+  const int cg = C / 8;
+  const int64_t total = rows * cg;
+  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < total; t += (int64_t)gridDim.x * NT) {
+    const int64_t r = t / cg;
+    const int c = (int)(t - r * cg) * 8;
+    float d[8], v[8];
+    ld8(dy + r * lddy + c, d);
+    ld8(y + r * ldy + c, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] = actb(d[k], v[k], a, s);
+    st8(dx + r * lddx + c, d);
+  }
+}
+
 // y = alpha*a + beta*b, optional activation
 __global__ __launch_bounds__(NT) void add_kernel(const u16* __restrict__ a, const u16* __restrict__ b, u16* __restrict__ y,
                                                    int64_t n, float alpha, float beta, int act, float s) {
@@ -303,12 +323,12 @@ __global__ void reflect_pad_bwd_kernel(const u16* __restrict__ dxp, u16* __restr
     const int w = (int)(r % W); r /= W;
     const int h = (int)(r % H);
     const int64_t n = r / H;
-    int hs[2], ws[2], nh = 1, nw = 1;
+    int hs[3], ws[3], nh = 1, nw = 1;
     hs[0] = h + ph; ws[0] = w + pw;
-    if (h >= 1 && h <= ph) hs[nh++] = ph - h;                     // top border reflects onto h
-    else if (h >= H - 1 - ph && h <= H - 2) hs[nh++] = 2 * (H - 1) - h + ph;  // bottom border
+    if (h >= 1 && h <= ph) hs[nh++] = ph - h;                          // top border reflects onto h
+    if (h >= H - 1 - ph && h <= H - 2) hs[nh++] = 2 * (H - 1) - h + ph;  // bottom border (both on tiny maps)
     if (w >= 1 && w <= pw) ws[nw++] = pw - w;
-    else if (w >= W - 1 - pw && w <= W - 2) ws[nw++] = 2 * (W - 1) - w + pw;
+    if (w >= W - 1 - pw && w <= W - 2) ws[nw++] = 2 * (W - 1) - w + pw;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int i = 0; i < nh; ++i)
       for (int j = 0; j < nw; ++j) {
@@ -338,6 +358,13 @@ void dv_act_fwd(const void* x, void* y, int64_t n, int act, float slope, hipStre
 }
 void dv_act_bwd(const void* dy, const void* y, void* dx, int64_t n, int act, float slope, hipStream_t st) {
   act_bwd_kernel<<<grid_for(n, 8), NT, 0, st>>>((const u16*)dy, (const u16*)y, (u16*)dx, n, act, slope);
+}
+int dv_act_bwd_rows(const void* dy, int lddy, const void* y, int ldy, void* dx, int lddx, int64_t rows, int C, int act,
+                    float slope, hipStream_t st) {
+  if (C % 8 || lddy % 8 || ldy % 8 || lddx % 8 || lddy < C || ldy < C || lddx < C) return -1;
+  act_bwd_rows_kernel<<<grid_for(rows * (C / 8)), NT, 0, st>>>((const u16*)dy, lddy, (const u16*)y, ldy, (u16*)dx, lddx,
+                                                              rows, C, act, slope);
+  return 0;
 }
 void dv_add(const void* a, const void* b, void* y, int64_t n, float alpha, float beta, int act, float slope, hipStream_t st) {
   add_kernel<<<grid_for(n, 8), NT, 0, st>>>((const u16*)a, (const u16*)b, (u16*)y, n, alpha, beta, act, slope);

@@ -105,6 +105,9 @@ void dv_upsample_bwd(const void* dy, void* dx, int N, int H, int W, int C, int f
 // ---- elementwise / layout (elementwise.hip) ----
 void dv_act_fwd(const void* x, void* y, int64_t n, int act, float slope, hipStream_t st);
 void dv_act_bwd(const void* dy, const void* y, void* dx, int64_t n, int act, float slope, hipStream_t st);
+// strided rows x C form (each tensor its own pixel stride); -1 when strides / C are not multiples of 8
+int dv_act_bwd_rows(const void* dy, int lddy, const void* y, int ldy, void* dx, int lddx, int64_t rows, int C, int act,
+                    float slope, hipStream_t st);
 void dv_add(const void* a, const void* b, void* y, int64_t n, float alpha, float beta, int act, float slope, hipStream_t st);
 void dv_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, hipStream_t st);
 void dv_wprep(const float* w, void* out, int G, int Og, int Ig, int R, int S, int Ipad, int mode, int Sp, hipStream_t st);

@@ -132,6 +132,21 @@ def empty_layout(ref: torch.Tensor) -> torch.Tensor:
     return empty_nhwc(N, C, H, W, ref.device)
 
 
+def act_grad(dy: torch.Tensor, y: torch.Tensor, act: int, slope: float) -> torch.Tensor:
+    """act'(y) * dy for a fused conv activation, as a DENSE NHWC tensor. ``y`` (the saved output)
+    and ``dy`` may be channel-slice views of concat buffers (pixel stride > C): the kernel walks
+    rows x C with each tensor's own stride, never the flat span of a strided view."""
+    N, C, H, W = y.shape
+    Cp = round8(C)
+    g = empty_nhwc(N, C, H, W, y.device)
+    for t in (dy, y):
+        if not is_nhwc(t) or ld_of(t) < Cp or ld_of(t) % 8:
+            raise ValueError("act_grad: operands must be NHWC with a padded pixel stride >= round8(C)")
+    lib().act_bwd_rows(ptr(dy), ld_of(dy), ptr(y), ld_of(y), ptr(g), ld_of(g), N * H * W, Cp, act, float(slope),
+                       stream_handle())
+    return g
+
+
 def nhwc_numel(t: torch.Tensor) -> int:
     """Elements spanned by an NHWC tensor including channel padding (flat kernel length)."""
     N, C, H, W = t.shape

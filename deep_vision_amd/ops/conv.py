@@ -15,7 +15,8 @@ import torch
 import torch.nn.functional as TF
 
 from . import wcache
-from .common import (ACT_IDS, BF16, CL, F32, alloc_cl, as_nhwc, empty_nhwc, grad_nhwc, grad_sink, is_nhwc, ld_of, lib,
+from .common import (ACT_IDS, BF16, CL, F32, act_grad, alloc_cl, as_nhwc, empty_nhwc, grad_nhwc, grad_sink, is_nhwc,
+                     ld_of, lib,
                      like_layout, empty_layout, native, nhwc_numel, ptr, round8, stream_handle)
 
 STAT_SHARDS = 64
@@ -322,11 +323,8 @@ class _ConvFn(torch.autograd.Function):
                 return (g, None, None) + (None,) * 13
             return (None,) * 16
         dy = grad_nhwc(dy)
-        if act:
-            dy = like_layout(dy, y)  # the saved output's exact layout (dy may be a concat slice)
-            g = empty_layout(y)
-            lib().act_bwd(ptr(dy), ptr(y), ptr(g), nhwc_numel(y), act, float(slope), stream_handle())
-            dy = g
+        if act:  # y and dy may be channel-slice views of concat buffers: strided rows kernel
+            dy = act_grad(dy, y, act, slope)
         dx = dw = db = None
         join, role = ctx.join
         if ctx.needs_input_grad[0]:
@@ -427,10 +425,7 @@ class _StemConvFn(torch.autograd.Function):
         N = xp.shape[0]
         dy = grad_nhwc(dy)
         if act:
-            dy = like_layout(dy, y)
-            g = empty_layout(y)
-            lib().act_bwd(ptr(dy), ptr(y), ptr(g), nhwc_numel(y), act, float(slope), stream_handle())
-            dy = g
+            dy = act_grad(dy, y, act, slope)
         dw = db = None
         if ctx.needs_input_grad[1]:
             ws = _wgrad_workspace(O * R * Sp * 4, xp.device)  # [O][R][Sp][4], zero on entry and exit
@@ -735,10 +730,7 @@ class _DWConvFn(torch.autograd.Function):
             return (None,) * 10
         dy = grad_nhwc(dy)
         if act:
-            dy = like_layout(dy, y)
-            g = empty_layout(y)
-            lib().act_bwd(ptr(dy), ptr(y), ptr(g), nhwc_numel(y), act, float(slope), stream_handle())
-            dy = g
+            dy = act_grad(dy, y, act, slope)
         N, C, H, W = x.shape
         K = weight.shape[2]
         P, Q = dy.shape[2], dy.shape[3]
