@@ -345,7 +345,7 @@ class _ConvFn(torch.autograd.Function):
                 dw = None
         if has_bias and ctx.needs_input_grad[2]:
             db = _channel_sum(dy)
-        return dx, dw, db, None, None, None, None, None, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 # ---------------------------------------------------------------------------------------
