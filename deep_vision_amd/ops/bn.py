@@ -288,6 +288,8 @@ def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None, residu
     mom = bn_momentum(bn) if bn.training and bn.track_running_stats else 0.0
     rm = bn.running_mean if bn.track_running_stats else None
     rv = bn.running_var if bn.track_running_stats else None
+    if not (x.dtype == BF16 and is_nhwc(x) and ld_of(x) == x.shape[1]):
+        x = x.to(dtype=BF16).contiguous(memory_format=torch.channels_last)
     if residual is not None and not (is_nhwc(residual) and ld_of(residual) == residual.shape[1]):
         residual = residual.to(dtype=BF16).contiguous(memory_format=torch.channels_last)
         residual_join = None  # the residual reaches its source through a copy
