@@ -26,11 +26,18 @@
 
 namespace {
 
-constexpr int NT = 256;
 constexpr int EPI_PITCH = 72;                      // bf16 elements per staged row (64 + 8 pad)
 constexpr int EPI_WAVE_BYTES = 64 * EPI_PITCH * 2;  // 9216
-constexpr int EPI_BYTES = 4 * EPI_WAVE_BYTES;       // 36864
-constexpr int STAT_BYTES = 2048;
+// every wave owns a WMT x 64 output sub-tile (WMT = 64 or 128 output pixels x 64 channels):
+// a BM x BN tile runs on (BM/WMT)*(BN/64) waves. A 128-row wave tile reads 12 LDS fragments per
+// 32 MFMAs instead of 8 per 16 and issues half the DMA instructions per MFMA.
+template <int BM_, int BN_, int WMT = 64>
+constexpr int n_waves() { return (BM_ / WMT) * (BN_ / 64); }
+template <int BM_, int BN_, int WMT = 64>
+constexpr int epi_bytes() { return n_waves<BM_, BN_, WMT>() * EPI_WAVE_BYTES; }
+// statistics scratch behind the staged tile: [WM][BN][2] (fwd BN stats) or [waves][64][2] (BNR)
+template <int BM_, int BN_, int WMT = 64>
+constexpr int stat_bytes() { return n_waves<BM_, BN_, WMT>() * 64 * 2 * 4; }
 
 enum { KM_FAST = 0, KM_GENERIC = 1, KM_TGATHER = 2 };
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_LEAKY = 2 };
@@ -59,6 +66,8 @@ struct FwdParams {
   const uint8_t* resbits;  // RES only: res is masked by act'() bits before the add
   int resact; float resslope;
   int reflect;             // generic loader: reflected instead of zero-filled out-of-image taps
+  int ksplit, kt_per;      // split-K: K-tiles [split*kt_per, +kt_per) per block (kernels.h)
+  float* ypart;            // split-K fp32 slabs [ksplit][M][N] (single group)
 };
 
 // ReflectionPad2d index map (pad < n): -1 -> 1, n -> n - 2
@@ -126,14 +135,24 @@ DV_DEVICE void wait_vm() {
 // layers the epilogue VALU outweighs the MFMA work).
 enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_FULL = 2 };
 
-template <int BM_, int BN_, int BK_, int KMODE, bool RES, int STAGES, bool BNR = false, int EPI = EPI_FULL>
-__global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
-  constexpr int WN = BN_ / 64, WM = BM_ / 64;
-  static_assert(WN * WM == 4, "4 waves of 64x64");
+// 256 threads (4 waves: one per SIMD, two blocks per CU) or 512 threads (8 waves: two per SIMD
+// from one block, whose deep LDS ring then holds one CU); __launch_bounds__' second argument is
+// waves per SIMD, so both forms get up to 256 VGPRs.
+template <int BM_, int BN_, int BK_, int KMODE, bool RES, int STAGES, bool BNR = false, int EPI = EPI_FULL,
+          int WMT = 64>
+__global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_kernel(FwdParams p) {
+  constexpr int WN = BN_ / 64, WM = BM_ / WMT;
+  constexpr int NW = WN * WM;
+  constexpr int FM = WMT / 16;         // M fragments per wave (4 or 8)
+  constexpr int HM = WMT / 64;         // 64-row epilogue passes per wave
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  static_assert(WMT == 64 || WMT == 128, "wave tile rows");
+  constexpr int EPI_BYTES = epi_bytes<BM_, BN_, WMT>();
   constexpr int CH = BK_ / 8;          // 16-B chunks per LDS row
   constexpr int RPI = 64 / CH;         // rows written by one 1-KB DMA wave-instruction
-  constexpr int MI = BM_ / RPI / 4;    // M-operand DMA instructions per wave per K-tile
-  constexpr int NI = BN_ / RPI / 4;    // N-operand DMA instructions per wave per K-tile
+  constexpr int MI = BM_ / RPI / NW;   // M-operand DMA instructions per wave per K-tile
+  constexpr int NI = BN_ / RPI / NW;   // N-operand DMA instructions per wave per K-tile
+  static_assert(MI * RPI * NW == BM_ && NI * RPI * NW == BN_, "loader rows must split evenly over the waves");
   constexpr int KK = BK_ / 32;         // 32-deep MFMA steps per K-tile
   constexpr int STAGE = stage_bytes<BM_, BN_, BK_>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -144,9 +163,13 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
   const int tiles_m = (p.M + BM_ - 1) / BM_, tiles_n = (p.N + BN_ - 1) / BN_;
   int logical = xcd_remap(blockIdx.x, gridDim.x);
   const int tn = logical % tiles_n; logical /= tiles_n;
-  const int tm = logical % tiles_m;
-  const int grp = logical / tiles_m;
+  const int tm = logical % tiles_m; logical /= tiles_m;
+  const int split = logical % p.ksplit;
+  const int grp = logical / p.ksplit;
   const int m0 = tm * BM_, n0 = tn * BN_;
+  const int nt_all = (p.K + BK_ - 1) / BK_;
+  const int kt0 = split * p.kt_per;                     // first K-tile of this block
+  const int nt = min(nt_all, kt0 + p.kt_per) - kt0;     // K-tiles of this block
   const char* zero = dv_zero_page;
   const int64_t goff_x = (int64_t)grp * p.Cg;
 
@@ -187,8 +210,13 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
     }
   }
 
-  // FASTC tap walker (wave-uniform)
+  // FASTC tap walker (wave-uniform), started at this block's first K-tile (every K-tile lies
+  // inside one tap: Cg % 64 == 0)
   int t_r = 0, t_s = 0, t_c = 0;
+  if (KMODE == KM_FAST && kt0 > 0) {
+    const int k0 = kt0 * BK_, rs = k0 / p.Cg;
+    t_c = k0 - rs * p.Cg; t_r = rs / p.S; t_s = rs - t_r * p.S;
+  }
   auto stage = [&](int kt, int buf) {
     char* img_n = smem + buf * STAGE;
     char* img_m = img_n + BN_ * BK_ * 2;
@@ -240,40 +268,40 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
     }
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[4][FM];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < FM; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nt = (p.K + BK_ - 1) / BK_;
   auto compute = [&](int buf) {
     const char* img_n = smem + buf * STAGE;
     const char* img_m = img_n + BN_ * BK_ * 2;
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
-      bf16x8 fa[4], fb[4];
+      bf16x8 fa[4], fb[FM];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < 4; ++j)
         fa[j] = read_kc<BK_>(img_n, wave_n * 64 + j * 16 + (lane & 15), kk * 4 + (lane >> 4));
-        fb[j] = read_kc<BK_>(img_m, wave_m * 64 + j * 16 + (lane & 15), kk * 4 + (lane >> 4));
-      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        fb[i] = read_kc<BK_>(img_m, wave_m * WMT + i * 16 + (lane & 15), kk * 4 + (lane >> 4));
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < FM; ++i)
           acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[j], fb[i], acc[j][i], 0, 0, 0);
     }
   };
   if constexpr (STAGES == 2) {
     // double buffer, one barrier per K-tile: the DMA of tile t+1 overlaps the MFMAs of tile t
-    stage(0, 0);
+    stage(kt0, 0);
     advance();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int t = 0; t < nt; ++t) {
       const int cur = t & 1;
-      if (t + 1 < nt) { stage(t + 1, cur ^ 1); advance(); }
+      if (t + 1 < nt) { stage(kt0 + t + 1, cur ^ 1); advance(); }
       compute(cur);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -285,7 +313,7 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
     constexpr int IPT = MI + NI;
 #pragma unroll
     for (int s = 0; s < STAGES - 1; ++s)
-      if (s < nt) { stage(s, s); advance(); }
+      if (s < nt) { stage(kt0 + s, s); advance(); }
     int cur = 0, nxt = STAGES - 1;
     for (int t = 0; t < nt; ++t) {
       const int ahead = min(nt - 1, t + STAGES - 2) - t;  // tiles issued after t
@@ -294,7 +322,7 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
       else wait_vm<0>();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      if (t + STAGES - 1 < nt) { stage(t + STAGES - 1, nxt); advance(); }
+      if (t + STAGES - 1 < nt) { stage(kt0 + t + STAGES - 1, nxt); advance(); }
       compute(cur);
       cur = cur + 1 == STAGES ? 0 : cur + 1;
       nxt = nxt + 1 == STAGES ? 0 : nxt + 1;
@@ -302,59 +330,129 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
     __syncthreads();  // every DMA retired (vmcnt(0) on the last tile): smem is free for the epilogue
   }
 
-  // ---------------- epilogue ----------------
-  // acc[j][i][r]: n_local = j*16 + (lane>>4)*4 + r, m_local = i*16 + (lane&15) within the wave tile
-  const int nw0 = n0 + wave_n * 64;  // first channel of this wave
-  float bsum[4][4], bsq[4][4];
-  u16* st = reinterpret_cast<u16*>(smem + wid * EPI_WAVE_BYTES);
+  // ---------------- split-K epilogue: raw fp32 partial tile -> this split's slab ----------------
+  if constexpr (EPI == EPI_FULL && !RES && !BNR) {
+    if (p.ypart) {
+      float* slab = p.ypart + (int64_t)split * p.M * p.N;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    float bv[4];
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wave_n * 64 + j * 16 + (lane >> 4) * 4;  // N % 4 == 0: whole float4 or none
+        if (n >= p.N) continue;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = nw0 + j * 16 + (lane >> 4) * 4 + r;
-      bv[r] = 0.f;
-      if constexpr (EPI == EPI_FULL) bv[r] = (p.bias && n < p.N) ? p.bias[grp * p.N + n] : 0.f;
-      bsum[j][r] = 0.f; bsq[j][r] = 0.f;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int ml = i * 16 + (lane & 15);
-      const bool mv = m0 + wave_m * 64 + ml < p.M;
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float t = acc[j][i][r];
-        if constexpr (EPI == EPI_FULL) {
-          t += bv[r];
-          if (p.act == ACT_RELU) t = fmaxf(t, 0.f);
-          else if (p.act == ACT_LEAKY) t = t > 0.f ? t : t * p.slope;
-        }
-        v[r] = t;
-        if constexpr (EPI != EPI_PLAIN) {
-          if (mv) { bsum[j][r] += t; bsq[j][r] += t * t; }
+        for (int i = 0; i < FM; ++i) {
+          const int m = m0 + wave_m * WMT + i * 16 + (lane & 15);
+          if (m < p.M) *reinterpret_cast<f32x4*>(slab + (int64_t)m * p.N + n) = acc[j][i];
         }
       }
-      uint2 pk; pk.x = pack2bf(v[0], v[1]); pk.y = pack2bf(v[2], v[3]);
-      *reinterpret_cast<uint2*>(st + ml * EPI_PITCH + j * 16 + (lane >> 4) * 4) = pk;
+      return;
     }
   }
-  // Prefetch what the store loop reads besides the staged tile (the residual gradient, the BN
-  // input and mask) for all 8 row groups now: issued in the loop they would each wait behind the
-  // previous iteration's stores (one vmcnt queue for loads and stores), 8 serial round trips.
+  // ---------------- epilogue ----------------
+  // acc[j][i][r]: n_local = j*16 + (lane>>4)*4 + r, m_local = i*16 + (lane&15) within the wave
+  // tile; a 128-row wave tile is written as two 64-row passes through the same staging rows.
+  const int nw0 = n0 + wave_n * 64;  // first channel of this wave
   const int64_t goff_y = (int64_t)grp * p.N;
   const bool vec = ((p.N & 7) == 0) && ((p.ldy & 7) == 0) && ((goff_y & 7) == 0);
   constexpr bool PF = RES || BNR;
-  int64_t pf_off[PF ? 8 : 1];
-  uint4 pf_res[RES ? 8 : 1], pf_x[BNR ? 8 : 1];
-  uint32_t pf_mb[BNR ? 8 : 1], pf_rmb[RES ? 8 : 1];
-  if constexpr (PF) {
+  float bsum[4][4], bsq[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { bsum[j][r] = 0.f; bsq[j][r] = 0.f; }
+  // BNR: this lane's 8 channels are fixed over the store loop (rows it*8 + lane/8)
+  float bs[8], bq[8], bmu[8], bis[8], bms[8], bmh[8];
+  if constexpr (BNR) {
+    const int nb = nw0 + (lane & 7) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      bs[e] = 0.f; bq[e] = 0.f;
+      const bool ok = nb + e < p.N;
+      bms[e] = ok ? p.bnprm[nb + e] : 0.f;
+      bmh[e] = ok ? p.bnprm[p.N + nb + e] : 0.f;
+      bmu[e] = ok ? p.bnprm[2 * p.N + nb + e] : 0.f;
+      bis[e] = ok ? p.bnprm[3 * p.N + nb + e] : 0.f;
+    }
+  }
+  u16* st = reinterpret_cast<u16*>(smem + wid * EPI_WAVE_BYTES);
+#pragma unroll
+  for (int h = 0; h < HM; ++h) {
+    const int mw0 = m0 + wave_m * WMT + h * 64;  // first output row of this 64-row pass
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float bv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = nw0 + j * 16 + (lane >> 4) * 4 + r;
+        bv[r] = 0.f;
+        if constexpr (EPI == EPI_FULL) bv[r] = (p.bias && n < p.N) ? p.bias[grp * p.N + n] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ml = i * 16 + (lane & 15);
+        const bool mv = mw0 + ml < p.M;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float t = acc[j][h * 4 + i][r];
+          if constexpr (EPI == EPI_FULL) {
+            t += bv[r];
+            if (p.act == ACT_RELU) t = fmaxf(t, 0.f);
+            else if (p.act == ACT_LEAKY) t = t > 0.f ? t : t * p.slope;
+          }
+          v[r] = t;
+          if constexpr (EPI != EPI_PLAIN) {
+            if (mv) { bsum[j][r] += t; bsq[j][r] += t * t; }
+          }
+        }
+        uint2 pk; pk.x = pack2bf(v[0], v[1]); pk.y = pack2bf(v[2], v[3]);
+        *reinterpret_cast<uint2*>(st + ml * EPI_PITCH + j * 16 + (lane >> 4) * 4) = pk;
+      }
+    }
+    // Prefetch what the store loop reads besides the staged tile (the residual gradient, the BN
+    // input and mask) for all 8 row groups now: issued in the loop they would each wait behind the
+    // previous iteration's stores (one vmcnt queue for loads and stores), 8 serial round trips.
+    int64_t pf_off[PF ? 8 : 1];
+    uint4 pf_res[RES ? 8 : 1], pf_x[BNR ? 8 : 1];
+    uint32_t pf_mb[BNR ? 8 : 1], pf_rmb[RES ? 8 : 1];
+    if constexpr (PF) {
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int m = mw0 + it * 8 + (lane >> 3);
+        const int n = nw0 + (lane & 7) * 8;
+        int64_t off = -1;
+        if (m < p.M && n < p.N) {
+          int64_t opix;
+          if (p.identity_map) opix = m;
+          else {
+            const int img = (int)fdiv((uint32_t)m, p.div_pq), rem = m - img * (p.P * p.Q);
+            const int pp = (int)fdiv((uint32_t)rem, p.div_q), qq = rem - pp * p.Q;
+            opix = ((int64_t)img * p.OH + pp * p.osh + p.oph) * p.OW + qq * p.osw + p.opw;
+          }
+          off = opix * p.ldy + goff_y + n;
+        }
+        pf_off[it] = off;
+        const bool ld = off >= 0 && vec;
+        if constexpr (RES) {
+          pf_res[it] = ld ? *reinterpret_cast<const uint4*>(p.res + off) : uint4{0u, 0u, 0u, 0u};
+          pf_rmb[it] = (off >= 0 && p.resbits) ? (uint32_t)p.resbits[off >> 3] : 0xffu;
+        }
+        if constexpr (BNR) {
+          pf_x[it] = ld ? *reinterpret_cast<const uint4*>(p.bnx + off) : uint4{0u, 0u, 0u, 0u};
+          pf_mb[it] = (ld && p.bnmode == 3) ? (uint32_t)p.bnbits[off >> 3] : 0u;
+        }
+      }
+    }
+    // staged rows -> global: each wave writes its 64 rows x 64 channels as 16-B pieces (the
+    // wave reads back only its own staging rows: LDS order within a wave, no barrier)
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
-      const int m = m0 + wave_m * 64 + it * 8 + (lane >> 3);
-      const int n = nw0 + (lane & 7) * 8;
-      int64_t off = -1;
-      if (m < p.M && n < p.N) {
+      const int rl = it * 8 + (lane >> 3), ch = (lane & 7) * 8;
+      const int m = mw0 + rl;
+      const int n = nw0 + ch;
+      if (m >= p.M || n >= p.N) continue;
+      int64_t yoff;
+      if constexpr (PF) yoff = pf_off[it];
+      else {
         int64_t opix;
         if (p.identity_map) opix = m;
         else {
@@ -362,17 +460,38 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
           const int pp = (int)fdiv((uint32_t)rem, p.div_q), qq = rem - pp * p.Q;
           opix = ((int64_t)img * p.OH + pp * p.osh + p.oph) * p.OW + qq * p.osw + p.opw;
         }
-        off = opix * p.ldy + goff_y + n;
+        yoff = opix * p.ldy + goff_y + n;
       }
-      pf_off[it] = off;
-      const bool ld = off >= 0 && vec;
-      if constexpr (RES) {
-        pf_res[it] = ld ? *reinterpret_cast<const uint4*>(p.res + off) : uint4{0u, 0u, 0u, 0u};
-        pf_rmb[it] = (off >= 0 && p.resbits) ? (uint32_t)p.resbits[off >> 3] : 0xffu;
-      }
-      if constexpr (BNR) {
-        pf_x[it] = ld ? *reinterpret_cast<const uint4*>(p.bnx + off) : uint4{0u, 0u, 0u, 0u};
-        pf_mb[it] = (ld && p.bnmode == 3) ? (uint32_t)p.bnbits[off >> 3] : 0u;
+      u16* dst = p.y + yoff;
+      const u16* src = st + rl * EPI_PITCH + ch;
+      if constexpr (RES) {  // residual-gradient join: dX += stashed gradient (fused instead of an add pass)
+        const u16* rp = p.res + yoff;
+        if (vec) {
+          uint4 a = *reinterpret_cast<const uint4*>(src), b = pf_res[it];
+          const u16* av = reinterpret_cast<const u16*>(&a);
+          const u16* bw = reinterpret_cast<const u16*>(&b);
+          uint4 o;
+          uint32_t* ov = reinterpret_cast<uint32_t*>(&o);
+          const uint32_t rmb = pf_rmb[it];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            ov[e] = pack2bf(bf2f(av[2 * e]) + masked_res(bf2f(bw[2 * e]), rmb, 2 * e, p.resact, p.resslope),
+                            bf2f(av[2 * e + 1]) + masked_res(bf2f(bw[2 * e + 1]), rmb, 2 * e + 1, p.resact, p.resslope));
+          *reinterpret_cast<uint4*>(dst) = o;
+          if constexpr (BNR) bn_bwd_accum(p, o, pf_x[it], pf_mb[it], bs, bq, bmu, bis, bms, bmh);
+        } else {
+          const uint32_t rmb = pf_rmb[it];
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (n + e < p.N) dst[e] = f2bf(bf2f(src[e]) + masked_res(bf2f(rp[e]), rmb, e, p.resact, p.resslope));
+        }
+      } else if (vec) {
+        const uint4 o = *reinterpret_cast<const uint4*>(src);
+        *reinterpret_cast<uint4*>(dst) = o;
+        if constexpr (BNR) bn_bwd_accum(p, o, pf_x[it], pf_mb[it], bs, bq, bmu, bis, bms, bmh);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) if (n + e < p.N) dst[e] = src[e];
       }
     }
   }
@@ -390,84 +509,18 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
           sh[(wave_m * BN_ + nl) * 2 + 1] = s2;
         }
       }
-  }
-  __syncthreads();
-  if (EPI != EPI_PLAIN && p.stats && threadIdx.x < BN_) {
-    const float* sh = reinterpret_cast<const float*>(smem + EPI_BYTES);
-    const int n = n0 + threadIdx.x;
-    if (n < p.N) {
-      float s1 = 0.f, s2 = 0.f;
+    __syncthreads();
+    if (threadIdx.x < BN_) {
+      const int n = n0 + threadIdx.x;
+      if (n < p.N) {
+        float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-      for (int w = 0; w < WM; ++w) { s1 += sh[(w * BN_ + threadIdx.x) * 2]; s2 += sh[(w * BN_ + threadIdx.x) * 2 + 1]; }
-      const int64_t ncols = (int64_t)p.G * p.N;
-      float* a = p.stats + (int64_t)(tm % DV_STAT_SHARDS) * 2 * ncols;
-      atomicAdd(a + grp * p.N + n, s1);
-      atomicAdd(a + ncols + grp * p.N + n, s2);
-    }
-  }
-  // staged tile -> global: each wave writes its 64 rows x 64 channels as 16-B pieces
-  // BNR: this lane's 8 channels are fixed over the store loop (rows it*8 + lane/8)
-  float bs[8], bq[8], bmu[8], bis[8], bms[8], bmh[8];
-  if constexpr (BNR) {
-    const int nb = nw0 + (lane & 7) * 8;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      bs[e] = 0.f; bq[e] = 0.f;
-      const bool ok = nb + e < p.N;
-      bms[e] = ok ? p.bnprm[nb + e] : 0.f;
-      bmh[e] = ok ? p.bnprm[p.N + nb + e] : 0.f;
-      bmu[e] = ok ? p.bnprm[2 * p.N + nb + e] : 0.f;
-      bis[e] = ok ? p.bnprm[3 * p.N + nb + e] : 0.f;
-    }
-  }
-#pragma unroll
-  for (int it = 0; it < 8; ++it) {
-    const int rl = it * 8 + (lane >> 3), ch = (lane & 7) * 8;
-    const int m = m0 + wave_m * 64 + rl;
-    const int n = nw0 + ch;
-    if (m >= p.M || n >= p.N) continue;
-    int64_t yoff;
-    if constexpr (PF) yoff = pf_off[it];
-    else {
-      int64_t opix;
-      if (p.identity_map) opix = m;
-      else {
-        const int img = (int)fdiv((uint32_t)m, p.div_pq), rem = m - img * (p.P * p.Q);
-        const int pp = (int)fdiv((uint32_t)rem, p.div_q), qq = rem - pp * p.Q;
-        opix = ((int64_t)img * p.OH + pp * p.osh + p.oph) * p.OW + qq * p.osw + p.opw;
+        for (int w = 0; w < WM; ++w) { s1 += sh[(w * BN_ + threadIdx.x) * 2]; s2 += sh[(w * BN_ + threadIdx.x) * 2 + 1]; }
+        const int64_t ncols = (int64_t)p.G * p.N;
+        float* a = p.stats + (int64_t)(tm % DV_STAT_SHARDS) * 2 * ncols;
+        atomicAdd(a + grp * p.N + n, s1);
+        atomicAdd(a + ncols + grp * p.N + n, s2);
       }
-      yoff = opix * p.ldy + goff_y + n;
-    }
-    u16* dst = p.y + yoff;
-    const u16* src = st + rl * EPI_PITCH + ch;
-    if constexpr (RES) {  // residual-gradient join: dX += stashed gradient (fused instead of an add pass)
-      const u16* rp = p.res + yoff;
-      if (vec) {
-        uint4 a = *reinterpret_cast<const uint4*>(src), b = pf_res[it];
-        const u16* av = reinterpret_cast<const u16*>(&a);
-        const u16* bw = reinterpret_cast<const u16*>(&b);
-        uint4 o;
-        uint32_t* ov = reinterpret_cast<uint32_t*>(&o);
-        const uint32_t rmb = pf_rmb[it];
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          ov[e] = pack2bf(bf2f(av[2 * e]) + masked_res(bf2f(bw[2 * e]), rmb, 2 * e, p.resact, p.resslope),
-                          bf2f(av[2 * e + 1]) + masked_res(bf2f(bw[2 * e + 1]), rmb, 2 * e + 1, p.resact, p.resslope));
-        *reinterpret_cast<uint4*>(dst) = o;
-        if constexpr (BNR) bn_bwd_accum(p, o, pf_x[it], pf_mb[it], bs, bq, bmu, bis, bms, bmh);
-      } else {
-        const uint32_t rmb = pf_rmb[it];
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-          if (n + e < p.N) dst[e] = f2bf(bf2f(src[e]) + masked_res(bf2f(rp[e]), rmb, e, p.resact, p.resslope));
-      }
-    } else if (vec) {
-      const uint4 o = *reinterpret_cast<const uint4*>(src);
-      *reinterpret_cast<uint4*>(dst) = o;
-      if constexpr (BNR) bn_bwd_accum(p, o, pf_x[it], pf_mb[it], bs, bq, bmu, bis, bms, bmh);
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) if (n + e < p.N) dst[e] = src[e];
     }
   }
   if constexpr (BNR) {
@@ -481,7 +534,7 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
         bq[e] += __shfl_xor(bq[e], off, 64);
       }
     }
-    float* sh = reinterpret_cast<float*>(smem + EPI_BYTES);  // [4 waves][64 channels][2]
+    float* sh = reinterpret_cast<float*>(smem + EPI_BYTES);  // [waves][64 channels][2]
     if (lane < 8) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -508,25 +561,35 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdParams p) {
   }
 }
 
+int g_last_ksplit = 1;  // splits actually launched by the last split-K launch (finalize pass)
+
 // the epilogue staging tile and the statistics scratch reuse the (drained) operand stages
-template <int BM_, int BN_, int BK_>
+template <int BM_, int BN_, int BK_, int WMT = 64>
 constexpr int lds_bytes(int stages) {
-  return stages * stage_bytes<BM_, BN_, BK_>() > EPI_BYTES + STAT_BYTES ? stages * stage_bytes<BM_, BN_, BK_>()
-                                                                       : EPI_BYTES + STAT_BYTES;
+  constexpr int epi = epi_bytes<BM_, BN_, WMT>() + stat_bytes<BM_, BN_, WMT>();
+  return stages * stage_bytes<BM_, BN_, BK_>() > epi ? stages * stage_bytes<BM_, BN_, BK_>() : epi;
 }
 
-template <int BM_, int BN_, int BK_, int KMODE, bool RES, int STAGES, bool BNR = false, int EPI = EPI_FULL>
+template <int BM_, int BN_, int BK_, int KMODE, bool RES, int STAGES, bool BNR = false, int EPI = EPI_FULL,
+          int WMT = 64>
 void launch_fwd(const FwdParams& p, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES, BNR, EPI>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes<BM_, BN_, BK_>(STAGES));
+    hipFuncSetAttribute((const void*)conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES, BNR, EPI, WMT>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes<BM_, BN_, BK_, WMT>(STAGES));
     attr = true;
   }
-  const int nt = (p.K + BK_ - 1) / BK_;
-  const size_t lds = lds_bytes<BM_, BN_, BK_>(nt < STAGES ? nt : STAGES);
-  const int blocks = ((p.M + BM_ - 1) / BM_) * ((p.N + BN_ - 1) / BN_) * p.G;
-  conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES, BNR, EPI><<<dim3(blocks), dim3(NT), lds, st>>>(p);
+  FwdParams q = p;
+  const int nt_all = (p.K + BK_ - 1) / BK_;
+  q.ksplit = p.ypart ? max(1, min(p.ksplit, nt_all)) : 1;
+  q.kt_per = (nt_all + q.ksplit - 1) / q.ksplit;
+  q.ksplit = (nt_all + q.kt_per - 1) / q.kt_per;  // no empty splits
+  const int nt = q.kt_per;
+  const size_t lds = lds_bytes<BM_, BN_, BK_, WMT>(nt < STAGES ? nt : STAGES);
+  const int blocks = ((p.M + BM_ - 1) / BM_) * ((p.N + BN_ - 1) / BN_) * p.G * q.ksplit;
+  conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES, BNR, EPI, WMT>
+      <<<dim3(blocks), dim3(64 * n_waves<BM_, BN_, WMT>()), lds, st>>>(q);
+  if (p.ypart) g_last_ksplit = q.ksplit;
 }
 
 int g_fwd_variant = 0;  // benchmarking override of the tile / pipeline choice (0 = heuristic)
@@ -536,10 +599,23 @@ int g_fwd_variant = 0;  // benchmarking override of the tile / pipeline choice (
 //    runs best with a 3-deep ring, long K with the plain double buffer;
 //  * N > 64: 128x128. K <= 64 is one K-tile (single stage, most blocks per CU); up to K < 2048
 //    BK=32 (32 KB of LDS: up to 4 blocks per CU) beats BK=64 by 5-25 %; long-K layers (3x3 x
-//    256+ channels, 2048-deep 1x1) keep BK=64.
+//    256+ channels, 2048-deep 1x1) keep BK=64;
+//  * N % 256 == 0, K >= 1024 and >= 192 tiles of 256x256: one 512-thread block per CU with
+//    128x64 wave tiles (half the LDS fragment reads and DMA instructions per MFMA) is 8-12 %
+//    faster (3x3x256 @14: 67 vs 76 us; 1x1 1024->256 @14: 38 vs 42 us); with fewer tiles
+//    (the 7x7 stage: 98 tiles on 256 CUs) it loses to the 4-block-per-CU 128x128 tile.
+//    (profiles/convbench_wave_tiles.txt)
+template <int KMODE>
+bool big_tile_ok(const FwdParams& p) {
+  if (KMODE != KM_FAST || p.N % 256 != 0 || p.K < 1024) return false;
+  const int64_t tiles = (int64_t)((p.M + 255) / 256) * (p.N / 256) * p.G;
+  return tiles >= 192 || g_fwd_variant == 100;  // 100: tests force it at small shapes
+}
+
 template <int KMODE, bool RES, bool BNR, int EPI>
 void launch_heuristic(const FwdParams& p, hipStream_t st) {
   if (KMODE == KM_FAST) {
+    if (big_tile_ok<KMODE>(p)) { launch_fwd<256, 256, 64, KMODE, RES, 2, BNR, EPI, 128>(p, st); return; }
     if (p.N <= 64) {
       if (p.K <= 256) launch_fwd<256, 64, 32, KMODE, RES, 3, BNR, EPI>(p, st);
       else launch_fwd<256, 64, 32, KMODE, RES, 2, BNR, EPI>(p, st);
@@ -570,9 +646,14 @@ void dispatch_res(const FwdParams& p, hipStream_t st) {
       case 7: return launch_fwd<128, 128, 32, KMODE, RES, 4>(p, st);
       case 8: return launch_fwd<128, 128, 32, KMODE, RES, 2>(p, st);
       case 9: return launch_fwd<256, 64, 32, KMODE, RES, 3>(p, st);
+      // 8-wave tiles (one 512-thread block per CU, deep LDS-DMA ring)
+      case 10: return launch_fwd<256, 128, 64, KMODE, RES, 3>(p, st);
+      // 128-row wave tiles (a wave = 128 pixels x 64 channels)
+      case 12: return launch_fwd<256, 128, 64, KMODE, RES, 2, false, EPI_FULL, 128>(p, st);  // 4 waves
+      case 14: return launch_fwd<256, 256, 64, KMODE, RES, 2, false, EPI_FULL, 128>(p, st);  // 8 waves
       default: break;
     }
-    const bool full = p.bias || p.act;
+    const bool full = p.bias || p.act || p.ypart;  // split-K slabs are written by the FULL form
     if (!full && !p.stats) launch_heuristic<KMODE, RES, false, EPI_PLAIN>(p, st);
     else if (!full) launch_heuristic<KMODE, RES, false, EPI_STATS>(p, st);
     else launch_heuristic<KMODE, RES, false, EPI_FULL>(p, st);
@@ -596,6 +677,30 @@ void dispatch_tile(const FwdParams& p, hipStream_t st) {
   else dispatch_res<KMODE, false>(p, st);
 }
 
+// y[m][n] = act(sum_s ypart[s][m][n] + bias[n]) in bf16; the slabs are summed in split order
+// (bitwise reproducible). 4 columns per thread.
+__global__ __launch_bounds__(256) void splitk_finalize_kernel(const float* __restrict__ ypart, int ksplit, int M, int N,
+                                                              const float* __restrict__ bias, int act, float slope,
+                                                              u16* __restrict__ y, int ldy) {
+  const int nq = N >> 2;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)M * nq) return;
+  const int m = (int)(i / nq), n = (int)(i - (int64_t)m * nq) * 4;
+  const int64_t slab = (int64_t)M * N;
+  f32x4 a = *reinterpret_cast<const f32x4*>(ypart + (int64_t)m * N + n);
+  for (int s = 1; s < ksplit; ++s) a += *reinterpret_cast<const f32x4*>(ypart + s * slab + (int64_t)m * N + n);
+  float v[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float t = a[r] + (bias ? bias[n + r] : 0.f);
+    if (act == ACT_RELU) t = fmaxf(t, 0.f);
+    else if (act == ACT_LEAKY) t = t > 0.f ? t : t * slope;
+    v[r] = t;
+  }
+  uint2 pk; pk.x = pack2bf(v[0], v[1]); pk.y = pack2bf(v[2], v[3]);
+  *reinterpret_cast<uint2*>(y + (int64_t)m * ldy + n) = pk;
+}
+
 }  // namespace
 
 void dv_conv_fwd_variant(int v) { g_fwd_variant = v; }
@@ -615,6 +720,14 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
   p.bnmode = a.bnmode; p.bnact = a.bnact; p.bnslope = a.bnslope;
   p.resbits = (const uint8_t*)a.resbits; p.resact = a.resact; p.resslope = a.resslope;
   p.reflect = a.reflect;
+  p.ksplit = 1; p.kt_per = 1 << 30; p.ypart = nullptr;
+  if (a.ksplit > 1 && a.ypart) {
+    // split-K serves plain GEMM-shaped convs: single group, identity output map, bias/act only
+    const bool ok = a.G == 1 && !a.tgather && !a.res && !a.stats && !a.bnmode && !a.reflect && (a.Kout % 4) == 0 &&
+                    (a.ldy % 4) == 0 && a.OH == a.P && a.OW == a.Q && a.osh == 1 && a.osw == 1 && !a.oph && !a.opw;
+    if (!ok) return -1;
+    p.ksplit = a.ksplit; p.ypart = a.ypart;
+  }
   if (p.reflect && (a.tgather || p.ph >= p.Hin || p.pw >= p.Win || p.ph < 0 || p.pw < 0 || p.bnmode)) return -1;
   // the mask bits are indexed by the dense element offset of y: a single-group tensor whose
   // pixel stride is its channel count, written by the identity-mapped (stride-1) epilogue
@@ -652,5 +765,10 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
   if (a.tgather) dispatch_tile<KM_TGATHER>(p, st);
   else if (p.Cg % 64 == 0 && p.R <= 16 && p.S <= 16 && !p.reflect) dispatch_tile<KM_FAST>(p, st);
   else dispatch_tile<KM_GENERIC>(p, st);
+  if (p.ypart) {
+    const int64_t n4 = (int64_t)p.M * (p.N / 4);
+    splitk_finalize_kernel<<<dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st>>>(
+        p.ypart, g_last_ksplit, p.M, p.N, p.bias, p.act, p.slope, p.y, p.ldy);
+  }
   return bn_status;
 }

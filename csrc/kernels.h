@@ -35,6 +35,12 @@ struct ConvFwdArgs {
   // 1: out-of-image taps read the reflected pixel (ReflectionPad2d fused into the gather;
   // CycleGAN R/CycleGAN/tensorflow/models.py:8-14) instead of zeros
   int reflect;
+  // split-K (short-M GEMMs such as Linear at batch 128: 25088->4096 is 32 tiles of 128x128 on
+  // 256 CUs): ksplit > 1 splits the K loop over blocks; each split writes an fp32 slab
+  // ypart[split][M][Kout] and a finalize pass sums the slabs in order, adds the bias, applies the
+  // activation and writes bf16 y (deterministic; bias/act only, no statistics / residual / BN)
+  int ksplit;
+  float* ypart;
 };
 
 struct ConvWgradArgs {

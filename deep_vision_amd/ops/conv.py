@@ -86,8 +86,22 @@ def _channel_sum(dy: torch.Tensor) -> torch.Tensor:
     return acc[:, 0, :C].sum(0)
 
 
+def gemm_ksplit(M, N, K):
+    """Split-K factor for a GEMM-shaped launch (Linear fwd/dgrad): the 128x128 (or 256x64 for
+    N <= 64) tile grid of a short-M GEMM leaves most of the 256 CUs idle -- VGG16's 25088->4096
+    at batch 128 is 32 tiles -- so K is split until there are ~256 blocks, keeping >= 512 of K
+    per split (csrc/conv_fwd.hip splitk_finalize_kernel sums the fp32 slabs in order)."""
+    if N % 4 or K < 1024:
+        return 1
+    tiles = -(-M // 256) if N <= 64 else -(-M // 128) * -(-N // 128)
+    if tiles >= 128:
+        return 1
+    return max(1, min(16, 256 // tiles, K // 512))
+
+
 def conv_fwd_raw(x, wk, y, bias, stats, N, H, W, Cg, ldx, G, Kout, P, Q, R, S, stride, padding, dilation,
-                 act=0, slope=0.0, tgather=0, omap=None, ldy=None, res=None, bnref=None, resmask=None, reflect=False):
+                 act=0, slope=0.0, tgather=0, omap=None, ldy=None, res=None, bnref=None, resmask=None, reflect=False,
+                 ksplit=1):
     """Launch the implicit-GEMM kernel. ``bnref`` (ops.bn.BNRef): also reduce that BatchNorm's
     backward statistics over ``y`` in the epilogue; returns True when that was done.
     ``resmask`` (bits, act, slope): ``res`` is a raw gradient masked by act'() before the add."""
@@ -103,6 +117,9 @@ def conv_fwd_raw(x, wk, y, bias, stats, N, H, W, Cg, ldx, G, Kout, P, Q, R, S, s
         bn.update(resbits=ptr(resmask[0]), resact=int(resmask[1]), resslope=float(resmask[2]))
     if reflect:
         bn["reflect"] = 1
+    if ksplit > 1:  # fp32 slabs [ksplit][M][Kout], summed + bias + act by the finalize pass
+        part = torch.empty((ksplit, N * P * Q, Kout), dtype=F32, device=y.device)
+        bn.update(ksplit=int(ksplit), ypart=ptr(part))
     r = lib().conv_fwd(ptr(x), ptr(wk), ptr(y), ptr(bias), ptr(stats), N, H, W, Cg, ldx, G, Kout, P, Q, R, S, sh, sw,
                        ph, pw, dh, dw, tgather, OH, OW, osh, osw, oph, opw, ldy if ldy is not None else ld_of(y), act,
                        float(slope), ptr(res), stream_handle(), **bn)
@@ -629,7 +646,7 @@ class _LinearFn(torch.autograd.Function):
         y_full = (torch.zeros if Op != O else torch.empty)((N, Op), dtype=BF16, device=x.device)
         b = bias.detach().float().contiguous() if bias is not None else None
         conv_fwd_raw(x, wk, y_full, b, None, N, 1, 1, Kp, Kp, 1, O, 1, 1, 1, 1, (1, 1), (0, 0), (1, 1), act=act,
-                     slope=slope, ldy=Op)
+                     slope=slope, ldy=Op, ksplit=gemm_ksplit(N, O, Kp))
         y = y_full if Op == O else y_full[:, :O]
         ctx.save_for_backward(x, weight, bias, y if act else None)
         ctx.cfg = (act, slope, bias is not None, Kp, Op)
@@ -654,7 +671,7 @@ class _LinearFn(torch.autograd.Function):
             wd = _prep_weight(weight.view(O, K, 1, 1), 1, Op, mode=1, param=weight)  # [K][Op]
             dx_full = (torch.zeros if Kp != K else torch.empty)((N, Kp), dtype=BF16, device=dy.device)
             conv_fwd_raw(dy, wd, dx_full, None, None, N, 1, 1, Op, Op, 1, K, 1, 1, 1, 1, (1, 1), (0, 0), (1, 1),
-                         ldy=Kp)
+                         ldy=Kp, ksplit=gemm_ksplit(N, K, Op))
             dx = dx_full if Kp == K else dx_full[:, :K]
         if ctx.needs_input_grad[1]:
             sink = grad_sink(weight)

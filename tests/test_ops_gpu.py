@@ -208,6 +208,37 @@ def test_linear_odd_sizes():
     assert _rel(w.grad, wr.grad) < 5e-2
 
 
+@pytest.mark.parametrize("shape", [(128, 25088, 4096, True), (128, 4096, 4096, True), (64, 9216, 1000, False),
+                                   (8, 2048, 1000, True)])
+def test_linear_splitk(shape):
+    """Short-M Linear layers (VGG16 fc6/fc7, AlexNet fc6 at batch 64, ResNet fc at batch 8) run
+    with the K loop split over blocks and an ordered fp32 slab reduction (fwd and dgrad)."""
+    from deep_vision_amd import ops as F
+    from deep_vision_amd.ops.conv import gemm_ksplit
+
+    N, K, O, bias = shape
+    assert gemm_ksplit(N, O, K) > 1
+    x32 = torch.randn(N, K, device=DEV).bfloat16().float()
+    w = (torch.randn(O, K, device=DEV) * K ** -0.5).requires_grad_(True)
+    b = torch.randn(O, device=DEV).requires_grad_(True) if bias else None
+    x = x32.clone().to(torch.bfloat16).requires_grad_(True)
+    y = F.linear(x, w, b, act="relu")
+    wr = w.detach().bfloat16().float().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True) if bias else None
+    xr = x32.clone().requires_grad_(True)
+    yr = TF.relu(TF.linear(xr, wr, br))
+    assert _rel(y, yr) < 2e-2
+    g = torch.randn_like(yr).bfloat16().float()
+    y.backward(g.to(torch.bfloat16))
+    yr.backward(g)
+    assert _rel(x.grad, xr.grad) < 3e-2 and _cos(x.grad, xr.grad) > 0.9999
+    assert _rel(w.grad, wr.grad) < 3e-2
+    if bias:
+        assert _rel(b.grad, br.grad) < 2e-2
+    y2 = F.linear(x.detach(), w.detach(), None if b is None else b.detach(), act="relu")
+    assert torch.equal(F.linear(x.detach(), w.detach(), None if b is None else b.detach(), act="relu"), y2)
+
+
 def test_conv_transpose():
     from deep_vision_amd import ops as F
 
@@ -372,10 +403,11 @@ def test_conv_act_grad_from_concat_slice():
     w2 = (torch.randn(40, 32, 3, 3, device=DEV) * 0.1).requires_grad_(True)
     x = _nhwc(x32).requires_grad_(True)
     y = torch.cat([F.conv2d(x, w1, act="relu"), F.conv2d(x, w2, padding=1, act="relu")], 1)
-    g = torch.randn(2, 64, 9, 9, device=DEV)
+    g = torch.randn(2, 64, 9, 9, device=DEV).bfloat16().float()  # the operands the kernels see
     y.backward(_nhwc(g))
     xr = x32.clone().requires_grad_(True)
-    w1r, w2r = w1.detach().clone().requires_grad_(True), w2.detach().clone().requires_grad_(True)
+    w1r = w1.detach().bfloat16().float().requires_grad_(True)
+    w2r = w2.detach().bfloat16().float().requires_grad_(True)
     yr = torch.cat([TF.relu(TF.conv2d(xr, w1r)), TF.relu(TF.conv2d(xr, w2r, padding=1))], 1)
     yr.backward(g)
     assert _cos(x.grad, xr.grad) > 0.999

@@ -1,0 +1,218 @@
+"""Numerics of the hot-path kernels at the shapes the ResNet-50 / MobileNet steps dispatch, against
+an fp32 PyTorch reference of the same computation.
+
+The unit tests in test_ops_gpu.py use toy maps (7-32 px, batch 2). Here every case runs at a
+production shape so the kernels actually selected by the tile heuristics are the ones checked:
+  * whole bottleneck blocks (conv -> BN -> ReLU x3, projection / identity shortcut, fused
+    residual + ReLU, the BN-backward statistics folded into the dgrad epilogue, the gradient join
+    of the shortcut) at stage-1/2/3 shapes, forward and every parameter gradient;
+  * the 256x256 / 128-row-wave-tile forward variant (forced at a small batch);
+  * split-K weight gradient with a reduction dimension of 200,704 pixels;
+  * depthwise fwd/dgrad/wgrad at 112x112;
+  * the tap-packed stem at 224x224.
+The reference is the same module run through the torch backend in fp32 on bf16-rounded inputs; the forward is held to a few percent max error, every gradient to twice the deviation of
+PyTorch's own bf16 (autocast) path from that fp32 reference (bf16 activations flip ReLU masks at
+z ~ 0, which bounds the attainable gradient cosine at ~0.998 for a bottleneck block).
+"""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as TF
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+
+
+def _cos(a, b):
+    a, b = a.float().flatten(), b.float().flatten()
+    return (a @ b / (a.norm() * b.norm()).clamp_min(1e-12)).item()
+
+
+def _nhwc(t):
+    return t.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _ext():
+    from deep_vision_amd._ext import lib
+
+    lib()
+    torch.manual_seed(0)
+    yield
+    lib().conv_fwd_variant(0)
+
+
+def _reference(module, x32, dy32, xgrad=True, autocast=False):
+    """torch-backend forward/backward of a copy of ``module``: fp32, or PyTorch's own bf16 path
+    (autocast) -- the precision-matched yardstick. Parameters are NOT rounded: the native path
+    keeps BatchNorm affine and depthwise filters in fp32 and rounds only MFMA conv operands, as
+    autocast does (rounding BN's beta in the reference alone shifts z and flips ReLU masks)."""
+    from deep_vision_amd import ops as F
+
+    ref = copy.deepcopy(module).float()
+    xr = x32.clone().requires_grad_(xgrad)
+    F.set_backend("torch")
+    try:
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+            yr = ref(xr)
+        yr.float().backward(dy32)
+    finally:
+        F.set_backend("native")
+    return ref, xr, yr
+
+
+def _check_module(module, x32, fwd_tol=3e-2, xgrad=True):
+    """Native forward/backward vs fp32. A bf16 chain flips ReLU masks (and max-pool arg-maxes)
+    wherever the fp32 pre-activation is within bf16 rounding of zero, so gradients are held to
+    PyTorch's own bf16 path: 1 - cos(native, fp32) <= 2 * (1 - cos(autocast bf16, fp32)) + 2e-4."""
+    x = _nhwc(x32).requires_grad_(xgrad)
+    y = module(x)
+    dy32 = torch.randn(y.shape, device=DEV).bfloat16().float()
+    ref, xr, yr = _reference(module, x32, dy32, xgrad)
+    ab, xb, _ = _reference(module, x32, dy32, xgrad, autocast=True)
+    y.backward(_nhwc(dy32))
+    assert y.shape == yr.shape
+    assert _rel(y, yr) < fwd_tol, _rel(y, yr)
+
+    def close(name, g, gr, gb):
+        dn, db = 1 - _cos(g, gr), 1 - _cos(gb, gr)
+        assert dn <= 2 * db + 2e-4, (name, dn, db)
+
+    if xgrad:
+        close("x", x.grad, xr.grad, xb.grad)
+    for (name, p), pr, pb in zip(module.named_parameters(), ref.parameters(), ab.parameters()):
+        assert p.grad is not None, name
+        close(name, p.grad, pr.grad, pb.grad)
+    return y
+
+
+# (in, mid, out, stride, downsample, H, batch): ResNet-50 blocks at their stage shapes
+BLOCKS = [
+    (64, 64, 256, 1, True, 56, 32),      # conv2_x block 0: projection, 64-channel 3x3 at 56x56
+    (256, 64, 256, 1, False, 56, 32),    # conv2_x identity block
+    (256, 128, 512, 2, True, 56, 32),    # conv3_x block 0: stride on the first 1x1 (V1)
+    (1024, 256, 1024, 1, False, 14, 64), # conv4_x identity block
+    (2048, 512, 2048, 1, False, 7, 64),  # conv5_x identity block
+]
+
+
+@pytest.mark.parametrize("cfg", BLOCKS, ids=lambda c: f"{c[0]}-{c[1]}-{c[2]}s{c[3]}@{c[5]}b{c[6]}")
+def test_bottleneck_block(cfg):
+    from deep_vision_amd.models.resnet import BottleneckBlock, _init
+
+    cin, mid, cout, s, ds, H, N = cfg
+    torch.manual_seed(1)
+    blk = BottleneckBlock(cin, mid, cout, stride=s, downsample=ds).to(DEV)
+    _init(blk)
+    for m in blk.modules():  # non-trivial BN affine parameters
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.weight.data.uniform_(0.5, 1.5)
+            m.bias.data.uniform_(-0.3, 0.3)
+    x32 = torch.randn(N, cin, H, H, device=DEV).bfloat16().float()
+    _check_module(blk, x32)
+
+
+def test_bottleneck_block_big_tiles():
+    """conv4_x identity block with the 256x256 tile / 128-row wave-tile forward forced on every
+    eligible conv (N % 256 == 0, K >= 1024: conv1's dgrad, conv3, conv2's 3x3 at 256 channels)."""
+    from deep_vision_amd._ext import lib
+    from deep_vision_amd.models.resnet import BottleneckBlock, _init
+
+    torch.manual_seed(2)
+    blk = BottleneckBlock(1024, 256, 1024).to(DEV)
+    _init(blk)
+    x32 = torch.randn(16, 1024, 14, 14, device=DEV).bfloat16().float()
+    lib().conv_fwd_variant(100)
+    try:
+        _check_module(blk, x32)
+    finally:
+        lib().conv_fwd_variant(0)
+
+
+def test_conv_fwd_big_tile_epilogues():
+    """256x256 / 128-row wave tiles with the bias+ReLU and residual-accumulate epilogues and an
+    M tail (M = 2 * 13 * 13 = 338: the second 64-row pass of a wave is partly out of range)."""
+    from deep_vision_amd._ext import lib
+    from deep_vision_amd import ops as F
+
+    x32 = torch.randn(2, 256, 13, 13, device=DEV).bfloat16().float()
+    w = torch.randn(512, 256, 3, 3, device=DEV) * 0.03
+    b = torch.randn(512, device=DEV)
+    lib().conv_fwd_variant(100)
+    try:
+        y = F.conv2d(_nhwc(x32), w, b, 1, 1, act="relu")
+    finally:
+        lib().conv_fwd_variant(0)
+    yr = TF.relu(TF.conv2d(x32, w.bfloat16().float(), b, 1, 1))
+    assert _rel(y, yr) < 2e-2
+
+
+def test_wgrad_splitk_200k():
+    """3x3 64->64 at 56x56, batch 64: the weight-gradient reduction runs over 200,704 pixels."""
+    from deep_vision_amd import ops as F
+
+    x32 = torch.randn(64, 64, 56, 56, device=DEV).bfloat16().float()
+    w = (torch.randn(64, 64, 3, 3, device=DEV) * 0.06).requires_grad_(True)
+    y = F.conv2d(_nhwc(x32), w, None, 1, 1)
+    dy32 = torch.randn(y.shape, device=DEV).bfloat16().float()
+    y.backward(_nhwc(dy32))
+    wr = w.detach().bfloat16().float().requires_grad_(True)
+    TF.conv2d(x32, wr, None, 1, 1).backward(dy32)
+    assert _rel(w.grad, wr.grad) < 1e-2
+    assert _cos(w.grad, wr.grad) > 0.9999
+
+
+@pytest.mark.parametrize("cfg", [(32, 112, 1), (64, 112, 2), (512, 14, 1)], ids=lambda c: f"c{c[0]}@{c[1]}s{c[2]}")
+def test_depthwise_bn_relu_production(cfg):
+    """MobileNet's depthwise -> BN -> ReLU at batch 64 (stats, mask bits and all three gradients)."""
+    from deep_vision_amd import nn
+
+    C, H, s = cfg
+
+    class DwBlock(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.dw = nn.Conv2d(C, C, 3, stride=s, padding=1, groups=C, bias=False)
+            self.bn = nn.BatchNorm2d(C)
+            self.act = nn.ReLU(inplace=True)
+
+        def forward(self, x):
+            from deep_vision_amd import ops as F
+
+            return F.conv_bn_act(x, self.dw, self.bn, "relu")
+
+    torch.manual_seed(3)
+    m = DwBlock().to(DEV)
+    m.bn.weight.data.uniform_(0.5, 1.5)
+    m.bn.bias.data.uniform_(-0.3, 0.3)
+    x32 = torch.randn(64, C, H, H, device=DEV).bfloat16().float()
+    _check_module(m, x32)
+
+
+def test_stem_production():
+    """ResNet-50 stem (7x7/2 conv -> BN -> ReLU -> 3x3/2 max-pool) at 224x224, batch 32."""
+    from deep_vision_amd import nn
+
+    class Stem(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+            self.bn1 = nn.BatchNorm2d(64)
+            self.pool = nn.MaxPool2d(3, 2, 1)
+
+        def forward(self, x):
+            from deep_vision_amd import ops as F
+
+            return self.pool(F.conv_bn_act(x, self.conv1, self.bn1, "relu"))
+
+    torch.manual_seed(4)
+    m = Stem().to(DEV)
+    x32 = torch.randn(32, 3, 224, 224, device=DEV).bfloat16().float()
+    _check_module(m, x32, xgrad=False)  # an image input needs no gradient: the tap-packed path
