@@ -213,6 +213,18 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("sumsq", [](uptr x, int64_t n, uptr out, uptr st) { dv_sumsq(CFP(x), n, FP(out), ST(st)); check_last("sumsq"); });
 
+  m.def("yolo_encode", [](uptr boxes, uptr classes, int N, int B, int C, std::vector<float> anchors, uptr y0, uptr y1,
+                          uptr y2, int g0, int g1, int g2, uptr st) {
+    if (anchors.size() != 18) throw std::runtime_error("yolo_encode: 9 anchors (w, h) expected");
+    dv_yolo_encode(CFP(boxes), reinterpret_cast<const int*>(classes), N, B, C, anchors.data(), FP(y0), FP(y1), FP(y2),
+                   g0, g1, g2, ST(st));
+    check_last("yolo_encode");
+  });
+  m.def("heatmaps", [](uptr px, uptr py, uptr vis, int N, int J, int H, int W, uptr out, uptr st) {
+    dv_heatmaps(reinterpret_cast<const int*>(px), reinterpret_cast<const int*>(py), reinterpret_cast<const int*>(vis),
+                N, J, H, W, FP(out), ST(st));
+    check_last("heatmaps");
+  });
   m.def("yolo_gather_boxes", [](uptr yt, int N, int cells, int D, uptr boxes, uptr counts, uptr st) {
     dv_yolo_gather_boxes(CFP(yt), N, cells, D, FP(boxes), reinterpret_cast<int*>(counts), ST(st));
     check_last("yolo_gather_boxes");

@@ -181,3 +181,11 @@ struct WprepDesc {  // 48 bytes, mirrored by deep_vision_amd/ops/wcache.py
   int G, Og, Ig, R, S, pad, mode, Sp;  // Sp: padded filter width (mode 2)
 };
 void dv_wprep_batched(const void* descs, const void* chunks, int nchunks, hipStream_t st);
+
+// ---- training targets on the device (csrc/labels.hip) ----
+// YOLOv3: boxes (N, B, 4) x1y1x2y2 normalised, classes (N, B) int (-1 = padding), anchors 9 x (w, h);
+// y0/y1/y2 (N, g, g, 3, 5 + C) fp32, zeroed by the caller
+void dv_yolo_encode(const float* boxes, const int* classes, int N, int B, int C, const float* anchors_wh, float* y0,
+                    float* y1, float* y2, int g0, int g1, int g2, hipStream_t st);
+// Stacked Hourglass: integer keypoint coordinates px/py and visibility (N, J) -> out (N, J, H, W) fp32
+void dv_heatmaps(const int* px, const int* py, const int* vis, int N, int J, int H, int W, float* out, hipStream_t st);

@@ -59,9 +59,10 @@ def crop_roi(image, kx, ky, scale, margin=0.2):
 
 
 class MPIITFRecordDataset:
-    def __init__(self, files, is_train, image_shape=(256, 256), heatmap_shape=(64, 64, 16)):
+    def __init__(self, files, is_train, image_shape=(256, 256), heatmap_shape=(64, 64, 16), encode_on_device=False):
         from .tfrecord import TFRecordIndex
 
+        self.encode_on_device = encode_on_device  # ship keypoint cells; ops.labels.render_heatmaps on the GPU
         self.index = TFRecordIndex(files)
         self.is_train = is_train
         self.image_shape = tuple(image_shape)
@@ -82,13 +83,32 @@ class MPIITFRecordDataset:
         margin = float(np.random.uniform(0.1, 0.3)) if self.is_train else 0.2
         image, kx, ky = crop_roi(image, kx, ky, scale, margin)
         image = resize(image, self.image_shape).astype(np.float32) / 127.5 - 1
+        if self.encode_on_device:
+            return np.ascontiguousarray(image.transpose(2, 0, 1)), _raw_keypoints(kx, ky, v, self.heatmap_shape)
         hm = make_heatmaps(kx, ky, v, self.heatmap_shape)
         return np.ascontiguousarray(image.transpose(2, 0, 1)), np.ascontiguousarray(hm.transpose(2, 0, 1))
 
 
+def _raw_keypoints(kx, ky, v, shape):
+    from ..ops.labels import keypoint_cells
+
+    px, py = keypoint_cells(kx, ky, shape)
+    return px, py, np.asarray(v, np.int32)
+
+
+def collate_raw(batch):
+    """Collate of an ``encode_on_device`` dataset: images + {'kind': 'pose', px, py, vis (N, J)}."""
+    import torch
+
+    imgs = torch.from_numpy(np.stack([b[0] for b in batch]))
+    px, py, vis = (torch.from_numpy(np.stack([b[1][k] for b in batch])) for k in range(3))
+    return imgs, {"kind": "pose", "px": px, "py": py, "vis": vis}
+
+
 class SyntheticPoseDataset:
-    def __init__(self, n=64, image_size=256, heatmap_shape=(64, 64, 16), seed=0):
+    def __init__(self, n=64, image_size=256, heatmap_shape=(64, 64, 16), seed=0, encode_on_device=False):
         self.n, self.image_size, self.heatmap_shape, self.seed = n, image_size, heatmap_shape, seed
+        self.encode_on_device = encode_on_device
 
     def __len__(self):
         return self.n
@@ -97,8 +117,10 @@ class SyntheticPoseDataset:
         rng = np.random.default_rng((self.seed, i))
         img = rng.uniform(-1, 1, (3, self.image_size, self.image_size)).astype(np.float32)
         k = self.heatmap_shape[2]
-        hm = make_heatmaps(rng.uniform(0.1, 0.9, k), rng.uniform(0.1, 0.9, k), rng.integers(0, 3, k),
-                           self.heatmap_shape)
+        kx, ky, v = rng.uniform(0.1, 0.9, k), rng.uniform(0.1, 0.9, k), rng.integers(0, 3, k)
+        if self.encode_on_device:
+            return img, _raw_keypoints(kx, ky, v, self.heatmap_shape)
+        hm = make_heatmaps(kx, ky, v, self.heatmap_shape)
         return img, np.ascontiguousarray(hm.transpose(2, 0, 1))
 
 

@@ -112,9 +112,10 @@ class YoloTFRecordDataset:
     [-1, 1], (y_small, y_medium, y_large)) exactly as Preprocessor.__call__ (preprocess.py:13-35):
     decode, random flip and box-preserving crop when training, resize to 416, /127.5 - 1, encode."""
 
-    def __init__(self, files, is_train, num_classes=80, output_shape=(416, 416), seed=0):
+    def __init__(self, files, is_train, num_classes=80, output_shape=(416, 416), seed=0, encode_on_device=False):
         from .tfrecord import TFRecordIndex
 
+        self.encode_on_device = encode_on_device  # ship padded boxes; ops.labels.yolo_encode on the GPU
         self.index = TFRecordIndex(files)
         self.is_train = is_train
         self.num_classes = num_classes
@@ -138,6 +139,10 @@ class YoloTFRecordDataset:
             image, boxes = random_flip(image, boxes, rng)
             image, boxes = random_crop(image, boxes, rng)
         image = resize(image, self.output_shape).astype(np.float32) / 127.5 - 1
+        if self.encode_on_device:
+            from ..ops.labels import pad_boxes
+
+            return np.ascontiguousarray(image.transpose(2, 0, 1)), pad_boxes(boxes, classes)
         labels = encode_labels(boxes, classes, self.num_classes, self.grids)
         return np.ascontiguousarray(image.transpose(2, 0, 1)), labels
 
@@ -145,9 +150,10 @@ class YoloTFRecordDataset:
 class SyntheticYoloDataset:
     """Random images + random ground truth of the training shapes (--synthetic)."""
 
-    def __init__(self, n=64, num_classes=80, size=416, seed=0):
+    def __init__(self, n=64, num_classes=80, size=416, seed=0, encode_on_device=False):
         self.n, self.num_classes, self.size, self.seed = n, num_classes, size, seed
         self.grids = tuple(size // s for s in (8, 16, 32))
+        self.encode_on_device = encode_on_device
 
     def __len__(self):
         return self.n
@@ -155,7 +161,22 @@ class SyntheticYoloDataset:
     def __getitem__(self, i):
         rng = np.random.default_rng((self.seed, i))
         img, boxes, classes = synthetic_sample(rng, self.num_classes, self.size)
+        if self.encode_on_device:
+            from ..ops.labels import pad_boxes
+
+            return img, pad_boxes(boxes, classes)
         return img, encode_labels(boxes, classes, self.num_classes, self.grids)
+
+
+def collate_raw(batch, grids=GRIDS):
+    """Collate of an ``encode_on_device`` dataset: images + {'kind': 'yolo', boxes (N, 100, 4),
+    classes (N, 100) int32} for ops.labels.device_targets."""
+    import torch
+
+    imgs = torch.from_numpy(np.stack([b[0] for b in batch]))
+    boxes = torch.from_numpy(np.stack([b[1][0] for b in batch]))
+    classes = torch.from_numpy(np.stack([b[1][1] for b in batch]))
+    return imgs, {"kind": "yolo", "boxes": boxes, "classes": classes, "grids": tuple(grids)}
 
 
 def collate(batch):

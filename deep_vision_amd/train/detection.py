@@ -72,18 +72,25 @@ def _files(pattern):
     return sorted(glob.glob(pattern)) if pattern else []
 
 
-def build_datasets(cfg: TrainConfig, train_glob=None, val_glob=None, synthetic=False, synthetic_size=64):
+def build_datasets(cfg: TrainConfig, train_glob=None, val_glob=None, synthetic=False, synthetic_size=64,
+                   encode_on_device=False):
+    """-> (train set, val set, collate). ``encode_on_device``: YOLO / Hourglass loaders ship raw
+    ground truth and the targets are built on the GPU (ops.labels.device_targets)."""
+    od = encode_on_device
     if cfg.family == "yolo":
+        from functools import partial
+
         from ..data import yolo as Y
 
         nc = cfg.model_params.get("num_classes", 80)
         size = cfg.input_shape[1]
         tr, va = _files(train_glob), _files(val_glob)
+        col = partial(Y.collate_raw, grids=tuple(size // s for s in (8, 16, 32))) if od else Y.collate
         if synthetic or not tr:
-            return (Y.SyntheticYoloDataset(synthetic_size, nc, size, 1),
-                    Y.SyntheticYoloDataset(max(8, synthetic_size // 4), nc, size, 2), Y.collate)
-        return (Y.YoloTFRecordDataset(tr, True, nc, (size, size)), Y.YoloTFRecordDataset(va, False, nc, (size, size)),
-                Y.collate)
+            return (Y.SyntheticYoloDataset(synthetic_size, nc, size, 1, encode_on_device=od),
+                    Y.SyntheticYoloDataset(max(8, synthetic_size // 4), nc, size, 2, encode_on_device=od), col)
+        return (Y.YoloTFRecordDataset(tr, True, nc, (size, size), encode_on_device=od),
+                Y.YoloTFRecordDataset(va, False, nc, (size, size), encode_on_device=od), col)
     if cfg.family == "hourglass":
         from ..data import pose as P
 
@@ -91,10 +98,12 @@ def build_datasets(cfg: TrainConfig, train_glob=None, val_glob=None, synthetic=F
         size = cfg.input_shape[1]
         hs = (size // 4, size // 4, k)
         tr, va = _files(train_glob), _files(val_glob)
+        col = P.collate_raw if od else None
         if synthetic or not tr:
-            return P.SyntheticPoseDataset(synthetic_size, size, hs, 1), P.SyntheticPoseDataset(
-                max(8, synthetic_size // 4), size, hs, 2), None
-        return P.MPIITFRecordDataset(tr, True, (size, size), hs), P.MPIITFRecordDataset(va, False, (size, size), hs), None
+            return (P.SyntheticPoseDataset(synthetic_size, size, hs, 1, encode_on_device=od),
+                    P.SyntheticPoseDataset(max(8, synthetic_size // 4), size, hs, 2, encode_on_device=od), col)
+        return (P.MPIITFRecordDataset(tr, True, (size, size), hs, encode_on_device=od),
+                P.MPIITFRecordDataset(va, False, (size, size), hs, encode_on_device=od), col)
     if cfg.family == "centernet":
         from ..data import centernet as CN
 
@@ -105,9 +114,17 @@ def build_datasets(cfg: TrainConfig, train_glob=None, val_glob=None, synthetic=F
     raise ValueError(cfg.family)
 
 
-def _to_device(batch, device):
+def _to_device(batch, device, cfg=None):
     imgs, labels = batch
     imgs = imgs.to(device, non_blocking=True)
+    if isinstance(labels, dict):  # raw ground truth: targets built on the device
+        from ..ops.labels import device_targets
+
+        raw = {k: (v.to(device, non_blocking=True) if torch.is_tensor(v) else v) for k, v in labels.items()}
+        k = cfg.model_params.get("num_heatmap", 16) if cfg is not None else 16
+        hs = (imgs.shape[-1] // 4, imgs.shape[-2] // 4, k)
+        nc = cfg.model_params.get("num_classes", 80) if cfg is not None else 80
+        return imgs, device_targets(raw, nc, hs)
     if isinstance(labels, (tuple, list)):
         labels = tuple(t.to(device, non_blocking=True) for t in labels)
     else:
@@ -164,7 +181,7 @@ class Trainer:
         for i, batch in enumerate(loader):
             if max_steps is not None and i >= max_steps:
                 break
-            images, labels = _to_device(batch, eng.device)
+            images, labels = _to_device(batch, eng.device, self.cfg)
             with eng.timer.step(samples=images.shape[0]):
                 with eng.timer.phase("fwd"):
                     outputs = self.model(images)
@@ -200,7 +217,7 @@ class Trainer:
         for i, batch in enumerate(loader):
             if max_steps is not None and i >= max_steps:
                 break
-            images, labels = _to_device(batch, eng.device)
+            images, labels = _to_device(batch, eng.device, self.cfg)
             outputs = self.model(images)
             loss, _ = self.compute_loss(outputs, labels, images.shape[0])
             v = eng.reduce_sum([loss.item()])[0] / eng.world
@@ -259,7 +276,10 @@ def train(cfg: TrainConfig, checkpoint=None, *, train_glob=None, val_glob=None, 
     seed_everything(cfg.extras.get("seed", 0) if seed is None else seed, eng.rank)
     if batch_size:
         cfg = cfg.replace(batch_size=batch_size)
-    tr, va, collate = build_datasets(cfg, train_glob, val_glob, synthetic, synthetic_size)
+    from ..ops.common import backend
+
+    on_dev = eng.device.type == "cuda" and backend() == "native" and cfg.extras.get("gpu_targets", True)
+    tr, va, collate = build_datasets(cfg, train_glob, val_glob, synthetic, synthetic_size, encode_on_device=on_dev)
     bs = cfg.per_rank_batch(eng.world)
     train_loader = make_loader(tr, bs, shuffle=True, num_workers=workers, collate_fn=collate)
     val_loader = make_loader(va, bs, shuffle=False, num_workers=workers, collate_fn=collate)
