@@ -213,6 +213,10 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("sumsq", [](uptr x, int64_t n, uptr out, uptr st) { dv_sumsq(CFP(x), n, FP(out), ST(st)); check_last("sumsq"); });
 
+  m.def("channel_sum", [](uptr x, int64_t rows, int ld, int C, uptr acc, uptr out, int accumulate, uptr st) {
+    dv_channel_sum(CP(x), rows, ld, C, FP(acc), FP(out), accumulate, ST(st));
+    check_last("channel_sum");
+  });
   m.def("yolo_encode", [](uptr boxes, uptr classes, int N, int B, int C, std::vector<float> anchors, uptr y0, uptr y1,
                           uptr y2, int g0, int g1, int g2, uptr st) {
     if (anchors.size() != 18) throw std::runtime_error("yolo_encode: 9 anchors (w, h) expected");

@@ -415,6 +415,22 @@ void dv_bn_stats(const void* x, int64_t rows, int C, float* acc, hipStream_t st)
   DISPATCH_VEC(C, bn_stats_kernel, <<<g, NT, 0, st>>>((const u16*)x, rows, C, acc))
 }
 
+// Per-channel sum of an NHWC tensor (conv / Linear bias gradient): the statistics reduction into
+// the self-cleaning shard accumulator, then one fold that zeroes the shards again and writes (or
+// adds into the live fp32 gradient buffer) the sums -- 2 launches, no memset, no fp32 copy of dy.
+__global__ void channel_sum_finalize_kernel(float* __restrict__ acc, int ld, int C, float* __restrict__ out,
+                                            int accumulate) {
+  double s, q;
+  if (!fold_shards(acc, ld, s, q)) return;
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (c < C) out[c] = accumulate ? out[c] + (float)s : (float)s;
+}
+
+void dv_channel_sum(const void* x, int64_t rows, int ld, int C, float* acc, float* out, int accumulate, hipStream_t st) {
+  dv_bn_stats(x, rows, ld, acc, st);
+  channel_sum_finalize_kernel<<<(ld + 63) / 64, 256, 0, st>>>(acc, ld, C, out, accumulate);
+}
+
 void dv_bn_finalize(float* acc, int C, double count, float eps, float momentum, const float* gamma,
                     const float* beta, float* rm, float* rv, float* save_mean, float* save_invstd, float* scale,
                     float* shift, hipStream_t st) {

@@ -189,3 +189,6 @@ void dv_yolo_encode(const float* boxes, const int* classes, int N, int B, int C,
                     float* y1, float* y2, int g0, int g1, int g2, hipStream_t st);
 // Stacked Hourglass: integer keypoint coordinates px/py and visibility (N, J) -> out (N, J, H, W) fp32
 void dv_heatmaps(const int* px, const int* py, const int* vis, int N, int J, int H, int W, float* out, hipStream_t st);
+// per-channel fp32 sum of a bf16 [rows][ld] tensor into out[C] (accumulate: +=); acc is a
+// zeroed [SHARDS][2][ld] workspace that the call leaves zeroed
+void dv_channel_sum(const void* x, int64_t rows, int ld, int C, float* acc, float* out, int accumulate, hipStream_t st);

@@ -77,13 +77,28 @@ def _prep_weight(weight: torch.Tensor, G: int, pad: int, mode: int, param=None) 
     return compute(None)
 
 
-def _channel_sum(dy: torch.Tensor) -> torch.Tensor:
-    """Per-channel sum of an NHWC bf16 tensor (fp32) via the BN statistics kernel."""
+_CSUM_WS = {}
+
+
+def _channel_sum(dy: torch.Tensor, out=None) -> torch.Tensor:
+    """Per-channel fp32 sum of an NHWC bf16 tensor (bias gradient): csrc/bn.hip dv_channel_sum, two
+    launches into a self-cleaning per-device workspace. ``out`` (a gradient sink): added into."""
     N, C, H, W = dy.shape
     ld = ld_of(dy)
-    acc = torch.zeros((STAT_SHARDS, 2, ld), dtype=F32, device=dy.device)
-    lib().bn_stats(ptr(dy), N * H * W, ld, ptr(acc), stream_handle())
-    return acc[:, 0, :C].sum(0)
+    key = (str(dy.device), ld)
+    acc = _CSUM_WS.get(key)
+    if acc is None:
+        acc = _CSUM_WS[key] = torch.zeros((STAT_SHARDS, 2, ld), dtype=F32, device=dy.device)
+    dst = out if out is not None else torch.empty(C, dtype=F32, device=dy.device)
+    lib().channel_sum(ptr(dy), N * H * W, ld, C, ptr(acc), ptr(dst), int(out is not None), stream_handle())
+    return dst
+
+
+def _bias_grad(bias, dy):
+    """Bias gradient straight into the live gradient buffer when there is one (None to autograd)."""
+    sink = grad_sink(bias)
+    db = _channel_sum(dy, out=sink)
+    return None if sink is not None else db
 
 
 def gemm_ksplit(M, N, K):
@@ -316,6 +331,7 @@ class _ConvFn(torch.autograd.Function):
         conv_fwd_raw(x, wk, y, b, stats, N, H, W, Cg_x, ldx, G, Og, P, Q, R, S, stride, padding, dilation,
                      act=act, slope=slope, reflect=reflect)
         ctx.save_for_backward(x, weight, y if act else None)
+        ctx.bias_param = bias  # leaf parameter (not saved): its gradient may sink in place
         ctx.cfg = (stride, padding, dilation, G, act, slope, Cg_x, bias is not None)
         ctx.reflect = reflect
         ctx.join = (join, join_role)
@@ -361,7 +377,7 @@ class _ConvFn(torch.autograd.Function):
             if sink is not None:
                 dw = None
         if has_bias and ctx.needs_input_grad[2]:
-            db = _channel_sum(dy)
+            db = _bias_grad(ctx.bias_param, dy)
         return dx, dw, db, None, None, None, None, None, None, None, None, None, None, None, None, None
 
 
@@ -424,6 +440,7 @@ class _StemConvFn(torch.autograd.Function):
         conv_fwd_raw(xp, wk, y, b, stats, N, Hp, Wp, 4 * Sp, 4, 1, O, P, Q, R, 1, stride, (0, 0), (1, 1), act=act,
                      slope=slope, tgather=2)
         ctx.save_for_backward(xp, weight, y if act else None)
+        ctx.bias_param = bias  # leaf parameter (not saved): its gradient may sink in place
         ctx.cfg = (stride, act, slope, geo, bias is not None)
         ctx.set_materialize_grads(False)
         if want_stats:
@@ -456,7 +473,7 @@ class _StemConvFn(torch.autograd.Function):
             else:
                 dw = full[..., :S].contiguous()
         if has_bias and ctx.needs_input_grad[2]:
-            db = _channel_sum(dy)
+            db = _bias_grad(ctx.bias_param, dy)
         return None, dw, db, None, None, None, None, None, None, None, None
 
 
@@ -583,6 +600,7 @@ class _ConvTFn(torch.autograd.Function):
                          dilation, tgather=1, ldy=G * Cpad)
         y = y_full if Cpad == Cog else y_full[:, :Cout]
         ctx.save_for_backward(x, weight)
+        ctx.bias_param = bias  # leaf parameter (not saved): its gradient may sink in place
         ctx.cfg = (stride, padding, dilation, G, bias is not None)
         return y
 
@@ -605,7 +623,7 @@ class _ConvTFn(torch.autograd.Function):
             # conv relationship: X_conv = dY (large), dY_conv = x (small)
             dw = _wgrad(dy, x, weight, Cg_dy, G, stride, padding, dilation)
         if has_bias and ctx.needs_input_grad[2]:
-            db = _channel_sum(dy)
+            db = _bias_grad(ctx.bias_param, dy)
         return dx, dw, db, None, None, None, None, None, None
 
 
@@ -732,6 +750,7 @@ class _DWConvFn(torch.autograd.Function):
         lib().dw_fwd(ptr(x), ptr(w), ptr(b), ptr(y), N, H, W, C, ld_of(x), P, Q, ld_of(y), K, stride[0], stride[1],
                      padding[0], padding[1], act, float(slope), ptr(stats), stream_handle())
         ctx.save_for_backward(x, weight, y if act else None)
+        ctx.bias_param = bias  # leaf parameter (not saved): its gradient may sink in place
         ctx.cfg = (stride, padding, act, slope, bias is not None)
         ctx.set_materialize_grads(False)
         if want_stats:
@@ -765,7 +784,7 @@ class _DWConvFn(torch.autograd.Function):
             if sink is None:
                 dw = buf
         if has_bias and ctx.needs_input_grad[2]:
-            db = _channel_sum(dy)
+            db = _bias_grad(ctx.bias_param, dy)
         return dx, dw, db, None, None, None, None, None, None, None
 
 
