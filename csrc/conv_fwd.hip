@@ -677,28 +677,59 @@ void dispatch_tile(const FwdParams& p, hipStream_t st) {
   else dispatch_res<KMODE, false>(p, st);
 }
 
-// y[m][n] = act(sum_s ypart[s][m][n] + bias[n]) in bf16; the slabs are summed in split order
-// (bitwise reproducible). 4 columns per thread.
+// y[m][n] = act(sum_s ypart[s][m][n] + bias[n]) (+ res[m][n]) in bf16, plus the BatchNorm
+// partial statistics of y when `stats` is set (the epilogue work the split blocks skipped). The
+// slabs are summed in split order (bitwise reproducible). Block = 64 column lanes x 4 columns
+// (256 channels) x 4 row lanes walking FR_ROWS rows; statistics meet in LDS, one coalesced atomic
+// row per block into shard blockIdx.y % SHARDS.
+constexpr int FR_ROWS = 64;
 __global__ __launch_bounds__(256) void splitk_finalize_kernel(const float* __restrict__ ypart, int ksplit, int M, int N,
                                                               const float* __restrict__ bias, int act, float slope,
+                                                              const u16* __restrict__ res, float* __restrict__ stats,
                                                               u16* __restrict__ y, int ldy) {
-  const int nq = N >> 2;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (int64_t)M * nq) return;
-  const int m = (int)(i / nq), n = (int)(i - (int64_t)m * nq) * 4;
+  __shared__ float red[2][4][256];
+  const int lc = threadIdx.x & 63, lr = threadIdx.x >> 6;
+  const int n = blockIdx.x * 256 + lc * 4;
+  const bool nv = n < N;  // N % 4 == 0: whole column quads
   const int64_t slab = (int64_t)M * N;
-  f32x4 a = *reinterpret_cast<const f32x4*>(ypart + (int64_t)m * N + n);
-  for (int s = 1; s < ksplit; ++s) a += *reinterpret_cast<const f32x4*>(ypart + s * slab + (int64_t)m * N + n);
-  float v[4];
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f}, bv[4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    float t = a[r] + (bias ? bias[n + r] : 0.f);
-    if (act == ACT_RELU) t = fmaxf(t, 0.f);
-    else if (act == ACT_LEAKY) t = t > 0.f ? t : t * slope;
-    v[r] = t;
+  for (int r = 0; r < 4; ++r) bv[r] = (bias && nv) ? bias[n + r] : 0.f;
+  const int m1 = min(M, (int)(blockIdx.y + 1) * FR_ROWS);
+  for (int m = blockIdx.y * FR_ROWS + lr; nv && m < m1; m += 4) {
+    f32x4 a = *reinterpret_cast<const f32x4*>(ypart + (int64_t)m * N + n);
+    for (int sp = 1; sp < ksplit; ++sp) a += *reinterpret_cast<const f32x4*>(ypart + sp * slab + (int64_t)m * N + n);
+    float rv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (res) {
+      const uint2 rr = *reinterpret_cast<const uint2*>(res + (int64_t)m * ldy + n);
+      rv[0] = bf2f(rr.x & 0xffff); rv[1] = bf2f(rr.x >> 16); rv[2] = bf2f(rr.y & 0xffff); rv[3] = bf2f(rr.y >> 16);
+    }
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float t = a[r] + bv[r];
+      if (act == ACT_RELU) t = fmaxf(t, 0.f);
+      else if (act == ACT_LEAKY) t = t > 0.f ? t : t * slope;
+      t += rv[r];
+      v[r] = t;
+      s1[r] += t; s2[r] += t * t;
+    }
+    uint2 pk; pk.x = pack2bf(v[0], v[1]); pk.y = pack2bf(v[2], v[3]);
+    *reinterpret_cast<uint2*>(y + (int64_t)m * ldy + n) = pk;
   }
-  uint2 pk; pk.x = pack2bf(v[0], v[1]); pk.y = pack2bf(v[2], v[3]);
-  *reinterpret_cast<uint2*>(y + (int64_t)m * ldy + n) = pk;
+  if (!stats) return;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) { red[0][lr][lc * 4 + r] = s1[r]; red[1][lr][lc * 4 + r] = s2[r]; }
+  __syncthreads();
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c < N) {
+    float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { t1 += red[0][q][threadIdx.x]; t2 += red[1][q][threadIdx.x]; }
+    float* sh = stats + (int64_t)(blockIdx.y % DV_STAT_SHARDS) * 2 * N;
+    atomicAdd(sh + c, t1);
+    atomicAdd(sh + N + c, t2);
+  }
 }
 
 }  // namespace
@@ -721,12 +752,17 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
   p.resbits = (const uint8_t*)a.resbits; p.resact = a.resact; p.resslope = a.resslope;
   p.reflect = a.reflect;
   p.ksplit = 1; p.kt_per = 1 << 30; p.ypart = nullptr;
+  const u16* fin_res = nullptr;
+  float* fin_stats = nullptr;
   if (a.ksplit > 1 && a.ypart) {
-    // split-K serves plain GEMM-shaped convs: single group, identity output map, bias/act only
-    const bool ok = a.G == 1 && !a.tgather && !a.res && !a.stats && !a.bnmode && !a.reflect && (a.Kout % 4) == 0 &&
+    // split-K: single group, identity output map; bias / activation / residual / BN statistics
+    // are applied by the finalize pass (no BN-backward statistics, no masked residual)
+    const bool ok = a.G == 1 && !a.tgather && !a.bnmode && !a.resbits && !a.reflect && (a.Kout % 4) == 0 &&
                     (a.ldy % 4) == 0 && a.OH == a.P && a.OW == a.Q && a.osh == 1 && a.osw == 1 && !a.oph && !a.opw;
     if (!ok) return -1;
     p.ksplit = a.ksplit; p.ypart = a.ypart;
+    fin_res = p.res; fin_stats = p.stats;  // applied by the finalize pass, not the split blocks
+    p.res = nullptr; p.stats = nullptr;
   }
   if (p.reflect && (a.tgather || p.ph >= p.Hin || p.pw >= p.Win || p.ph < 0 || p.pw < 0 || p.bnmode)) return -1;
   // the mask bits are indexed by the dense element offset of y: a single-group tensor whose
@@ -766,9 +802,9 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
   else if (p.Cg % 64 == 0 && p.R <= 16 && p.S <= 16 && !p.reflect) dispatch_tile<KM_FAST>(p, st);
   else dispatch_tile<KM_GENERIC>(p, st);
   if (p.ypart) {
-    const int64_t n4 = (int64_t)p.M * (p.N / 4);
-    splitk_finalize_kernel<<<dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st>>>(
-        p.ypart, g_last_ksplit, p.M, p.N, p.bias, p.act, p.slope, p.y, p.ldy);
+    const dim3 grid((unsigned)((p.N + 255) / 256), (unsigned)((p.M + FR_ROWS - 1) / FR_ROWS));
+    splitk_finalize_kernel<<<grid, dim3(256), 0, st>>>(p.ypart, g_last_ksplit, p.M, p.N, p.bias, p.act, p.slope,
+                                                       fin_res, fin_stats, p.y, p.ldy);
   }
   return bn_status;
 }

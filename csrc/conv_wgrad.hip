@@ -371,7 +371,12 @@ int dv_conv_wgrad_splits(const ConvWgradArgs& a) {
   // ~1.5 blocks per CU: measured 5-15 % faster than 3 per CU on the ResNet-50 3x3 / strided
   // layers (half the atomic epilogues), equal on the rest (profiles/wgbench_variants.txt)
   int splits = cdiv(384 * g_wg_split_pct / 100, tiles);
-  splits = std::min(splits, std::max(1, ktiles / 32));   // >= 2048 pixels per split (atomic budget)
+  int cap = ktiles / 32;  // >= 2048 pixels per split (atomic budget)
+  // few output tiles (small maps / few channels: the Hourglass 8x8-32x32 scales had 9-36 blocks
+  // on 256 CUs): trade atomic traffic for parallelism down to 512 pixels per split, until the
+  // grid covers the chip (profiles/hourglass_conv_bench.txt)
+  if ((int64_t)tiles * cap < 256) cap = std::max(cap, std::min(ktiles / 8, cdiv(256, tiles)));
+  splits = std::min(splits, std::max(1, cap));
   return std::max(1, std::min(splits, ktiles));
 }
 

@@ -47,7 +47,8 @@ class BottleneckBlock(tnn.Module):
         y = F.batch_norm_act(x, self.bn1, "relu")
         y = F.conv_bn_act(y, self.conv1, self.bn2, "relu")
         y = F.conv_bn_act(y, self.conv2, self.bn3, "relu")
-        return F.add(self.conv3(y), identity)
+        # the residual add rides in conv3's store epilogue (ops.conv2d residual=)
+        return F.conv2d(y, self.conv3.weight, self.conv3.bias, residual=identity)
 
 
 class HourglassModule(tnn.Module):

@@ -114,6 +114,18 @@ def gemm_ksplit(M, N, K):
     return max(1, min(16, 256 // tiles, K // 512))
 
 
+def conv_ksplit(M, O, K, G=1):
+    """Split-K factor of a conv whose output grid is too small to fill the chip (Hourglass /
+    CenterNet 4x4-16x16 scales: 4-64 tiles): the finalize pass then applies bias, activation,
+    residual and the BatchNorm statistics (csrc/conv_fwd.hip splitk_finalize_kernel)."""
+    if G != 1 or O % 4 or K < 512:
+        return 1
+    tiles = -(-M // 256) if O <= 64 else -(-M // 128) * -(-O // 128)
+    if tiles >= 64:
+        return 1
+    return max(1, min(16, 192 // tiles, K // 128))
+
+
 def conv_fwd_raw(x, wk, y, bias, stats, N, H, W, Cg, ldx, G, Kout, P, Q, R, S, stride, padding, dilation,
                  act=0, slope=0.0, tgather=0, omap=None, ldy=None, res=None, bnref=None, resmask=None, reflect=False,
                  ksplit=1):
@@ -309,7 +321,7 @@ def _wgrad_workspace(numel, device):
 class _ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats, stats_buf=None,
-                extra=(0, 0), join=None, join_role=None, reflect=False, out_box=None):
+                extra=(0, 0), join=None, join_role=None, reflect=False, out_box=None, residual=None):
         N, Cx, H, W = x.shape
         O, Ig, R, S = weight.shape
         G = groups
@@ -328,8 +340,11 @@ class _ConvFn(torch.autograd.Function):
         if want_stats:
             stats = stats_buf if stats_buf is not None else torch.zeros((STAT_SHARDS, 2, O), dtype=F32, device=x.device)
         b = bias.detach().float().contiguous() if bias is not None else None
+        # residual: y = conv + b + residual in the store epilogue (same NHWC layout as y)
+        ks = 1 if reflect else conv_ksplit(N * P * Q, Og, R * S * Cg_x, G)
         conv_fwd_raw(x, wk, y, b, stats, N, H, W, Cg_x, ldx, G, Og, P, Q, R, S, stride, padding, dilation,
-                     act=act, slope=slope, reflect=reflect)
+                     act=act, slope=slope, reflect=reflect, res=residual, ksplit=ks)
+        ctx.has_residual = residual is not None
         ctx.save_for_backward(x, weight, y if act else None)
         ctx.bias_param = bias  # leaf parameter (not saved): its gradient may sink in place
         ctx.cfg = (stride, padding, dilation, G, act, slope, Cg_x, bias is not None)
@@ -353,8 +368,8 @@ class _ConvFn(torch.autograd.Function):
                 g = join.take()  # nothing to add to: hand a stashed shortcut gradient through
                 if isinstance(g, MaskedGrad):
                     g = g.materialize()
-                return (g, None, None) + (None,) * 13
-            return (None,) * 16
+                return (g, None, None) + (None,) * 14
+            return (None,) * 17
         dy = grad_nhwc(dy)
         if act:  # y and dy may be channel-slice views of concat buffers: strided rows kernel
             dy = act_grad(dy, y, act, slope)
@@ -378,7 +393,8 @@ class _ConvFn(torch.autograd.Function):
                 dw = None
         if has_bias and ctx.needs_input_grad[2]:
             db = _bias_grad(ctx.bias_param, dy)
-        return dx, dw, db, None, None, None, None, None, None, None, None, None, None, None, None, None
+        dres = dy if ctx.has_residual and ctx.needs_input_grad[16] else None  # y = ... + residual
+        return dx, dw, db, None, None, None, None, None, None, None, None, None, None, None, None, None, dres
 
 
 # ---------------------------------------------------------------------------------------
@@ -478,14 +494,22 @@ class _StemConvFn(torch.autograd.Function):
 
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=None, slope=0.0,
-           want_stats=False, stats_buf=None, join=None, join_role=None, pad_mode="zeros", out=None):
+           want_stats=False, stats_buf=None, join=None, join_role=None, pad_mode="zeros", out=None, residual=None):
     """Conv2d (+fused bias/activation). Returns y, or (y, stats) when want_stats (GPU only).
 
     ``padding`` may be (top, bottom, left, right) for TF/Keras asymmetric 'same' padding.
     ``pad_mode='reflect'``: ReflectionPad2d(padding) fused into the im2col gather (the taps
     outside the image read the mirrored pixels; no padded copy of the input).
     ``out``: a preallocated NHWC (channel-slice) view the output is written into (write-into-slice
-    concat, ops.concat.slice_cat); native path only."""
+    concat, ops.concat.slice_cat); native path only.
+    ``residual``: y = conv(x) + bias + residual, the add fused into the store epilogue (no
+    activation / statistics; Hourglass bottleneck output, R/Hourglass/tensorflow/hourglass104.py:62-67)."""
+    if residual is not None and (act or want_stats or out is not None or not native(x)):
+        y = conv2d(x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats, stats_buf, join,
+                   join_role, pad_mode, out)
+        if want_stats:
+            raise NotImplementedError("conv2d residual= with want_stats")
+        return y + residual if not native(x) else _add_native(y, residual)
     if isinstance(padding, str):
         raise NotImplementedError("string padding: use nn.Conv2d(padding='same_keras')")
     stride, dilation = _pair(stride), _pair(dilation)
@@ -539,8 +563,25 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=
         if join_role == "consumer":  # the gradient reaches x through the layout copy: no join
             join.consumer_done = True
         join = None
+    res = None
+    if residual is not None:
+        if dw or padded_groups or geo is not None:
+            return _add_native(conv2d(x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats,
+                                      stats_buf, join, join_role, pad_mode, out), residual)
+        res = as_nhwc(residual, pad_to8=True)
+        if ld_of(res) != round8(weight.shape[0]) or res.data_ptr() % 16:
+            res = res.contiguous(memory_format=torch.channels_last) if round8(weight.shape[0]) == weight.shape[0] else None
+        if res is None:
+            return _add_native(conv2d(x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats,
+                                      stats_buf, join, join_role, pad_mode, out), residual)
     return _ConvFn.apply(xn, weight, bias, stride, padding, dilation, groups, ACT_IDS[act], float(slope), want_stats,
-                         stats_buf, extra, join, join_role, reflect, [out] if out is not None else None)
+                         stats_buf, extra, join, join_role, reflect, [out] if out is not None else None, res)
+
+
+def _add_native(a, b):
+    from .act import add
+
+    return add(a, b)
 
 
 def _block_diagonal(weight, groups, cin):

@@ -239,6 +239,44 @@ def test_linear_splitk(shape):
     assert torch.equal(F.linear(x.detach(), w.detach(), None if b is None else b.detach(), act="relu"), y2)
 
 
+@pytest.mark.parametrize("case", [(32, 128, 8, 128, 3), (32, 256, 4, 256, 3), (8, 512, 7, 512, 1)])
+def test_conv_splitk_small_maps(case):
+    """Small output grids (Hourglass 4x4 / 8x8 scales) run split-K with the bias, residual and
+    BatchNorm statistics applied by the finalize pass."""
+    from deep_vision_amd import nn, ops as F
+    from deep_vision_amd.ops.conv import conv_ksplit
+
+    N, C, H, O, k = case
+    assert conv_ksplit(N * H * H, O, k * k * C) > 1
+    x32 = torch.randn(N, C, H, H, device=DEV).bfloat16().float()
+    w = (torch.randn(O, C, k, k, device=DEV) * (2.0 / (C * k * k)) ** 0.5).requires_grad_(True)
+    b = torch.randn(O, device=DEV).requires_grad_(True)
+    r32 = torch.randn(N, O, H, H, device=DEV).bfloat16().float()
+    x = _nhwc(x32).requires_grad_(True)
+    res = _nhwc(r32).requires_grad_(True)
+    y = F.conv2d(x, w, b, 1, k // 2, residual=res)
+    xr, rr = x32.clone().requires_grad_(True), r32.clone().requires_grad_(True)
+    wr = w.detach().bfloat16().float().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True)
+    yr = TF.conv2d(xr, wr, br, 1, k // 2) + rr
+    assert _rel(y, yr) < 2e-2
+    g = torch.randn_like(yr).bfloat16().float()
+    y.backward(_nhwc(g))
+    yr.backward(g)
+    assert _rel(x.grad, xr.grad) < 3e-2 and _rel(w.grad, wr.grad) < 3e-2
+    assert _rel(b.grad, br.grad) < 1e-2 and _rel(res.grad, rr.grad) < 1e-2
+    # conv -> BN -> ReLU with the statistics from the finalize pass
+    conv = nn.Conv2d(C, O, k, padding=k // 2).to(DEV)
+    bn = nn.BatchNorm2d(O).to(DEV)
+    yb = F.conv_bn_act(_nhwc(x32), conv, bn, "relu")
+    cr = torch.nn.Conv2d(C, O, k, padding=k // 2).to(DEV)
+    cr.weight.data.copy_(conv.weight.data.bfloat16().float())
+    cr.bias.data.copy_(conv.bias.data)
+    ybr = TF.relu(TF.batch_norm(cr(x32), None, None, None, None, True, 0.1, bn.eps))
+    assert _rel(yb, ybr) < 3e-2
+    assert torch.allclose(bn.running_mean, 0.1 * cr(x32).mean((0, 2, 3)), atol=2e-3, rtol=2e-2)
+
+
 def test_conv_transpose():
     from deep_vision_amd import ops as F
 

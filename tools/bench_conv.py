@@ -33,6 +33,14 @@ LAYERS = [
 ]
 
 
+# Stacked Hourglass (batch 32) bottleneck convs at the 64x64 and 32x32 scales
+HOURGLASS = [
+    ("hg64_1x1_256_128", 64, 256, 128, 1, 1), ("hg64_3x3_128", 64, 128, 128, 3, 1), ("hg64_1x1_128_256", 64, 128, 256, 1, 1),
+    ("hg32_1x1_256_128", 32, 256, 128, 1, 1), ("hg32_3x3_128", 32, 128, 128, 3, 1), ("hg32_1x1_128_256", 32, 128, 256, 1, 1),
+    ("hg16_3x3_128", 16, 128, 128, 3, 1), ("hg8_3x3_128", 8, 128, 128, 3, 1),
+]
+
+
 def run(name, H, Cin, Cout, k, s, N, variants, iters):
     pad = k // 2
     P = (H + 2 * pad - k) // s + 1
@@ -117,11 +125,12 @@ def main():
     ap.add_argument("--wgrad", action="store_true")
     ap.add_argument("--splits", default="100")
     ap.add_argument("--layers", default="", help="comma-separated layer names (default: all)")
+    ap.add_argument("--set", default="resnet50", choices=["resnet50", "hourglass"])
     a = ap.parse_args()
     keep = set(a.layers.split(",")) if a.layers else None
     vs = [int(v) for v in a.variants.split(",")]
     out = {}
-    for L in LAYERS:
+    for L in (HOURGLASS if a.set == "hourglass" else LAYERS):
         if keep is not None and L[0] not in keep:
             continue
         if a.wgrad:
