@@ -126,6 +126,21 @@ PYBIND11_MODULE(_C, m) {
                           int sw, int ph, int pw, uptr st) {
     dv_maxpool_bwd(CP(dy), reinterpret_cast<const uint8_t*>(idx), P(dx), N, H, W, C, P_, Q, kh, kw, sh, sw, ph, pw, ST(st)); check_last("maxpool_bwd");
   });
+  m.def("bn_act_maxpool_fwd", [](uptr x, uptr y, uptr idx, int N, int H, int W, int C, int P_, int Q, int kh, int kw, int sh,
+                                 int sw, int ph, int pw, uptr scale, uptr shift, int act, float slope, uptr st) {
+    const int r = dv_bn_act_maxpool_fwd(CP(x), P(y), reinterpret_cast<uint8_t*>(idx), N, H, W, C, P_, Q, kh, kw, sh, sw, ph, pw,
+                                        CFP(scale), CFP(shift), act, slope, ST(st));
+    check_last("bn_act_maxpool_fwd");
+    return r;
+  });
+  m.def("bn_act_maxpool_bwd", [](uptr dy, uptr idx, uptr x, uptr dx, int N, int H, int W, int C, int P_, int Q, int kh, int kw,
+                                 int sh, int sw, int ph, int pw, uptr prm, uptr coef, int act, float slope, uptr acc, int apply,
+                                 uptr st) {
+    const int r = dv_bn_act_maxpool_bwd(CP(dy), reinterpret_cast<const uint8_t*>(idx), CP(x), P(dx), N, H, W, C, P_, Q, kh, kw,
+                                        sh, sw, ph, pw, CFP(prm), CFP(coef), act, slope, FP(acc), apply, ST(st));
+    check_last("bn_act_maxpool_bwd");
+    return r;
+  });
   m.def("avgpool_fwd", [](uptr x, uptr y, int N, int H, int W, int C, int P_, int Q, int kh, int kw, int sh, int sw, int ph,
                           int pw, int cip, int divover, uptr st) {
     dv_avgpool_fwd(CP(x), P(y), N, H, W, C, P_, Q, kh, kw, sh, sw, ph, pw, cip, divover, ST(st)); check_last("avgpool_fwd");

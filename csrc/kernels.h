@@ -99,6 +99,13 @@ void dv_maxpool_fwd(const void* x, void* y, uint8_t* idx, int N, int H, int W, i
                     int sh, int sw, int ph, int pw, hipStream_t st);
 void dv_maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, int N, int H, int W, int C, int P, int Q, int kh,
                     int kw, int sh, int sw, int ph, int pw, hipStream_t st);
+// fused BatchNorm apply + activation + max pool (ResNet stem); -1 = shape not covered
+int dv_bn_act_maxpool_fwd(const void* x, void* y, uint8_t* idx, int N, int H, int W, int C, int P, int Q, int kh, int kw,
+                          int sh, int sw, int ph, int pw, const float* scale, const float* shift, int act, float slope,
+                          hipStream_t st);
+int dv_bn_act_maxpool_bwd(const void* dy, const uint8_t* idx, const void* x, void* dx, int N, int H, int W, int C, int P,
+                          int Q, int kh, int kw, int sh, int sw, int ph, int pw, const float* prm, const float* coef,
+                          int act, float slope, float* acc, int apply, hipStream_t st);
 void dv_avgpool_fwd(const void* x, void* y, int N, int H, int W, int C, int P, int Q, int kh, int kw, int sh, int sw,
                     int ph, int pw, int cip, int divover, hipStream_t st);
 void dv_avgpool_bwd(const void* dy, void* dx, int N, int H, int W, int C, int P, int Q, int kh, int kw, int sh, int sw,

@@ -241,6 +241,193 @@ __global__ __launch_bounds__(NT) void upsample_bwd_kernel(const u16* __restrict_
   }
 }
 
+// ---- BatchNorm apply + activation + max pool as one pass: the conv -> BN -> ReLU -> MaxPool stem
+// (R/ResNet/pytorch/models/resnet50.py:33-35,72-75). The BN output (411 MB for the ResNet-50 stem
+// at batch 256) is never written, and the backward never materialises its gradient.
+DV_DEVICE float pool_act(float z, int act, float slope) {
+  if (act == 1) return fmaxf(z, 0.f);
+  if (act == 2) return z > 0.f ? z : z * slope;
+  return z;
+}
+
+// Window geometry: compile-time for the 3x3 / stride-2 stem pool (KH = 0: runtime g.kh ...). Every
+// input row / column is covered by at most WIN = ceil(k / s) windows per dimension.
+template <int KH, int KW, int SH, int SW>
+struct PoolWin {
+  DV_DEVICE static int kh(const PoolGeo& g) { return KH ? KH : g.kh; }
+  DV_DEVICE static int kw(const PoolGeo& g) { return KW ? KW : g.kw; }
+  DV_DEVICE static int sh(const PoolGeo& g) { return SH ? SH : g.sh; }
+  DV_DEVICE static int sw(const PoolGeo& g) { return SW ? SW : g.sw; }
+  static constexpr int WH = KH ? (KH + SH - 1) / SH : 16;  // loop bound (runtime form breaks out early)
+  static constexpr int WW = KW ? (KW + SW - 1) / SW : 16;
+};
+
+// Forward: out = max over the window of bf16(act(x*scale + shift)). The bf16 rounding of the
+// unfused BN pass is applied before the comparison, so values and window indices are exactly the
+// unfused ones. One thread per (n, p, q, 8-channel group), grid-stride (stride % cg == 0: a
+// thread keeps its channels and their scale/shift); every window load is issued before the max.
+template <int KH, int KW, int SH, int SW>
+__global__ __launch_bounds__(NT) void bn_act_maxpool_fwd_kernel(const u16* __restrict__ x, u16* __restrict__ y,
+                                                                uint8_t* __restrict__ idx, PoolGeo g, FastDiv div_cg,
+                                                                FastDiv div_q, FastDiv div_p, int64_t total,
+                                                                const float* __restrict__ scale,
+                                                                const float* __restrict__ shift, int act, float slope) {
+  using Wn = PoolWin<KH, KW, SH, SW>;
+  const int kh = Wn::kh(g), kw = Wn::kw(g), sh = Wn::sh(g), sw = Wn::sw(g);
+  const uint32_t t0 = blockIdx.x * NT + threadIdx.x;
+  const int lc = (int)(t0 - fdiv(t0, div_cg) * div_cg.d), c = lc * 8;
+  float sc[8], sf[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { sc[i] = scale[c + i]; sf[i] = shift[c + i]; }
+  for (uint32_t t = t0; t < total; t += gridDim.x * NT) {
+    const uint32_t pix = fdiv(t, div_cg);
+    const uint32_t row = fdiv(pix, div_q);
+    const int q = (int)(pix - row * div_q.d);
+    const int n = (int)fdiv(row, div_p), p = (int)(row - n * div_p.d);
+    const int h0 = p * sh - g.ph, w0 = q * sw - g.pw;
+    float best[8]; int bi[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { best[i] = -INFINITY; bi[i] = 0; }
+    const u16* xb = x + ((int64_t)n * g.H * g.W) * g.C + c;
+#pragma unroll
+    for (int r = 0; r < (KH ? KH : 16); ++r) {
+      if (!KH && r >= kh) break;
+      const int h = h0 + r;
+      uint4 raw[KW ? KW : 1];
+      bool ok[KW ? KW : 1];
+      if constexpr (KW != 0) {
+#pragma unroll
+        for (int s = 0; s < KW; ++s) {  // issue the row's loads together
+          const int w = w0 + s;
+          ok[s] = h >= 0 && h < g.H && w >= 0 && w < g.W;
+          raw[s] = ok[s] ? *reinterpret_cast<const uint4*>(xb + ((int64_t)h * g.W + w) * g.C) : uint4{0u, 0u, 0u, 0u};
+        }
+      }
+      for (int s = 0; s < kw; ++s) {
+        const int w = w0 + s;
+        float v[8];
+        if constexpr (KW != 0) {
+          if (!ok[s]) continue;
+          const uint32_t wd[4] = {raw[s].x, raw[s].y, raw[s].z, raw[s].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { v[2 * e] = bf2f(wd[e] & 0xffff); v[2 * e + 1] = bf2f(wd[e] >> 16); }
+        } else {
+          if (h < 0 || h >= g.H || w < 0 || w >= g.W) continue;
+          V<8>::ld(xb + ((int64_t)h * g.W + w) * g.C, v);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float a = bf2f(f2bf(pool_act(fmaf(v[i], sc[i], sf[i]), act, slope)));
+          if (a > best[i] || (a != a && best[i] == best[i])) { best[i] = a; bi[i] = r * kw + s; }
+        }
+      }
+    }
+    const int64_t o = (int64_t)pix * g.C + c;
+    V<8>::st(y + o, best);
+    uint2 pk;
+    pk.x = (uint32_t)bi[0] | ((uint32_t)bi[1] << 8) | ((uint32_t)bi[2] << 16) | ((uint32_t)bi[3] << 24);
+    pk.y = (uint32_t)bi[4] | ((uint32_t)bi[5] << 8) | ((uint32_t)bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    *reinterpret_cast<uint2*>(idx + o) = pk;
+  }
+}
+
+// Backward, per input element: da = sum of the pooled gradients whose window index points at it
+// (the maxpool gather, bf16-rounded like the unfused pass's stored da), dz = act'(z) * da with
+// z = x*mscale + mshift recomputed from the BN input.
+//   REDUCE: per-channel (sum dz, sum dz*(x-mean)*invstd) into the BN shard accumulator
+//           acc[SHARDS][2][C] (csrc/bn.hip layout; bn_bwd_finalize folds it);
+//   APPLY : dx = kA*dz + kB*x + kC (coefficients from bn_bwd_finalize).
+// One thread per (n, h, w, 8-channel group), grid-stride (cg | 256, so a thread's channels are
+// fixed and the block's partial sums meet in LDS for one coalesced atomic row per block).
+template <bool APPLY, int KH, int KW, int SH, int SW>
+__global__ __launch_bounds__(NT) void bn_act_maxpool_bwd_kernel(const u16* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                                                const u16* __restrict__ x, u16* __restrict__ dx, PoolGeo g,
+                                                                FastDiv div_cg, FastDiv div_w, FastDiv div_h, int64_t total,
+                                                                const float* __restrict__ prm,
+                                                                const float* __restrict__ coef, int act, float slope,
+                                                                float* __restrict__ acc) {
+  using Wn = PoolWin<KH, KW, SH, SW>;
+  const int kh = Wn::kh(g), kw = Wn::kw(g), sh = Wn::sh(g), sw = Wn::sw(g);
+  const int cg = g.C / 8;
+  const uint32_t t0 = blockIdx.x * NT + threadIdx.x;
+  const int lc = (int)(t0 - fdiv(t0, div_cg) * div_cg.d), c = lc * 8;
+  // prm = [scale; shift; mean; invstd] x C, coef = [kA; kB; kC] x C
+  float ms[8], mh[8], k0[8], k1[8], k2[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    ms[i] = prm[c + i]; mh[i] = prm[g.C + c + i];
+    if (APPLY) { k0[i] = coef[c + i]; k1[i] = coef[g.C + c + i]; k2[i] = coef[2 * g.C + c + i]; }
+    else { k0[i] = prm[2 * g.C + c + i]; k1[i] = prm[3 * g.C + c + i]; k2[i] = 0.f; }
+  }
+  float s1[8], s2[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { s1[i] = 0.f; s2[i] = 0.f; }
+  for (uint32_t t = t0; t < total; t += gridDim.x * NT) {
+    const uint32_t pix = fdiv(t, div_cg);
+    const uint32_t row = fdiv(pix, div_w);
+    const int w = (int)(pix - row * div_w.d);
+    const int n = (int)fdiv(row, div_h), h = (int)(row - n * div_h.d);
+    // windows covering (h, w): p*sh - ph <= h <= p*sh - ph + kh - 1
+    const int hp = h + g.ph, wp = w + g.pw;
+    const int p_hi = min(hp / sh, g.P - 1), q_hi = min(wp / sw, g.Q - 1);
+    const int64_t xo = (int64_t)pix * g.C + c;
+    float xv[8];
+    V<8>::ld(x + xo, xv);
+    float da[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) da[i] = 0.f;
+#pragma unroll
+    for (int a = 0; a < Wn::WH; ++a) {
+      const int p = p_hi - a, r = hp - p * sh;
+      if (!KH && r >= kh) break;
+      if (p < 0 || r >= kh) continue;
+#pragma unroll
+      for (int b = 0; b < Wn::WW; ++b) {
+        const int q = q_hi - b, s = wp - q * sw;
+        if (!KW && s >= kw) break;
+        if (q < 0 || s >= kw) continue;
+        const int64_t o = (((int64_t)n * g.P + p) * g.Q + q) * g.C + c;
+        float d[8];
+        V<8>::ld(dy + o, d);
+        const uint2 ib = *reinterpret_cast<const uint2*>(idx + o);
+        const uint32_t pos = (uint32_t)(r * kw + s);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const uint32_t bsel = ((i < 4 ? ib.x : ib.y) >> (8 * (i & 3))) & 0xffu;
+          if (bsel == pos) da[i] += d[i];
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float d = bf2f(f2bf(da[i]));
+      const float z = fmaf(xv[i], ms[i], mh[i]);
+      const float dz = act == 1 ? (z > 0.f ? d : 0.f) : (act == 2 ? (z > 0.f ? d : d * slope) : d);
+      if (APPLY) da[i] = fmaf(k0[i], dz, fmaf(k1[i], xv[i], k2[i]));
+      else { s1[i] += dz; s2[i] += dz * (xv[i] - k0[i]) * k1[i]; }
+    }
+    if (APPLY) V<8>::st(dx + xo, da);
+  }
+  if (APPLY) return;
+  // per-channel totals over the block's pixel lanes, one coalesced atomic row per block
+  __shared__ float sh_[2][NT * 8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { sh_[0][threadIdx.x * 8 + i] = s1[i]; sh_[1][threadIdx.x * 8 + i] = s2[i]; }
+  __syncthreads();
+  const int lanes = NT / cg;
+  float* a = acc + (int64_t)(blockIdx.x % DV_STAT_SHARDS) * 2 * g.C;
+  for (int ch = threadIdx.x; ch < g.C; ch += NT) {
+    const int gi = ch / 8, e = ch % 8;
+    float t1 = 0.f, t2 = 0.f;
+    for (int l = 0; l < lanes; ++l) {
+      t1 += sh_[0][(l * cg + gi) * 8 + e];
+      t2 += sh_[1][(l * cg + gi) * 8 + e];
+    }
+    atomicAdd(a + ch, t1);
+    atomicAdd(a + g.C + ch, t2);
+  }
+}
+
 inline int grid_for(int64_t total) {
   int64_t g = (total + NT - 1) / NT;
   return (int)std::min<int64_t>(std::max<int64_t>(g, 1), 256 * 16);
@@ -262,6 +449,45 @@ void dv_maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, int N, int H, 
   const int v = C % 8 == 0 ? 8 : 1;
   const int64_t total = (int64_t)N * H * W * (C / v);
   VDISPATCH(C, maxpool_bwd_kernel, <<<grid_for(total), NT, 0, st>>>((const u16*)dy, idx, (u16*)dx, g, total));
+}
+// fused BN-apply + activation + max pool: C % 8 == 0 and C/8 a divisor of 256 (else -1); the
+// 3x3 / stride-2 window (ResNet / Inception stems) is compiled, other windows take the runtime form
+static bool stem_window(int kh, int kw, int sh, int sw) { return kh == 3 && kw == 3 && sh == 2 && sw == 2; }
+
+int dv_bn_act_maxpool_fwd(const void* x, void* y, uint8_t* idx, int N, int H, int W, int C, int P, int Q, int kh, int kw,
+                          int sh, int sw, int ph, int pw, const float* scale, const float* shift, int act, float slope,
+                          hipStream_t st) {
+  const int64_t total = (int64_t)N * P * Q * (C / 8);
+  if (C % 8 || NT % (C / 8) || kh * kw > 255 || kh > 16 || total >= (1ll << 31)) return -1;
+  PoolGeo g{N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw};
+  const FastDiv dc = make_fastdiv(C / 8), dq = make_fastdiv(Q), dp = make_fastdiv(P);
+  const int grid = (int)std::min<int64_t>((total + NT - 1) / NT, 256 * 32);
+#define FWD_ARGS <<<grid, NT, 0, st>>>((const u16*)x, (u16*)y, idx, g, dc, dq, dp, total, scale, shift, act, slope)
+  if (stem_window(kh, kw, sh, sw)) bn_act_maxpool_fwd_kernel<3, 3, 2, 2> FWD_ARGS;
+  else bn_act_maxpool_fwd_kernel<0, 0, 0, 0> FWD_ARGS;
+#undef FWD_ARGS
+  return 0;
+}
+int dv_bn_act_maxpool_bwd(const void* dy, const uint8_t* idx, const void* x, void* dx, int N, int H, int W, int C, int P,
+                          int Q, int kh, int kw, int sh, int sw, int ph, int pw, const float* prm, const float* coef,
+                          int act, float slope, float* acc, int apply, hipStream_t st) {
+  const int64_t total = (int64_t)N * H * W * (C / 8);
+  if (C % 8 || NT % (C / 8) || kh * kw > 255 || kh > 16 || total >= (1ll << 31)) return -1;
+  PoolGeo g{N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw};
+  const FastDiv dc = make_fastdiv(C / 8), dw = make_fastdiv(W), dh = make_fastdiv(H);
+  // the reduction's atomics are one row per block: a bounded grid (~2k blocks) keeps them cheap
+  const int grid = (int)std::min<int64_t>((total + NT - 1) / NT, apply ? 256 * 32 : 2048);
+#define BWD_ARGS <<<grid, NT, 0, st>>>((const u16*)dy, idx, (const u16*)x, (u16*)dx, g, dc, dw, dh, total, prm, coef, act, slope, acc)
+  const bool stem = stem_window(kh, kw, sh, sw);
+  if (apply) {
+    if (stem) bn_act_maxpool_bwd_kernel<true, 3, 3, 2, 2> BWD_ARGS;
+    else bn_act_maxpool_bwd_kernel<true, 0, 0, 0, 0> BWD_ARGS;
+  } else {
+    if (stem) bn_act_maxpool_bwd_kernel<false, 3, 3, 2, 2> BWD_ARGS;
+    else bn_act_maxpool_bwd_kernel<false, 0, 0, 0, 0> BWD_ARGS;
+  }
+#undef BWD_ARGS
+  return 0;
 }
 void dv_avgpool_fwd(const void* x, void* y, int N, int H, int W, int C, int P, int Q, int kh, int kw, int sh, int sw,
                     int ph, int pw, int cip, int divover, hipStream_t st) {

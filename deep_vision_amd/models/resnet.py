@@ -96,8 +96,9 @@ class _ResNetBase(tnn.Module):
         self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
 
     def forward(self, x):
-        x = F.conv_bn_act(x, self.conv1, self.bn1, "relu")
-        x = self.maxpool(x)
+        # conv -> BN -> ReLU -> maxpool: BN apply, ReLU and the pool run as one pass on the GPU
+        # (the 112x112x64 BN output is never materialised; ops.bn._BNActPoolFn)
+        x = F.conv_bn_act_maxpool(x, self.conv1, self.bn1, "relu", self.maxpool)
         x = self.conv2x(x)
         x = self.conv3x(x)
         x = self.conv4x(x)

@@ -4,7 +4,7 @@ On CUDA (ROCm) tensors every op runs a hand-written gfx950 HIP kernel from ``csr
 on CPU tensors the same call runs the PyTorch reference op (numerics oracle / CPU plumbing).
 """
 from .act import activation, add, dropout, leaky_relu, relu  # noqa: F401
-from .bn import batch_norm_act, conv_bn_act, conv_bn_deferred  # noqa: F401
+from .bn import batch_norm_act, batch_norm_act_maxpool, conv_bn_act, conv_bn_act_maxpool, conv_bn_deferred  # noqa: F401
 from .common import as_nhwc, backend, native, set_backend  # noqa: F401
 from .concat import channel_shuffle, concat, concat_slices, slice_cat  # noqa: F401
 from .conv import conv2d, conv_transpose2d, linear  # noqa: F401

@@ -215,6 +215,120 @@ def _residual_bn_backward(ctx, dout, bits, r_x, rprm, r_weight, r_bias, act, slo
     return (dr if ctx.needs_input_grad[6] else None), dgamma, dbeta
 
 
+class _BNActPoolFn(torch.autograd.Function):
+    """Training-mode BatchNorm -> activation -> MaxPool2d as one forward pass and two backward
+    passes (csrc/pool.hip bn_act_maxpool_*): the BN output is never materialised, its gradient
+    never written. Forward reads x once and writes the pooled output + u8 window indices;
+    backward = fused (maxpool gather -> act' -> BN reduction), bn_bwd_finalize, fused (gather ->
+    act' -> dx = kA*dz + kB*x + kC). Values, indices and gradients equal the unfused
+    bn_apply -> maxpool chain (the BN output's bf16 rounding is kept before the max)."""
+
+    @staticmethod
+    def forward(ctx, x, stats, weight, bias, running_mean, running_var, momentum, eps, act, slope, ws_fwd, ws_bwd,
+                k, s, p, P, Q):
+        N, C, H, W = x.shape
+        dev = x.device
+        st = stream_handle()
+        L = lib()
+        prm = torch.empty((4, C), dtype=F32, device=dev)  # scale, shift, mean, invstd
+        g = weight.detach() if weight is not None else None
+        b = bias.detach() if bias is not None else None
+        if stats is None:
+            stats = ws_fwd
+            L.bn_stats(ptr(x), N * H * W, C, ptr(stats), st)
+        L.bn_finalize(ptr(stats), C, float(N * H * W), float(eps), float(momentum), ptr(g), ptr(b), ptr(running_mean),
+                      ptr(running_var), ptr(prm[2]), ptr(prm[3]), ptr(prm[0]), ptr(prm[1]), st)
+        y = torch.empty((N, C, P, Q), dtype=BF16, device=dev, memory_format=torch.channels_last)
+        idx = torch.empty((N, P, Q, C), dtype=torch.uint8, device=dev)
+        r = L.bn_act_maxpool_fwd(ptr(x), ptr(y), ptr(idx), N, H, W, C, P, Q, k[0], k[1], s[0], s[1], p[0], p[1],
+                                 ptr(prm[0]), ptr(prm[1]), act, float(slope), st)
+        if r != 0:
+            raise RuntimeError("bn_act_maxpool_fwd: shape not covered (check bn_act_maxpool_ok first)")
+        ctx.save_for_backward(x, idx, weight, bias, prm)
+        ctx.cfg = (act, slope, k, s, p, P, Q)
+        ctx.ws_bwd = ws_bwd
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, idx, weight, bias, prm = ctx.saved_tensors
+        act, slope, k, s, p, P, Q = ctx.cfg
+        N, C, H, W = x.shape
+        dev = x.device
+        st = stream_handle()
+        L = lib()
+        dy = grad_nhwc(dy)
+        if ld_of(dy) != C or not dy.is_contiguous(memory_format=torch.channels_last):
+            dy = dy.contiguous(memory_format=torch.channels_last)
+        geo = (N, H, W, C, P, Q, k[0], k[1], s[0], s[1], p[0], p[1])
+        acc = ctx.ws_bwd
+        L.bn_act_maxpool_bwd(ptr(dy), ptr(idx), ptr(x), 0, *geo, ptr(prm), 0, act, float(slope), ptr(acc), 0, st)
+        sg = grad_sink(weight) if ctx.needs_input_grad[2] else None
+        sb = grad_sink(bias) if ctx.needs_input_grad[3] else None
+        dgamma = dbeta = None
+        coef = torch.empty((3, C), dtype=F32, device=dev)
+        direct = sg is not None and sb is not None
+        if weight is not None and not direct:
+            dgamma = torch.empty(C, dtype=F32, device=dev)
+            dbeta = torch.empty(C, dtype=F32, device=dev)
+        L.bn_bwd_finalize(ptr(acc), C, float(N * H * W), ptr(weight.detach() if weight is not None else None),
+                          ptr(prm[2]), ptr(prm[3]), ptr(sg if direct else dgamma), ptr(sb if direct else dbeta),
+                          int(direct), ptr(coef[0]), ptr(coef[1]), ptr(coef[2]), st)
+        dx = torch.empty_like(x)
+        L.bn_act_maxpool_bwd(ptr(dy), ptr(idx), ptr(x), ptr(dx), *geo, ptr(prm), ptr(coef), act, float(slope), ptr(acc),
+                             1, st)
+        return (dx, None, dgamma, dbeta) + (None,) * 13
+
+
+def bn_act_maxpool_ok(x, bn, pool):
+    """Whether BN(training) -> act -> ``pool`` (an nn.MaxPool2d) can run as one fused op."""
+    k = pool.kernel_size if isinstance(pool.kernel_size, tuple) else (pool.kernel_size, pool.kernel_size)
+    d = pool.dilation if isinstance(pool.dilation, tuple) else (pool.dilation, pool.dilation)
+    C = x.shape[1]
+    return (native(x) and bn.training and bn.track_running_stats and C % 8 == 0 and 256 % (C // 8) == 0
+            and d == (1, 1) and not pool.return_indices and k[0] * k[1] <= 255 and torch.is_grad_enabled())
+
+
+def batch_norm_act_maxpool(x, bn, act, slope, pool, stats=None):
+    """maxpool(act(BN(x))) with a training-mode ``bn`` as one fused native op (see _BNActPoolFn)."""
+    from .pool import _pair, pool_out
+
+    k, s, p = _pair(pool.kernel_size), _pair(pool.stride if pool.stride is not None else pool.kernel_size), _pair(pool.padding)
+    N, C, H, W = x.shape
+    P = pool_out(H, k[0], s[0], p[0], pool.ceil_mode)
+    Q = pool_out(W, k[1], s[1], p[1], pool.ceil_mode)
+    if bn.num_batches_tracked is not None:
+        _count_batch(bn)
+    ws_fwd = workspace(bn, "bn_fwd", (STAT_SHARDS, 2, C), x.device)
+    ws_bwd = workspace(bn, "bn_bwd", (STAT_SHARDS, 2, C), x.device)
+    return _BNActPoolFn.apply(x, stats, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn_momentum(bn), bn.eps,
+                              ACT_IDS[act], float(slope), ws_fwd, ws_bwd, k, s, p, P, Q)
+
+
+def conv_bn_act_maxpool(x, conv, bn, act, pool, slope=0.0):
+    """conv -> BN -> act -> MaxPool2d (the ResNet stem): BN statistics from the conv epilogue, then
+    the fused BN/act/pool op when it applies, else the unfused chain."""
+    from .conv import conv2d
+    from .pool import max_pool2d
+
+    if not native(x):
+        return pool(_torch_bn_act(conv(x), bn, act, slope, None))
+    want = bn.training and bn.track_running_stats and conv.out_channels % 8 == 0
+    if not want:
+        return max_pool2d(conv_bn_act(x, conv, bn, act, slope), pool.kernel_size, pool.stride, pool.padding, pool.ceil_mode)
+    sbuf = workspace(bn, "bn_fwd", (STAT_SHARDS, 2, conv.out_channels), x.device)
+    pad = conv.native_padding(x.shape[2], x.shape[3]) if hasattr(conv, "native_padding") else conv.padding
+    y, stats = conv2d(x, conv.weight, conv.bias, conv.stride, pad, conv.dilation, conv.groups, want_stats=True,
+                      stats_buf=sbuf)
+    if y.shape[1] % 8 != 0 or ld_of(y) != y.shape[1] or not bn_act_maxpool_ok(y, bn, pool):
+        if ld_of(y) != y.shape[1]:
+            y = y.contiguous(memory_format=torch.channels_last)
+            stats = None
+        z = batch_norm_act(y, bn, act, slope, None, stats)
+        return max_pool2d(z, pool.kernel_size, pool.stride, pool.padding, pool.ceil_mode)
+    return batch_norm_act_maxpool(y, bn, act, slope, pool, stats)
+
+
 def masked_grad(grad, bits, act, slope):
     """act'(z) * grad with the mask stored as bits (1 per element, dense NHWC): the materialised
     form of a MaskedGrad, via the BN backward apply pass with unit coefficients."""

@@ -216,3 +216,97 @@ def test_stem_production():
     m = Stem().to(DEV)
     x32 = torch.randn(32, 3, 224, 224, device=DEV).bfloat16().float()
     _check_module(m, x32, xgrad=False)  # an image input needs no gradient: the tap-packed path
+
+
+def _same_up_to_stat_rounding(a, b):
+    """Equal except where the batch statistics' last fp32 bit moved an element across a bf16
+    rounding boundary: the statistics are reduced with float atomics, so two runs of the same
+    BatchNorm may differ in their summation order (a handful of elements by one bf16 ulp)."""
+    a, b = a.float(), b.float()
+    d = (a - b).abs()
+    assert (d <= b.abs() * 2.0 ** -7 + 1e-30).all(), d.max().item()
+    assert (d > 0).float().mean().item() < 1e-3
+
+
+class _FusedStem(torch.nn.Module):
+    """ResNet stem through the fused BN -> ReLU -> max-pool op (ops.bn._BNActPoolFn)."""
+
+    def __init__(self, fused=True):
+        super().__init__()
+        from deep_vision_amd import nn
+
+        self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.pool = nn.MaxPool2d(3, 2, 1)
+        self.fused = fused
+
+    def forward(self, x):
+        from deep_vision_amd import ops as F
+
+        if self.fused:
+            return F.conv_bn_act_maxpool(x, self.conv1, self.bn1, "relu", self.pool)
+        return self.pool(F.conv_bn_act(x, self.conv1, self.bn1, "relu"))
+
+
+def test_stem_fused_production():
+    """Fused stem (BN apply + ReLU + max-pool in one pass, gather-form backward) at 224x224,
+    batch 32, against the fp32 reference."""
+    torch.manual_seed(4)
+    m = _FusedStem().to(DEV)
+    m.bn1.weight.data.uniform_(0.5, 1.5)
+    m.bn1.bias.data.uniform_(-0.2, 0.2)
+    x32 = torch.randn(32, 3, 224, 224, device=DEV).bfloat16().float()
+    _check_module(m, x32, xgrad=False)
+
+
+def test_stem_fused_matches_unfused():
+    """The fused op reproduces the unfused native chain: identical pooled output (the BN output's
+    bf16 rounding is kept before the max), equal running statistics, and gradients equal up to
+    the order of the BN-backward reductions."""
+    torch.manual_seed(5)
+    a = _FusedStem(fused=True).to(DEV)
+    b = _FusedStem(fused=False).to(DEV)
+    b.load_state_dict(a.state_dict())
+    for m in (a, b):
+        m.bn1.weight.data.uniform_(0.5, 1.5)
+    b.bn1.weight.data.copy_(a.bn1.weight.data)
+    x = _nhwc(torch.randn(16, 3, 224, 224, device=DEV))
+    ya, yb = a(x), b(x)
+    _same_up_to_stat_rounding(ya, yb)
+    dy = _nhwc(torch.randn(ya.shape, device=DEV))
+    ya.backward(dy)
+    yb.backward(dy)
+    torch.cuda.synchronize()
+    assert torch.allclose(a.bn1.running_mean, b.bn1.running_mean, rtol=1e-5, atol=1e-6)
+    assert torch.allclose(a.bn1.running_var, b.bn1.running_var, rtol=1e-5, atol=1e-6)
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        assert _rel(pa.grad, pb.grad) < 2e-3, (n, _rel(pa.grad, pb.grad))
+
+
+@pytest.mark.parametrize("cfg", [(64, 3, 2, 1, False), (32, 2, 2, 0, False), (128, 3, 1, 1, False), (16, 3, 2, 0, True)],
+                         ids=lambda c: f"c{c[0]}k{c[1]}s{c[2]}p{c[3]}{'ceil' if c[4] else ''}")
+def test_bn_act_maxpool_windows(cfg):
+    """Fused BN -> ReLU -> max-pool vs the unfused native chain for the compiled 3x3/s2 window and
+    the runtime-window form (2x2/s2, 3x3/s1, ceil mode)."""
+    from deep_vision_amd import nn
+    from deep_vision_amd import ops as F
+
+    C, k, s, p, ceil = cfg
+    torch.manual_seed(6)
+    bn_a, bn_b = nn.BatchNorm2d(C).to(DEV), nn.BatchNorm2d(C).to(DEV)
+    bn_a.weight.data.uniform_(0.5, 1.5)
+    bn_a.bias.data.uniform_(-0.3, 0.3)
+    bn_b.load_state_dict(bn_a.state_dict())
+    pool = nn.MaxPool2d(k, s, p, ceil_mode=ceil)
+    x = _nhwc(torch.randn(8, C, 29, 31, device=DEV))
+    xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    ya = F.batch_norm_act_maxpool(xa, bn_a, "relu", 0.0, pool)
+    yb = F.max_pool2d(F.batch_norm_act(xb, bn_b, "relu"), k, s, p, ceil)
+    assert ya.shape == yb.shape
+    _same_up_to_stat_rounding(ya, yb)
+    dy = _nhwc(torch.randn(ya.shape, device=DEV))
+    ya.backward(dy)
+    yb.backward(dy)
+    assert _rel(xa.grad, xb.grad) < 2e-2 and _cos(xa.grad, xb.grad) > 0.9999
+    assert _rel(bn_a.weight.grad, bn_b.weight.grad) < 2e-3
+    assert _rel(bn_a.bias.grad, bn_b.bias.grad) < 2e-3

@@ -3,7 +3,8 @@
 #   tools/gpu.sh check           GPU tests, smoke, 1-GPU ResNet-50 bench
 #   tools/gpu.sh bench [args]    bench.py with the given args (default ResNet-50, 1 GPU)
 #   tools/gpu.sh prof MODEL      rocprofv3 kernel trace + stats of bench.py --model MODEL
-#   tools/gpu.sh pmc  LAYERS     PMC counter passes (one run per counter group) over tools/bench_conv.py layers
+#   tools/gpu.sh pmc  LAYERS [PAT] PMC counter passes (one run per counter group) over tools/bench_conv.py layers
+#                                (PMC_ARGS=--wgrad for the weight-gradient kernels; PAT filters kernel names)
 #   tools/gpu.sh models          bench every BASELINE.json GPU config (native and torch/MIOpen reference)
 #   tools/gpu.sh tests [-k EXPR] GPU tests only
 # Every GPU step has its own time limit and the steps are chained with &&: after a fault,
@@ -37,9 +38,9 @@ case "$mode" in
   pmc)
     L=${1:-s2_1x1_128_512,s4_3x3_512,s1_1x1_64_256,s2_3x3_128}
     mkdir -p gpurun_out/pmc && cd /tmp && export TMPDIR=/tmp && \
-    timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VMEM SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE -d "$R/gpurun_out/pmc/p1" -o run --output-format csv -- python3 "$R/tools/bench_conv.py" --layers "$L" --variants 0 --iters 3 > "$R/gpurun_out/pmc/p1.log" 2>&1 && \
-    timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM TCC_HIT TCC_MISS -d "$R/gpurun_out/pmc/p2" -o run --output-format csv -- python3 "$R/tools/bench_conv.py" --layers "$L" --variants 0 --iters 3 > "$R/gpurun_out/pmc/p2.log" 2>&1 && \
-    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE TA_BUSY_avr -d "$R/gpurun_out/pmc/p3" -o run --output-format csv -- python3 "$R/tools/bench_conv.py" --layers "$L" --variants 0 --iters 3 > "$R/gpurun_out/pmc/p3.log" 2>&1
+    timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VMEM SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE -d "$R/gpurun_out/pmc/p1" -o run --output-format csv -- python3 "$R/tools/bench_conv.py" --layers "$L" --variants 0 --iters 3 $PMC_ARGS > "$R/gpurun_out/pmc/p1.log" 2>&1 && \
+    timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM TCC_HIT TCC_MISS -d "$R/gpurun_out/pmc/p2" -o run --output-format csv -- python3 "$R/tools/bench_conv.py" --layers "$L" --variants 0 --iters 3 $PMC_ARGS > "$R/gpurun_out/pmc/p2.log" 2>&1 && \
+    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE TA_BUSY_avr -d "$R/gpurun_out/pmc/p3" -o run --output-format csv -- python3 "$R/tools/bench_conv.py" --layers "$L" --variants 0 --iters 3 $PMC_ARGS > "$R/gpurun_out/pmc/p3.log" 2>&1
     rc=$?; cd "$R"
     python tools/pmc_summary.py "${2:-conv_}" $(find gpurun_out/pmc -name '*counter_collection.csv') > gpurun_out/pmc/summary.txt 2>&1
     sed -n '1,80p' gpurun_out/pmc/summary.txt ;;
