@@ -73,13 +73,24 @@ DV_DEVICE void wait_vm() {
   __builtin_amdgcn_s_waitcnt((N & 0xF) | (0x7 << 4) | (0xF << 8) | ((N >> 4) << 14));
 }
 
-template <int BM_, int BN_, bool PLAIN, int BK = 64, int STAGES = 2>
-__global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgParams p) {
-  constexpr int WN = BN_ / 64, WM = BM_ / 64;
-  static_assert(WN * WM == 4, "4 waves of 64x64");
+// Waves: (BM_ / WMT) x (BN_ / 64), each a WMT x 64 (M x N) sub-tile; WMT = 128 halves the LDS
+// fragment reads and DMA instructions per MFMA (the 8-wave 256x256 tile, cf. conv_fwd.hip).
+template <int BM_, int BN_, int WMT = 64>
+constexpr int wg_waves() { return (BM_ / WMT) * (BN_ / 64); }
+// epilogue rows staged per pass: the whole tile, or halves when BM_ x BN_ fp32 exceeds the LDS
+template <int BM_, int BN_>
+constexpr int wg_epi_rows() { return BM_ * (BN_ + F32_PAD) * 4 > 96 * 1024 ? BM_ / 2 : BM_; }
+
+template <int BM_, int BN_, bool PLAIN, int BK = 64, int STAGES = 2, int WMT = 64>
+__global__ __launch_bounds__((64 * wg_waves<BM_, BN_, WMT>()), 2) void conv_wgrad_kernel(WgParams p) {
+  constexpr int WN = BN_ / 64, WM = BM_ / WMT;
+  constexpr int NW = WN * WM;
+  constexpr int FM = WMT / 16;
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   constexpr int MCH = BM_ / 8, NCH = BN_ / 8;        // 16-B chunks per image row
   constexpr int MRPI = 64 / MCH, NRPI = 64 / NCH;    // image rows per 1-KB DMA instruction
-  constexpr int MI = (BK / MRPI) / 4, NI = (BK / NRPI) / 4;  // DMA instructions per wave per tile
+  constexpr int MI = (BK / MRPI) / NW, NI = (BK / NRPI) / NW;  // DMA instructions per wave per tile
+  static_assert(MI * MRPI * NW == BK && NI * NRPI * NW == BK, "loader rows must split evenly over the waves");
   constexpr int MBYTES = BK * BM_ * 2, STAGE = BK * (BM_ + BN_) * 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -179,27 +190,26 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgParams p) {
     }
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[4][FM];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < FM; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto compute = [&](int buf) {
     const char* img_m = smem + buf * STAGE;
     const char* img_n = img_m + MBYTES;
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
-      bf16x8 fa[4], fb[4];
+      bf16x8 fa[4], fb[FM];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        fa[j] = read_mn<BN_>(img_n, wave_n * 64 + j * 16, kk * 32, lane);
-        fb[j] = read_mn<BM_>(img_m, wave_m * 64 + j * 16, kk * 32, lane);
-      }
+      for (int j = 0; j < 4; ++j) fa[j] = read_mn<BN_>(img_n, wave_n * 64 + j * 16, kk * 32, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) fb[i] = read_mn<BM_>(img_m, wave_m * WMT + i * 16, kk * 32, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < FM; ++i)
           acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[j], fb[i], acc[j][i], 0, 0, 0);
     }
   };
@@ -240,18 +250,11 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgParams p) {
   }
 
   // ---- epilogue: fp32 tile through LDS, then 256-B row segments (atomic or plain) ----
-  // acc[j][i][r]: n_local = wave_n*64 + j*16 + (lane>>4)*4 + r ; m_local = wave_m*64 + i*16 + (lane&15)
+  // acc[j][i][r]: n_local = wave_n*64 + j*16 + (lane>>4)*4 + r ; m_local = wave_m*WMT + i*16 + (lane&15)
+  // A tile larger than the LDS budget goes out in ER-row passes.
   constexpr int LD = BN_ + F32_PAD;
-  float* T = reinterpret_cast<float*>(smem);  // [BM_][LD]
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int nl = wave_n * 64 + j * 16 + (lane >> 4) * 4;
-      const int ml = wave_m * 64 + i * 16 + (lane & 15);
-      *reinterpret_cast<f32x4*>(&T[ml * LD + nl]) = acc[j][i];
-    }
-  __syncthreads();
+  constexpr int ER = wg_epi_rows<BM_, BN_>();
+  float* T = reinterpret_cast<float*>(smem);  // [ER][LD]
   // destination of column n: packed [G][M][N] row offset n, or the parameter's OIRS position
   // (n = (r, s, c) -> c*R*S + r*S + s; padded channels c >= oirs_ig are dropped)
   const int64_t row_stride = p.oirs_ig > 0 ? (int64_t)p.oirs_ig * p.R * p.S : p.N;
@@ -266,16 +269,31 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgParams p) {
       coff[h] = c < p.oirs_ig ? (int64_t)c * p.R * p.S + rs : -1;
     }
   }
-  for (int rr = wid; rr < BM_; rr += 4) {
-    const int m = m0 + rr;
-    if (m >= p.M) break;
 #pragma unroll
-    for (int h = 0; h < BN_ / 64; ++h) {
-      if (coff[h] >= 0) {
-        const float v = T[rr * LD + h * 64 + lane];
-        float* dst = dwp + (int64_t)m * row_stride + coff[h];
-        if (p.atomic_out) atomicAdd(dst, v);
-        else *dst = p.accumulate ? *dst + v : v;
+  for (int pass = 0; pass < BM_ / ER; ++pass) {
+    if (pass) __syncthreads();  // the previous pass's rows have been read back
+    if (wave_m * WMT / ER == pass) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int nl = wave_n * 64 + j * 16 + (lane >> 4) * 4;
+          const int ml = wave_m * WMT + i * 16 + (lane & 15) - pass * ER;
+          *reinterpret_cast<f32x4*>(&T[ml * LD + nl]) = acc[j][i];
+        }
+    }
+    __syncthreads();
+    for (int rr = wid; rr < ER; rr += NW) {
+      const int m = m0 + pass * ER + rr;
+      if (m >= p.M) break;
+#pragma unroll
+      for (int h = 0; h < BN_ / 64; ++h) {
+        if (coff[h] >= 0) {
+          const float v = T[rr * LD + h * 64 + lane];
+          float* dst = dwp + (int64_t)m * row_stride + coff[h];
+          if (p.atomic_out) atomicAdd(dst, v);
+          else *dst = p.accumulate ? *dst + v : v;
+        }
       }
     }
   }
@@ -283,23 +301,26 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgParams p) {
 
 template <int BM_, int BN_, int BKW, int STAGES>
 constexpr int wg_lds_bytes() {
-  constexpr int st = STAGES * BKW * (BM_ + BN_) * 2, ep = BM_ * (BN_ + F32_PAD) * 4;
+  constexpr int st = STAGES * BKW * (BM_ + BN_) * 2, ep = wg_epi_rows<BM_, BN_>() * (BN_ + F32_PAD) * 4;
   return st > ep ? st : ep;
 }
 
 // p.ktiles_per_split arrives in 64-pixel units; BKW = 32 kernels walk twice as many tiles
-template <int BM_, int BN_, bool PLAIN, int BKW = 64, int STAGES = 2>
+template <int BM_, int BN_, bool PLAIN, int BKW = 64, int STAGES = 2, int WMT = 64>
 void launch_wg(WgParams p, int blocks, hipStream_t st) {
   static bool attr = false;
   constexpr int lds = wg_lds_bytes<BM_, BN_, BKW, STAGES>();
   if (!attr) {
-    hipFuncSetAttribute((const void*)conv_wgrad_kernel<BM_, BN_, PLAIN, BKW, STAGES>,
+    hipFuncSetAttribute((const void*)conv_wgrad_kernel<BM_, BN_, PLAIN, BKW, STAGES, WMT>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
   p.ktiles_per_split *= BK / BKW;
-  conv_wgrad_kernel<BM_, BN_, PLAIN, BKW, STAGES><<<dim3(blocks), dim3(NT), lds, st>>>(p);
+  conv_wgrad_kernel<BM_, BN_, PLAIN, BKW, STAGES, WMT>
+      <<<dim3(blocks), dim3(64 * wg_waves<BM_, BN_, WMT>()), lds, st>>>(p);
 }
+
+inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 // 64x256 tiles only when the weight gradient is 64 rows by >= 256 columns (else 3/4 of the tile idles)
 inline bool wg_narrow(int M, int N) { return M <= 64 && N >= 192; }
@@ -309,7 +330,12 @@ int g_wg_split_pct = 100;   // benchmarking scale of the split-K heuristic
 
 template <bool PLAIN>
 void dispatch_wg(const WgParams& p, int blocks_narrow, int blocks_wide, hipStream_t st) {
+  const int blocks_big = cdiv(p.M, 256) * cdiv(p.N, 256) * p.G * p.splits;
+  const int blocks_tall = cdiv(p.M, 256) * cdiv(p.N, 128) * p.G * p.splits;
   switch (g_wg_variant) {
+    // 128-row wave tiles: 8 waves on 256x256 (one block per CU), 4 waves on 256x128
+    case 8: return launch_wg<256, 256, PLAIN, 64, 2, 128>(p, blocks_big, st);
+    case 9: return launch_wg<256, 128, PLAIN, 32, 2, 128>(p, blocks_tall, st);
     case 1: return launch_wg<128, 128, PLAIN, 64, 2>(p, blocks_wide, st);
     case 2: return launch_wg<64, 256, PLAIN, 64, 2>(p, blocks_narrow, st);
     case 3: return launch_wg<128, 128, PLAIN, 32, 2>(p, blocks_wide, st);
@@ -322,8 +348,6 @@ void dispatch_wg(const WgParams& p, int blocks_narrow, int blocks_wide, hipStrea
   if (wg_narrow(p.M, p.N)) launch_wg<64, 256, PLAIN>(p, blocks_narrow, st);
   else launch_wg<128, 128, PLAIN>(p, blocks_wide, st);
 }
-
-inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 // deterministic split-K: dst[i] (+)= sum over s of slab[s][i], in split order
 __global__ void slab_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dst, int64_t n, int splits,
@@ -366,11 +390,14 @@ int dv_conv_wgrad_splits(const ConvWgradArgs& a) {
   const int M = a.Kout, N = a.R * a.S * a.Cg, K = a.Nb * a.P * a.Q;
   const bool narrow = g_wg_variant == 2 || g_wg_variant == 4 || g_wg_variant == 6 ||
                       (g_wg_variant == 0 && wg_narrow(M, N));
-  const int tiles = cdiv(M, narrow ? 64 : 128) * cdiv(N, narrow ? 256 : 128) * a.G;
+  int tm = narrow ? 64 : 128, tn = narrow ? 256 : 128, target = 384;
+  if (g_wg_variant == 8) { tm = 256; tn = 256; target = 256; }  // one 8-wave block per CU
+  if (g_wg_variant == 9) { tm = 256; tn = 128; target = 384; }
+  const int tiles = cdiv(M, tm) * cdiv(N, tn) * a.G;
   const int ktiles = cdiv(K, BK);
   // ~1.5 blocks per CU: measured 5-15 % faster than 3 per CU on the ResNet-50 3x3 / strided
   // layers (half the atomic epilogues), equal on the rest (profiles/wgbench_variants.txt)
-  int splits = cdiv(384 * g_wg_split_pct / 100, tiles);
+  int splits = cdiv(target * g_wg_split_pct / 100, tiles);
   int cap = ktiles / 32;  // >= 2048 pixels per split (atomic budget)
   // few output tiles (small maps / few channels: the Hourglass 8x8-32x32 scales had 9-36 blocks
   // on 256 CUs): trade atomic traffic for parallelism down to 512 pixels per split, until the
