@@ -43,11 +43,11 @@ PYBIND11_MODULE(_C, m) {
                        int Kout, int P_, int Q, int R, int S, int sh, int sw, int ph, int pw, int dh, int dw, int tgather,
                        int OH, int OW, int osh, int osw, int oph, int opw, int ldy, int act, float slope, uptr res,
                        uptr st, uptr bnx, uptr bnbits, uptr bnprm, uptr bnacc, int bnmode, int bnact, float bnslope,
-                       uptr resbits, int resact, float resslope, int reflect, int ksplit, uptr ypart) {
+                       uptr resbits, int resact, float resslope, int reflect, int ksplit, uptr ypart, int zfill) {
     ConvFwdArgs a{CP(x), CP(w), P(y), CFP(bias), FP(stats), Nb, H, W, Cg, ldx, G, Kout, P_, Q, R, S, sh, sw, ph, pw,
                   dh, dw, tgather, OH, OW, osh, osw, oph, opw, ldy, act, slope, CP(res),
                   CP(bnx), CP(bnbits), CFP(bnprm), FP(bnacc), bnmode, bnact, bnslope, CP(resbits), resact, resslope,
-                  reflect, ksplit, FP(ypart)};
+                  reflect, ksplit, FP(ypart), zfill};
     int r = dv_conv_fwd(a, ST(st));
     if (r < 0) throw std::runtime_error("conv_fwd: unsupported geometry (channels must be a multiple of 8)");
     check_last("conv_fwd");
@@ -59,7 +59,7 @@ PYBIND11_MODULE(_C, m) {
      py::arg("ldy"), py::arg("act"), py::arg("slope"), py::arg("res"), py::arg("st"), py::arg("bnx") = 0,
      py::arg("bnbits") = 0, py::arg("bnprm") = 0, py::arg("bnacc") = 0, py::arg("bnmode") = 0, py::arg("bnact") = 0,
      py::arg("bnslope") = 0.f, py::arg("resbits") = 0, py::arg("resact") = 0, py::arg("resslope") = 0.f,
-     py::arg("reflect") = 0, py::arg("ksplit") = 1, py::arg("ypart") = 0);
+     py::arg("reflect") = 0, py::arg("ksplit") = 1, py::arg("ypart") = 0, py::arg("zfill") = 0);
   m.def("conv_fwd_variant", [](int v) { dv_conv_fwd_variant(v); });
   m.def("bn_tuning", [](int blocks, int unroll) { dv_bn_tuning(blocks, unroll); });
   m.def("dw_variant", [](int v) { dv_dw_variant(v); });

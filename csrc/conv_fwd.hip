@@ -68,6 +68,7 @@ struct FwdParams {
   int reflect;             // generic loader: reflected instead of zero-filled out-of-image taps
   int ksplit, kt_per;      // split-K: K-tiles [split*kt_per, +kt_per) per block (kernels.h)
   float* ypart;            // split-K fp32 slabs [ksplit][M][N] (single group)
+  int zfill;               // strided scatter output: also zero the untouched sibling pixels (kernels.h)
 };
 
 // ReflectionPad2d index map (pad < n): -1 -> 1, n -> n - 2
@@ -458,7 +459,17 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
         else {
           const int img = (int)fdiv((uint32_t)m, p.div_pq), rem = m - img * (p.P * p.Q);
           const int pp = (int)fdiv((uint32_t)rem, p.div_q), qq = rem - pp * p.Q;
-          opix = ((int64_t)img * p.OH + pp * p.osh + p.oph) * p.OW + qq * p.osw + p.opw;
+          const int oh = pp * p.osh + p.oph, ow = qq * p.osw + p.opw;
+          opix = ((int64_t)img * p.OH + oh) * p.OW + ow;
+          if constexpr (!RES) {
+            if (p.zfill && vec) {  // the (osh x osw) - 1 pixels no tap of this output row reaches
+              for (int a = 0; a < p.osh; ++a)
+                for (int b = 0; b < p.osw; ++b)
+                  if ((a | b) && oh + a < p.OH && ow + b < p.OW)
+                    *reinterpret_cast<uint4*>(p.y + (opix + (int64_t)a * p.OW + b) * p.ldy + goff_y + n) =
+                        uint4{0u, 0u, 0u, 0u};
+            }
+          }
         }
         yoff = opix * p.ldy + goff_y + n;
       }
@@ -752,6 +763,12 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
   p.resbits = (const uint8_t*)a.resbits; p.resact = a.resact; p.resslope = a.resslope;
   p.reflect = a.reflect;
   p.ksplit = 1; p.kt_per = 1 << 30; p.ypart = nullptr;
+  // zero-filling scatter: plain epilogue, no residual, a strided map with no offset whose
+  // siblings tile the output grid (OH <= P*osh, OW <= Q*osw), vector stores
+  p.zfill = a.zfill;
+  if (p.zfill && (a.bias || a.act || a.stats || a.res || a.bnmode || a.tgather || a.oph || a.opw || a.ksplit > 1 ||
+                  a.OH > a.P * a.osh || a.OW > a.Q * a.osw || (a.Kout % 8) || (a.ldy % 8)))
+    return -1;
   const u16* fin_res = nullptr;
   float* fin_stats = nullptr;
   if (a.ksplit > 1 && a.ypart) {

@@ -41,6 +41,10 @@ struct ConvFwdArgs {
   // activation and writes bf16 y (deterministic; bias/act only, no statistics / residual / BN)
   int ksplit;
   float* ypart;
+  // 1: strided output map (osh/osw > 1, no offset) of a scatter-form dgrad: every stored chunk
+  // also zeroes the (osh x osw) - 1 output pixels its tap never reaches, so the output needs no
+  // separate zero fill (1x1 stride-s dgrad: every pixel of the input grid is written once)
+  int zfill = 0;
 };
 
 struct ConvWgradArgs {

@@ -128,7 +128,7 @@ def conv_ksplit(M, O, K, G=1):
 
 def conv_fwd_raw(x, wk, y, bias, stats, N, H, W, Cg, ldx, G, Kout, P, Q, R, S, stride, padding, dilation,
                  act=0, slope=0.0, tgather=0, omap=None, ldy=None, res=None, bnref=None, resmask=None, reflect=False,
-                 ksplit=1):
+                 ksplit=1, zfill=0):
     """Launch the implicit-GEMM kernel. ``bnref`` (ops.bn.BNRef): also reduce that BatchNorm's
     backward statistics over ``y`` in the epilogue; returns True when that was done.
     ``resmask`` (bits, act, slope): ``res`` is a raw gradient masked by act'() before the add."""
@@ -144,6 +144,8 @@ def conv_fwd_raw(x, wk, y, bias, stats, N, H, W, Cg, ldx, G, Kout, P, Q, R, S, s
         bn.update(resbits=ptr(resmask[0]), resact=int(resmask[1]), resslope=float(resmask[2]))
     if reflect:
         bn["reflect"] = 1
+    if zfill:
+        bn["zfill"] = 1
     if ksplit > 1:  # fp32 slabs [ksplit][M][Kout], summed + bias + act by the finalize pass
         part = torch.empty((ksplit, N * P * Q, Kout), dtype=F32, device=y.device)
         bn.update(ksplit=int(ksplit), ypart=ptr(part))
@@ -197,10 +199,14 @@ def _dgrad(dy, weight, x_shape, Cg_x, G, stride, padding, dilation, device, accu
             accum = accum.grad
         else:
             accum = accum.materialize()
+    zfill = 0
     if accum is not None and Cg_x == Ig and _accumulable(accum, (N, G * Cg_x, H, W)):
         dX, res = accum, accum  # scattered positions get res + val, the others keep res
     else:
-        dX, res = alloc_cl((N, G * Cg_x, H, W), zero=(scatter or Cg_x != Ig), device=device), None
+        # a strided 1x1 scatter zeroes the pixels its taps never reach in the same epilogue
+        # (no separate fill pass) when the output is one dense group
+        zfill = int(scatter and Cg_x == Ig and G == 1 and Ig % 8 == 0 and H <= P * sh and W <= Q * sw)
+        dX, res = alloc_cl((N, G * Cg_x, H, W), zero=((scatter and not zfill) or Cg_x != Ig), device=device), None
     if (sh, sw) == (1, 1):
         fuse = bnref if (bnref is not None and G == 1 and Cg_x == Ig and (res is not None or accum is None)) else None
         if conv_fwd_raw(dy, wd, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, H, W, R, S, (1, 1), (-ph, -pw),
@@ -208,7 +214,7 @@ def _dgrad(dy, weight, x_shape, Cg_x, G, stride, padding, dilation, device, accu
             fuse.mark_fused(dX)
     elif scatter:
         conv_fwd_raw(dy, wd, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, P, Q, 1, 1, (1, 1), (0, 0), (1, 1),
-                     omap=(H, W, sh, sw, 0, 0), ldy=G * Cg_x, res=res)
+                     omap=(H, W, sh, sw, 0, 0), ldy=G * Cg_x, res=res, zfill=zfill)
     else:
         conv_fwd_raw(dy, wd, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, H, W, R, S, stride, padding, dilation,
                      tgather=1, ldy=G * Cg_x, res=res)

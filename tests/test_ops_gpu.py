@@ -41,6 +41,8 @@ CONV_CASES = [
     (2, 64, 14, 14, 64, 1, 1, 0, 1),
     (2, 64, 14, 14, 128, 3, 1, 1, 1),
     (2, 256, 14, 14, 128, 1, 2, 0, 1),
+    (2, 64, 15, 13, 64, 1, 2, 0, 1),     # 1x1 stride-2 scatter dgrad, odd map: zero-filling epilogue
+    (2, 64, 14, 16, 32, 1, 3, 0, 1),     # 1x1 stride-3 scatter: 8 zero siblings per written pixel
     (2, 3, 32, 32, 64, 7, 2, 3, 1),      # stem, C padded 3 -> 8
     (2, 32, 17, 15, 48, 3, 2, 1, 1),     # stride-2 3x3: divisibility-gather dgrad
     (2, 64, 9, 9, 255, 1, 1, 0, 1),      # YOLO head: 255 outputs (padded channel stride)
