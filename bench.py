@@ -131,6 +131,9 @@ def main():
     ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"],
                     help="gradient all-reduce wire format (fp32 master gradients either way)")
     ap.add_argument("--device", default=None, help="cpu to force the CPU plumbing path")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the training step as a HIP graph and replay it (single process; "
+                         "deep_vision_amd/train/graph.py) -- for launch-bound models")
     args = ap.parse_args()
 
     import os
@@ -180,6 +183,14 @@ def main():
             ddp.finish()
         opt.step(grad_scale=gscale)
         return loss
+
+    if args.graph:
+        if ddp or not cuda or amp:
+            raise SystemExit("[bench] --graph needs a single native GPU process")
+        from deep_vision_amd.train.graph import CapturedStep
+
+        cap = CapturedStep(step, opt, model=model, warmup=2)  # 2 eager side-stream steps, then capture
+        step = cap  # noqa: F811 - replays from here on
 
     for _ in range(args.warmup):
         loss = step()
@@ -242,6 +253,7 @@ def main():
                 "bucket_mb": args.bucket_mb,
                 "optimizer": f"{type(opt).__name__} {SPECS[args.model][3]}",
                 "backend": args.backend,
+                "hip_graph": bool(args.graph),
                 "device": str(device),
                 "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],
             },

@@ -67,9 +67,12 @@ __global__ __launch_bounds__(NT) void softmax_xent_kernel(const void* __restrict
   }
 }
 
+// hp (optional, device): [lr, bc1, bc2, step] written by the host before a HIP-graph replay, so a
+// captured optimizer step follows LR schedules / Adam bias correction without re-capture
 __global__ __launch_bounds__(NT) void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ buf,
                                                    int64_t n, float lr, float momentum, float dampening, float wd,
-                                                   int nesterov, int first, float gscale) {
+                                                   int nesterov, int first, float gscale, const float* __restrict__ hp) {
+  if (hp) lr = hp[0];
   for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
     const float pv = p[i];
     float d = g[i] * gscale + wd * pv;
@@ -84,7 +87,9 @@ __global__ __launch_bounds__(NT) void sgd_kernel(float* __restrict__ p, const fl
 
 __global__ __launch_bounds__(NT) void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                                                     float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps,
-                                                    float wd, int decoupled, float bc1, float bc2, float gscale) {
+                                                    float wd, int decoupled, float bc1, float bc2, float gscale,
+                                                    const float* __restrict__ hp) {
+  if (hp) { lr = hp[0]; bc1 = hp[1]; bc2 = hp[2]; }
   for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
     float pv = p[i];
     float gv = g[i] * gscale;
@@ -99,7 +104,9 @@ __global__ __launch_bounds__(NT) void adam_kernel(float* __restrict__ p, const f
 
 __global__ __launch_bounds__(NT) void rmsprop_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ sq,
                                                        float* __restrict__ mom, float* __restrict__ gavg, int64_t n, float lr,
-                                                       float alpha, float eps, float wd, float momentum, int centered, float gscale) {
+                                                       float alpha, float eps, float wd, float momentum, int centered, float gscale,
+                                                       const float* __restrict__ hp) {
+  if (hp) lr = hp[0];
   for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
     const float pv = p[i];
     const float gv = g[i] * gscale + wd * pv;
@@ -134,16 +141,16 @@ void dv_softmax_xent(const void* logits, int is_bf16, const int64_t* labels, int
   else softmax_xent_kernel<false><<<rows, NT, 0, st>>>(logits, labels, C, loss_rows, grad, grad_scale, label_smoothing);
 }
 void dv_sgd(float* p, const float* g, float* buf, int64_t n, float lr, float momentum, float dampening, float wd,
-            int nesterov, int first, float gscale, hipStream_t st) {
-  sgd_kernel<<<grid_for(n), NT, 0, st>>>(p, g, buf, n, lr, momentum, dampening, wd, nesterov, first, gscale);
+            int nesterov, int first, float gscale, const float* hp, hipStream_t st) {
+  sgd_kernel<<<grid_for(n), NT, 0, st>>>(p, g, buf, n, lr, momentum, dampening, wd, nesterov, first, gscale, hp);
 }
 void dv_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps, float wd,
-             int decoupled, float bc1, float bc2, float gscale, hipStream_t st) {
-  adam_kernel<<<grid_for(n), NT, 0, st>>>(p, g, m, v, n, lr, b1, b2, eps, wd, decoupled, bc1, bc2, gscale);
+             int decoupled, float bc1, float bc2, float gscale, const float* hp, hipStream_t st) {
+  adam_kernel<<<grid_for(n), NT, 0, st>>>(p, g, m, v, n, lr, b1, b2, eps, wd, decoupled, bc1, bc2, gscale, hp);
 }
 void dv_rmsprop(float* p, const float* g, float* sq, float* mom, float* gavg, int64_t n, float lr, float alpha, float eps,
-                float wd, float momentum, int centered, float gscale, hipStream_t st) {
-  rmsprop_kernel<<<grid_for(n), NT, 0, st>>>(p, g, sq, mom, gavg, n, lr, alpha, eps, wd, momentum, centered, gscale);
+                float wd, float momentum, int centered, float gscale, const float* hp, hipStream_t st) {
+  rmsprop_kernel<<<grid_for(n), NT, 0, st>>>(p, g, sq, mom, gavg, n, lr, alpha, eps, wd, momentum, centered, gscale, hp);
 }
 void dv_sumsq(const float* x, int64_t n, float* out, hipStream_t st) {
   sumsq_kernel<<<std::min(grid_for(n), 1024), NT, 0, st>>>(x, n, out);

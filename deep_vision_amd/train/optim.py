@@ -81,6 +81,36 @@ class _FlatOptimizer(torch.optim.Optimizer):
         return dict(param=pflat, grad=gflat, views=views, gviews=gviews, offsets=offs, states=states, step=0,
                     first=True)
 
+    # ---------------- device-side hyperparameters (HIP-graph replay) ----------------
+    def use_device_hparams(self, on: bool = True):
+        """Kernels read (lr, bias corrections) from a per-group device tensor ``hp`` instead of
+        launch arguments, so a step captured in a HIP graph (train.graph.CapturedStep) follows LR
+        schedules and Adam's step count: ``graph_tick()`` writes the next step's values before
+        each replay."""
+        for f in self._flat:
+            if f is not None:
+                f["hp"] = torch.zeros(4, dtype=torch.float32, device=f["param"].device) if on else None
+
+    def _hparams(self, group, step):
+        """(lr, bias-correction-1, bias-correction-2) of step number ``step`` (1-based)."""
+        return float(group["lr"]), 1.0, 1.0
+
+    @torch.no_grad()
+    def graph_tick(self):
+        """Advance the host step counters as one eager step() would, and write the device
+        hyperparameters of that step (ordered on the current stream before the replay)."""
+        for group, f in zip(self.param_groups, self._flat):
+            if f is None:
+                continue
+            f["step"] += 1
+            f["first"] = False
+            lr, bc1, bc2 = self._hparams(group, f["step"])
+            f["hp"].copy_(torch.tensor([lr, bc1, bc2, float(f["step"])], dtype=torch.float32))
+
+    def _hp_ptr(self, f):
+        hp = f.get("hp")
+        return 0 if hp is None else ptr(hp)
+
     def param_views(self):
         return [v for f in self._flat if f for v in f["views"]]
 
@@ -209,7 +239,8 @@ class FusedSGD(_FlatOptimizer):
         buf = f["states"]["momentum_buffer"][off:off + n]
         if p.is_cuda:
             lib().sgd(ptr(p), ptr(gr), ptr(buf), n, float(g["lr"]), float(g["momentum"]), float(g["dampening"]),
-                      float(g["weight_decay"]), int(g["nesterov"]), int(f["first"]), float(gs), stream_handle())
+                      float(g["weight_decay"]), int(g["nesterov"]), int(f["first"]), float(gs), stream_handle(),
+                      hp=self._hp_ptr(f))
             return
         d = gr * gs + g["weight_decay"] * p
         if g["momentum"] != 0:
@@ -227,18 +258,21 @@ class FusedAdam(_FlatOptimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, decoupled=False):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, decoupled=decoupled))
 
+    def _hparams(self, group, step):
+        b1, b2 = group["betas"]
+        return float(group["lr"]), 1 - b1 ** step, 1 - b2 ** step
+
     def _update(self, g, f, off, n, gs):
         b1, b2 = g["betas"]
-        t = f["step"]
-        bc1 = 1 - b1 ** t
-        bc2 = 1 - b2 ** t
+        _, bc1, bc2 = self._hparams(g, f["step"])
         p = f["param"][off:off + n]
         gr = f["grad"][off:off + n]
         m = f["states"]["exp_avg"][off:off + n]
         v = f["states"]["exp_avg_sq"][off:off + n]
         if p.is_cuda:
             lib().adam(ptr(p), ptr(gr), ptr(m), ptr(v), n, float(g["lr"]), float(b1), float(b2), float(g["eps"]),
-                       float(g["weight_decay"]), int(g["decoupled"]), float(bc1), float(bc2), float(gs), stream_handle())
+                       float(g["weight_decay"]), int(g["decoupled"]), float(bc1), float(bc2), float(gs), stream_handle(),
+                       hp=self._hp_ptr(f))
             return
         grad = gr * gs
         if g["decoupled"]:
@@ -267,7 +301,7 @@ class FusedRMSprop(_FlatOptimizer):
         if p.is_cuda:
             lib().rmsprop(ptr(p), ptr(gr), ptr(sq), ptr(mom), ptr(ga), n, float(g["lr"]), float(g["alpha"]),
                           float(g["eps"]), float(g["weight_decay"]), float(g["momentum"]), int(g["centered"]), float(gs),
-                          stream_handle())
+                          stream_handle(), hp=self._hp_ptr(f))
             return
         grad = gr * gs + g["weight_decay"] * p
         sq.mul_(g["alpha"]).addcmul_(grad, grad, value=1 - g["alpha"])

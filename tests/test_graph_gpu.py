@@ -1,0 +1,75 @@
+"""HIP-graph captured training step (deep_vision_amd/train/graph.py): replays must reproduce the
+eager trajectory -- same parameters after N steps with SGD-momentum and with Adam (device-side LR /
+bias correction), LR changes between replays honoured, BatchNorm batch counts advanced."""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _net():
+    from deep_vision_amd import nn
+
+    torch.manual_seed(0)
+    return torch.nn.Sequential(nn.Conv2d(8, 32, 3, padding=1, bias=False), nn.BatchNorm2d(32), nn.ReLU(),
+                               nn.Conv2d(32, 16, 3, stride=2, padding=1), nn.AdaptiveAvgPool2d((1, 1)),
+                               torch.nn.Flatten(), nn.Linear(16, 10)).to(DEV)
+
+
+@pytest.mark.parametrize("opt_name", ["SGD", "Adam"])
+def test_captured_step_matches_eager(opt_name):
+    from deep_vision_amd import ops as F
+    from deep_vision_amd.train.graph import CapturedStep
+    from deep_vision_amd.train.optim import OPTIMIZERS
+
+    kw = dict(lr=0.05, momentum=0.9, weight_decay=1e-4) if opt_name == "SGD" else dict(lr=1e-3)
+    a = _net()
+    b = copy.deepcopy(a)
+    oa, ob = OPTIMIZERS[opt_name](a.parameters(), **kw), OPTIMIZERS[opt_name](b.parameters(), **kw)
+    xs = [torch.randn(16, 8, 20, 20, device=DEV) for _ in range(8)]
+    ys = [torch.randint(0, 10, (16,), device=DEV) for _ in range(8)]
+
+    def make_step(model, opt):
+        def step(x, y):
+            opt.zero_grad()
+            loss = F.cross_entropy(model(x), y)
+            loss.backward()
+            opt.step()
+            return loss
+        return step
+
+    sa = make_step(a, oa)
+    for i in range(8):  # eager reference: 8 steps, LR halved after step 5
+        if i == 5:
+            for g in oa.param_groups:
+                g["lr"] *= 0.5
+        sa(xs[i], ys[i])
+    # captured: 2 eager warm-up steps on a side stream (the first two batches), then replays
+    xst, yst = xs[0].clone(), ys[0].clone()
+    it = iter(range(2))
+    warm = [(xs[0], ys[0]), (xs[1], ys[1])]
+    step_b = make_step(b, ob)
+
+    def step_fn(x, y):
+        k = next(it, None)
+        if k is not None:  # the warm-up calls consume the first two batches
+            x.copy_(warm[k][0]); y.copy_(warm[k][1])
+        return step_fn.inner(x, y)
+
+    step_fn.inner = step_b
+    cap = CapturedStep(step_fn, ob, (xst, yst), model=b, warmup=2)
+    for i in range(2, 8):
+        if i == 5:
+            for g in ob.param_groups:
+                g["lr"] *= 0.5
+        cap(xs[i], ys[i])
+    torch.cuda.synchronize()
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        err = ((pa - pb).abs().max() / pa.abs().max().clamp_min(1e-6)).item()
+        assert err < 1e-3, (n, err)
+    assert ob._flat[0]["step"] == oa._flat[0]["step"] == 8
+    assert int(b[1].state_dict()["num_batches_tracked"]) == int(a[1].state_dict()["num_batches_tracked"]) == 8
