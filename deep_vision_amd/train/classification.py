@@ -119,10 +119,8 @@ def train(loader, net, optimizer, epoch, loggers, eng: Engine, cfg: TrainConfig,
         image = data["image"].to(eng.device, non_blocking=True)
         target = data[key].to(eng.device, dtype=torch.long, non_blocking=True)
         with eng.timer.step(samples=image.shape[0]):
-            with eng.timer.phase("fwd"):
-                loss, main = _criterion(net(image), target, aux_w)
             lr = C.get_lr(optimizer)
-            eng.backward_step(loss, net, optimizer)
+            loss, main = eng.train_step(net, optimizer, lambda im, t: _criterion(net(im), t, aux_w), image, target)
         if epoch_stats is not None:
             a1, a5 = accuracy(main.detach(), target, topk=(1, min(5, main.shape[1])))
             n = target.numel()
@@ -220,8 +218,8 @@ def validate(loader, net, epoch, loggers, eng: Engine, cfg: TrainConfig, max_ste
 
 def run_epochs(config: TrainConfig, checkpoint_path=None, *, device=None, data_dir=None, synthetic=False,
                epochs=None, max_steps=None, val_steps=None, synthetic_size=512, num_workers=None, seed=0,
-               checkpoint_dir=None, profile=False, batch_size=None, tensorboard_dir=None):
-    eng = Engine(device=device, profile=profile)
+               checkpoint_dir=None, profile=False, batch_size=None, tensorboard_dir=None, graph=False):
+    eng = Engine(device=device, profile=profile, graph=graph)
     seed_everything(seed, eng.rank)
     eng.log("CUDA is available: {}".format(torch.cuda.is_available()))
     cfg = config
@@ -302,6 +300,8 @@ def add_common_args(ap: argparse.ArgumentParser):
                          "rocprofv3 --kernel-trace --stats (counters are collected in separate runs)")
     ap.add_argument("--tensorboard-dir", default=None, help="TensorBoard root (Keras configs: ./tensorboard)")
     ap.add_argument("--nproc", type=int, default=None, help="spawn N ranks (one per GPU) via torch.distributed.run")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the training step as a HIP graph and replay it (single GPU; train/graph.py)")
     return ap
 
 
@@ -332,4 +332,4 @@ def main(argv=None, choices=None, default=None):
     run_epochs(cfg, ck, device=a.device, data_dir=a.data_dir, synthetic=a.synthetic, epochs=a.epochs,
                max_steps=a.max_steps, val_steps=a.val_steps, synthetic_size=a.synthetic_size, num_workers=a.workers,
                seed=a.seed, checkpoint_dir=a.checkpoint_dir, profile=a.profile == "timer", batch_size=a.batch_size,
-               tensorboard_dir=a.tensorboard_dir)
+               tensorboard_dir=a.tensorboard_dir, graph=a.graph)

@@ -172,6 +172,9 @@ class Trainer:
         total, _ = centernet_loss(outputs, labels)
         return total, None
 
+    def _forward_loss(self, images, labels):
+        return self.compute_loss(self.model(images), labels, images.shape[0])
+
     def train_epoch(self, loader, epoch, max_steps=None):
         self.model.train()
         eng = self.eng
@@ -183,10 +186,7 @@ class Trainer:
                 break
             images, labels = _to_device(batch, eng.device, self.cfg)
             with eng.timer.step(samples=images.shape[0]):
-                with eng.timer.phase("fwd"):
-                    outputs = self.model(images)
-                    loss, comps = self.compute_loss(outputs, labels, images.shape[0])
-                eng.backward_step(loss, self.model, self.optimizer)
+                loss, comps = eng.train_step(self.model, self.optimizer, self._forward_loss, images, labels)
             nb += 1
             total += loss.detach().float()
             acc[0] += loss.detach().float()
@@ -271,8 +271,8 @@ class Trainer:
 
 def train(cfg: TrainConfig, checkpoint=None, *, train_glob=None, val_glob=None, synthetic=False, synthetic_size=64,
           epochs=None, max_steps=None, val_steps=None, device=None, workers=2, log_every=10, checkpoint_dir=None,
-          seed=None, batch_size=None, profile=False, tensorboard_dir=None):
-    eng = Engine(device=device, log_every=log_every, profile=profile)
+          seed=None, batch_size=None, profile=False, tensorboard_dir=None, graph=False):
+    eng = Engine(device=device, log_every=log_every, profile=profile, graph=graph)
     seed_everything(cfg.extras.get("seed", 0) if seed is None else seed, eng.rank)
     if batch_size:
         cfg = cfg.replace(batch_size=batch_size)
@@ -312,6 +312,7 @@ def add_args(ap):
     ap.add_argument("--profile", nargs="?", const="timer", default=None, choices=["timer", "rocprof"])
     ap.add_argument("--tensorboard-dir", default=None)
     ap.add_argument("--nproc", type=int, default=None)
+    ap.add_argument("--graph", action="store_true", help="HIP-graph replay of the training step (single GPU)")
     return ap
 
 
@@ -334,4 +335,4 @@ def main(family_config: str, argv=None, tfrecords_default="./dataset/tfrecords")
                  val_glob=os.path.join(a.tfrecords, "val*"), synthetic=a.synthetic, synthetic_size=a.synthetic_size,
                  epochs=a.epochs, max_steps=a.max_steps, val_steps=a.val_steps, device=a.device, workers=a.workers,
                  log_every=a.log_every, checkpoint_dir=a.checkpoint_dir, batch_size=a.batch_size,
-                 profile=a.profile == "timer", tensorboard_dir=a.tensorboard_dir)
+                 profile=a.profile == "timer", tensorboard_dir=a.tensorboard_dir, graph=a.graph)

@@ -46,7 +46,7 @@ def make_optimizer(name, params, kw):
 
 class Engine:
     def __init__(self, device: str | None = None, backend: str | None = None, bucket_mb: float = 64.0,
-                 log_every: int = 10, watchdog_s: float | None = None, profile: bool = False):
+                 log_every: int = 10, watchdog_s: float | None = None, profile: bool = False, graph: bool = False):
         if device == "cpu":
             backend = backend or "gloo"
         install_backend_error_handling()  # RCCL async errors abort the communicator (before init)
@@ -63,6 +63,12 @@ class Engine:
         # then tears the job down) instead of blocking the whole job forever
         self.comm_watchdog = CommWatchdog().start() if self.world > 1 else None
         self.step_count = 0
+        # HIP-graph replay of the whole step (train/graph.py): single GPU process only; the
+        # non-finite skip and fault injection need the eager step and are off in this mode
+        self.graph = bool(graph) and self.world == 1 and self.device.type == "cuda"
+        if graph and not self.graph:
+            self.log("[dv] --graph needs a single GPU process: running eagerly")
+        self._graphed = {}
 
     def log(self, *a, **kw):
         if self.is_main:
@@ -117,6 +123,27 @@ class Engine:
         if self.watchdog is not None:
             self.watchdog.beat()
         return ok
+
+    def train_step(self, model, optimizer, forward_loss, *inputs):
+        """One optimisation step: ``forward_loss(*inputs) -> (loss, extra)``, backward, all-reduce,
+        optimizer step. Returns (loss, extra). With ``graph`` the step is captured on the first
+        batch of each input signature and replayed (train.graph.GraphedTrainStep)."""
+        def eager(*args):
+            with self.timer.phase("fwd"):
+                loss, extra = forward_loss(*args)
+            self.backward_step(loss, model, optimizer)
+            return loss, extra
+
+        if not self.graph:
+            return eager(*inputs)
+        from .graph import GraphedTrainStep
+
+        key = (id(model), id(optimizer), getattr(forward_loss, "__code__", forward_loss))
+        g = self._graphed.get(key)
+        if g is None:
+            g = self._graphed[key] = GraphedTrainStep(model, optimizer, forward_loss, eager)
+        self.step_count += 1
+        return g(*inputs)
 
     def reduce_sum(self, values):
         return D.all_reduce_scalars(list(values), device=self.device if self.device.type == "cuda" else "cpu")

@@ -56,6 +56,7 @@ class CapturedStep:
                     self._bns.append(m)
         self.graph = torch.cuda.CUDAGraph()
         self.outputs = None
+        self.warmup_outputs = None  # what the last eager warm-up step returned (a real step)
         self._capture(warmup)
 
     def _capture(self, warmup):
@@ -63,7 +64,7 @@ class CapturedStep:
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(max(1, warmup)):  # real steps: allocator warm-up, first-step optimizer state
-                self.step_fn(*self.static_inputs)
+                self.warmup_outputs = self.step_fn(*self.static_inputs)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         self.opt.use_device_hparams(True)
@@ -88,3 +89,47 @@ class CapturedStep:
             m._dv_nbt_pending = m.__dict__.get("_dv_nbt_pending", 0) + 1
         self.graph.replay()
         return self.outputs
+
+
+class GraphedTrainStep:
+    """Trainer-side wrapper (train.engine.Engine.train_step): ``forward_loss(*inputs) -> (loss,
+    extra)`` plus backward and optimizer step, captured on the first batch of each new input
+    signature (shapes / dtypes of the flattened inputs) and replayed for every later batch with
+    that signature. The capturing call trains on its own batch (the eager warm-up step); batches
+    of a different signature (e.g. a short last batch) run eagerly through ``eager_step``."""
+
+    def __init__(self, model, optimizer, forward_loss: Callable, eager_step: Callable, max_graphs: int = 2):
+        self.model, self.opt, self.forward_loss, self.eager_step = model, optimizer, forward_loss, eager_step
+        self.max_graphs = max_graphs
+        self.graphs = {}  # signature -> (CapturedStep, treespec)
+
+    @staticmethod
+    def _signature(flat):
+        return tuple((tuple(t.shape), t.dtype, t.device) if isinstance(t, torch.Tensor) else ("const", t) for t in flat)
+
+    def __call__(self, *inputs):
+        from torch.utils._pytree import tree_flatten, tree_unflatten
+
+        flat, spec = tree_flatten(inputs)
+        if not all(isinstance(t, torch.Tensor) and t.is_cuda for t in flat):
+            return self.eager_step(*inputs)
+        sig = self._signature(flat)
+        entry = self.graphs.get(sig)
+        if entry is not None:
+            return entry[0](*flat)
+        if len(self.graphs) >= self.max_graphs:
+            return self.eager_step(*inputs)
+        static = [t.detach().clone() for t in flat]
+        fl, opt = self.forward_loss, self.opt
+
+        def step_fn(*st):
+            args = tree_unflatten(list(st), spec)
+            opt.zero_grad()
+            loss, extra = fl(*args)
+            loss.backward()
+            opt.step()
+            return loss, extra
+
+        cap = CapturedStep(step_fn, opt, static, model=self.model, warmup=1)
+        self.graphs[sig] = (cap, spec)
+        return cap.warmup_outputs

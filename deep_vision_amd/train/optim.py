@@ -95,6 +95,10 @@ class _FlatOptimizer(torch.optim.Optimizer):
         """(lr, bias-correction-1, bias-correction-2) of step number ``step`` (1-based)."""
         return float(group["lr"]), 1.0, 1.0
 
+    def _write_hp(self, group, f):
+        lr, bc1, bc2 = self._hparams(group, f["step"])
+        f["hp"].copy_(torch.tensor([lr, bc1, bc2, float(f["step"])], dtype=torch.float32))
+
     @torch.no_grad()
     def graph_tick(self):
         """Advance the host step counters as one eager step() would, and write the device
@@ -104,8 +108,7 @@ class _FlatOptimizer(torch.optim.Optimizer):
                 continue
             f["step"] += 1
             f["first"] = False
-            lr, bc1, bc2 = self._hparams(group, f["step"])
-            f["hp"].copy_(torch.tensor([lr, bc1, bc2, float(f["step"])], dtype=torch.float32))
+            self._write_hp(group, f)
 
     def _hp_ptr(self, f):
         hp = f.get("hp")
@@ -164,6 +167,10 @@ class _FlatOptimizer(torch.optim.Optimizer):
                 continue
             segs = self._sync_grads(group, f)
             f["step"] += 1
+            # device hyperparameters: an eager step writes its own; inside a graph capture the
+            # values come from graph_tick() before each replay (a captured copy would replay stale)
+            if f.get("hp") is not None and not torch.cuda.is_current_stream_capturing():
+                self._write_hp(group, f)
             for off, n in segs:
                 self._update(group, f, off, n, grad_scale)
             f["first"] = False

@@ -73,3 +73,27 @@ def test_captured_step_matches_eager(opt_name):
         assert err < 1e-3, (n, err)
     assert ob._flat[0]["step"] == oa._flat[0]["step"] == 8
     assert int(b[1].state_dict()["num_batches_tracked"]) == int(a[1].state_dict()["num_batches_tracked"]) == 8
+
+
+def test_classifier_trainer_graph_mode(tmp_path):
+    """run_epochs(..., graph=True): the step is captured on the first batch and replayed; the
+    short last batch of the epoch runs eagerly (a second signature would be captured, capped at 2)."""
+    from deep_vision_amd.config import get_config
+    from deep_vision_amd.train.classification import run_epochs
+
+    cfg = get_config("lenet5")
+    last, loggers = run_epochs(cfg, None, device="cuda", synthetic=True, synthetic_size=200, num_workers=0, epochs=1,
+                               max_steps=4, val_steps=1, checkpoint_dir=str(tmp_path) + "/", graph=True)
+    assert last
+    assert all(v == v for v in loggers["train_loss"]["value"])  # finite (no NaN) losses
+
+
+def test_hourglass_trainer_graph_mode(tmp_path):
+    from deep_vision_amd.config import get_config
+    from deep_vision_amd.train.detection import train
+
+    cfg = get_config("hourglass", input_shape=(3, 64, 64), batch_size=2)
+    cfg = cfg.replace(model_params={**cfg.model_params, "num_stack": 2})
+    best = train(cfg, synthetic=True, synthetic_size=6, epochs=1, device="cuda", workers=0, log_every=1,
+                 checkpoint_dir=str(tmp_path), tensorboard_dir=str(tmp_path / "tb"), graph=True)
+    assert best
