@@ -41,8 +41,18 @@ struct WgParams {
   FastDiv div_pq, div_q, div_cg, div_s;
 };
 
-DV_DEVICE void glds16(const void* src, char* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds(GLB_PTR(src), LDS_PTR(lds_wave_base), 16, 0, 0);
+// LDS-DMA of one 1-KB wave piece, issued from inline asm (M0 written and restored in the same
+// statement). The builtin form makes hipcc treat the transposed LDS reads (ds_read_b64_tr_b16,
+// no alias scope) as possibly aliasing the in-flight DMA: it then put an s_waitcnt vmcnt(0) in
+// front of every compute phase, draining the next tile's prefetch and serialising load and MFMA
+// (measured: wgrad at 18-20 % MFMA busy). Asm DMAs are invisible to that bookkeeping; the
+// explicit vmcnt waits before each barrier below are what order them.
+DV_DEVICE void glds16(const void* src, uint32_t dst) {  // dst: wave-uniform LDS byte address
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(dst)
+               : "memory");
 }
 // 16-byte-chunk XOR key of pixel row k (multiples of 2 chunks = 32-B blocks). Rows of >= 256 B
 // take 8 keys; 128-B rows (64 columns) take 4 keys and rely on the row parity for the other
@@ -104,6 +114,7 @@ __global__ __launch_bounds__((64 * wg_waves<BM_, BN_, WMT>()), 2) void conv_wgra
   const int split = logical % p.splits, grp = logical / p.splits;
   const int m0 = tm * BM_, n0 = tn * BN_;
   const char* zero = dv_zero_page;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem));  // LDS address of smem
   const int kt0 = split * p.ktiles_per_split;
   const int kt1 = min((p.K + BK - 1) / BK, kt0 + p.ktiles_per_split);
   const int nt = kt1 - kt0;
@@ -157,7 +168,8 @@ __global__ __launch_bounds__((64 * wg_waves<BM_, BN_, WMT>()), 2) void conv_wgra
     for (int j = 0; j < MI; ++j) {
       const int row = (wid * MI + j) * MRPI + lane / MCH;
       const bool ok = mok[j] && (k0 + row < p.K);
-      glds16(ok ? (const void*)(mrow[j] + (int64_t)k0 * p.ldm) : (const void*)zero, img_m + (wid * MI + j) * 1024);
+      glds16(ok ? (const void*)(mrow[j] + (int64_t)k0 * p.ldm) : (const void*)zero,
+             lds0 + buf * STAGE + (wid * MI + j) * 1024);
     }
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
@@ -175,7 +187,7 @@ __global__ __launch_bounds__((64 * wg_waves<BM_, BN_, WMT>()), 2) void conv_wgra
         if (nok[j] && k0 + row < p.K && (unsigned)h < (unsigned)p.Hin && (unsigned)w < (unsigned)p.Win)
           src = p.x + (((int64_t)w_img[j] * p.Hin + h) * p.Win + w) * p.ldx + goff_x + n_c[j];
       }
-      glds16(src, img_n + (wid * NI + j) * 1024);
+      glds16(src, lds0 + buf * STAGE + MBYTES + (wid * NI + j) * 1024);
     }
   };
   auto advance = [&]() {
@@ -196,22 +208,33 @@ __global__ __launch_bounds__((64 * wg_waves<BM_, BN_, WMT>()), 2) void conv_wgra
 #pragma unroll
     for (int b = 0; b < FM; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // every fragment of the tile is read before the first MFMA (sched_barrier): left to itself the
+  // scheduler recycled one fragment register per 4 MFMAs and waited on each re-read, exposing
+  // the LDS latency every 4 MFMAs; here it is exposed once per tile, the in-order LDS returns
+  // release the MFMAs as they arrive
   auto compute = [&](int buf) {
     const char* img_m = smem + buf * STAGE;
     const char* img_n = img_m + MBYTES;
+    constexpr int KK = BK / 32;
+    bf16x8 fa[KK][4], fb[KK][FM];
 #pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk) {
-      bf16x8 fa[4], fb[FM];
+    for (int kk = 0; kk < KK; ++kk) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fa[j] = read_mn<BN_>(img_n, wave_n * 64 + j * 16, kk * 32, lane);
+      for (int j = 0; j < 4; ++j) fa[kk][j] = read_mn<BN_>(img_n, wave_n * 64 + j * 16, kk * 32, lane);
 #pragma unroll
-      for (int i = 0; i < FM; ++i) fb[i] = read_mn<BM_>(img_m, wave_m * WMT + i * 16, kk * 32, lane);
+      for (int i = 0; i < FM; ++i) fb[kk][i] = read_mn<BM_>(img_m, wave_m * WMT + i * 16, kk * 32, lane);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int i = 0; i < FM; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[j], fb[i], acc[j][i], 0, 0, 0);
-    }
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][j], fb[kk][i], acc[j][i], 0, 0, 0);
+    // keep the MFMAs ahead of the caller's DMA wait + barrier (the scheduler may otherwise hoist
+    // that wait above them and expose the next tile's load latency)
+    __builtin_amdgcn_sched_barrier(0);
   };
   if constexpr (STAGES == 2) {
     if (nt > 0) {
