@@ -109,11 +109,13 @@ PYBIND11_MODULE(_C, m) {
     check_last("bn_bwd_finalize");
   });
   m.def("bn_bwd_apply", [](uptr dout, uptr out, uptr x, uptr dx, uptr dres, int64_t n, int C, uptr kA, uptr kB, uptr kC,
-                           uptr mscale, uptr mshift, int act, float slope, int mask_bits, uptr st) {
+                           uptr mscale, uptr mshift, int act, float slope, int mask_bits, uptr st, uptr addend) {
     dv_bn_bwd_apply(CP(dout), CP(out), CP(x), P(dx), P(dres), n, C, CFP(kA), CFP(kB), CFP(kC), CFP(mscale), CFP(mshift), act, slope,
-                    mask_bits, ST(st));
+                    mask_bits, CP(addend), ST(st));
     check_last("bn_bwd_apply");
-  });
+  }, py::arg("dout"), py::arg("out"), py::arg("x"), py::arg("dx"), py::arg("dres"), py::arg("n"), py::arg("C"), py::arg("kA"),
+     py::arg("kB"), py::arg("kC"), py::arg("mscale"), py::arg("mshift"), py::arg("act"), py::arg("slope"),
+     py::arg("mask_bits"), py::arg("st"), py::arg("addend") = 0);
   m.def("bn_bwd_eval", [](uptr dout, uptr out, uptr dx, uptr dres, int64_t n, int C, uptr scale, int act, float slope, uptr st) {
     dv_bn_bwd_eval(CP(dout), CP(out), P(dx), P(dres), n, C, CFP(scale), act, slope, ST(st)); check_last("bn_bwd_eval");
   });

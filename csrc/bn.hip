@@ -304,14 +304,17 @@ __global__ void bn_bwd_finalize_kernel(float* __restrict__ acc, int C, double co
   kC[c] = (float)(a * ((double)mean[c] * is * mdzx - mdz));
 }
 
-// dx = kA*dz + kB*x + kC ; optionally dres = dz
+// dx = kA*dz + kB*x + kC (+ addend) ; optionally dres = dz. ``addend``: another gradient of the
+// same input (e.g. a pre-activation block's residual path, models/hourglass.py) summed in this pass
+// instead of a separate add; it may alias dx (each element is read before it is written by the
+// same thread), hence no __restrict__ on the two.
 template <int VEC, int MM>
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const u16* __restrict__ dout, const u16* __restrict__ out,
-                                                            const u16* __restrict__ x, u16* __restrict__ dx, u16* __restrict__ dres,
+                                                            const u16* __restrict__ x, u16* dx, u16* __restrict__ dres,
                                                             int64_t rows, int C, int64_t rows_per_block, const float* __restrict__ kA,
                                                             const float* __restrict__ kB, const float* __restrict__ kC,
                                                             const float* __restrict__ mscale, const float* __restrict__ mshift,
-                                                            int act, float slope) {
+                                                            int act, float slope, const u16* addend) {
   RowTile t(C, VEC);
   if (t.lane_r >= t.rpi) return;
   const int64_t r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
@@ -326,10 +329,11 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const u16* __restrict_
 #pragma unroll 2
     for (int64_t r = r0 + t.lane_r; r < r1; r += t.rpi) {
       const int64_t o = r * C + g * VEC;
-      float d[VEC], ov[VEC], xv[VEC], rr[VEC];
+      float d[VEC], ov[VEC], xv[VEC], rr[VEC], av[VEC];
       VecIO<VEC>::load(dout + o, d);
       VecIO<VEC>::load(x + o, xv);
       if constexpr (MM == MM_OUT) VecIO<VEC>::load(out + o, ov);
+      if (addend) VecIO<VEC>::load(addend + o, av);
       uint32_t mb = 0;
       if constexpr (MM == MM_BITS) mb = reinterpret_cast<const uint8_t*>(out)[o >> 3];
 #pragma unroll
@@ -340,6 +344,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const u16* __restrict_
         if constexpr (MM == MM_X) dz = act_bwd(d[k], fmaf(xv[k], ms[k], mh[k]), act, slope);
         rr[k] = dz;
         d[k] = fmaf(a[k], dz, fmaf(b[k], xv[k], cc[k]));
+        if (addend) d[k] += av[k];
       }
       VecIO<VEC>::store(dx + o, d);
       if (dres) VecIO<VEC>::store(dres + o, rr);
@@ -512,8 +517,8 @@ void dv_bn_bwd_finalize(float* acc, int C, double count, const float* gamma, con
 template <int MM>
 static void bwd_apply_launch(int g, const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t rows,
                              int C, int64_t rpb, const float* kA, const float* kB, const float* kC, const float* mscale,
-                             const float* mshift, int act, float slope, hipStream_t st) {
-#define BA_ARGS <<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, (u16*)dx, (u16*)dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope)
+                             const float* mshift, int act, float slope, const void* addend, hipStream_t st) {
+#define BA_ARGS <<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, (u16*)dx, (u16*)dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, (const u16*)addend)
   switch (vec_for(C)) {
     case 8: bn_bwd_apply_kernel<8, MM> BA_ARGS; break;
     case 4: bn_bwd_apply_kernel<4, MM> BA_ARGS; break;
@@ -525,19 +530,20 @@ static void bwd_apply_launch(int g, const void* dout, const void* out, const voi
 
 void dv_bn_bwd_apply(const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t n, int C,
                      const float* kA, const float* kB, const float* kC, const float* mscale, const float* mshift, int act,
-                     float slope, int mask_bits, hipStream_t st) {
+                     float slope, int mask_bits, const void* addend, hipStream_t st) {
   const int v = vec_for(C);
   const int64_t rows = n / C;
   const int64_t rpb = apply_rows_per_block(rows, C, v);
   const int g = (int)((rows + rpb - 1) / rpb);
   if (act && mask_bits && v == 8) {
     bn_bwd_apply_kernel<8, MM_BITS><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, (u16*)dx,
-                                                        (u16*)dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope);
+                                                        (u16*)dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope,
+                                                        (const u16*)addend);
     return;
   }
-  if (!act) bwd_apply_launch<MM_NONE>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, st);
-  else if (out) bwd_apply_launch<MM_OUT>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, st);
-  else bwd_apply_launch<MM_X>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, st);
+  if (!act) bwd_apply_launch<MM_NONE>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, addend, st);
+  else if (out) bwd_apply_launch<MM_OUT>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, addend, st);
+  else bwd_apply_launch<MM_X>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, addend, st);
 }
 
 void dv_bn_bwd_eval(const void* dout, const void* out, void* dx, void* dres, int64_t n, int C, const float* scale,

@@ -94,7 +94,7 @@ void dv_bn_bwd_finalize(float* acc, int C, double count, const float* gamma, con
                         float* dgamma, float* dbeta, int accumulate, float* kA, float* kB, float* kC, hipStream_t st);
 void dv_bn_bwd_apply(const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t n, int C,
                      const float* kA, const float* kB, const float* kC, const float* mscale, const float* mshift, int act,
-                     float slope, int mask_bits, hipStream_t st);
+                     float slope, int mask_bits, const void* addend, hipStream_t st);
 void dv_bn_bwd_eval(const void* dout, const void* out, void* dx, void* dres, int64_t n, int C, const float* scale,
                     int act, float slope, hipStream_t st);
 

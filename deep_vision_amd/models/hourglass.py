@@ -25,6 +25,7 @@ import torch.nn as tnn
 
 from .. import nn
 from .. import ops as F
+from ..ops.conv import GradJoin
 
 
 def _bn(c):
@@ -43,12 +44,15 @@ class BottleneckBlock(tnn.Module):
         self.conv3 = nn.Conv2d(filters // 2, filters, 1)
 
     def forward(self, x):
+        # identity blocks: x's two gradients (the residual path's dy and BN1's dx) meet in BN1's
+        # backward apply pass (GradJoin) instead of an autograd add -- 73 add passes per step
+        j = GradJoin() if self.downsample is None and F.native(x) else None
         identity = self.downsample(x) if self.downsample is not None else x
-        y = F.batch_norm_act(x, self.bn1, "relu")
+        y = F.batch_norm_act(x, self.bn1, "relu", input_join=j)
         y = F.conv_bn_act(y, self.conv1, self.bn2, "relu")
         y = F.conv_bn_act(y, self.conv2, self.bn3, "relu")
         # the residual add rides in conv3's store epilogue (ops.conv2d residual=)
-        return F.conv2d(y, self.conv3.weight, self.conv3.bias, residual=identity)
+        return F.conv2d(y, self.conv3.weight, self.conv3.bias, residual=identity, residual_join=j)
 
 
 class HourglassModule(tnn.Module):

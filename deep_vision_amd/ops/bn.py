@@ -68,7 +68,9 @@ class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, stats, weight, bias, running_mean, running_var, residual, training, momentum, eps, act,
                 slope, ws_fwd, ws_bwd, join=None, refbox=None, r_stats=None, r_weight=None, r_bias=None, r_rm=None,
-                r_rv=None, r_cfg=None):
+                r_rv=None, r_cfg=None, xjoin=None):
+        # xjoin (conv.GradJoin): another consumer of ``x`` stashes its gradient there (e.g. the
+        # identity path of a pre-activation block); the backward apply pass adds it in place
         # r_*: a second, training-mode BatchNorm applied to ``residual`` inside the same pass
         # (a residual block's projection BN): out = act(bn(x) + bn_r(residual)); bn_r's output is
         # never materialised and its backward reads (dout, mask bits, residual) directly
@@ -117,6 +119,7 @@ class _BNActFn(torch.autograd.Function):
         ctx.cfg = (training, act, slope, residual is not None)
         ctx.ws_bwd = ws_bwd
         ctx.join = join
+        ctx.xjoin = xjoin
         ctx.bnref = None
         if refbox is not None and training and ws_bwd is not None and C % 8 == 0 and (not act or bits or residual is None):
             mode = 3 if bits else (2 if act else 1)
@@ -137,7 +140,13 @@ class _BNActFn(torch.autograd.Function):
         dev = x.device
         st = stream_handle()
         L = lib()
-        dx = torch.empty_like(x)
+        xg = ctx.xjoin.take() if ctx.xjoin is not None else None
+        if xg is not None and not isinstance(xg, torch.Tensor):
+            xg = xg.materialize()
+        # the other consumer's gradient is summed inside the apply pass, written over its own buffer
+        fold_x = (xg is not None and training and xg.dtype == BF16 and tuple(xg.shape) == tuple(x.shape)
+                  and xg.is_contiguous(memory_format=torch.channels_last))
+        dx = xg if fold_x else torch.empty_like(x)
         # identity shortcut of a residual block: hand the shortcut consumer's dgrad the raw dout +
         # mask bits instead of writing dres = act'(z)*dout (csrc/conv_fwd.hip resbits epilogue)
         lazy = (LAZY_SHORTCUT and training and has_res and ctx.needs_input_grad[6] and ctx.bits and ctx.join is not None
@@ -167,7 +176,8 @@ class _BNActFn(torch.autograd.Function):
                               ptr(coef[0]), ptr(coef[1]), ptr(coef[2]), st)
         if training:
             L.bn_bwd_apply(ptr(dout), ptr(out), ptr(x), ptr(dx), ptr(dres), x.numel(), C, ptr(coef[0]), ptr(coef[1]),
-                           ptr(coef[2]), ptr(scale), ptr(shift), act, float(slope), int(ctx.bits), st)
+                           ptr(coef[2]), ptr(scale), ptr(shift), act, float(slope), int(ctx.bits), st,
+                           addend=ptr(xg) if fold_x else 0)
         else:
             if act and out is None:  # eval backward needs the mask: rebuild the output
                 out = torch.empty_like(x)
@@ -183,8 +193,10 @@ class _BNActFn(torch.autograd.Function):
             dres = ctx.join.produce(MaskedGrad(dout, out, act, slope))  # `out` holds the mask bits
         elif ctx.join is not None and dres is not None:
             dres = ctx.join.produce(dres)  # folded into the shortcut consumer's dgrad epilogue
+        if xg is not None and not fold_x:
+            dx = dx + xg
         return (dx, None, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None, None, None,
-                None, r_dgamma, r_dbeta, None, None, None)
+                None, r_dgamma, r_dbeta, None, None, None, None)
 
 
 def _residual_bn_backward(ctx, dout, bits, r_x, rprm, r_weight, r_bias, act, slope):
@@ -380,8 +392,11 @@ def bn_momentum(bn) -> float:
     return bn.momentum
 
 
-def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None, residual_join=None, residual_bn=None):
+def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None, residual_join=None, residual_bn=None,
+                   input_join=None):
     """act(BN(x) (+ residual)) with ``bn`` an nn.BatchNorm2d (parameters, buffers, mode).
+    ``input_join`` (conv.GradJoin): x's gradient from another consumer, stashed there by its
+    producer, is added inside this BN's backward apply pass.
     ``residual_bn=(bn_r, stats_r)``: ``residual`` is a raw conv output still to be normalised by
     ``bn_r`` (training mode, batch statistics ``stats_r`` from its conv epilogue); the two BNs,
     the add and the activation run as one pass (see conv_bn_deferred)."""
@@ -419,8 +434,10 @@ def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None, residu
         rargs = (rstats, rbn.weight, rbn.bias, rbn.running_mean, rbn.running_var,
                  (bn_momentum(rbn), rbn.eps, workspace(rbn, "bn_fwd", (STAT_SHARDS, 2, C), x.device),
                   workspace(rbn, "bn_bwd", (STAT_SHARDS, 2, C), x.device)))
+    if not rargs:
+        rargs = (None,) * 6
     y = _BNActFn.apply(x, stats, bn.weight, bn.bias, rm, rv, residual, training, mom,
-                       bn.eps, ACT_IDS[act], float(slope), ws_fwd, ws_bwd, residual_join, refbox, *rargs)
+                       bn.eps, ACT_IDS[act], float(slope), ws_fwd, ws_bwd, residual_join, refbox, *rargs, input_join)
     if refbox:
         y._dv_bnref = refbox[0]  # read by the consumer conv (ops.conv._ConvFn)
     return y

@@ -327,7 +327,7 @@ def _wgrad_workspace(numel, device):
 class _ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats, stats_buf=None,
-                extra=(0, 0), join=None, join_role=None, reflect=False, out_box=None, residual=None):
+                extra=(0, 0), join=None, join_role=None, reflect=False, out_box=None, residual=None, residual_join=None):
         N, Cx, H, W = x.shape
         O, Ig, R, S = weight.shape
         G = groups
@@ -351,6 +351,7 @@ class _ConvFn(torch.autograd.Function):
         conv_fwd_raw(x, wk, y, b, stats, N, H, W, Cg_x, ldx, G, Og, P, Q, R, S, stride, padding, dilation,
                      act=act, slope=slope, reflect=reflect, res=residual, ksplit=ks)
         ctx.has_residual = residual is not None
+        ctx.rjoin = residual_join  # the residual's gradient (= dy) is stashed there for its other consumer
         ctx.save_for_backward(x, weight, y if act else None)
         ctx.bias_param = bias  # leaf parameter (not saved): its gradient may sink in place
         ctx.cfg = (stride, padding, dilation, G, act, slope, Cg_x, bias is not None)
@@ -374,8 +375,8 @@ class _ConvFn(torch.autograd.Function):
                 g = join.take()  # nothing to add to: hand a stashed shortcut gradient through
                 if isinstance(g, MaskedGrad):
                     g = g.materialize()
-                return (g, None, None) + (None,) * 14
-            return (None,) * 17
+                return (g, None, None) + (None,) * 15
+            return (None,) * 18
         dy = grad_nhwc(dy)
         if act:  # y and dy may be channel-slice views of concat buffers: strided rows kernel
             dy = act_grad(dy, y, act, slope)
@@ -400,7 +401,9 @@ class _ConvFn(torch.autograd.Function):
         if has_bias and ctx.needs_input_grad[2]:
             db = _bias_grad(ctx.bias_param, dy)
         dres = dy if ctx.has_residual and ctx.needs_input_grad[16] else None  # y = ... + residual
-        return dx, dw, db, None, None, None, None, None, None, None, None, None, None, None, None, None, dres
+        if dres is not None and ctx.rjoin is not None:
+            dres = ctx.rjoin.produce(dres)
+        return dx, dw, db, None, None, None, None, None, None, None, None, None, None, None, None, None, dres, None
 
 
 # ---------------------------------------------------------------------------------------
@@ -500,7 +503,8 @@ class _StemConvFn(torch.autograd.Function):
 
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=None, slope=0.0,
-           want_stats=False, stats_buf=None, join=None, join_role=None, pad_mode="zeros", out=None, residual=None):
+           want_stats=False, stats_buf=None, join=None, join_role=None, pad_mode="zeros", out=None, residual=None,
+           residual_join=None):
     """Conv2d (+fused bias/activation). Returns y, or (y, stats) when want_stats (GPU only).
 
     ``padding`` may be (top, bottom, left, right) for TF/Keras asymmetric 'same' padding.
@@ -580,8 +584,11 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=
         if res is None:
             return _add_native(conv2d(x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats,
                                       stats_buf, join, join_role, pad_mode, out), residual)
+    if res is None:
+        residual_join = None
     return _ConvFn.apply(xn, weight, bias, stride, padding, dilation, groups, ACT_IDS[act], float(slope), want_stats,
-                         stats_buf, extra, join, join_role, reflect, [out] if out is not None else None, res)
+                         stats_buf, extra, join, join_role, reflect, [out] if out is not None else None, res,
+                         residual_join)
 
 
 def _add_native(a, b):

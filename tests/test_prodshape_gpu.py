@@ -310,3 +310,20 @@ def test_bn_act_maxpool_windows(cfg):
     assert _rel(xa.grad, xb.grad) < 2e-2 and _cos(xa.grad, xb.grad) > 0.9999
     assert _rel(bn_a.weight.grad, bn_b.weight.grad) < 2e-3
     assert _rel(bn_a.bias.grad, bn_b.bias.grad) < 2e-3
+
+
+@pytest.mark.parametrize("cin,filters,H", [(256, 256, 32), (128, 256, 32)], ids=["identity", "projection"])
+def test_hourglass_bottleneck_block(cin, filters, H):
+    """Stacked Hourglass pre-activation bottleneck in training mode: the identity block sums x's
+    two gradients (residual path dy + BN1's dx) inside BN1's backward apply pass (GradJoin input
+    join); the projection block keeps the autograd sum."""
+    from deep_vision_amd.models.hourglass import BottleneckBlock
+
+    torch.manual_seed(3)
+    blk = BottleneckBlock(cin, filters, downsample=cin != filters).to(DEV)
+    for m in blk.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.weight.data.uniform_(0.5, 1.5)
+            m.bias.data.uniform_(-0.3, 0.3)
+    x32 = torch.randn(16, cin, H, H, device=DEV).bfloat16().float()
+    _check_module(blk, x32)
