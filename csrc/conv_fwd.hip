@@ -809,8 +809,20 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
     if (g_fwd_variant == 5) launch_fwd<256, 64, 32, KM_FAST, false, 4>(p, st);
     else if (g_fwd_variant == 7) launch_fwd<128, 128, 32, KM_FAST, false, 4>(p, st);
     else if (g_fwd_variant == 8) launch_fwd<128, 128, 32, KM_FAST, false, 2>(p, st);
-    else if (p.N <= 64) launch_fwd<256, 64, 32, KM_FAST, false, 3>(p, st);
-    else launch_fwd<128, 128, 32, KM_FAST, false, 2>(p, st);
+    else {
+      // compile-time epilogue as in dispatch_res: the ResNet / Inception stems feed a BatchNorm
+      // (statistics, no bias / activation) -- the runtime-flag epilogue cost ~8 VALU per element
+      const bool full = p.bias || p.act || p.ypart;
+      if (p.N <= 64) {
+        if (full) launch_fwd<256, 64, 32, KM_FAST, false, 3, false, EPI_FULL>(p, st);
+        else if (p.stats) launch_fwd<256, 64, 32, KM_FAST, false, 3, false, EPI_STATS>(p, st);
+        else launch_fwd<256, 64, 32, KM_FAST, false, 3, false, EPI_PLAIN>(p, st);
+      } else {
+        if (full) launch_fwd<128, 128, 32, KM_FAST, false, 2, false, EPI_FULL>(p, st);
+        else if (p.stats) launch_fwd<128, 128, 32, KM_FAST, false, 2, false, EPI_STATS>(p, st);
+        else launch_fwd<128, 128, 32, KM_FAST, false, 2, false, EPI_PLAIN>(p, st);
+      }
+    }
     return bn_status;
   }
   if (p.Cg % 8 != 0 || p.ldx % 8 != 0) return -1;
