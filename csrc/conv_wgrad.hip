@@ -413,7 +413,9 @@ int dv_conv_wgrad_splits(const ConvWgradArgs& a) {
   const int M = a.Kout, N = a.R * a.S * a.Cg, K = a.Nb * a.P * a.Q;
   const bool narrow = g_wg_variant == 2 || g_wg_variant == 4 || g_wg_variant == 6 ||
                       (g_wg_variant == 0 && wg_narrow(M, N));
-  int tm = narrow ? 64 : 128, tn = narrow ? 256 : 128, target = 384;
+  // narrow 64x256 tiles (64-output-channel layers, few tiles): twice the blocks (s1 3x3x64 at
+  // 56x56: 195 vs 214 us, profiles/wgbench_asm_dma.txt; the 1x1 narrow layers are flat)
+  int tm = narrow ? 64 : 128, tn = narrow ? 256 : 128, target = narrow ? 768 : 384;
   if (g_wg_variant == 8) { tm = 256; tn = 256; target = 256; }  // one 8-wave block per CU
   if (g_wg_variant == 9) { tm = 256; tn = 128; target = 384; }
   const int tiles = cdiv(M, tm) * cdiv(N, tn) * a.G;
