@@ -791,7 +791,11 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
   // single-group tensor on the fast loader (the dgrads of stride-1 convs)
   int bn_status = 0;
   if (p.bnmode) {
-    const bool ok = a.tgather == 0 && p.identity_map && p.G == 1 && (p.N & 7) == 0 && p.ldy == p.N &&
+    // identity map, or the strided scatter of a 1x1 stride-s dgrad (no offset): the pixels it does
+    // not write hold zero gradient and add nothing to either sum. Not with zfill (its sibling
+    // zeroing lives in the non-prefetching store path).
+    const bool map_ok = p.identity_map || (a.oph == 0 && a.opw == 0 && !p.zfill);
+    const bool ok = a.tgather == 0 && map_ok && p.G == 1 && (p.N & 7) == 0 && p.ldy == p.N &&
                     p.Cg % 64 == 0 && p.ldx % 8 == 0 && p.R <= 16 && p.S <= 16 && p.bnx && p.bnprm && p.bnacc &&
                     (p.bnmode != 3 || p.bnbits);
     if (!ok) { p.bnmode = 0; bn_status = 1; }

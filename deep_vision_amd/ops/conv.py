@@ -213,8 +213,13 @@ def _dgrad(dy, weight, x_shape, Cg_x, G, stride, padding, dilation, device, accu
                         (-dh, -dw), ldy=G * Cg_x, res=res, bnref=fuse, resmask=resmask):
             fuse.mark_fused(dX)
     elif scatter:
-        conv_fwd_raw(dy, wd, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, P, Q, 1, 1, (1, 1), (0, 0), (1, 1),
-                     omap=(H, W, sh, sw, 0, 0), ldy=G * Cg_x, res=res, zfill=zfill)
+        # the BatchNorm-backward sums ride on the scatter too (the unwritten pixels' zero gradient
+        # adds nothing): the stage-transition blocks' shortcut + conv1 dgrads, accumulating last
+        fuse = (bnref if (bnref is not None and G == 1 and Cg_x == Ig and not zfill and (res is not None or accum is None))
+                else None)
+        if conv_fwd_raw(dy, wd, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, P, Q, 1, 1, (1, 1), (0, 0), (1, 1),
+                        omap=(H, W, sh, sw, 0, 0), ldy=G * Cg_x, res=res, zfill=zfill, bnref=fuse):
+            fuse.mark_fused(dX)
     else:
         conv_fwd_raw(dy, wd, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, H, W, R, S, stride, padding, dilation,
                      tgather=1, ldy=G * Cg_x, res=res)
