@@ -266,7 +266,20 @@ struct PoolWin {
 // unfused BN pass is applied before the comparison, so values and window indices are exactly the
 // unfused ones. One thread per (n, p, q, 8-channel group), grid-stride (stride % cg == 0: a
 // thread keeps its channels and their scale/shift); every window load is issued before the max.
-template <int KH, int KW, int SH, int SW>
+// RELU (compiled windows): the comparison runs on one integer key per element, bf16(z) bits in the
+// high half and (last window index - index) in the low bits -- a signed max picks the largest value and,
+// on ties, the first window position (the unfused pool's strict '>'); negative z (ReLU zeros, whose
+// gradient is zero whichever position is kept) order below every non-negative key and leave as +0.
+// (v_perm_b32 byte selects: one op per key; bytes 4-7 are pk, 0-3 lowc, 0x0c reads zero)
+DV_DEVICE uint32_t pool_pk_bf16(float a, float b) {  // one v_cvt_pk_bf16_f32, a in the low half
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){a, b}, b2));
+}
+DV_DEVICE uint32_t pool_key_lo(uint32_t pk, uint32_t lowc) { return __builtin_amdgcn_perm(pk, lowc, 0x05040c00u); }
+DV_DEVICE uint32_t pool_key_hi(uint32_t pk, uint32_t lowc) { return __builtin_amdgcn_perm(pk, lowc, 0x07060c00u); }
+
+template <int KH, int KW, int SH, int SW, bool RELU>
 __global__ __launch_bounds__(NT) void bn_act_maxpool_fwd_kernel(const u16* __restrict__ x, u16* __restrict__ y,
                                                                 uint8_t* __restrict__ idx, PoolGeo g, FastDiv div_cg,
                                                                 FastDiv div_q, FastDiv div_p, int64_t total,
@@ -285,6 +298,49 @@ __global__ __launch_bounds__(NT) void bn_act_maxpool_fwd_kernel(const u16* __res
     const int q = (int)(pix - row * div_q.d);
     const int n = (int)fdiv(row, div_p), p = (int)(row - n * div_p.d);
     const int h0 = p * sh - g.ph, w0 = q * sw - g.pw;
+    if constexpr (RELU) {
+      static_assert(KH != 0 && KW != 0, "integer-key path is for compiled windows");
+      const u16* xb = x + ((int64_t)n * g.H * g.W) * g.C + c;
+      uint4 raw[KH * KW];
+      bool ok[KH * KW];
+#pragma unroll
+      for (int r = 0; r < KH; ++r)
+#pragma unroll
+        for (int s = 0; s < KW; ++s) {  // all window loads in flight together
+          const int h = h0 + r, w = w0 + s;
+          ok[r * KW + s] = h >= 0 && h < g.H && w >= 0 && w < g.W;
+          raw[r * KW + s] = ok[r * KW + s] ? *reinterpret_cast<const uint4*>(xb + ((int64_t)h * g.W + w) * g.C)
+                                           : uint4{0u, 0u, 0u, 0u};
+        }
+      int key[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) key[i] = INT32_MIN;
+#pragma unroll
+      for (int k = 0; k < KH * KW; ++k) {
+        if (!ok[k]) continue;
+        const uint32_t lowc = (uint32_t)(KH * KW - 1 - k);  // an inline constant (VOP3 takes no literal)
+        const uint32_t wd[4] = {raw[k].x, raw[k].y, raw[k].z, raw[k].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float lo = __uint_as_float(wd[e] << 16), hi = __uint_as_float(wd[e] & 0xffff0000u);
+          const uint32_t pk = pool_pk_bf16(fmaf(lo, sc[2 * e], sf[2 * e]), fmaf(hi, sc[2 * e + 1], sf[2 * e + 1]));
+          key[2 * e] = max(key[2 * e], (int)pool_key_lo(pk, lowc));
+          key[2 * e + 1] = max(key[2 * e + 1], (int)pool_key_hi(pk, lowc));
+        }
+      }
+      const int64_t o = (int64_t)pix * g.C + c;
+      uint4 out;
+      uint32_t ow[4], iw[2] = {0u, 0u};
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        ow[e] = ((uint32_t)max(key[2 * e], 0) >> 16) | ((uint32_t)max(key[2 * e + 1], 0) & 0xffff0000u);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) iw[i >> 2] |= ((uint32_t)(KH * KW - 1) - ((uint32_t)key[i] & 0xffu)) << (8 * (i & 3));
+      out.x = ow[0]; out.y = ow[1]; out.z = ow[2]; out.w = ow[3];
+      *reinterpret_cast<uint4*>(y + o) = out;
+      *reinterpret_cast<uint2*>(idx + o) = uint2{iw[0], iw[1]};
+      continue;
+    }
     float best[8]; int bi[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) { best[i] = -INFINITY; bi[i] = 0; }
@@ -428,6 +484,116 @@ __global__ __launch_bounds__(NT) void bn_act_maxpool_bwd_kernel(const u16* __res
   }
 }
 
+// Backward for the 3x3 / stride-2 / pad-1 window with H = 2P, W = 2Q (the ResNet stem), one thread
+// per (n, p, q, 8-channel group) owning the 2x2 input block rows {2p, 2p+1} x cols {2q, 2q+1}: row
+// 2p lies only in window row p (r = 1), row 2p+1 in window rows p (r = 2) and p+1 (r = 0), columns
+// alike -- the block's gradients come from windows (p,q), (p,q+1), (p+1,q), (p+1,q+1), nine
+// (input, window) pairs per channel, branch-free (a window past the edge reads as never selected).
+// Same REDUCE / APPLY contract as bn_act_maxpool_bwd_kernel; REDUCE accumulates dz*(x-mean) and
+// scales by invstd once per thread.
+DV_DEVICE float pool_pick(uint32_t iw, int i, uint32_t pos, float d) {
+  return ((iw >> (8 * (i & 3))) & 0xffu) == pos ? d : 0.f;
+}
+DV_DEVICE float half_bf(uint32_t w, int hi) { return __uint_as_float(hi ? (w & 0xffff0000u) : (w << 16)); }
+
+template <bool APPLY, int ACT>
+__global__ __launch_bounds__(NT) void bn_act_maxpool_bwd_s2_kernel(const u16* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                                                   const u16* __restrict__ x, u16* __restrict__ dx,
+                                                                   PoolGeo g, FastDiv div_cg, FastDiv div_q, FastDiv div_p,
+                                                                   int64_t total, const float* __restrict__ prm,
+                                                                   const float* __restrict__ coef, float slope,
+                                                                   float* __restrict__ acc) {
+  const int cg = g.C / 8;
+  const uint32_t t0 = blockIdx.x * NT + threadIdx.x;
+  const int lc = (int)(t0 - fdiv(t0, div_cg) * div_cg.d), c = lc * 8;
+  float ms[8], mh[8], k0[8], k1[8], k2[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    ms[i] = prm[c + i]; mh[i] = prm[g.C + c + i];
+    if (APPLY) { k0[i] = coef[c + i]; k1[i] = coef[g.C + c + i]; k2[i] = coef[2 * g.C + c + i]; }
+    else { k0[i] = prm[2 * g.C + c + i]; k1[i] = prm[3 * g.C + c + i]; k2[i] = 0.f; }
+  }
+  float s1[8], s2[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { s1[i] = 0.f; s2[i] = 0.f; }
+  const int64_t rowC = (int64_t)g.W * g.C;
+  for (uint32_t t = t0; t < total; t += gridDim.x * NT) {
+    const uint32_t pix = fdiv(t, div_cg);
+    const uint32_t row = fdiv(pix, div_q);
+    const int q = (int)(pix - row * div_q.d);
+    const int n = (int)fdiv(row, div_p), p = (int)(row - n * div_p.d);
+    const bool pr = p + 1 < g.P, qr = q + 1 < g.Q;
+    const int64_t o = (int64_t)pix * g.C + c, oq = (int64_t)g.Q * g.C;
+    const uint4 z4{0u, 0u, 0u, 0u};
+    const uint2 none{0xffffffffu, 0xffffffffu};
+    const uint4 d00 = *reinterpret_cast<const uint4*>(dy + o);
+    const uint4 d01 = qr ? *reinterpret_cast<const uint4*>(dy + o + g.C) : z4;
+    const uint4 d10 = pr ? *reinterpret_cast<const uint4*>(dy + o + oq) : z4;
+    const uint4 d11 = pr && qr ? *reinterpret_cast<const uint4*>(dy + o + oq + g.C) : z4;
+    const uint2 i00 = *reinterpret_cast<const uint2*>(idx + o);
+    const uint2 i01 = qr ? *reinterpret_cast<const uint2*>(idx + o + g.C) : none;
+    const uint2 i10 = pr ? *reinterpret_cast<const uint2*>(idx + o + oq) : none;
+    const uint2 i11 = pr && qr ? *reinterpret_cast<const uint2*>(idx + o + oq + g.C) : none;
+    const int64_t xo = (((int64_t)n * g.H + 2 * p) * g.W + 2 * q) * g.C + c;
+    uint4 xr[4];
+    xr[0] = *reinterpret_cast<const uint4*>(x + xo);
+    xr[1] = *reinterpret_cast<const uint4*>(x + xo + g.C);
+    xr[2] = *reinterpret_cast<const uint4*>(x + xo + rowC);
+    xr[3] = *reinterpret_cast<const uint4*>(x + xo + rowC + g.C);
+    uint32_t ow[4][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int e = i >> 1, hi = i & 1;
+      const uint32_t w00 = (&d00.x)[e], w01 = (&d01.x)[e], w10 = (&d10.x)[e], w11 = (&d11.x)[e];
+      const uint32_t j00 = i < 4 ? i00.x : i00.y, j01 = i < 4 ? i01.x : i01.y;
+      const uint32_t j10 = i < 4 ? i10.x : i10.y, j11 = i < 4 ? i11.x : i11.y;
+      const float g00 = half_bf(w00, hi), g01 = half_bf(w01, hi), g10 = half_bf(w10, hi), g11 = half_bf(w11, hi);
+      float da[4];
+      da[0] = pool_pick(j00, i, 4, g00);
+      da[1] = pool_pick(j00, i, 5, g00) + pool_pick(j01, i, 3, g01);
+      da[2] = pool_pick(j00, i, 7, g00) + pool_pick(j10, i, 1, g10);
+      da[3] = (pool_pick(j00, i, 8, g00) + pool_pick(j01, i, 6, g01)) + (pool_pick(j10, i, 2, g10) + pool_pick(j11, i, 0, g11));
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const float xv = half_bf((&xr[b].x)[e], hi);
+        const float d = bf2f(f2bf(da[b]));
+        const float z = fmaf(xv, ms[i], mh[i]);
+        const float dz = ACT == 1 ? (z > 0.f ? d : 0.f) : (ACT == 2 ? (z > 0.f ? d : d * slope) : d);
+        if (APPLY) {
+          const uint32_t v = f2bf(fmaf(k0[i], dz, fmaf(k1[i], xv, k2[i])));
+          ow[b][e] = hi ? (ow[b][e] | (v << 16)) : v;
+        } else {
+          s1[i] += dz;
+          s2[i] = fmaf(dz, xv - k0[i], s2[i]);
+        }
+      }
+    }
+    if (APPLY) {
+      *reinterpret_cast<uint4*>(dx + xo) = uint4{ow[0][0], ow[0][1], ow[0][2], ow[0][3]};
+      *reinterpret_cast<uint4*>(dx + xo + g.C) = uint4{ow[1][0], ow[1][1], ow[1][2], ow[1][3]};
+      *reinterpret_cast<uint4*>(dx + xo + rowC) = uint4{ow[2][0], ow[2][1], ow[2][2], ow[2][3]};
+      *reinterpret_cast<uint4*>(dx + xo + rowC + g.C) = uint4{ow[3][0], ow[3][1], ow[3][2], ow[3][3]};
+    }
+  }
+  if (APPLY) return;
+  __shared__ float sh_[2][NT * 8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { sh_[0][threadIdx.x * 8 + i] = s1[i]; sh_[1][threadIdx.x * 8 + i] = s2[i] * k1[i]; }
+  __syncthreads();
+  const int lanes = NT / cg;
+  float* a = acc + (int64_t)(blockIdx.x % DV_STAT_SHARDS) * 2 * g.C;
+  for (int ch = threadIdx.x; ch < g.C; ch += NT) {
+    const int gi = ch / 8, e = ch % 8;
+    float t1 = 0.f, t2 = 0.f;
+    for (int l = 0; l < lanes; ++l) {
+      t1 += sh_[0][(l * cg + gi) * 8 + e];
+      t2 += sh_[1][(l * cg + gi) * 8 + e];
+    }
+    atomicAdd(a + ch, t1);
+    atomicAdd(a + g.C + ch, t2);
+  }
+}
+
 inline int grid_for(int64_t total) {
   int64_t g = (total + NT - 1) / NT;
   return (int)std::min<int64_t>(std::max<int64_t>(g, 1), 256 * 16);
@@ -463,8 +629,9 @@ int dv_bn_act_maxpool_fwd(const void* x, void* y, uint8_t* idx, int N, int H, in
   const FastDiv dc = make_fastdiv(C / 8), dq = make_fastdiv(Q), dp = make_fastdiv(P);
   const int grid = (int)std::min<int64_t>((total + NT - 1) / NT, 256 * 32);
 #define FWD_ARGS <<<grid, NT, 0, st>>>((const u16*)x, (u16*)y, idx, g, dc, dq, dp, total, scale, shift, act, slope)
-  if (stem_window(kh, kw, sh, sw)) bn_act_maxpool_fwd_kernel<3, 3, 2, 2> FWD_ARGS;
-  else bn_act_maxpool_fwd_kernel<0, 0, 0, 0> FWD_ARGS;
+  if (stem_window(kh, kw, sh, sw) && act == 1) bn_act_maxpool_fwd_kernel<3, 3, 2, 2, true> FWD_ARGS;
+  else if (stem_window(kh, kw, sh, sw)) bn_act_maxpool_fwd_kernel<3, 3, 2, 2, false> FWD_ARGS;
+  else bn_act_maxpool_fwd_kernel<0, 0, 0, 0, false> FWD_ARGS;
 #undef FWD_ARGS
   return 0;
 }
@@ -474,6 +641,21 @@ int dv_bn_act_maxpool_bwd(const void* dy, const uint8_t* idx, const void* x, voi
   const int64_t total = (int64_t)N * H * W * (C / 8);
   if (C % 8 || NT % (C / 8) || kh * kw > 255 || kh > 16 || total >= (1ll << 31)) return -1;
   PoolGeo g{N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw};
+  if (stem_window(kh, kw, sh, sw) && ph == 1 && pw == 1 && H == 2 * P && W == 2 * Q && act >= 0 && act <= 2) {
+    // 2x2 input block per thread (bn_act_maxpool_bwd_s2_kernel)
+    const int64_t blocks = (int64_t)N * P * Q * (C / 8);
+    const FastDiv dc = make_fastdiv(C / 8), dq = make_fastdiv(Q), dp = make_fastdiv(P);
+    const int grid = (int)std::min<int64_t>((blocks + NT - 1) / NT, apply ? 256 * 32 : 2048);
+#define S2_ARGS <<<grid, NT, 0, st>>>((const u16*)dy, idx, (const u16*)x, (u16*)dx, g, dc, dq, dp, blocks, prm, coef, slope, acc)
+#define S2_ACT(A) do { if (act == 0) bn_act_maxpool_bwd_s2_kernel<A, 0> S2_ARGS; \
+                       else if (act == 1) bn_act_maxpool_bwd_s2_kernel<A, 1> S2_ARGS; \
+                       else bn_act_maxpool_bwd_s2_kernel<A, 2> S2_ARGS; } while (0)
+    if (apply) S2_ACT(true);
+    else S2_ACT(false);
+#undef S2_ACT
+#undef S2_ARGS
+    return 0;
+  }
   const FastDiv dc = make_fastdiv(C / 8), dw = make_fastdiv(W), dh = make_fastdiv(H);
   // the reduction's atomics are one row per block: a bounded grid (~2k blocks) keeps them cheap
   const int grid = (int)std::min<int64_t>((total + NT - 1) / NT, apply ? 256 * 32 : 2048);
