@@ -349,7 +349,8 @@ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 inline bool wg_narrow(int M, int N) { return M <= 64 && N >= 192; }
 
 int g_wg_variant = 0;       // benchmarking override of tile / K-depth / pipeline (0 = heuristic)
-int g_wg_split_pct = 100;   // benchmarking scale of the split-K heuristic
+int g_wg_split_pct = 100;
+int g_wg_fill = 0;           // > 0: splits = floor(fill / tiles) (benchmarking)   // benchmarking scale of the split-K heuristic
 
 template <bool PLAIN>
 void dispatch_wg(const WgParams& p, int blocks_narrow, int blocks_wide, hipStream_t st) {
@@ -423,6 +424,16 @@ int dv_conv_wgrad_splits(const ConvWgradArgs& a) {
   // ~1.5 blocks per CU: measured 5-15 % faster than 3 per CU on the ResNet-50 3x3 / strided
   // layers (half the atomic epilogues), equal on the rest (profiles/wgbench_variants.txt)
   int splits = cdiv(target * g_wg_split_pct / 100, tiles);
+  // im2col layers (3x3, strided 1x1, stems): a grid of whole waves of the 512 block slots (2 per
+  // CU for both tile shapes) instead of ~1.5 blocks per CU, which left a tail of half-empty CUs:
+  // 3x3 layers 10-15 % faster (s1 3x3x64 198 -> 169 us, s3 3x3x256 111 -> 99 us); single-tile
+  // layers (the 7x7 stem, 3.2M-pixel reduction) fill three waves (254 -> 242 us). The plain 1x1
+  // layers keep the target form (a full wave there was 0-8 % slower). profiles/wgbench_fill.txt
+  const bool plain = a.R == 1 && a.S == 1 && a.sh == 1 && a.sw == 1 && a.ph == 0 && a.pw == 0 && a.P == a.H &&
+                     a.Q == a.W && !a.reflect;
+  const bool tuned = g_wg_variant == 0 && g_wg_split_pct == 100;
+  if (g_wg_fill > 0) splits = std::max(1, g_wg_fill / tiles);  // benchmarking: whole waves of `fill` block slots
+  else if (tuned && !plain) splits = std::max(1, (tiles == 1 ? 3 * 512 : 512) / tiles);
   int cap = ktiles / 32;  // >= 2048 pixels per split (atomic budget)
   // few output tiles (small maps / few channels: the Hourglass 8x8-32x32 scales had 9-36 blocks
   // on 256 CUs): trade atomic traffic for parallelism down to 512 pixels per split, until the
@@ -437,6 +448,7 @@ int dv_conv_stats_tiles(int Nb, int P, int Q) { return cdiv(Nb * P * Q, 128); }
 void dv_conv_wgrad_tuning(int variant, int split_pct) {
   g_wg_variant = variant;
   g_wg_split_pct = split_pct > 0 ? split_pct : 100;
+  g_wg_fill = split_pct < 0 ? -split_pct : 0;
 }
 
 int dv_conv_wgrad(const ConvWgradArgs& a, hipStream_t st) {
