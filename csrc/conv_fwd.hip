@@ -816,11 +816,14 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
     else {
       // compile-time epilogue as in dispatch_res: the ResNet / Inception stems feed a BatchNorm
       // (statistics, no bias / activation) -- the runtime-flag epilogue cost ~8 VALU per element
+      // 256x64 for the 64-channel stems with the plain double buffer: 40 KB of LDS, 4 blocks per
+      // CU (the 3-deep ring fit 2): the 7-tile K loop is latency-bound, more resident blocks hide
+      // it (ResNet-50 stem incl. pack 292 -> 246 us, tools/stem_sweep.py)
       const bool full = p.bias || p.act || p.ypart;
       if (p.N <= 64) {
-        if (full) launch_fwd<256, 64, 32, KM_FAST, false, 3, false, EPI_FULL>(p, st);
-        else if (p.stats) launch_fwd<256, 64, 32, KM_FAST, false, 3, false, EPI_STATS>(p, st);
-        else launch_fwd<256, 64, 32, KM_FAST, false, 3, false, EPI_PLAIN>(p, st);
+        if (full) launch_fwd<256, 64, 32, KM_FAST, false, 2, false, EPI_FULL>(p, st);
+        else if (p.stats) launch_fwd<256, 64, 32, KM_FAST, false, 2, false, EPI_STATS>(p, st);
+        else launch_fwd<256, 64, 32, KM_FAST, false, 2, false, EPI_PLAIN>(p, st);
       } else {
         if (full) launch_fwd<128, 128, 32, KM_FAST, false, 2, false, EPI_FULL>(p, st);
         else if (p.stats) launch_fwd<128, 128, 32, KM_FAST, false, 2, false, EPI_STATS>(p, st);
