@@ -283,25 +283,30 @@ def test_stem_fused_matches_unfused():
         assert _rel(pa.grad, pb.grad) < 2e-3, (n, _rel(pa.grad, pb.grad))
 
 
-@pytest.mark.parametrize("cfg", [(64, 3, 2, 1, False), (32, 2, 2, 0, False), (128, 3, 1, 1, False), (16, 3, 2, 0, True)],
-                         ids=lambda c: f"c{c[0]}k{c[1]}s{c[2]}p{c[3]}{'ceil' if c[4] else ''}")
+@pytest.mark.parametrize("cfg", [(64, 3, 2, 1, False, 29, 31, "relu"), (64, 3, 2, 1, False, 30, 32, "relu"),
+                                 (32, 3, 2, 1, False, 30, 32, "leaky"), (64, 3, 2, 1, False, 29, 31, "leaky"),
+                                 (32, 2, 2, 0, False, 29, 31, "relu"), (128, 3, 1, 1, False, 29, 31, "relu"),
+                                 (16, 3, 2, 0, True, 29, 31, "relu")],
+                         ids=lambda c: f"c{c[0]}k{c[1]}s{c[2]}p{c[3]}{'ceil' if c[4] else ''}_{c[5]}x{c[6]}_{c[7]}")
 def test_bn_act_maxpool_windows(cfg):
-    """Fused BN -> ReLU -> max-pool vs the unfused native chain for the compiled 3x3/s2 window and
-    the runtime-window form (2x2/s2, 3x3/s1, ceil mode)."""
+    """Fused BN -> act -> max-pool vs the unfused native chain: the compiled 3x3/s2 window (integer-
+    key ReLU forward; even maps take the 2x2-input-block backward, odd maps the per-input gather),
+    LeakyReLU (float-compare forward) and the runtime-window form (2x2/s2, 3x3/s1, ceil mode)."""
     from deep_vision_amd import nn
     from deep_vision_amd import ops as F
 
-    C, k, s, p, ceil = cfg
+    C, k, s, p, ceil, H, W, act = cfg
     torch.manual_seed(6)
     bn_a, bn_b = nn.BatchNorm2d(C).to(DEV), nn.BatchNorm2d(C).to(DEV)
     bn_a.weight.data.uniform_(0.5, 1.5)
     bn_a.bias.data.uniform_(-0.3, 0.3)
     bn_b.load_state_dict(bn_a.state_dict())
     pool = nn.MaxPool2d(k, s, p, ceil_mode=ceil)
-    x = _nhwc(torch.randn(8, C, 29, 31, device=DEV))
+    x = _nhwc(torch.randn(8, C, H, W, device=DEV))
     xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
-    ya = F.batch_norm_act_maxpool(xa, bn_a, "relu", 0.0, pool)
-    yb = F.max_pool2d(F.batch_norm_act(xb, bn_b, "relu"), k, s, p, ceil)
+    slope = 0.1 if act == "leaky" else 0.0
+    ya = F.batch_norm_act_maxpool(xa, bn_a, act, slope, pool)
+    yb = F.max_pool2d(F.batch_norm_act(xb, bn_b, act, slope), k, s, p, ceil)
     assert ya.shape == yb.shape
     _same_up_to_stat_rounding(ya, yb)
     dy = _nhwc(torch.randn(ya.shape, device=DEV))
