@@ -68,6 +68,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_deterministic", [](bool on) { dv_set_deterministic(on ? 1 : 0); });
   m.def("deterministic", []() { return dv_deterministic() != 0; });
   m.def("conv_wgrad_tuning", [](int v, int split_pct) { dv_conv_wgrad_tuning(v, split_pct); });
+  // host-side split-K heuristic of conv_wgrad (no GPU work): tests pin the grid sizing
+  m.def("conv_wgrad_splits", [](int Nb, int H, int W, int Cg, int Kout, int P_, int Q, int R, int S, int sh, int sw,
+                                int ph, int pw) {
+    ConvWgradArgs a{};
+    a.Nb = Nb; a.H = H; a.W = W; a.Cg = Cg; a.ldx = Cg; a.G = 1; a.Kout = Kout; a.P = P_; a.Q = Q; a.ldy = Kout;
+    a.R = R; a.S = S; a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw; a.dh = 1; a.dw_ = 1;
+    return dv_conv_wgrad_splits(a);
+  });
   m.def("conv_wgrad", [](uptr x, uptr dy, uptr dw, int Nb, int H, int W, int Cg, int ldx, int G, int Kout, int P_, int Q,
                          int ldy, int R, int S, int sh, int sw, int ph, int pw, int dh, int dwl, int splits, int accumulate,
                          int oirs_ig, uptr st, int reflect) {
