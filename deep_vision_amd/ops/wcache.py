@@ -80,17 +80,20 @@ def _build_table(device):
     return (len(_entries), dbuf, cbuf, len(chunks), live)
 
 
-def _table_valid(t) -> bool:
+def _table_params(t):
+    """The table's parameters as strong references (held across the launch: a garbage-collected
+    model could otherwise free one between the check and the bookkeeping), or None when the
+    table is stale (an entry added / dropped, a parameter dead or re-allocated)."""
     if t[0] != len(_entries):
-        return False
+        return None
+    params = []
     for k in t[4]:
         e = _entries.get(k)
-        if e is None:
-            return False
-        p = e[0]()
+        p = e[0]() if e is not None else None
         if p is None or p.data_ptr() != e[4]:
-            return False
-    return True
+            return None
+        params.append(p)
+    return params
 
 
 def after_step(device=None):
@@ -101,16 +104,17 @@ def after_step(device=None):
         return
     device = device or torch.device("cuda", torch.cuda.current_device())
     t = _tables.get(device)
-    if t is None or not _table_valid(t):
+    params = _table_params(t) if t is not None else None
+    while params is None:
         t = _build_table(device)  # (drops dead entries; bakes in the current data pointers)
         if t is None:
             _tables.pop(device, None)
             return
         _tables[device] = t
+        params = _table_params(t)  # None only if a parameter died while the table was built
     lib().wprep_batched(ptr(t[1]), ptr(t[2]), t[3], stream_handle())
-    for k in t[4]:
+    for k, p in zip(t[4], params):
         e = _entries[k]
-        p = e[0]()
         e[2], e[3], e[4] = _epoch, p._version, p.data_ptr()
 
 
