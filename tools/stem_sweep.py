@@ -29,7 +29,10 @@ def main():
     ap.add_argument("--fwd", default="0")
     ap.add_argument("--wg", default="0")
     ap.add_argument("--splits", default="100")
+    ap.add_argument("--det", action="store_true", help="deterministic slab split-K (plain stores + ordered reduce)")
     a = ap.parse_args()
+    if a.det:
+        lib().set_deterministic(True)
     x = torch.randn(256, 3, 224, 224, device="cuda")
     w = (torch.randn(64, 3, 7, 7, device="cuda") * 0.05).requires_grad_(True)
     flops = 2.0 * 256 * 112 * 112 * 64 * 147
