@@ -61,21 +61,34 @@ SPECS = {
 }
 
 
-def build(args, device):
-    """-> (module, loss_fn(out) -> scalar, x, labels, optimizer)."""
+def _sample_cls(i, cin, size, ncls):
+    """Global sample ``i`` of the synthetic classification set (a pure function of i, so the
+    global batch is the same whatever the world size: rank r holds samples [r*B, (r+1)*B))."""
+    import torch
+
+    g = torch.Generator().manual_seed(7919 * i + 17)
+    return torch.randn(cin, size, size, generator=g), int(torch.randint(0, ncls, (1,), generator=g))
+
+
+def build(args, device, rank=0):
+    """-> (module, loss_fn(out) -> scalar, x, B, size). The optimizer is NOT built here: it is
+    constructed after the data-parallel wrapper has laid the parameters out (main())."""
     import torch
 
     from deep_vision_amd import ops as F
     from deep_vision_amd.models import get_model
-    from deep_vision_amd.train.optim import OPTIMIZERS
 
-    B, size, opt_name, opt_kw, fam = SPECS[args.model]
+    B, size, _, _, fam = SPECS[args.model]
     B = args.batch or B
+    lo = rank * B  # this rank's slice of the global synthetic batch
     if fam == "cls":
         model = get_model(args.model).to(device)
         cin = 1 if args.model == "lenet5" else 3
-        x = torch.randn(B, cin, size, size, device=device)
-        y = torch.randint(0, 10 if args.model == "lenet5" else 1000, (B,), device=device)
+        ncls = 10 if args.model == "lenet5" else 1000
+        smp = [_sample_cls(lo + i, cin, size, ncls) for i in range(B)]
+        x = torch.stack([a for a, _ in smp]).to(device)
+        y = torch.tensor([b for _, b in smp], dtype=torch.int64).to(device)
+        del smp
         if args.model == "inception1":
             def loss_fn(out):  # main + 0.3 x aux heads (SURVEY A3)
                 if isinstance(out, tuple):
@@ -92,7 +105,8 @@ def build(args, device):
         from deep_vision_amd.train.detection import yolo_loss
 
         model = get_model("yolov3", num_classes=80).to(device)
-        imgs, labels = Y.collate([Y.SyntheticYoloDataset(B, 80, size, 1)[i] for i in range(B)])
+        ds = Y.SyntheticYoloDataset(lo + B, 80, size, 1)
+        imgs, labels = Y.collate([ds[lo + i] for i in range(B)])
         x = imgs.to(device)
         lab = tuple(t.to(device) for t in labels)
 
@@ -103,9 +117,10 @@ def build(args, device):
         from deep_vision_amd.train.detection import hourglass_loss
 
         model = get_model("hourglass104", num_stack=4, num_residual=1, num_heatmap=16).to(device)
-        ds = P.SyntheticPoseDataset(B, size, (size // 4, size // 4, 16), 1)
-        x = torch.stack([torch.from_numpy(ds[i][0]) for i in range(B)]).to(device)
-        hm = torch.stack([torch.from_numpy(ds[i][1]) for i in range(B)]).to(device)
+        ds = P.SyntheticPoseDataset(lo + B, size, (size // 4, size // 4, 16), 1)
+        items = [ds[lo + i] for i in range(B)]
+        x = torch.stack([torch.from_numpy(a) for a, _ in items]).to(device)
+        hm = torch.stack([torch.from_numpy(b) for _, b in items]).to(device)
 
         def loss_fn(out):
             return hourglass_loss(out, hm)[0] / B
@@ -114,8 +129,7 @@ def build(args, device):
     if args.backend == "torch" and device.type == "cuda":
         model = model.to(memory_format=torch.channels_last)
         x = x.contiguous(memory_format=torch.channels_last)
-    opt = OPTIMIZERS[opt_name](model.parameters(), **opt_kw)
-    return model, loss_fn, x, opt, B, size
+    return model, loss_fn, x, B, size
 
 
 def main():
@@ -131,6 +145,9 @@ def main():
     ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"],
                     help="gradient all-reduce wire format (fp32 master gradients either way)")
     ap.add_argument("--device", default=None, help="cpu to force the CPU plumbing path")
+    ap.add_argument("--force-dp", action="store_true",
+                    help="wrap in DataParallel and all-reduce over a process group even at world size 1 "
+                         "(exercises the RCCL bucket path on one GPU)")
     ap.add_argument("--graph", action="store_true",
                     help="capture the training step as a HIP graph and replay it (single process; "
                          "deep_vision_amd/train/graph.py) -- for launch-bound models")
@@ -151,7 +168,7 @@ def main():
     from deep_vision_amd.parallel.ddp import DataParallel
     from deep_vision_amd.parallel.dist import barrier, init_distributed, is_dist
 
-    world, rank, local, device = init_distributed("gloo" if args.device == "cpu" else None)
+    world, rank, local, device = init_distributed("gloo" if args.device == "cpu" else None, force=args.force_dp)
     if args.device == "cpu":
         device = torch.device("cpu")
     if world != args.gpus and args.device != "cpu":
@@ -165,10 +182,16 @@ def main():
         if cuda:
             torch.cuda.synchronize()
 
-    model, loss_fn, x, opt, B, size = build(args, device)
-    ddp = (DataParallel(model, bucket_mb=args.bucket_mb, timing=cuda,
+    from deep_vision_amd.train.optim import OPTIMIZERS
+
+    model, loss_fn, x, B, size = build(args, device, rank)
+    ddp = (DataParallel(model, bucket_mb=args.bucket_mb, timing=cuda, always_reduce=args.force_dp,
                         comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32)
-           if is_dist() else None)
+           if (is_dist() or args.force_dp) else None)
+    # the optimizer binds to the flat parameter buffer AFTER DataParallel laid it out (it would
+    # also re-bind transparently: train.optim._FlatOptimizer._check_binding)
+    _, _, opt_name, opt_kw, _ = SPECS[args.model]
+    opt = OPTIMIZERS[opt_name](model.parameters(), **opt_kw)
     gscale = ddp.grad_scale if ddp else 1.0
     net = ddp if ddp else model
     amp = args.backend == "torch" and cuda
@@ -184,9 +207,17 @@ def main():
         opt.step(grad_scale=gscale)
         return loss
 
+    def global_loss(loss):
+        """Mean of the per-rank losses = the loss over the global batch (equal shards)."""
+        v = loss.detach().float().reshape(1).to(torch.float64)
+        if is_dist():
+            dist.all_reduce(v)
+            v /= world
+        return float(v.item())
+
     if args.graph:
-        if ddp or not cuda or amp:
-            raise SystemExit("[bench] --graph needs a single native GPU process")
+        if not cuda or amp:
+            raise SystemExit("[bench] --graph needs the native GPU path")
         from deep_vision_amd.train.graph import CapturedStep
 
         cap = CapturedStep(step, opt, model=model, warmup=2)  # 2 eager side-stream steps, then capture
@@ -195,7 +226,7 @@ def main():
     for _ in range(args.warmup):
         loss = step()
     sync()
-    first_loss = float(loss.item()) if args.warmup else float("nan")
+    first_loss = global_loss(loss) if args.warmup else float("nan")
 
     barrier()
     sync()
@@ -211,7 +242,7 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    last_loss = float(loss.item())
+    last_loss = global_loss(loss)
     ms = dt / args.steps * 1e3
     imgs = B * world * args.steps / dt
     comm_ms = ddp.exposed_comm_ms(last=args.steps) if (ddp is not None and cuda) else 0.0
@@ -236,6 +267,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(imgs / base, 3) if base else None,
+            "vs_baseline_basis": ("BASELINE.md reference proxy: images/s of a whole 8-GPU K80-era fp32 node "
+                                  "(not like-for-like; see vs_same_box_miopen)") if base else None,
             "vs_same_box_miopen": (round(imgs / (SAME_BOX_MIOPEN[args.model] * world), 3)
                                    if args.model in SAME_BOX_MIOPEN and cuda and args.backend == "native" else None),
             "per_gpu": round(imgs / max(1, world), 2),

@@ -22,6 +22,7 @@ from .common import (ACT_IDS, BF16, F32, grad_nhwc, grad_sink, is_nhwc, ld_of, l
                      stream_handle, workspace)
 
 STAT_SHARDS = 64
+STAT_ROWS = 2 * STAT_SHARDS + 1  # forward statistics: shard sums + the shift row (csrc/kernels.h)
 FUSE_BWD_STATS = True  # fold the backward reduction into the consumer conv's dgrad epilogue
 LAZY_SHORTCUT = True   # identity-shortcut gradient masked inside the consumer's dgrad epilogue
 FOLD_RESIDUAL_BN = True  # projection-shortcut BN applied inside the block's last BN pass
@@ -311,7 +312,7 @@ def batch_norm_act_maxpool(x, bn, act, slope, pool, stats=None):
     Q = pool_out(W, k[1], s[1], p[1], pool.ceil_mode)
     if bn.num_batches_tracked is not None:
         _count_batch(bn)
-    ws_fwd = workspace(bn, "bn_fwd", (STAT_SHARDS, 2, C), x.device)
+    ws_fwd = workspace(bn, "bn_fwd", (STAT_ROWS, C), x.device)
     ws_bwd = workspace(bn, "bn_bwd", (STAT_SHARDS, 2, C), x.device)
     return _BNActPoolFn.apply(x, stats, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn_momentum(bn), bn.eps,
                               ACT_IDS[act], float(slope), ws_fwd, ws_bwd, k, s, p, P, Q)
@@ -328,7 +329,7 @@ def conv_bn_act_maxpool(x, conv, bn, act, pool, slope=0.0):
     want = bn.training and bn.track_running_stats and conv.out_channels % 8 == 0
     if not want:
         return max_pool2d(conv_bn_act(x, conv, bn, act, slope), pool.kernel_size, pool.stride, pool.padding, pool.ceil_mode)
-    sbuf = workspace(bn, "bn_fwd", (STAT_SHARDS, 2, conv.out_channels), x.device)
+    sbuf = workspace(bn, "bn_fwd", (STAT_ROWS, conv.out_channels), x.device)
     pad = conv.native_padding(x.shape[2], x.shape[3]) if hasattr(conv, "native_padding") else conv.padding
     y, stats = conv2d(x, conv.weight, conv.bias, conv.stride, pad, conv.dilation, conv.groups, want_stats=True,
                       stats_buf=sbuf)
@@ -423,7 +424,7 @@ def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None, residu
         residual = residual.to(dtype=BF16).contiguous(memory_format=torch.channels_last)
         residual_join = None  # the residual reaches its source through a copy
     C = x.shape[1]
-    ws_fwd = workspace(bn, "bn_fwd", (STAT_SHARDS, 2, C), x.device) if training else None
+    ws_fwd = workspace(bn, "bn_fwd", (STAT_ROWS, C), x.device) if training else None
     ws_bwd = workspace(bn, "bn_bwd", (STAT_SHARDS, 2, C), x.device) if training else None
     refbox = [] if FUSE_BWD_STATS and torch.is_grad_enabled() else None
     rargs = ()
@@ -432,7 +433,7 @@ def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None, residu
         if rbn.num_batches_tracked is not None:
             _count_batch(rbn)
         rargs = (rstats, rbn.weight, rbn.bias, rbn.running_mean, rbn.running_var,
-                 (bn_momentum(rbn), rbn.eps, workspace(rbn, "bn_fwd", (STAT_SHARDS, 2, C), x.device),
+                 (bn_momentum(rbn), rbn.eps, workspace(rbn, "bn_fwd", (STAT_ROWS, C), x.device),
                   workspace(rbn, "bn_bwd", (STAT_SHARDS, 2, C), x.device)))
     if not rargs:
         rargs = (None,) * 6
@@ -454,7 +455,7 @@ def conv_bn_deferred(x, conv, bn, join=None, join_role=None):
           and conv.out_channels % 8 == 0 and torch.is_grad_enabled())
     if not ok:
         return conv_bn_act(x, conv, bn, join=join, join_role=join_role), None
-    sbuf = workspace(bn, "bn_fwd", (STAT_SHARDS, 2, conv.out_channels), x.device)
+    sbuf = workspace(bn, "bn_fwd", (STAT_ROWS, conv.out_channels), x.device)
     pad = conv.native_padding(x.shape[2], x.shape[3]) if hasattr(conv, "native_padding") else conv.padding
     y, stats = conv2d(x, conv.weight, conv.bias, conv.stride, pad, conv.dilation, conv.groups, want_stats=True,
                       stats_buf=sbuf, join=join, join_role=join_role)
@@ -480,7 +481,7 @@ def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None, join=None, join
     # BN kernels need dense channels: a channel count that is not a multiple of 8 comes back as a
     # padded view, which is compacted below and gets its statistics from a separate pass
     want = (bn.training or not bn.track_running_stats) and conv.out_channels % 8 == 0
-    sbuf = workspace(bn, "bn_fwd", (STAT_SHARDS, 2, conv.out_channels), x.device) if want else None
+    sbuf = workspace(bn, "bn_fwd", (STAT_ROWS, conv.out_channels), x.device) if want else None
     pad = conv.native_padding(x.shape[2], x.shape[3]) if hasattr(conv, "native_padding") else conv.padding
     mode = "zeros"
     if reflect_pad is not None:  # ReflectionPad2d in front of a pad-0 conv: fused into the gather

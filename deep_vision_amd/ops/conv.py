@@ -20,6 +20,7 @@ from .common import (ACT_IDS, BF16, CL, F32, act_grad, alloc_cl, as_nhwc, empty_
                      like_layout, empty_layout, native, nhwc_numel, ptr, round8, stream_handle)
 
 STAT_SHARDS = 64
+STAT_ROWS = 2 * STAT_SHARDS + 1  # forward statistics: shard sums + the shift row (csrc/kernels.h)
 
 
 def _pair(v):
@@ -88,7 +89,7 @@ def _channel_sum(dy: torch.Tensor, out=None) -> torch.Tensor:
     key = (str(dy.device), ld)
     acc = _CSUM_WS.get(key)
     if acc is None:
-        acc = _CSUM_WS[key] = torch.zeros((STAT_SHARDS, 2, ld), dtype=F32, device=dy.device)
+        acc = _CSUM_WS[key] = torch.zeros((STAT_ROWS, ld), dtype=F32, device=dy.device)
     dst = out if out is not None else torch.empty(C, dtype=F32, device=dy.device)
     lib().channel_sum(ptr(dy), N * H * W, ld, C, ptr(acc), ptr(dst), int(out is not None), stream_handle())
     return dst
@@ -349,7 +350,7 @@ class _ConvFn(torch.autograd.Function):
             y = empty_nhwc(N, O, P, Q, x.device)
         stats = None
         if want_stats:
-            stats = stats_buf if stats_buf is not None else torch.zeros((STAT_SHARDS, 2, O), dtype=F32, device=x.device)
+            stats = stats_buf if stats_buf is not None else torch.zeros((STAT_ROWS, O), dtype=F32, device=x.device)
         b = bias.detach().float().contiguous() if bias is not None else None
         # residual: y = conv + b + residual in the store epilogue (same NHWC layout as y)
         ks = 1 if reflect else conv_ksplit(N * P * Q, Og, R * S * Cg_x, G)
@@ -465,7 +466,7 @@ class _StemConvFn(torch.autograd.Function):
         y = empty_nhwc(N, O, P, Q, x.device)
         stats = None
         if want_stats:
-            stats = stats_buf if stats_buf is not None else torch.zeros((STAT_SHARDS, 2, O), dtype=F32, device=x.device)
+            stats = stats_buf if stats_buf is not None else torch.zeros((STAT_ROWS, O), dtype=F32, device=x.device)
         b = bias.detach().float().contiguous() if bias is not None else None
         conv_fwd_raw(xp, wk, y, b, stats, N, Hp, Wp, 4 * Sp, 4, 1, O, P, Q, R, 1, stride, (0, 0), (1, 1), act=act,
                      slope=slope, tgather=2)
@@ -805,7 +806,7 @@ class _DWConvFn(torch.autograd.Function):
         b = bias.detach().float().contiguous() if bias is not None else None
         stats = None
         if want_stats:
-            stats = stats_buf if stats_buf is not None else torch.zeros((STAT_SHARDS, 2, C), dtype=F32, device=x.device)
+            stats = stats_buf if stats_buf is not None else torch.zeros((STAT_ROWS, C), dtype=F32, device=x.device)
         lib().dw_fwd(ptr(x), ptr(w), ptr(b), ptr(y), N, H, W, C, ld_of(x), P, Q, ld_of(y), K, stride[0], stride[1],
                      padding[0], padding[1], act, float(slope), ptr(stats), stream_handle())
         ctx.save_for_backward(x, weight, y if act else None)

@@ -32,12 +32,12 @@ Design (MI355X-first, not a translation of DataParallel / MirroredStrategy):
 """
 from __future__ import annotations
 
+import collections
 import contextlib
 
 import torch
 import torch.distributed as dist
 
-from .dist import is_dist, world_size
 from .flat import flatten_parameters
 
 
@@ -61,16 +61,25 @@ class _Bucket:
 
 class DataParallel(torch.nn.Module):
     def __init__(self, module: torch.nn.Module, bucket_mb: float = 32.0, broadcast: bool = True,
-                 process_group=None, comm=None, comm_dtype: torch.dtype = torch.float32, timing: bool = False):
+                 process_group=None, comm=None, comm_dtype: torch.dtype = torch.float32, timing: bool = False,
+                 always_reduce: bool = False):
         super().__init__()
         self.module = module
         self.pg = process_group
         self.comm = comm  # optional injected communicator (tests): callable(tensor) -> None (sum in place)
-        self.world = world_size() if comm is None else getattr(comm, "world", 1)
+        pg_up = dist.is_available() and dist.is_initialized()
+        if comm is not None:
+            self.world = getattr(comm, "world", 1)
+            self.reduce = self.world > 1
+        else:
+            self.world = dist.get_world_size(self.pg) if pg_up else 1
+            # always_reduce: run the whole bucketed all-reduce path even on a world-1 process group
+            # (exercises RCCL, the bf16 wire and HIP-graph capture of collectives on one GPU)
+            self.reduce = pg_up and (self.world > 1 or always_reduce)
         self.comm_dtype = comm_dtype
         self.pflat, self.gflat, layout = flatten_parameters(module, reverse=True)
         self._sync_enabled = True
-        if broadcast and is_dist():
+        if broadcast and self.reduce and comm is None:
             with torch.no_grad():
                 dist.broadcast(self.pflat, 0, group=self.pg)
                 for b in module.buffers():
@@ -100,7 +109,9 @@ class DataParallel(torch.nn.Module):
         for p in self.params:
             self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(p)))
         self.timing = timing and self.gflat.is_cuda
-        self.comm_stats = {"allreduce_calls": 0, "allreduce_bytes": 0, "exposed_ms": [], "steps": 0}
+        self.comm_stats = {"allreduce_calls": 0, "allreduce_bytes": 0, "steps": 0,
+                           # bounded: one HIP event pair per step (an unbounded list leaks)
+                           "exposed_ms": collections.deque(maxlen=1024)}
         self._reset()
 
     # ------------------------------------------------------------------ readiness
@@ -116,7 +127,7 @@ class DataParallel(torch.nn.Module):
         bi = self._bucket_of[pid]
 
         def hook(param):
-            if not self._sync_enabled or self.world <= 1:
+            if not self._sync_enabled or not self.reduce:
                 return
             if pid in self._done:
                 raise DoubleReadyError(f"parameter {tuple(param.shape)} reported ready twice in one backward "
@@ -168,7 +179,7 @@ class DataParallel(torch.nn.Module):
 
     def finish(self):
         """Issue incomplete buckets and make the current stream wait for all reductions."""
-        if self.world <= 1 or not self._sync_enabled:
+        if not self.reduce or not self._sync_enabled:
             return
         for b in self.buckets:
             if not b.issued:
@@ -190,7 +201,7 @@ class DataParallel(torch.nn.Module):
 
     def exposed_comm_ms(self, last: int | None = None) -> float:
         """Mean compute-stream time spent waiting on gradient all-reduces (synchronises)."""
-        evs = self.comm_stats["exposed_ms"]
+        evs = list(self.comm_stats["exposed_ms"])
         if last:
             evs = evs[-last:]
         if not evs:

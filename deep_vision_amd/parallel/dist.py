@@ -17,8 +17,9 @@ def env_world():
     return int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
 
 
-def init_distributed(backend: str | None = None, timeout_s: int = 600):
-    """Initialise the default process group if WORLD_SIZE > 1. Returns (world, rank, local_rank, device)."""
+def init_distributed(backend: str | None = None, timeout_s: int = 600, force: bool = False):
+    """Initialise the default process group if WORLD_SIZE > 1 (or always with ``force``: a world-1
+    group, e.g. to exercise the RCCL path on one GPU). Returns (world, rank, local_rank, device)."""
     world, rank, local = env_world()
     backend = backend or os.environ.get("DV_DIST_BACKEND") or None
     use_cuda = torch.cuda.is_available() and (backend != "gloo" or os.environ.get("DV_DIST_BACKEND") == "gloo")
@@ -27,8 +28,14 @@ def init_distributed(backend: str | None = None, timeout_s: int = 600):
     device = torch.device(f"cuda:{local % max(1, torch.cuda.device_count())}") if use_cuda else torch.device("cpu")
     if use_cuda:
         torch.cuda.set_device(device)
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1 and "MASTER_PORT" not in os.environ:
+            from ..launch import free_port
+
+            os.environ["MASTER_PORT"] = str(free_port())
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         be = backend or ("nccl" if use_cuda else "gloo")
         kw = dict(backend=be, timeout=datetime.timedelta(seconds=timeout_s))
         if be == "nccl":

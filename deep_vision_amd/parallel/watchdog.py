@@ -79,9 +79,18 @@ class CommWatchdog:
 
     @staticmethod
     def _is_comm_error(e: BaseException) -> bool:
-        msg = f"{type(e).__name__} {e}".lower()
-        return any(k in msg for k in ("nccl", "rccl", "gloo", "distbackenderror", "connection", "timed out",
-                                      "peer", "collective"))
+        """By exception TYPE (torch.distributed's backend / network / store errors), plus gloo's
+        transport failures, which surface as a RuntimeError raised from gloo's own sources (the
+        message carries the ``gloo/transport`` source path). Anything else propagates normally
+        (free-text keywords killed ranks on unrelated errors)."""
+        import torch.distributed as dist
+
+        types = tuple(t for t in (getattr(dist, n, None) for n in ("DistBackendError", "DistNetworkError",
+                                                                  "DistStoreError", "DistError"))
+                      if isinstance(t, type))
+        if types and isinstance(e, types):
+            return True
+        return type(e) is RuntimeError and "gloo/transport" in str(e)
 
     def _abort(self, code: int, why: str):
         self.fired = why

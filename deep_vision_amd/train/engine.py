@@ -142,8 +142,11 @@ class Engine:
         g = self._graphed.get(key)
         if g is None:
             g = self._graphed[key] = GraphedTrainStep(model, optimizer, forward_loss, eager)
-        self.step_count += 1
-        return g(*inputs)
+        before = self.step_count
+        out = g(*inputs)
+        if self.step_count == before:  # replay / capture: backward_step (which counts) did not run
+            self.step_count += 1
+        return out
 
     def reduce_sum(self, values):
         return D.all_reduce_scalars(list(values), device=self.device if self.device.type == "cuda" else "cpu")

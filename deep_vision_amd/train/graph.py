@@ -95,8 +95,12 @@ class GraphedTrainStep:
     """Trainer-side wrapper (train.engine.Engine.train_step): ``forward_loss(*inputs) -> (loss,
     extra)`` plus backward and optimizer step, captured on the first batch of each new input
     signature (shapes / dtypes of the flattened inputs) and replayed for every later batch with
-    that signature. The capturing call trains on its own batch (the eager warm-up step); batches
-    of a different signature (e.g. a short last batch) run eagerly through ``eager_step``."""
+    that signature. The capturing call trains on its own batch (the eager warm-up step). Up to
+    ``max_graphs`` signatures are captured (default 2: the full batch and a short last batch of
+    an epoch each get a graph and a private memory pool); further signatures run eagerly through
+    ``eager_step``. All graphs of one optimizer share its single device hyperparameter tensor
+    (``_FlatOptimizer.use_device_hparams`` never re-allocates it), so ``graph_tick`` before a
+    replay reaches whichever graph runs."""
 
     def __init__(self, model, optimizer, forward_loss: Callable, eager_step: Callable, max_graphs: int = 2):
         self.model, self.opt, self.forward_loss, self.eager_step = model, optimizer, forward_loss, eager_step

@@ -126,3 +126,116 @@ def test_gloo_ranks_share_gpu_multi_use_weight():
 @pytest.mark.skipif(torch.cuda.device_count() < 2, reason="RCCL DP needs >= 2 GPUs")
 def test_rccl_dp2_matches_single_process():
     _check(_run("nccl", 2), 2)
+
+
+# ------------------------------------------------------------------------------------------------
+# Multi-step trajectories: the optimizer must update the buffer DataParallel
+# reduces into whichever order the two were built in, through the native kernels.
+# ------------------------------------------------------------------------------------------------
+STEPS = 5
+
+
+def _traj_worker(rank, world, port, backend, order, comm_dtype, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), DV_DIST_BACKEND=backend)
+    import torch.distributed as dist
+
+    from deep_vision_amd import ops as F
+    from deep_vision_amd.parallel.ddp import DataParallel
+    from deep_vision_amd.parallel.dist import init_distributed
+    from deep_vision_amd.train.optim import FusedSGD
+
+    _, _, _, dev = init_distributed(backend, force=True)
+    torch.manual_seed(5)
+    net = _make_net().to(dev)
+    p0 = torch.cat([p.detach().reshape(-1).cpu() for p in net.parameters()])
+    kw = dict(bucket_mb=0.05, always_reduce=True, comm_dtype=comm_dtype)
+    if order == "opt_first":
+        opt = FusedSGD(net.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
+        ddp = DataParallel(net, **kw)
+    else:
+        ddp = DataParallel(net, **kw)
+        opt = FusedSGD(net.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
+    x, y = _data(world, rank, dev)
+    losses = []
+    for _ in range(STEPS):
+        opt.zero_grad()
+        loss = F.cross_entropy(ddp(x), y)
+        loss.backward()
+        ddp.finish()
+        opt.step(grad_scale=ddp.grad_scale)
+        losses.append(float(loss))
+    torch.cuda.synchronize()
+    assert opt._flat[0]["param"].data_ptr() == ddp.pflat.data_ptr()
+    p = torch.cat([p.detach().reshape(-1).cpu() for p in net.parameters()])
+    q.put((rank, p0.numpy(), p.numpy(), losses, ddp.comm_stats["allreduce_calls"], len(ddp.buckets)))
+    dist.destroy_process_group()
+
+
+def _run_traj(backend, world, order, comm_dtype=torch.float32):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_traj_worker, args=(r, world, port, backend, order, comm_dtype, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=180) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def _single_traj(world):
+    """One process, no DataParallel, the global batch."""
+    from deep_vision_amd import ops as F
+    from deep_vision_amd.train.optim import FusedSGD
+
+    dev = torch.device("cuda:0")
+    torch.manual_seed(5)
+    net = _make_net().to(dev)
+    opt = FusedSGD(net.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
+    x, y = _data(world, None, dev)
+    losses = []
+    for _ in range(STEPS):
+        opt.zero_grad()
+        loss = F.cross_entropy(net(x), y)
+        loss.backward()
+        opt.step()
+        losses.append(float(loss))
+    torch.cuda.synchronize()
+    return torch.cat([p.detach().reshape(-1).cpu() for p in net.parameters()]), losses
+
+
+@pytest.mark.parametrize("order", ["ddp_first", "opt_first"])
+def test_gloo_dp2_five_step_trajectory(order):
+    res = _run_traj("gloo", 2, order)
+    p0, p, losses, calls, nb = res[0]
+    assert (res[1][1] == p).all(), "replicas diverged"
+    assert calls == STEPS * nb
+    ref, ref_losses = _single_traj(2)
+    p0 = torch.from_numpy(p0)
+    d, dref = torch.from_numpy(p) - p0, ref - p0
+    assert dref.norm() > 0 and d.norm() > 0.5 * dref.norm(), "the DP model did not move"
+    err = (d - dref).norm() / dref.norm()
+    assert err < 5e-2, float(err)
+    glob = [(a + b) / 2 for a, b in zip(losses, res[1][2])]
+    assert glob[-1] < glob[0]
+    assert glob[-1] == pytest.approx(ref_losses[-1], rel=2e-2)
+
+
+@pytest.mark.parametrize("comm_dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("order", ["ddp_first", "opt_first"])
+def test_rccl_world1_bucket_path(order, comm_dtype):
+    """A world-1 ``nccl`` (RCCL) process group with DataParallel forced on: every bucket goes
+    through the async RCCL all-reduce (and the bf16 wire), five steps track the plain run."""
+    res = _run_traj("nccl", 1, order, comm_dtype)
+    p0, p, losses, calls, nb = res[0]
+    assert calls == STEPS * nb and nb >= 3
+    ref, ref_losses = _single_traj(1)
+    p0 = torch.from_numpy(p0)
+    d, dref = torch.from_numpy(p) - p0, ref - p0
+    err = (d - dref).norm() / dref.norm()
+    assert err < (1e-3 if comm_dtype == torch.float32 else 2e-2), float(err)
+    assert losses[-1] < losses[0]

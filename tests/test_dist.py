@@ -33,7 +33,7 @@ class Net(torch.nn.Module):
         return self.c(torch.tanh(self.b(torch.relu(self.a(x)))))
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, order="ddp_first"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     import torch.distributed as dist
@@ -45,8 +45,12 @@ def _worker(rank, world, port, q):
     init_distributed("gloo")
     torch.manual_seed(100 + rank)  # different init per rank: broadcast must fix it
     net = Net()
-    ddp = DataParallel(net, bucket_mb=0.01)  # tiny buckets -> several all-reduces
-    opt = FusedSGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    if order == "opt_first":  # the optimizer flattens first; DataParallel re-lays the params out
+        opt = FusedSGD(net.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+        ddp = DataParallel(net, bucket_mb=0.01)
+    else:
+        ddp = DataParallel(net, bucket_mb=0.01)  # tiny buckets -> several all-reduces
+        opt = FusedSGD(ddp.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
     g = torch.Generator().manual_seed(0)
     xs = [torch.randn(8, 16, generator=g) for _ in range(3)]
     ys = [torch.randn(8, 4, generator=g) for _ in range(3)]
@@ -65,17 +69,21 @@ def _worker(rank, world, port, q):
         ddp.finish()
     s = all_reduce_scalars([float(rank + 1)], device="cpu")[0]
     # numpy copies: pickled by value (tensors would be shared through fds of an exiting process)
+    # the optimizer must update the very buffer DataParallel reduces into
+    assert opt._flat[0]["param"].data_ptr() == ddp.pflat.data_ptr()
+    assert opt._flat[0]["grad"].data_ptr() == ddp.gflat.data_ptr()
     q.put((rank, {k: v.detach().numpy().copy() for k, v in net.state_dict().items()}, issued, len(ddp.buckets), s,
            net.a.weight.grad.numpy().copy()))
     dist.destroy_process_group()
 
 
-def test_ddp_gloo_matches_single_process():
+@pytest.mark.parametrize("order", ["ddp_first", "opt_first"])
+def test_ddp_gloo_matches_single_process(order):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, order)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}

@@ -97,3 +97,48 @@ def test_hourglass_trainer_graph_mode(tmp_path):
     best = train(cfg, synthetic=True, synthetic_size=6, epochs=1, device="cuda", workers=0, log_every=1,
                  checkpoint_dir=str(tmp_path), tensorboard_dir=str(tmp_path / "tb"), graph=True)
     assert best
+
+
+def test_two_signatures_share_device_hparams():
+    """a second capture (short last batch) must not replace the device LR tensor
+    the first graph baked in. Sequence: full, full, short (2nd capture), LR x0.1, full (replay of
+    graph 1), short (replay of graph 2), full -- equal to the same steps run eagerly."""
+    from deep_vision_amd import ops as F
+    from deep_vision_amd.train.graph import GraphedTrainStep
+    from deep_vision_amd.train.optim import OPTIMIZERS
+
+    a = _net()
+    b = copy.deepcopy(a)
+    kw = dict(lr=1e-2, betas=(0.9, 0.999))
+    oa, ob = OPTIMIZERS["Adam"](a.parameters(), **kw), OPTIMIZERS["Adam"](b.parameters(), **kw)
+    sizes = [16, 16, 8, 16, 8, 16]
+    xs = [torch.randn(n, 8, 20, 20, device=DEV) for n in sizes]
+    ys = [torch.randint(0, 10, (n,), device=DEV) for n in sizes]
+
+    def fl_a(x, y):
+        return F.cross_entropy(a(x), y), None
+
+    def fl_b(x, y):
+        return F.cross_entropy(b(x), y), None
+
+    def eager_a(x, y):
+        oa.zero_grad()
+        loss = fl_a(x, y)[0]
+        loss.backward()
+        oa.step()
+        return loss, None
+
+    gs = GraphedTrainStep(b, ob, fl_b, eager_step=None, max_graphs=2)
+    for i in range(len(sizes)):
+        if i == 3:
+            for o in (oa, ob):
+                for g in o.param_groups:
+                    g["lr"] *= 0.1
+        eager_a(xs[i], ys[i])
+        gs(xs[i], ys[i])
+    torch.cuda.synchronize()
+    assert len(gs.graphs) == 2
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        err = ((pa - pb).abs().max() / pa.abs().max().clamp_min(1e-6)).item()
+        assert err < 2e-3, (n, err)
+    assert ob._flat[0]["step"] == oa._flat[0]["step"] == len(sizes)

@@ -18,8 +18,10 @@ case "$mode" in
   check)
     timeout -k 10 900 $PYT tests -m gpu > gpurun_out/tests.log 2>&1 && \
     timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
-    timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1
-    rc=$?; tail -3 gpurun_out/tests.log; tail -1 gpurun_out/bench.log | cut -c1-300 ;;
+    timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1 && \
+    timeout -k 10 300 python bench.py --steps 20 --warmup 5 --force-dp > gpurun_out/bench_dp1.log 2>&1
+    rc=$?; tail -3 gpurun_out/tests.log; grep -E "^FAILED" gpurun_out/tests.log | head
+    tail -1 gpurun_out/bench.log | cut -c1-300; tail -1 gpurun_out/bench_dp1.log | cut -c1-300 ;;
   tests)
     timeout -k 10 900 $PYT tests -m gpu "$@" > gpurun_out/tests.log 2>&1
     rc=$?; grep -E "PASSED|FAILED|ERROR" gpurun_out/tests.log | tail -40; tail -3 gpurun_out/tests.log ;;
