@@ -2,11 +2,16 @@
 // per-channel batch statistics, fused BN-apply + ReLU/LeakyReLU
 // (+ residual add) forward, fused activation-backward + BN-backward.
 //
-// Statistics travel through a sharded fp32 accumulator `acc[SHARDS][2][C]`:
-//   * the conv epilogue (igemm.hip) or `bn_stats_kernel` atomically adds per-block partial
-//     (sum, sumsq) into shard blockIdx % SHARDS — spreads same-address atomics 64 ways;
-//   * `bn_finalize_kernel` folds the shards into mean / invstd / scale / shift and updates
-//     the running statistics with PyTorch semantics (unbiased running_var).
+// Statistics travel through a sharded fp32 accumulator `acc[SHARDS][2][C]` + a shift row `[C]`
+// (kernels.h DV_STAT_ROWS):
+//   * the conv epilogue (conv_fwd.hip), the depthwise forward or `bn_stats_kernel` atomically
+//     adds per-block partial sums of d = x - K and d^2 into shard blockIdx % SHARDS (spreads
+//     same-address atomics 64 ways), K = the shift row: this BN's previous batch mean;
+//   * `bn_finalize_kernel` folds the shards into mean = K + E[d], var = E[d^2] - E[d]^2,
+//     invstd / scale / shift, updates the running statistics with PyTorch semantics (unbiased
+//     running_var) and stores the batch mean as the next shift. With K = 0 (first step) this is
+//     the plain single-pass form; afterwards the E[x^2] - mean^2 cancellation (large |mean| /
+//     std) is gone.
 // Backward uses the same shard layout for (sum dz, sum dz*xhat).
 #include "common.h"
 #include "kernels.h"
@@ -107,16 +112,18 @@ template <int VEC>
 __global__ __launch_bounds__(NT) void bn_stats_kernel(const u16* __restrict__ x, int64_t rows, int C,
                                                         float* __restrict__ acc) {
   SlabTile t(C, VEC, rows);
-  float s[VEC], q[VEC];
+  float s[VEC], q[VEC], kq[VEC];
 #pragma unroll
-  for (int i = 0; i < VEC; ++i) { s[i] = 0.f; q[i] = 0.f; }
+  for (int i = 0; i < VEC; ++i) { s[i] = 0.f; q[i] = 0.f; kq[i] = 0.f; }
   if (t.active()) {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) kq[i] = stat_shift(acc, C)[t.g * VEC + i];
 #pragma unroll 2
     for (int64_t r = t.r0 + t.lane_r; r < t.r1; r += t.rpi) {
       float v[VEC];
       VecIO<VEC>::load(x + r * C + t.g * VEC, v);
 #pragma unroll
-      for (int i = 0; i < VEC; ++i) { s[i] += v[i]; q[i] += v[i] * v[i]; }
+      for (int i = 0; i < VEC; ++i) { const float d = v[i] - kq[i]; s[i] += d; q[i] = fmaf(d, d, q[i]); }
     }
   }
   slab_commit<VEC>(t, s, q, acc, C);
@@ -163,9 +170,14 @@ __global__ void bn_finalize_kernel(float* __restrict__ acc, int C, double count,
   double s, q;
   if (!fold_shards(acc, C, s, q)) return;
   const int c = blockIdx.x * 64 + threadIdx.x;
-  const double mean = s / count;
-  double var = q / count - mean * mean;
+  // the producers summed d = x - K and d^2 with the per-channel shift K: var = E[d^2] - E[d]^2
+  // cancels only by (mean - K)^2 / var, which is small once K tracks the batch mean
+  float* shiftp = stat_shift(acc, C) + c;
+  const double dm = s / count;
+  const double mean = (double)*shiftp + dm;
+  double var = q / count - dm * dm;
   if (var < 0) var = 0;
+  *shiftp = (float)mean;  // the next batch's shift
   const float invstd = (float)(1.0 / sqrt(var + (double)eps));
   const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
   save_mean[c] = (float)mean; save_invstd[c] = invstd;

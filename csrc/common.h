@@ -96,3 +96,7 @@ DV_DEVICE uint32_t fdiv(uint32_t n, const FastDiv& f) { return (__umulhi(n, f.mu
 static __device__ __attribute__((aligned(16))) char dv_zero_page[256];
 
 #define DV_CHECK_LAUNCH() (void)hipGetLastError()
+
+// Per-channel shift row of a forward BatchNorm statistics accumulator of `ncols` channels
+// (layout: kernels.h DV_STAT_ROWS; 64 = DV_STAT_SHARDS, asserted there).
+DV_DEVICE float* stat_shift(float* acc, int64_t ncols) { return acc + (int64_t)2 * 64 * ncols; }

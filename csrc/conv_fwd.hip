@@ -380,12 +380,15 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
     const int mw0 = m0 + wave_m * WMT + h * 64;  // first output row of this 64-row pass
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      float bv[4];
+      float bv[4], kq[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int n = nw0 + j * 16 + (lane >> 4) * 4 + r;
         bv[r] = 0.f;
+        kq[r] = 0.f;
         if constexpr (EPI == EPI_FULL) bv[r] = (p.bias && n < p.N) ? p.bias[grp * p.N + n] : 0.f;
+        // shifted statistics: sums of (t - K), K = this BN's previous batch mean (stat_shift)
+        if constexpr (EPI != EPI_PLAIN) kq[r] = (p.stats && n < p.N) ? stat_shift(p.stats, (int64_t)p.G * p.N)[grp * p.N + n] : 0.f;
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -402,7 +405,7 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
           }
           v[r] = t;
           if constexpr (EPI != EPI_PLAIN) {
-            if (mv) { bsum[j][r] += t; bsq[j][r] += t * t; }
+            if (mv) { const float d = t - kq[r]; bsum[j][r] += d; bsq[j][r] = fmaf(d, d, bsq[j][r]); }
           }
         }
         uint2 pk; pk.x = pack2bf(v[0], v[1]); pk.y = pack2bf(v[2], v[3]);
@@ -703,9 +706,12 @@ __global__ __launch_bounds__(256) void splitk_finalize_kernel(const float* __res
   const int n = blockIdx.x * 256 + lc * 4;
   const bool nv = n < N;  // N % 4 == 0: whole column quads
   const int64_t slab = (int64_t)M * N;
-  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f}, bv[4];
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f}, bv[4], kq[4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) bv[r] = (bias && nv) ? bias[n + r] : 0.f;
+  for (int r = 0; r < 4; ++r) {
+    bv[r] = (bias && nv) ? bias[n + r] : 0.f;
+    kq[r] = (stats && nv) ? stat_shift(stats, N)[n + r] : 0.f;
+  }
   const int m1 = min(M, (int)(blockIdx.y + 1) * FR_ROWS);
   for (int m = blockIdx.y * FR_ROWS + lr; nv && m < m1; m += 4) {
     f32x4 a = *reinterpret_cast<const f32x4*>(ypart + (int64_t)m * N + n);
@@ -723,7 +729,8 @@ __global__ __launch_bounds__(256) void splitk_finalize_kernel(const float* __res
       else if (act == ACT_LEAKY) t = t > 0.f ? t : t * slope;
       t += rv[r];
       v[r] = t;
-      s1[r] += t; s2[r] += t * t;
+      const float d = t - kq[r];
+      s1[r] += d; s2[r] = fmaf(d, d, s2[r]);
     }
     uint2 pk; pk.x = pack2bf(v[0], v[1]); pk.y = pack2bf(v[2], v[3]);
     *reinterpret_cast<uint2*>(y + (int64_t)m * ldy + n) = pk;

@@ -69,9 +69,12 @@ __global__ __launch_bounds__(NT, OCC) void dw_fwd_kernel(const u16* __restrict__
   for (int tp = 0; tp < KS * KS; ++tp)
 #pragma unroll
     for (int k = 0; k < 8; ++k) wr[tp][k] = w[(t.c0 + k) * KS * KS + (FLIP ? KS * KS - 1 - tp : tp)];
-  float bv[8], ssum[8], ssq[8];
+  float bv[8], ssum[8], ssq[8], kq[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) { bv[k] = bias ? bias[t.c0 + k] : 0.f; ssum[k] = 0.f; ssq[k] = 0.f; }
+  for (int k = 0; k < 8; ++k) {
+    bv[k] = bias ? bias[t.c0 + k] : 0.f; ssum[k] = 0.f; ssq[k] = 0.f;
+    kq[k] = stats ? stat_shift(stats, g.C)[t.c0 + k] : 0.f;  // shifted statistics (bn.hip)
+  }
   const int qstrips = (g.Q + QT - 1) / QT;
   const int64_t nstrips = (int64_t)g.N * g.P * qstrips;
   const int64_t s0 = (int64_t)blockIdx.x * strips_per_block, s1 = min(nstrips, s0 + strips_per_block);
@@ -120,7 +123,8 @@ __global__ __launch_bounds__(NT, OCC) void dw_fwd_kernel(const u16* __restrict__
           if (act == 1) v = fmaxf(v, 0.f);
           else if (act == 2) v = v > 0.f ? v : v * slope;
           acc[i][k] = v;
-          ssum[k] += v; ssq[k] += v * v;
+          const float d = v - kq[k];
+          ssum[k] += d; ssq[k] = fmaf(d, d, ssq[k]);
         }
         st8(y + (((int64_t)n * g.P + p) * g.Q + q) * g.ldy + t.c0, acc[i]);
       }

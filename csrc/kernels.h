@@ -5,6 +5,12 @@
 #include <algorithm>
 
 #define DV_STAT_SHARDS 64
+// Forward BatchNorm statistics accumulator of C channels: [DV_STAT_SHARDS][2][C] shard partial
+// sums of (x - K) and (x - K)^2, then one row [C] holding the per-channel shift K (the previous
+// batch mean of that BN; csrc/bn.hip bn_finalize_kernel). Shifting keeps the single-pass
+// variance free of E[x^2] - mean^2 cancellation when |mean| >> std.
+#define DV_STAT_ROWS (2 * DV_STAT_SHARDS + 1)
+static_assert(DV_STAT_SHARDS == 64, "common.h stat_shift() hard-codes the shard count");
 
 struct ConvFwdArgs {
   const void* x;      // bf16 NHWC gathered tensor (input, or dY for dgrad)

@@ -211,15 +211,19 @@ def build_synset_lookup(metadata_file):
     return out
 
 
-def build_imagenet(flat_dir, synsets_file, out_dir, split="train", num_shards=1024, workers=8, bbox_csv=None,
+def build_imagenet(flat_dir, synsets_file=None, out_dir=None, split="train", num_shards=1024, workers=8, bbox_csv=None,
                    metadata_file=None):
     """From a flattened directory (``nXXXXXXXX_*.JPEG``); labels start at 1 (TF-models convention,
     ``data.imagenet_tf.ImageNetTFRecordDataset`` subtracts 1). ``bbox_csv`` /
     ``metadata_file`` fill the bounding-box and human-text features by file name / synset."""
-    syn = [l.split()[0] for l in open(synsets_file) if l.strip()]
+    from . import imagenet_meta
+
+    # default: the packaged synset list / human-readable names (SURVEY T1d)
+    syn = [l.split()[0] for l in open(synsets_file) if l.strip()] if synsets_file else imagenet_meta.wnids()
     idx = {s: i + 1 for i, s in enumerate(syn)}
     boxes = build_bounding_box_lookup(bbox_csv) if bbox_csv else {}
-    human = build_synset_lookup(metadata_file) if metadata_file else {}
+    human = (build_synset_lookup(metadata_file) if metadata_file
+             else dict(zip(imagenet_meta.wnids(), imagenet_meta.names())))
     items = []
     for f in sorted(os.listdir(flat_dir)):
         s0 = f.split("_")[0]
@@ -391,7 +395,7 @@ def main(argv=None):
     m.add_argument("--shards", type=int, default=16)
     i = sub.add_parser("imagenet")
     i.add_argument("--flat-dir", required=True)
-    i.add_argument("--synsets", required=True)
+    i.add_argument("--synsets", default=None, help="synsets.txt (default: the packaged ImageNet-2012 list)")
     i.add_argument("--out", required=True)
     i.add_argument("--split", default="train")
     i.add_argument("--shards", type=int, default=1024)

@@ -81,14 +81,22 @@ class MnistDataset(Dataset):
         return {"image": self.images[idx], "label": self.labels[idx]}
 
 
-def read_synsets(labels_file: str):
-    """``synsets.txt`` lines ``nXXXXXXXX name ...`` -> (label->idx, idx->name)."""
+def read_synsets(labels_file: str | None = None):
+    """``synsets.txt`` lines ``nXXXXXXXX name ...`` -> (label->idx, idx->name). ``None`` reads the
+    packaged copy (data.imagenet_meta). Names keep the reference's space-dropping
+    join (R/ResNet/pytorch/data_load.py:27-44)."""
+    if labels_file is None:
+        from .imagenet_meta import render
+
+        lines = render("synsets.txt").split("\n")
+    else:
+        with open(labels_file) as f:
+            lines = f.read().split("\n")
     label_to_idx, idx_to_name = {}, {}
-    with open(labels_file) as f:
-        for idx, line in enumerate(l for l in f if l.strip()):
-            parts = line.strip().split(" ")
-            label_to_idx[parts[0]] = idx
-            idx_to_name[idx] = "".join(parts[1:])
+    for idx, line in enumerate(l for l in lines if l.strip()):
+        parts = line.strip().split(" ")
+        label_to_idx[parts[0]] = idx
+        idx_to_name[idx] = "".join(parts[1:])
     return label_to_idx, idx_to_name
 
 
@@ -106,7 +114,7 @@ def load_rgb(path: str) -> np.ndarray:
 class ImageNet2012Dataset(Dataset):
     """A flattened directory (``nXXXXXXXX_<file>.JPEG``, T1c) with labels from the synset prefix."""
 
-    def __init__(self, root_dir, labels_file, transform=None):
+    def __init__(self, root_dir, labels_file=None, transform=None):
         self.root_dir = root_dir
         self.images = sorted(f for f in os.listdir(root_dir) if isfile(join(root_dir, f)))
         self.transform = transform

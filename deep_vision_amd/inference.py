@@ -57,7 +57,9 @@ def class_names(path=None):
         from .data.datasets import read_synsets
 
         return read_synsets(path)[1]
-    return {}
+    from .data.imagenet_meta import idx_to_name  # packaged ImageNet-2012 names (indices.json)
+
+    return idx_to_name()
 
 
 @torch.no_grad()

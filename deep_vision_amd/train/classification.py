@@ -85,7 +85,9 @@ def build_datasets(cfg: TrainConfig, data_dir=None, synthetic=False, synthetic_s
         root = data_dir or "../dataset"
         labels = os.path.join(root, "synsets.txt")
         tr, va = os.path.join(root, "train_flatten"), os.path.join(root, "val_flatten")
-        if os.path.isdir(tr) and os.path.isfile(labels):
+        if not os.path.isfile(labels):
+            labels = None  # the packaged ImageNet-2012 synset list (data.imagenet_meta)
+        if os.path.isdir(tr):
             return (ImageNet2012Dataset(tr, labels, T.imagenet_train_transform()),
                     ImageNet2012Dataset(va, labels, T.imagenet_val_transform()))
     return (SyntheticClassification(synthetic_size, cfg.input_shape, nc, key, seed=1),

@@ -36,6 +36,9 @@ case "$mode" in
     rc=$?; cd "$R"
     f=$(find gpurun_out/prof_$m -name '*kernel_stats.csv' -print -quit)
     [ -n "$f" ] && python tools/prof_summary.py "$f" 7 "$m bench.py --steps 5 --warmup 2" > gpurun_out/prof_$m.txt 2>&1
+    t=$(find gpurun_out/prof_$m -name '*kernel_trace.csv' -print -quit)
+    [ -n "$t" ] && python tools/trace_step.py "$t" > gpurun_out/trace_$m.txt 2>&1
+    rm -f "$t"
     cat gpurun_out/prof_$m.txt | cut -c1-160 | sed -n '1,45p' ;;
   pmc)
     L=${1:-s2_1x1_128_512,s4_3x3_512,s1_1x1_64_256,s2_3x3_128}
