@@ -149,8 +149,8 @@ def main():
                     help="wrap in DataParallel and all-reduce over a process group even at world size 1 "
                          "(exercises the RCCL bucket path on one GPU)")
     ap.add_argument("--graph", action="store_true",
-                    help="capture the training step as a HIP graph and replay it (single process; "
-                         "deep_vision_amd/train/graph.py) -- for launch-bound models")
+                    help="capture the training step (data-parallel all-reduces included) as a HIP graph and "
+                         "replay it (deep_vision_amd/train/graph.py) -- for launch-bound models")
     args = ap.parse_args()
 
     import os
@@ -161,6 +161,16 @@ def main():
 
         sys.exit(spawn(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
 
+    import threading
+
+    def heartbeat():  # long silent phases (MIOpen kernel search of the torch arm) print to stderr
+        t0 = time.time()
+        while True:
+            time.sleep(60)
+            print(f"[bench] alive {time.time() - t0:.0f}s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=heartbeat, daemon=True).start()
+
     import torch
     import torch.distributed as dist
 
@@ -168,6 +178,10 @@ def main():
     from deep_vision_amd.parallel.ddp import DataParallel
     from deep_vision_amd.parallel.dist import barrier, init_distributed, is_dist
 
+    if args.graph:
+        from deep_vision_amd.train.graph import prepare_capture_env
+
+        prepare_capture_env()  # captured RCCL all-reduces (train/graph.py), before the group exists
     world, rank, local, device = init_distributed("gloo" if args.device == "cpu" else None, force=args.force_dp)
     if args.device == "cpu":
         device = torch.device("cpu")

@@ -7,7 +7,9 @@ Design (MI355X-first, not a translation of DataParallel / MirroredStrategy):
   * one process per GPU; parameters live in one flat fp32 buffer laid out in reverse
     registration order (parallel.flat), gradients in a matching flat buffer;
   * buckets are contiguous slices of that gradient buffer (default 32 MB — a ring all-reduce
-    over xGMI is per-link bound at ~153 GB/s, so a few large messages beat many small ones);
+    over xGMI is per-link bound at ~153 GB/s, so a few large messages beat many small ones),
+    except the last (first-layer) one, capped at ``tail_mb`` (4 MB): nothing is left to overlap
+    its all-reduce, so it is kept small;
   * a parameter is *complete* when autograd's post-accumulate-grad hook fires for it. The
     engine runs a parameter's AccumulateGrad node once per backward, after EVERY node with an
     edge to it -- i.e. after the last use's backward -- even when all uses are native ops that
@@ -62,7 +64,7 @@ class _Bucket:
 class DataParallel(torch.nn.Module):
     def __init__(self, module: torch.nn.Module, bucket_mb: float = 32.0, broadcast: bool = True,
                  process_group=None, comm=None, comm_dtype: torch.dtype = torch.float32, timing: bool = False,
-                 always_reduce: bool = False):
+                 always_reduce: bool = False, tail_mb: float = 4.0):
         super().__init__()
         self.module = module
         self.pg = process_group
@@ -85,12 +87,18 @@ class DataParallel(torch.nn.Module):
                 for b in module.buffers():
                     if b.numel():
                         dist.broadcast(b, 0, group=self.pg)
-        # build buckets over the flat layout (params never split across buckets)
+        # build buckets over the flat layout (params never split across buckets). The LAST bucket
+        # holds the first layers' gradients, complete only at the very end of backward: its
+        # all-reduce cannot overlap anything, so it is capped at tail_mb (the rest of the tail
+        # moves into the bucket before it, which still overlaps the stem's wgrad).
         cap = max(1, int(bucket_mb * 1024 * 1024 / 4))
+        tail_cap = max(1, int(min(bucket_mb, tail_mb) * 1024 * 1024 / 4))
+        total = self.gflat.numel()
         self.buckets = []
         cur = _Bucket(0)
         for p, off, n in layout:
-            if cur.params and (cur.end - cur.start) + n > cap:
+            in_tail = off >= total - tail_cap
+            if cur.params and ((cur.end - cur.start) + n > cap or (in_tail and cur.start < total - tail_cap)):
                 self.buckets.append(cur)
                 cur = _Bucket(off)
             cur.params.append(p)
@@ -185,7 +193,7 @@ class DataParallel(torch.nn.Module):
             if not b.issued:
                 self._issue(b)
         ev = None
-        if self.timing:
+        if self.timing and not torch.cuda.is_current_stream_capturing():
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
         for b in self.buckets:

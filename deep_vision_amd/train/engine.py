@@ -49,6 +49,10 @@ class Engine:
                  log_every: int = 10, watchdog_s: float | None = None, profile: bool = False, graph: bool = False):
         if device == "cpu":
             backend = backend or "gloo"
+        if graph:
+            from .graph import prepare_capture_env
+
+            prepare_capture_env()  # captured RCCL collectives: async error handling off (before init)
         install_backend_error_handling()  # RCCL async errors abort the communicator (before init)
         self.world, self.rank, self.local_rank, dev = D.init_distributed(backend)
         self.device = torch.device(device) if device and device != "cuda" else dev
@@ -63,11 +67,11 @@ class Engine:
         # then tears the job down) instead of blocking the whole job forever
         self.comm_watchdog = CommWatchdog().start() if self.world > 1 else None
         self.step_count = 0
-        # HIP-graph replay of the whole step (train/graph.py): single GPU process only; the
-        # non-finite skip and fault injection need the eager step and are off in this mode
-        self.graph = bool(graph) and self.world == 1 and self.device.type == "cuda"
+        # HIP-graph replay of the whole step (train/graph.py), data-parallel all-reduces included;
+        # the non-finite skip and fault injection need the eager step and are off in this mode
+        self.graph = bool(graph) and self.device.type == "cuda"
         if graph and not self.graph:
-            self.log("[dv] --graph needs a single GPU process: running eagerly")
+            self.log("[dv] --graph needs a GPU: running eagerly")
         self._graphed = {}
 
     def log(self, *a, **kw):

@@ -18,8 +18,15 @@ What a replay does and does not redo:
     updated on the device by the captured finalize kernels);
   * Python-side control flow is frozen at capture: shapes, the set of parameters that receive
     gradients and data-dependent branches must not change between steps.
-Single-process only: the data-parallel bucketed all-reduce (parallel/ddp.py) issues collectives
-from autograd hooks and stays eager.
+Data parallel steps are captured too: the bucketed all-reduces that
+parallel.DataParallel issues from autograd hooks during the capture are RCCL collectives on the
+process group's stream, forked from and joined back to the capturing stream by events -- both
+recorded into the graph -- so every replay re-runs the reductions in the captured bucket order,
+overlapped with the captured backward exactly as in eager mode. Requirements: every rank captures
+and replays the same step (lockstep), the communicator is initialised by the eager warm-up steps,
+and ProcessGroupNCCL's async error handling is off (``TORCH_NCCL_ASYNC_ERROR_HANDLING=0``: its
+watchdog cannot query events of a captured collective). ``DataParallel.comm_stats`` counts the
+capture's issues only.
 """
 from __future__ import annotations
 
@@ -38,9 +45,16 @@ class CapturedStep:
 
     def __init__(self, step_fn: Callable, optimizer, static_inputs: Sequence[torch.Tensor] = (), model=None,
                  warmup: int = 2):
+        import os
+
         if torch.distributed.is_available() and torch.distributed.is_initialized() \
-                and torch.distributed.get_world_size() > 1:
-            raise RuntimeError("CapturedStep is single-process: the DDP all-reduce runs from autograd hooks")
+                and torch.distributed.get_backend() == "nccl" \
+                and os.environ.get("TORCH_NCCL_ASYNC_ERROR_HANDLING", "") not in ("0",):
+            raise RuntimeError("capturing RCCL collectives needs TORCH_NCCL_ASYNC_ERROR_HANDLING=0 set before the "
+                               "process group is created (train.graph.prepare_capture_env)")
+        if torch.distributed.is_available() and torch.distributed.is_initialized() \
+                and torch.distributed.get_backend() == "gloo":
+            raise RuntimeError("gloo collectives run on the host and cannot be captured in a HIP graph")
         if not hasattr(optimizer, "use_device_hparams"):
             raise TypeError("CapturedStep needs a fused optimizer (train.optim) with device hyperparameters")
         self.step_fn = step_fn
@@ -91,6 +105,13 @@ class CapturedStep:
         return self.outputs
 
 
+def prepare_capture_env() -> None:
+    """Call before the process group is created when steps will be captured (see module doc)."""
+    import os
+
+    os.environ["TORCH_NCCL_ASYNC_ERROR_HANDLING"] = "0"
+
+
 class GraphedTrainStep:
     """Trainer-side wrapper (train.engine.Engine.train_step): ``forward_loss(*inputs) -> (loss,
     extra)`` plus backward and optimizer step, captured on the first batch of each new input
@@ -105,6 +126,9 @@ class GraphedTrainStep:
     def __init__(self, model, optimizer, forward_loss: Callable, eager_step: Callable, max_graphs: int = 2):
         self.model, self.opt, self.forward_loss, self.eager_step = model, optimizer, forward_loss, eager_step
         self.max_graphs = max_graphs
+        from ..parallel.ddp import DataParallel
+
+        self.ddp = model if isinstance(model, DataParallel) else None
         self.graphs = {}  # signature -> (CapturedStep, treespec)
 
     @staticmethod
@@ -124,16 +148,18 @@ class GraphedTrainStep:
         if len(self.graphs) >= self.max_graphs:
             return self.eager_step(*inputs)
         static = [t.detach().clone() for t in flat]
-        fl, opt = self.forward_loss, self.opt
+        fl, opt, ddp = self.forward_loss, self.opt, self.ddp
 
         def step_fn(*st):
             args = tree_unflatten(list(st), spec)
             opt.zero_grad()
             loss, extra = fl(*args)
             loss.backward()
-            opt.step()
+            if ddp is not None:
+                ddp.finish()  # joins the bucket all-reduces back into the (captured) stream
+            opt.step(grad_scale=ddp.grad_scale if ddp is not None else 1.0)
             return loss, extra
 
-        cap = CapturedStep(step_fn, opt, static, model=self.model, warmup=1)
+        cap = CapturedStep(step_fn, opt, static, model=ddp.module if ddp is not None else self.model, warmup=1)
         self.graphs[sig] = (cap, spec)
         return cap.warmup_outputs

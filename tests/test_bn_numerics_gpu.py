@@ -24,7 +24,7 @@ def _check(bn, ref, step, offset):
     em = ((bn.running_mean.double() - mean).abs() / var.sqrt()).max().item()
     ev = ((bn.running_var.double() - var).abs() / var).max().item()
     # step 0 runs unshifted (K = 0): allow the cancellation error of E[x^2] - mean^2 there
-    tol_v = 1e-3 if step > 0 else max(1e-3, 2e-6 * offset ** 2)
+    tol_v = 1e-3 if step > 0 else max(1e-3, 5e-6 * offset ** 2)
     assert em < 1e-3, (step, em)
     assert ev < tol_v, (step, ev)
 
@@ -36,8 +36,9 @@ def test_unfused_bn_stats_offset(offset):
     torch.manual_seed(1)
     C = 64
     bn = nn.BatchNorm2d(C, momentum=1.0).to(DEV)
+    base = (1 + torch.rand(C, device=DEV))[None, :, None, None]  # per-channel means in [offset, 2 offset]
     for step in range(3):
-        mu = offset * (1 + 0.05 * step) * (1 + torch.rand(C, device=DEV))[None, :, None, None]
+        mu = offset * (1 + 0.05 * step) * base  # the batch mean drifts 5 % per step
         x = _nhwc(mu + torch.randn(8, C, 12, 12, device=DEV))
         y = bn(x)
         torch.cuda.synchronize()
@@ -86,7 +87,7 @@ def test_depthwise_epilogue_stats_offset(offset):
         mean, var = k + sh[0] / n, sh[1] / n - (sh[0] / n) ** 2
         rm, rv = ref.mean((0, 2, 3)), ref.var((0, 2, 3), unbiased=False)
         assert ((mean - rm).abs() / rv.sqrt()).max() < 1e-3
-        tol = 2e-3 if step > 0 else max(2e-3, 2e-6 * offset ** 2)
+        tol = 2e-3 if step > 0 else max(2e-3, 5e-6 * offset ** 2)
         assert ((var - rv).abs() / rv).max() < tol
         # emulate the finalize: re-zero the shards, next shift = this batch mean
         st[:128].zero_()

@@ -142,3 +142,84 @@ def test_two_signatures_share_device_hparams():
         err = ((pa - pb).abs().max() / pa.abs().max().clamp_min(1e-6)).item()
         assert err < 2e-3, (n, err)
     assert ob._flat[0]["step"] == oa._flat[0]["step"] == len(sizes)
+
+
+def _graph_dp_worker(port, q):
+    """World-1 RCCL group, DataParallel forced on: 10 eager DP steps vs 2 eager warm-up + 8 replays
+    of the captured DP step (bucket all-reduces inside the graph)."""
+    import os
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    from deep_vision_amd import nn, ops as F, set_deterministic
+    from deep_vision_amd.parallel.ddp import DataParallel
+    from deep_vision_amd.parallel.dist import init_distributed
+    from deep_vision_amd.train.graph import CapturedStep, prepare_capture_env
+    from deep_vision_amd.train.optim import FusedSGD
+
+    prepare_capture_env()
+    init_distributed("nccl", force=True)
+    set_deterministic(True)
+
+    def net():
+        torch.manual_seed(0)
+        return torch.nn.Sequential(nn.Conv2d(8, 64, 3, padding=1, bias=False), nn.ReLU(),
+                                   nn.Conv2d(64, 64, 3, padding=1, bias=False), nn.ReLU(),
+                                   nn.Conv2d(64, 16, 1, bias=False), nn.AdaptiveAvgPool2d((1, 1)),
+                                   torch.nn.Flatten(), nn.Linear(16, 10, bias=False)).to(DEV)
+
+    xs = [torch.randn(16, 8, 20, 20, device=DEV) for _ in range(10)]
+    ys = [torch.randint(0, 10, (16,), device=DEV) for _ in range(10)]
+    res = []
+    for mode in ("eager", "graph"):
+        m = net()
+        ddp = DataParallel(m, bucket_mb=0.02, always_reduce=True)
+        opt = FusedSGD(m.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
+        xst, yst = xs[0].clone(), ys[0].clone()
+        it = iter(range(2))
+
+        def step(x, y):
+            k = next(it, None) if mode == "graph" else None
+            if k is not None:  # the warm-up calls consume the first two batches
+                x.copy_(xs[k]); y.copy_(ys[k])
+            opt.zero_grad()
+            loss = F.cross_entropy(ddp(x), y)
+            loss.backward()
+            ddp.finish()
+            opt.step(grad_scale=ddp.grad_scale)
+            return loss
+
+        if mode == "eager":
+            for i in range(10):
+                step(xs[i], ys[i])
+        else:
+            cap = CapturedStep(step, opt, (xst, yst), model=m, warmup=2)
+            calls = ddp.comm_stats["allreduce_calls"]
+            for i in range(2, 10):
+                cap(xs[i], ys[i])
+            assert ddp.comm_stats["allreduce_calls"] == calls  # replays run no Python hooks
+        torch.cuda.synchronize()
+        res.append(torch.cat([p.detach().reshape(-1).cpu() for p in m.parameters()]).numpy())
+        nb = len(ddp.buckets)
+    q.put((res, nb))
+    import torch.distributed as dist
+
+    dist.destroy_process_group()
+
+
+def test_dp_step_captured_with_rccl_allreduce():
+    """the DP step (bucketed RCCL all-reduce included) captured in a HIP graph
+    replays the eager DP trajectory over 10 steps."""
+    import torch.multiprocessing as mp
+
+    from deep_vision_amd.launch import free_port
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_graph_dp_worker, args=(free_port(), q))
+    p.start()
+    (eager, graph), nb = q.get(timeout=180)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert nb >= 2
+    e, g = torch.from_numpy(eager), torch.from_numpy(graph)
+    assert ((e - g).abs().max() / e.abs().max()).item() < 1e-5

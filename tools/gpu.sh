@@ -56,6 +56,18 @@ case "$mode" in
       timeout -k 10 300 python bench.py --model $m --steps 10 --warmup 3 --backend torch > gpurun_out/bench_${m}_torch.log 2>&1 || { rc=$?; break; }
     done
     for f in gpurun_out/bench_*.log; do echo "$f: $(tail -1 $f | cut -c1-200)"; done ;;
+  zoo)
+    # per-model bench, native and PyTorch/MIOpen arms (MODELS overrides the list)
+    rc=0
+    for m in ${MODELS:-resnet50 inception1 alexnet2 vgg16 shufflenet1}; do
+      timeout -k 10 300 python bench.py --model $m --steps 20 --warmup 5 > gpurun_out/bench_$m.log 2>&1 || { rc=$?; break; }
+      timeout -k 10 300 python bench.py --model $m --steps 20 --warmup 5 --backend torch > gpurun_out/bench_${m}_torch.log 2>&1 || { rc=$?; break; }
+    done
+    for f in gpurun_out/bench_*.log; do echo "$f: $(grep '^{' $f | tail -1 | cut -c1-160)"; done ;;
+  lc)
+    timeout -k 10 600 python tools/lc_sweep.py --models ${MODELS:-resnet50} --grid ${GRID:-0.05:1.0,0.02:1.0} \
+      --out gpurun_out/lc_sweep.txt > gpurun_out/lc_sweep.log 2>&1
+    rc=$?; cat gpurun_out/lc_sweep.log | cut -c1-200 ;;
   *) echo "unknown mode $mode"; exit 2 ;;
 esac
 echo "rc=$rc"
