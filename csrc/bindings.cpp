@@ -218,6 +218,18 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("p"), py::arg("g"), py::arg("sq"), py::arg("mom"), py::arg("gavg"), py::arg("n"), py::arg("lr"), py::arg("alpha"),
      py::arg("eps"), py::arg("wd"), py::arg("momentum"), py::arg("centered"), py::arg("gscale"), py::arg("st"),
      py::arg("hp") = 0);
+  m.def("gconv", [](uptr x, int ldx, int Cin, int in_sg, uptr w, int Orows, uptr y, int ldy, int Cout, int out_sg, int M,
+                    int G, int Cg, int Og, int Kp, uptr stats, uptr st) {
+    if (dv_gconv(CP(x), ldx, Cin, in_sg, CP(w), Orows, P(y), ldy, Cout, out_sg, M, G, Cg, Og, Kp, FP(stats), ST(st)))
+      throw std::runtime_error("gconv: unsupported shape");
+    check_last("gconv");
+  });
+  m.def("gconv_wgrad", [](uptr x, int ldx, int Cin, int in_sg, uptr dy, int ldy, int Cout, int out_sg, uptr dw, int M,
+                          int G, int Cg, int Og, uptr st) {
+    if (dv_gconv_wgrad(CP(x), ldx, Cin, in_sg, CP(dy), ldy, Cout, out_sg, FP(dw), M, G, Cg, Og, ST(st)))
+      throw std::runtime_error("gconv_wgrad: unsupported shape");
+    check_last("gconv_wgrad");
+  });
   m.def("dw_fwd", [](uptr x, uptr w, uptr bias, uptr y, int N, int H, int W, int C, int ldx, int P_, int Q, int ldy, int K,
                      int sh, int sw, int ph, int pw, int act, float slope, uptr stats, uptr st) {
     if (dv_dw_fwd(CP(x), CFP(w), CFP(bias), P(y), N, H, W, C, ldx, P_, Q, ldy, K, sh, sw, ph, pw, act, slope, FP(stats), ST(st)))

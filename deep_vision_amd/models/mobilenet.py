@@ -110,7 +110,12 @@ class MobileNetV1TF(tnn.Module):
 class ShuffleUnit(tnn.Module):
     """ShuffleNet V1 unit (Zhang et al. 2017, Fig. 2b/c): grouped 1x1 -> BN -> ReLU -> channel
     shuffle -> depthwise 3x3 (stride) -> BN -> grouped 1x1 -> BN, residual add (stride 1) or
-    concat with a 3x3/2 average-pooled shortcut (stride 2), ReLU."""
+    concat with a 3x3/2 average-pooled shortcut (stride 2), ReLU.
+
+    The shuffle is applied right after the first grouped 1x1 (conv -> shuffle -> BN -> ReLU):
+    BN and ReLU act per channel, so this is the paper's block with bn1's parameters indexed in the
+    shuffled channel order, and it lets the shuffle ride on the grouped conv's store
+    (csrc/gconv.hip) instead of a separate pass. The torch path runs the same order."""
 
     def __init__(self, cin, cout, groups, stride, first_group=True):
         super().__init__()
@@ -120,15 +125,14 @@ class ShuffleUnit(tnn.Module):
         g1 = groups if first_group else 1
         self.gconv1 = nn.Conv2d(cin, mid, 1, groups=g1, bias=False)
         self.bn1 = nn.BatchNorm2d(mid)
-        self.shuffle = nn.ChannelShuffle(groups)
+        self.groups = groups
         self.dwconv = nn.Conv2d(mid, mid, 3, stride=stride, padding=1, groups=mid, bias=False)
         self.bn2 = nn.BatchNorm2d(mid)
         self.gconv2 = nn.Conv2d(mid, out, 1, groups=groups, bias=False)
         self.bn3 = nn.BatchNorm2d(out)
 
     def forward(self, x):
-        y = F.conv_bn_act(x, self.gconv1, self.bn1, "relu")
-        y = self.shuffle(y)
+        y = F.conv_bn_act(x, self.gconv1, self.bn1, "relu", shuffle=self.groups)
         y = F.conv_bn_act(y, self.dwconv, self.bn2, None)
         if self.stride == 1:
             return F.conv_bn_act(y, self.gconv2, self.bn3, "relu", residual=x)

@@ -463,8 +463,11 @@ def conv_bn_deferred(x, conv, bn, join=None, join_role=None):
 
 
 def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None, join=None, join_role=None, residual_join=None,
-                residual_bn=None, reflect_pad=None):
+                residual_bn=None, reflect_pad=None, shuffle=0):
     """Fused conv -> BN (batch stats from the conv epilogue) -> (+residual) -> activation.
+
+    ``shuffle=g``: conv -> channel shuffle (g groups) -> BN -> act, the shuffle fused into the
+    grouped conv's store (csrc/gconv.hip; ShuffleNet V1).
 
     ``join`` / ``join_role`` ('consumer' | 'producer') and ``residual_join``: a conv.GradJoin
     shared by the two consumers of a block input (see models/resnet.py) so the gradient sum
@@ -477,7 +480,12 @@ def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None, join=None, join
         if reflect_pad is not None:
             p = (reflect_pad, reflect_pad) if isinstance(reflect_pad, int) else tuple(reflect_pad)
             x = TF.pad(x, (p[1], p[1], p[0], p[0]), mode="reflect")
-        return _torch_bn_act(conv(x), bn, act, slope, residual)
+        y = conv(x)
+        if shuffle and shuffle > 1:
+            from .concat import channel_shuffle
+
+            y = channel_shuffle(y, shuffle)
+        return _torch_bn_act(y, bn, act, slope, residual)
     # BN kernels need dense channels: a channel count that is not a multiple of 8 comes back as a
     # padded view, which is compacted below and gets its statistics from a separate pass
     want = (bn.training or not bn.track_running_stats) and conv.out_channels % 8 == 0
@@ -487,7 +495,7 @@ def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None, join=None, join
     if reflect_pad is not None:  # ReflectionPad2d in front of a pad-0 conv: fused into the gather
         pad, mode = reflect_pad, "reflect"
     r = conv2d(x, conv.weight, conv.bias, conv.stride, pad, conv.dilation, conv.groups, want_stats=want,
-               stats_buf=sbuf, join=join, join_role=join_role, pad_mode=mode)
+               stats_buf=sbuf, join=join, join_role=join_role, pad_mode=mode, shuffle=shuffle)
     y, stats = r if want else (r, None)
     if y.shape[1] % 8 != 0:  # padded view: BN kernels require dense channels
         y = y.contiguous(memory_format=torch.channels_last)

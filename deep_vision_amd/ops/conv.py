@@ -510,8 +510,11 @@ class _StemConvFn(torch.autograd.Function):
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=None, slope=0.0,
            want_stats=False, stats_buf=None, join=None, join_role=None, pad_mode="zeros", out=None, residual=None,
-           residual_join=None):
+           residual_join=None, shuffle=0):
     """Conv2d (+fused bias/activation). Returns y, or (y, stats) when want_stats (GPU only).
+
+    ``shuffle=g`` (> 1): the output channels are channel-shuffled in g groups (ShuffleNet V1;
+    fused into the grouped 1x1 kernel's store on the native path, csrc/gconv.hip).
 
     ``padding`` may be (top, bottom, left, right) for TF/Keras asymmetric 'same' padding.
     ``pad_mode='reflect'``: ReflectionPad2d(padding) fused into the im2col gather (the taps
@@ -520,6 +523,17 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=
     concat, ops.concat.slice_cat); native path only.
     ``residual``: y = conv(x) + bias + residual, the add fused into the store epilogue (no
     activation / statistics; Hourglass bottleneck output, R/Hourglass/tensorflow/hourglass104.py:62-67)."""
+    if shuffle and shuffle > 1:
+        if native(x) and _gconv_ok(x, weight, bias, stride, padding, dilation, groups, act, join=join, out=out,
+                                   residual=residual, pad_mode=pad_mode):
+            return _gconv(x, weight, groups, shuffle, want_stats, stats_buf)
+        from .concat import channel_shuffle
+
+        r = conv2d(x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats, stats_buf, join,
+                   join_role, pad_mode, out, residual, residual_join)
+        if want_stats:  # the statistics were taken in the unshuffled order: recompute downstream
+            return channel_shuffle(r[0], shuffle), None
+        return channel_shuffle(r, shuffle)
     if residual is not None and (act or want_stats or out is not None or not native(x)):
         y = conv2d(x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats, stats_buf, join,
                    join_role, pad_mode, out)
@@ -562,10 +576,13 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=
         raise NotImplementedError("conv2d out= on depthwise / channel-padded grouped convs")
     if dw:
         return depthwise_conv2d(x, weight, bias, stride, padding, act, slope, want_stats, stats_buf, extra)
+    if padded_groups and _gconv_ok(x, weight, bias, stride, padding, dilation, groups, act, join=join, out=out,
+                                   residual=residual, pad_mode=pad_mode):
+        # channels per group not a multiple of 8 (ShuffleNet V1 g=3: 20 per group): the grouped
+        # 1x1 kernel (csrc/gconv.hip) -- per-group MFMA tiles, no block-diagonal expansion
+        return _gconv(x, weight, groups, 0, want_stats, stats_buf)
     if padded_groups:
-        # channels per group not a multiple of 8 (ShuffleNet V1 g=3: 20 / 40 / 80): run as a dense
-        # conv with a block-diagonal weight -- the activations are read and written once, in
-        # place, no channel-padding copies (the FLOPs x groups are negligible for these 1x1s)
+        # other shapes (k > 1, strided): a dense conv with a block-diagonal weight
         weight = _block_diagonal(weight, groups, x.shape[1])
         groups = 1
     geo = _stem_geometry(x, weight, stride, padding, dilation, groups, extra)
@@ -595,6 +612,81 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=
     return _ConvFn.apply(xn, weight, bias, stride, padding, dilation, groups, ACT_IDS[act], float(slope), want_stats,
                          stats_buf, extra, join, join_role, reflect, [out] if out is not None else None, res,
                          residual_join)
+
+
+def _gconv_ok(x, weight, bias, stride, padding, dilation, groups, act, join=None, out=None, residual=None,
+              pad_mode="zeros"):
+    """Shapes the grouped 1x1 kernel serves: 1x1, stride 1, no padding / bias / activation /
+    residual / concat slice, 4-aligned channels per group (wgrad register blocks)."""
+    O, Cg, R, S = weight.shape
+    C = x.shape[1]
+    return (R == 1 and S == 1 and _pair(stride) == (1, 1) and _pair(dilation) == (1, 1)
+            and all(v == 0 for v in norm_padding(padding)[0]) and norm_padding(padding)[1] == (0, 0)
+            and bias is None and not act and out is None and residual is None and pad_mode == "zeros" and join is None
+            and C == Cg * groups and O % groups == 0 and Cg % 4 == 0 and (O // groups) % 4 == 0 and x.dim() == 4)
+
+
+class _GConvFn(torch.autograd.Function):
+    """Grouped 1x1 conv (+ fused output channel shuffle, + BN statistics) on csrc/gconv.hip."""
+
+    @staticmethod
+    def forward(ctx, x, weight, groups, shuffle, want_stats, stats_buf):
+        N, C, H, W = x.shape
+        O, Cg = weight.shape[0], weight.shape[1]
+        G, Og = groups, weight.shape[0] // groups
+        Kp = (Cg + 31) // 32 * 32
+        wk = _prep_weight(weight, G, Kp, mode=0)  # [G][Og][Kp]
+        y = empty_nhwc(N, O, H, W, x.device)
+        stats = None
+        if want_stats:
+            stats = stats_buf if stats_buf is not None else torch.zeros((STAT_ROWS, O), dtype=F32, device=x.device)
+        lib().gconv(ptr(x), ld_of(x), C, 0, ptr(wk), Og, ptr(y), ld_of(y), O, int(shuffle), N * H * W, G, Cg, Og, Kp,
+                    ptr(stats), stream_handle())
+        ctx.save_for_backward(x, weight)
+        ctx.cfg = (G, int(shuffle))
+        ctx.set_materialize_grads(False)
+        if want_stats:
+            ctx.mark_non_differentiable(stats)
+            return y, stats
+        return y
+
+    @staticmethod
+    def backward(ctx, dy, *unused):
+        x, weight = ctx.saved_tensors
+        G, sg = ctx.cfg
+        if dy is None:
+            return (None,) * 6
+        dy = grad_nhwc(dy)
+        if dy.data_ptr() % 16:
+            dy = dy.contiguous(memory_format=torch.channels_last)
+        N, C, H, W = x.shape
+        O, Cg = weight.shape[0], weight.shape[1]
+        Og = O // G
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            Kp = (Og + 31) // 32 * 32
+            wt = _prep_weight(weight, G, Kp, mode=1)  # [G][Cg][Kp]: per-group transpose
+            dx = empty_nhwc(N, C, H, W, x.device)
+            lib().gconv(ptr(dy), ld_of(dy), O, sg, ptr(wt), Cg, ptr(dx), ld_of(dx), C, 0, N * H * W, G, Og, Cg, Kp, 0,
+                        stream_handle())
+        if ctx.needs_input_grad[1]:
+            sink = grad_sink(weight)
+            acc = sink if sink is not None else torch.zeros(weight.shape, dtype=F32, device=x.device)
+            lib().gconv_wgrad(ptr(x), ld_of(x), C, 0, ptr(dy), ld_of(dy), O, sg, ptr(acc), N * H * W, G, Cg, Og,
+                              stream_handle())
+            dw = None if sink is not None else acc
+        return dx, dw, None, None, None, None
+
+
+def _gconv(x, weight, groups, shuffle, want_stats, stats_buf):
+    C = x.shape[1]
+    xn = as_nhwc(x, pad_to8=True)
+    if xn.shape[1] != C:  # as_nhwc padded the logical channels: keep the padded storage, view C
+        xn = xn[:, :C]
+    if xn.data_ptr() % 16 or ld_of(xn) < round8(C) or ld_of(xn) % 8:
+        xn = empty_nhwc(*xn.shape, x.device)
+        xn.copy_(x)
+    return _GConvFn.apply(xn, weight, groups, shuffle, want_stats, stats_buf)
 
 
 def _add_native(a, b):
