@@ -254,7 +254,7 @@ def test_yolov3_model():
     def loss2(heads):
         return sum(D.yolo_loss(h, y, ANCHORS_WH[list(m)], 80).sum() for h, y, m in zip(heads, ys2, ANCHOR_MASKS)) / 4
 
-    _compare_model(lambda: YoloV3(80), (x2,), loss2, out_cos=0.98, grad_cos=0.8)
+    _compare_model(lambda: YoloV3(80), (x2,), loss2, out_cos=0.98, grad_cos=0.9)
 
 
 def test_hourglass_model():
@@ -266,9 +266,13 @@ def test_hourglass_model():
     make = lambda: StackedHourglassNetwork(num_stack=2)  # noqa: E731
     loss = lambda ys: sum(L.heatmap_mse(y, t) for y in ys)  # noqa: E731
     _compare_model(make, (x,), loss, out_cos=0.995, grad_cos=0.98, train=False)
-    # train mode: outputs only (BN batch statistics over 2x2 maps make the gradients of this
-    # random-init 2-stack net ill-conditioned: bias-before-BN grads are ~1e-7 noise in fp32 too)
-    _compare_model(make, (x,), loss, out_cos=0.8, grad_cos=None)
+    # train mode at 256 px / batch 4: the innermost 4x4 maps give every BN >= 64 samples per
+    # channel (at 128 px / batch 2 only 8, where batch statistics turn bf16 rounding into noise);
+    # gradients are held to the torch-bf16 baseline (_compare_model)
+    x2 = torch.randn(4, 3, 256, 256, device=DEV)
+    t2 = torch.rand(4, 16, 64, 64, device=DEV) * (torch.rand(4, 16, 64, 64, device=DEV) > 0.9)
+    loss2 = lambda ys: sum(L.heatmap_mse(y, t2) for y in ys)  # noqa: E731
+    _compare_model(make, (x2,), loss2, out_cos=0.95, grad_cos=0.9)
 
 
 def test_centernet_model():
