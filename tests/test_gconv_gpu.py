@@ -81,6 +81,14 @@ def test_shufflenet_unit_native_vs_torch():
         y.backward(_nhwc(g))
         yr.backward(g)
         assert TF.cosine_similarity(x.grad.float().flatten(), xr.grad.float().flatten(), 0).item() > 0.995
+        named = dict(ref.named_parameters())
         for (n, a), b in zip(u.named_parameters(), ref.parameters()):
+            # bn1.weight / bn2.bias have an exactly-zero true gradient (the depthwise conv -> bn2
+            # chain is invariant to them, tests/test_concat_gpu.py): both backends return rounding
+            # noise there -- it must be small next to the sibling parameter's gradient
+            sib = named.get(n.rsplit(".", 1)[0] + (".bias" if n.endswith("weight") else ".weight"))
+            if sib is not None and b.grad.norm() < 1e-3 * sib.grad.norm():
+                assert a.grad.norm() < 2e-2 * sib.grad.norm(), n
+                continue
             c = TF.cosine_similarity(a.grad.float().flatten(), b.grad.float().flatten(), 0).item()
             assert c > 0.99, (n, c)

@@ -56,6 +56,15 @@ case "$mode" in
       timeout -k 10 300 python bench.py --model $m --steps 10 --warmup 3 --backend torch > gpurun_out/bench_${m}_torch.log 2>&1 || { rc=$?; break; }
     done
     for f in gpurun_out/bench_*.log; do echo "$f: $(tail -1 $f | cut -c1-200)"; done ;;
+  pmcdw)
+    # PMC passes over the depthwise kernels (tools/dw_bench.py, variant 0)
+    mkdir -p gpurun_out/pmcdw && cd /tmp && export TMPDIR=/tmp && \
+    timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d "$R/gpurun_out/pmcdw/p1" -o run --output-format csv -- python3 "$R/tools/dw_bench.py" --variants 0 --iters 3 > "$R/gpurun_out/pmcdw/p1.log" 2>&1 && \
+    timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VMEM SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_SALU TCC_HIT TCC_MISS GRBM_GUI_ACTIVE -d "$R/gpurun_out/pmcdw/p2" -o run --output-format csv -- python3 "$R/tools/dw_bench.py" --variants 0 --iters 3 > "$R/gpurun_out/pmcdw/p2.log" 2>&1 && \
+    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE TA_BUSY_avr -d "$R/gpurun_out/pmcdw/p3" -o run --output-format csv -- python3 "$R/tools/dw_bench.py" --variants 0 --iters 3 > "$R/gpurun_out/pmcdw/p3.log" 2>&1
+    rc=$?; cd "$R"
+    python tools/pmc_summary.py "dw_" $(find gpurun_out/pmcdw -name '*counter_collection.csv') > gpurun_out/pmcdw/summary.txt 2>&1
+    sed -n '1,60p' gpurun_out/pmcdw/summary.txt ;;
   zoo)
     # per-model bench, native and PyTorch/MIOpen arms (MODELS overrides the list)
     rc=0
