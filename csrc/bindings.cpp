@@ -218,15 +218,17 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("p"), py::arg("g"), py::arg("sq"), py::arg("mom"), py::arg("gavg"), py::arg("n"), py::arg("lr"), py::arg("alpha"),
      py::arg("eps"), py::arg("wd"), py::arg("momentum"), py::arg("centered"), py::arg("gscale"), py::arg("st"),
      py::arg("hp") = 0);
-  m.def("gconv", [](uptr x, int ldx, int Cin, int in_sg, uptr w, int Orows, uptr y, int ldy, int Cout, int out_sg, int M,
+  m.def("gconv", [](uptr x, int ldx, int Cin, uptr tin, uptr w, int Orows, uptr y, int ldy, int Cout, uptr tout, int M,
                     int G, int Cg, int Og, int Kp, uptr stats, uptr st) {
-    if (dv_gconv(CP(x), ldx, Cin, in_sg, CP(w), Orows, P(y), ldy, Cout, out_sg, M, G, Cg, Og, Kp, FP(stats), ST(st)))
+    if (dv_gconv(CP(x), ldx, Cin, reinterpret_cast<const int16_t*>(tin), CP(w), Orows, P(y), ldy, Cout,
+                 reinterpret_cast<const int16_t*>(tout), M, G, Cg, Og, Kp, FP(stats), ST(st)))
       throw std::runtime_error("gconv: unsupported shape");
     check_last("gconv");
   });
-  m.def("gconv_wgrad", [](uptr x, int ldx, int Cin, int in_sg, uptr dy, int ldy, int Cout, int out_sg, uptr dw, int M,
-                          int G, int Cg, int Og, uptr st) {
-    if (dv_gconv_wgrad(CP(x), ldx, Cin, in_sg, CP(dy), ldy, Cout, out_sg, FP(dw), M, G, Cg, Og, ST(st)))
+  m.def("gconv_wgrad", [](uptr x, int ldx, uptr tin, uptr dy, int ldy, uptr tout, uptr dw, int M, int G, int Cg, int Og,
+                          uptr st) {
+    if (dv_gconv_wgrad(CP(x), ldx, reinterpret_cast<const int16_t*>(tin), CP(dy), ldy,
+                       reinterpret_cast<const int16_t*>(tout), FP(dw), M, G, Cg, Og, ST(st)))
       throw std::runtime_error("gconv_wgrad: unsupported shape");
     check_last("gconv_wgrad");
   });

@@ -4,147 +4,177 @@
 //
 //   y[m][pos_out(g*Og + j)] = sum_{k < Cg} x[m][pos_in(g*Cg + k)] * W[g*Og + j][k]
 //
-// pos(l) is the identity or the ShuffleNet permutation of C channels in `sg` groups (logical
-// channel l = a*(C/sg) + b stored at b*sg + a). The forward of ShuffleNet's first grouped 1x1
-// stores its output shuffled (pos_out); its dgrad reads that gradient back through the same map
-// (pos_in) -- the shuffle never runs as a separate pass.
+// pos() is the identity or the ShuffleNet permutation (logical channel l = a*(C/sg) + b stored at
+// b*sg + a), passed as a small int16 table (nullptr = identity): the forward of ShuffleNet's
+// first grouped 1x1 stores its output shuffled, its dgrad and wgrad read that gradient back
+// through the same table -- the shuffle never runs as a separate pass.
 //
-// Structure (one 256-thread block = BM pixel rows x ALL output channels):
-//   1. the BM input rows are copied into LDS with 16-B loads (rows are 16-B aligned NHWC);
-//   2. LDS "repack": per group, the Cg channels are gathered (through pos_in) into a logical
-//      image [BM][G*Kp], each group zero-padded to Kp = round32(Cg) -- from here on every MFMA
-//      fragment is one aligned ds_read_b128 whatever Cg, the group offset or the permutation;
-//   3. each wave takes (16-row fragment, group, 4 output-column fragments) items:
-//      v_mfma_f32_16x16x32_bf16 with the weights [G][Orows][Kp] (wcache layout) as the A operand;
-//   4. the epilogue writes bf16 results into an LDS output tile at pos_out (the shuffle), folds
+// Forward / dgrad (gconv_kernel, one 256-thread block = BM pixel rows x ALL output channels):
+//   1. the rows are loaded straight into a logical LDS image [BM][G*Kp] (each group's Cg
+//      channels zero-padded to Kp = round32(Cg)): aligned 8-channel pieces by one 16-B load,
+//      unaligned / permuted ones element-wise -- every MFMA fragment is then one ds_read_b128;
+//   2. each wave takes (16-row fragment, group, 4 output-column fragments) items:
+//      v_mfma_f32_16x16x32_bf16, weights [G][Orows][Kp] (ops/wcache layouts) as the A operand;
+//   3. the epilogue writes bf16 results into an LDS output tile at pos_out (the shuffle), folds
 //      the shifted BatchNorm partial statistics (DPP row sums, LDS, one sharded atomic row per
 //      block, csrc/kernels.h DV_STAT_ROWS) and stores whole rows with vector stores.
-// The weight gradient (gconv_wgrad_kernel) reduces over pixels with 4x4 register blocks per
-// thread (these layers are memory-bound: a few tens of MACs per loaded byte).
+// Weight gradient (gconv_wgrad_kernel): per group dW_g = dY_g^T X_g, a GEMM whose reduction runs
+// over the pixels. 64-pixel tiles of both operands are staged row-major with an XOR swizzle and
+// read as MFMA fragments by the hardware-transposed ds_read_b64_tr_b16 (as conv_wgrad.hip);
+// blocks split the pixels (split-K) and add their fp32 tiles into dW once.
 #include "common.h"
 #include "kernels.h"
 
 namespace {
 constexpr int NT = 256;
+inline __host__ __device__ int r8(int v) { return (v + 7) & ~7; }
+// operand load modes (uniform per launch): 8 aligned channels per 16-B load / even offsets in
+// 4-byte pairs / a permuted or odd layout gathered element-wise through an LDS position table
+enum { GW_V16 = 0, GW_PAIR = 1, GW_GATHER = 2 };
 
 struct GcParams {
   const u16* x;
-  int ldx, Cin, in_sg;
-  const u16* w;  // [G][Orows][Kp] bf16 (rows >= Og are never used)
+  int ldx, Cin;
+  const int16_t* tin;  // logical -> stored input channel, or nullptr (identity)
+  const u16* w;        // [G][Orows][Kp] bf16 (rows >= Og are never used)
   int Orows;
   u16* y;
-  int ldy, Cout, out_sg;
+  int ldy, Cout;
+  const int16_t* tout;  // logical -> stored output channel, or nullptr
   int M, G, Cg, Og, Kp;
   float* stats;  // shifted BN statistics of y by stored channel position, or nullptr
+  FastDiv div_upr, div_kc;  // chunks per row (G*Kp/8), chunks per group (Kp/8)
 };
 
-DV_DEVICE int perm_pos(int l, int C, int sg) {
-  if (sg <= 1) return l;
-  const int cpg = C / sg;
-  return (l % cpg) * sg + l / cpg;
+inline __host__ __device__ size_t gc_lds_bytes(int BM, int G, int Kp, int Cout, bool stats) {
+  // [BM][G*Kp + 8] logical input image | [BM][r8(Cout) + 8] output tile | [Cout] table | stats
+  return (size_t)BM * ((G * Kp + 8) + (r8(Cout) + 8)) * 2 + (size_t)Cout * 2 + (stats ? (size_t)2 * Cout * 4 : 0) + 16 +
+         (size_t)G * Kp * 2;  // + the input position table
 }
 
-struct GcLayout {
-  int RP, PK, PP, YP;
-  bool direct;  // the input rows already are the logical padded image (no repack)
-};
-inline __host__ __device__ int r8(int v) { return (v + 7) & ~7; }
-inline __host__ __device__ GcLayout gc_layout(int Cin, int G, int Cg, int Kp, int in_sg, int Cout) {
-  GcLayout L;
-  L.direct = in_sg <= 1 && Cg == Kp && Cin == G * Cg;
-  L.RP = r8(Cin) + 8;
-  L.PK = G * Kp;
-  L.PP = L.direct ? L.RP : L.PK + 8;
-  L.YP = r8(Cout) + 8;
-  return L;
-}
-inline __host__ __device__ size_t gc_lds_bytes(const GcLayout& L, int BM, int Cout, bool stats) {
-  // [BM][RP] input rows | [BM][PP] logical image (unless direct) | [BM][YP] output tile | stats
-  return (size_t)BM * (L.RP + (L.direct ? 0 : L.PP) + L.YP) * 2 + (stats ? (size_t)2 * Cout * 4 : 0);
-}
-
-template <int BM>
+template <int BM, int MODE>
 __global__ __launch_bounds__(NT) void gconv_kernel(GcParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const GcLayout L = gc_layout(p.Cin, p.G, p.Cg, p.Kp, p.in_sg, p.Cout);
-  u16* raw = reinterpret_cast<u16*>(smem);
-  u16* pk = L.direct ? raw : raw + BM * L.RP;
-  u16* ys = pk + (L.direct ? BM * L.RP : BM * L.PP);
-  float* st = reinterpret_cast<float*>(ys + BM * L.YP);
+  const int PK = p.G * p.Kp, PP = PK + 8, YP = r8(p.Cout) + 8;
+  u16* pk = reinterpret_cast<u16*>(smem);
+  u16* ys = pk + BM * PP;
+  int16_t* tout = reinterpret_cast<int16_t*>(ys + BM * YP);
+  float* st = reinterpret_cast<float*>(smem + (((size_t)BM * (PP + YP) * 2 + (size_t)p.Cout * 2 + 15) & ~(size_t)15));
+  int16_t* tin = reinterpret_cast<int16_t*>(st + (p.stats ? 2 * p.Cout : 0));  // [G*Kp] (GATHER)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int m0 = blockIdx.x * BM;
 
-  // 1. input rows -> LDS (whole 16-B chunks; the channel padding of the NHWC storage rides along)
-  const int cpr = r8(p.Cin) / 8;
-  for (int i = tid; i < BM * cpr; i += NT) {
-    const int r = i / cpr, c = i - r * cpr;
-    const int m = m0 + r;
-    uint4 v = {0u, 0u, 0u, 0u};
-    if (m < p.M) v = *reinterpret_cast<const uint4*>(p.x + (int64_t)m * p.ldx + c * 8);
-    *reinterpret_cast<uint4*>(raw + r * L.RP + c * 8) = v;
-  }
-  if (p.stats)
-    for (int i = tid; i < 2 * p.Cout; i += NT) st[i] = 0.f;
-  __syncthreads();
-  // 2. logical zero-padded image, 8 channels (one 16-B LDS write) per step
-  if (!L.direct) {
-    const int upr = L.PK / 8;
-    for (int i = tid; i < BM * upr; i += NT) {
-      const int r = i / upr, u = i - r * upr;
-      const int g = (u * 8) / p.Kp, k0 = u * 8 - g * p.Kp;
-      uint32_t w4[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int ka = k0 + 2 * e, kb = ka + 1;
-        const uint32_t lo = ka < p.Cg ? raw[r * L.RP + perm_pos(g * p.Cg + ka, p.Cin, p.in_sg)] : 0u;
-        const uint32_t hi = kb < p.Cg ? raw[r * L.RP + perm_pos(g * p.Cg + kb, p.Cin, p.in_sg)] : 0u;
-        w4[e] = lo | (hi << 16);
-      }
-      *reinterpret_cast<uint4*>(pk + r * L.PP + u * 8) = uint4{w4[0], w4[1], w4[2], w4[3]};
+  for (int c = tid; c < p.Cout; c += NT) tout[c] = p.tout ? p.tout[c] : (int16_t)c;
+  if constexpr (MODE == GW_GATHER) {
+    for (int u = tid; u < PK; u += NT) {  // logical padded channel -> stored channel (-1: padding)
+      const int g = u / p.Kp, k = u - g * p.Kp;
+      tin[u] = k < p.Cg ? (p.tin ? p.tin[g * p.Cg + k] : (int16_t)(g * p.Cg + k)) : (int16_t)-1;
     }
     __syncthreads();
   }
-  // 3. MFMA items: (row fragment, group, chunk of 4 output-column fragments)
-  const int nrf = BM / 16;
+  if (p.stats)
+    for (int i = tid; i < 2 * p.Cout; i += NT) st[i] = 0.f;
+  // 1. logical zero-padded input image, one 8-channel piece per step. The loads of 8 pieces are
+  // issued before any LDS write and never sit behind a branch (hipcc waits for a load right at
+  // a branch around it): padding / out-of-range pieces read the zero page instead.
+  const int upr = PK / 8;
+  const int total = BM * upr;
+  const u16* zp = reinterpret_cast<const u16*>(dv_zero_page);
+  for (int base = tid; base < total; base += 8 * NT) {
+    uint4 v[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const int i = min(base + b * NT, total - 1);
+      const int r = (int)fdiv((uint32_t)i, p.div_upr), u = i - r * upr;
+      const int g = (int)fdiv((uint32_t)u, p.div_kc), k0 = (u - g * (p.Kp / 8)) * 8;
+      const int m = m0 + r;
+      const int l0 = g * p.Cg + k0;
+      const bool ok = m < p.M && k0 < p.Cg;
+      const u16* row = p.x + (int64_t)(ok ? m : 0) * p.ldx;
+      if constexpr (MODE == GW_V16) {
+        v[b] = *reinterpret_cast<const uint4*>(ok ? row + l0 : zp);
+      } else if constexpr (MODE == GW_PAIR) {
+        uint32_t w4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool va = ok && k0 + 2 * e < p.Cg;
+          const uint32_t x2 = *reinterpret_cast<const uint32_t*>(row + (va ? l0 + 2 * e : 0));
+          w4[e] = va ? x2 : 0u;
+        }
+        v[b] = uint4{w4[0], w4[1], w4[2], w4[3]};
+      } else {
+        uint32_t w4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int pa = tin[u * 8 + 2 * e], pb = tin[u * 8 + 2 * e + 1];
+          const uint32_t lo = row[(ok && pa >= 0) ? pa : 0], hi = row[(ok && pb >= 0) ? pb : 0];
+          w4[e] = ((ok && pa >= 0) ? lo : 0u) | (((ok && pb >= 0) ? hi : 0u) << 16);
+        }
+        v[b] = uint4{w4[0], w4[1], w4[2], w4[3]};
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const int i = base + b * NT;
+      if (i < total) {
+        const int r = (int)fdiv((uint32_t)i, p.div_upr), u = i - r * upr;
+        *reinterpret_cast<uint4*>(pk + r * PP + u * 8) = v[b];
+      }
+    }
+  }
+  __syncthreads();
+  // 2. MFMA items: (row fragment, group, chunk of 4 output-column fragments)
+  constexpr int NRF = BM / 16;
   const int ncf = (p.Og + 15) / 16;
   const int ncc = (ncf + 3) / 4;
-  const int nitems = nrf * p.G * ncc;
+  const int nitems = NRF * p.G * ncc;
   const int nkc = p.Kp / 32;
   const float* shift = p.stats ? stat_shift(p.stats, p.Cout) : nullptr;
   for (int it = wid; it < nitems; it += NT / 64) {
-    const int rf = it % nrf;
-    const int t = it / nrf;
+    const int rf = it % NRF;
+    const int t = it / NRF;
     const int cc = t % ncc, g = t / ncc;
     f32x4 acc[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int row = rf * 16 + (lane & 15);
-    for (int kc = 0; kc < nkc; ++kc) {
-      const bf16x8 b = *reinterpret_cast<const bf16x8*>(pk + row * L.PP + g * p.Kp + kc * 32 + 8 * (lane >> 4));
+    // weight fragments come from L2: the next k-chunk's four are loaded while this chunk's MFMAs
+    // run (unconditional loads from clamped rows: rows >= Og give discarded results)
+    const u16* wq[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int cf = cc * 4 + q;
-        if (cf < ncf) {  // wave-uniform
-          const int j = min(cf * 16 + (lane & 15), p.Og - 1);  // rows >= Og: discarded results
-          const bf16x8 a = *reinterpret_cast<const bf16x8*>(p.w + ((int64_t)g * p.Orows + j) * p.Kp + kc * 32 +
-                                                          8 * (lane >> 4));
-          acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[q], 0, 0, 0);
-        }
-      }
+    for (int q = 0; q < 4; ++q)
+      wq[q] = p.w + ((int64_t)g * p.Orows + min((cc * 4 + q) * 16 + (lane & 15), p.Og - 1)) * p.Kp + 8 * (lane >> 4);
+    bf16x8 a[4], an[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a[q] = *reinterpret_cast<const bf16x8*>(wq[q]);
+    for (int kc = 0; kc < nkc; ++kc) {
+      const int kn = min(kc + 1, nkc - 1) * 32;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) an[q] = *reinterpret_cast<const bf16x8*>(wq[q] + kn);
+      const bf16x8 b = *reinterpret_cast<const bf16x8*>(pk + row * PP + g * p.Kp + kc * 32 + 8 * (lane >> 4));
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (cc * 4 + q < ncf) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[q], b, acc[q], 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[q] = an[q];
     }
-    // 4. acc[q][r] = y[pixel row][channel j = cf*16 + (lane>>4)*4 + r] of group g
+    // 3. acc[q][r] = y[pixel row][channel j = cf*16 + (lane>>4)*4 + r] of group g
     const bool mv = m0 + row < p.M;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int cf = cc * 4 + q;
       if (cf >= ncf) break;
+      const int j4 = cf * 16 + (lane >> 4) * 4;  // Og % 4 == 0: the 4 channels are all valid or none
+      if (!p.tout && j4 < p.Og)  // contiguous output channels: one 8-byte LDS write
+        *reinterpret_cast<uint2*>(ys + row * YP + g * p.Og + j4) =
+            uint2{pack2bf(acc[q][0], acc[q][1]), pack2bf(acc[q][2], acc[q][3])};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int j = cf * 16 + (lane >> 4) * 4 + r;
+        const int j = j4 + r;
         const bool jv = j < p.Og;
-        const int pos = jv ? perm_pos(g * p.Og + j, p.Cout, p.out_sg) : 0;
+        const int pos = jv ? tout[g * p.Og + j] : 0;
         const float v = acc[q][r];
-        if (jv) ys[row * L.YP + pos] = f2bf(v);
+        if (jv && p.tout) ys[row * YP + pos] = f2bf(v);
         if (p.stats) {  // wave-uniform
           const float d = (jv && mv) ? v - shift[pos] : 0.f;
           const float s1 = row16_sum(d), s2 = row16_sum(d * d);
@@ -164,7 +194,7 @@ __global__ __launch_bounds__(NT) void gconv_kernel(GcParams p) {
       atomicAdd(a + p.Cout + c, st[p.Cout + c]);
     }
   }
-  // 5. output rows: 16-B / 8-B / 2-B pieces by alignment
+  // 4. output rows: 16-B / 8-B / 2-B pieces by alignment
   const int vw = (p.Cout % 8 == 0 && p.ldy % 8 == 0) ? 8 : (p.Cout % 4 == 0 && p.ldy % 4 == 0) ? 4 : 1;
   const int ppr = p.Cout / vw;
   for (int i = tid; i < BM * ppr; i += NT) {
@@ -172,150 +202,241 @@ __global__ __launch_bounds__(NT) void gconv_kernel(GcParams p) {
     const int m = m0 + r;
     if (m >= p.M) continue;
     u16* dst = p.y + (int64_t)m * p.ldy + c;
-    const u16* src = ys + r * L.YP + c;
+    const u16* src = ys + r * YP + c;
     if (vw == 8) *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
     else if (vw == 4) *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(src);
     else *dst = *src;
   }
 }
 
-// ---- weight gradient: dW[g*Og + j][k] += sum_m dy[m][pos_out(g*Og+j)] * x[m][pos_in(g*Cg+k)] ----
-// Block = a chunk of rows (in tiles of WB pixels) x a chunk of 256 (4 j x 4 k) output blocks; the
-// tiles are repacked into logical (unpermuted, dense) order in LDS, each thread accumulates its
-// 16 outputs in fp32 registers over all the chunk's rows and adds them into dW once.
+// ---- weight gradient: dW[g*Og + j][k] += sum_m dy[m][tout(g*Og+j)] * x[m][tin(g*Cg+k)] ----
+constexpr int FPW = 4;    // output fragments per wave; a block = 16 fragments, dealt round-robin
+
 struct GwParams {
   const u16* x;
-  int ldx, Cin, in_sg;
+  int ldx;
+  const int16_t* tin;
   const u16* dy;
-  int ldy, Cout, out_sg;
+  int ldy;
+  const int16_t* tout;
   float* dw;  // [G*Og][Cg] fp32, accumulated
-  int M, G, Cg, Og, rows_per_block, WB;  // WB: rows per LDS tile (64 / 32 / 16, LDS budget)
+  int M, G, Cg, Og;
+  int CJ, CK;        // image widths (columns): 64 or a multiple of 128
+  int WT;            // pixels per tile: 64, or 32 for wide images (LDS / staging registers)
+  int nkf, nfrag;    // fragments: ceil(Og/16) x ceil(Cg/16), row-major over (jf, kf)
+  int fchunks;       // blockIdx.y = g * fchunks + fragment chunk (4 * FPW fragments)
+  int tiles_per_block;
 };
 
+// 16-byte-chunk XOR key of pixel row k (conv_wgrad.hip mn_swz): 8 keys for rows >= 256 B,
+// 4 keys for 128-B rows; conflict-free transposed reads for rows that are multiples of 256 B
+DV_DEVICE int gw_swz(int k, int cols) {
+  if (cols >= 128) return ((k & 3) | ((k >> 1) & 4)) << 1;
+  return (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 1;
+}
+DV_DEVICE bf16x8 gw_read(const char* img, int cols, int col0, int kbase, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int k1 = kbase + 8 * g + q, k2 = k1 + 4;
+  const int u = (col0 >> 2) + p;
+  const char* a1 = img + k1 * (cols * 2) + ((u ^ (gw_swz(k1, cols) << 1)) << 3);
+  const char* a2 = img + k2 * (cols * 2) + ((u ^ (gw_swz(k2, cols) << 1)) << 3);
+  i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((i16x4 __attribute__((address_space(3)))*)LDS_PTR(a1));
+  i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((i16x4 __attribute__((address_space(3)))*)LDS_PTR(a2));
+  i16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+// 8 logical channels [c0, c0 + 8) of group g of one pixel row (zeros past nch / when !ok);
+// unconditional loads (the zero page or clamped indices), see gconv_kernel; MODE: GW_*
+template <int MODE>
+DV_DEVICE uint4 gw_piece(const u16* row, bool ok, const int16_t* pos, int base, int c0, int nch) {
+  const int l0 = base + c0;
+  if constexpr (MODE == GW_V16) {
+    return *reinterpret_cast<const uint4*>(ok && c0 < nch ? row + l0 : reinterpret_cast<const u16*>(dv_zero_page));
+  } else if constexpr (MODE == GW_PAIR) {
+    uint32_t w4[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const bool va = ok && c0 + 2 * e < nch;
+      const uint32_t v = *reinterpret_cast<const uint32_t*>(row + (va ? l0 + 2 * e : 0));
+      w4[e] = va ? v : 0u;
+    }
+    return uint4{w4[0], w4[1], w4[2], w4[3]};
+  } else {
+    uint32_t w4[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int ka = c0 + 2 * e, kb = ka + 1;
+      const bool va = ok && ka < nch, vb = ok && kb < nch;
+      const uint32_t lo = row[va ? pos[2 * e] : 0], hi = row[vb ? pos[2 * e + 1] : 0];
+      w4[e] = (va ? lo : 0u) | ((vb ? hi : 0u) << 16);
+    }
+    return uint4{w4[0], w4[1], w4[2], w4[3]};
+  }
+}
+
+template <int MY, int MX, int MAXP>
 __global__ __launch_bounds__(NT) void gconv_wgrad_kernel(GwParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int XL = p.G * p.Cg, YL = p.G * p.Og;  // logical row lengths (multiples of 4)
-  const int XP = XL + 4, YPp = YL + 4;         // pitches (8-B aligned rows)
-  const int XR = r8(p.Cin) + 8, YR = r8(p.Cout) + 8;
-  const int WB = p.WB;
-  u16* xraw = reinterpret_cast<u16*>(smem);
-  u16* yraw = xraw + WB * XR;
-  u16* xl = yraw + WB * YR;
-  u16* yl = xl + WB * XP;
-  const int tid = threadIdx.x;
-  // this thread's 4x4 output block
-  const int jb = p.Og / 4, kb = p.Cg / 4;
-  const int item = blockIdx.y * NT + tid;
-  const bool active = item < p.G * jb * kb;
-  const int g = active ? item / (jb * kb) : 0;
-  const int rem = active ? item - g * jb * kb : 0;
-  const int j0 = (rem / kb) * 4, k0 = (rem % kb) * 4;
-  float acc[4][4];
+  const int WT = p.WT;
+  char* yimg = smem;                  // [WT][CJ] dY of group g, swizzled 16-B chunks
+  char* ximg = smem + WT * p.CJ * 2;  // [WT][CK] X of group g
+  int16_t* posy = reinterpret_cast<int16_t*>(ximg + WT * p.CK * 2);  // [Og] stored dY channels of g
+  int16_t* posx = posy + p.Og;                                        // [Cg] stored X channels of g
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = blockIdx.y / p.fchunks, fc = blockIdx.y - g * p.fchunks;
+  if constexpr (MY == GW_GATHER)
+    for (int j = tid; j < p.Og; j += NT) posy[j] = p.tout ? p.tout[g * p.Og + j] : (int16_t)(g * p.Og + j);
+  if constexpr (MX == GW_GATHER)
+    for (int k = tid; k < p.Cg; k += NT) posx[k] = p.tin ? p.tin[g * p.Cg + k] : (int16_t)(g * p.Cg + k);
+  if constexpr (MY == GW_GATHER || MX == GW_GATHER) __syncthreads();
+  f32x4 acc[FPW];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int f = 0; f < FPW; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int ntiles = (p.M + WT - 1) / WT;
+  const int t0 = blockIdx.x * p.tiles_per_block, t1 = min(ntiles, t0 + p.tiles_per_block);
+  const int cj8 = p.CJ / 8, ck8 = p.CK / 8;
+  const int total = WT * (cj8 + ck8);  // <= MAXP * NT (host check)
+  uint4 v[MAXP];
+  // the next tile's pieces are loaded into registers while the current tile's MFMAs run
+  auto fetch = [&](int t) {
 #pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = 0.f;
-  const int rbeg = blockIdx.x * p.rows_per_block, rend = min(p.M, rbeg + p.rows_per_block);
-  const int xc = r8(p.Cin) / 8, yc = r8(p.Cout) / 8;
-  for (int t0 = rbeg; t0 < rend; t0 += WB) {
-    __syncthreads();  // the previous tile's logical images are no longer read
-    for (int i = tid; i < WB * (xc + yc); i += NT) {
-      const bool isx = i < WB * xc;
-      const int ii = isx ? i : i - WB * xc;
-      const int cpr = isx ? xc : yc;
-      const int r = ii / cpr, c = ii - r * cpr;
-      const int m = t0 + r;
-      uint4 v = {0u, 0u, 0u, 0u};
-      if (m < rend) v = *reinterpret_cast<const uint4*>((isx ? p.x : p.dy) + (int64_t)m * (isx ? p.ldx : p.ldy) + c * 8);
-      *reinterpret_cast<uint4*>((isx ? xraw + r * XR : yraw + r * YR) + c * 8) = v;
+    for (int b = 0; b < MAXP; ++b) {
+      const int i = min(tid + b * NT, total - 1);
+      const bool isy = i < WT * cj8;
+      const int ii = isy ? i : i - WT * cj8;
+      const int c8 = isy ? cj8 : ck8;
+      const int r = ii / c8, c = ii - r * c8;
+      const int m = t * WT + r;
+      const bool ok = m < p.M;
+      const int mm = ok ? m : 0;
+      v[b] = isy ? gw_piece<MY>(p.dy + (int64_t)mm * p.ldy, ok, posy + c * 8, g * p.Og, c * 8, p.Og)
+                 : gw_piece<MX>(p.x + (int64_t)mm * p.ldx, ok, posx + c * 8, g * p.Cg, c * 8, p.Cg);
+    }
+  };
+  if (t0 < t1) fetch(t0);
+  for (int t = t0; t < t1; ++t) {
+    __syncthreads();  // the previous tile's fragments are read
+#pragma unroll
+    for (int b = 0; b < MAXP; ++b) {
+      const int i = tid + b * NT;
+      if (i < total) {
+        const bool isy = i < WT * cj8;
+        const int ii = isy ? i : i - WT * cj8;
+        const int c8 = isy ? cj8 : ck8;
+        const int r = ii / c8, c = ii - r * c8;
+        const int cols = isy ? p.CJ : p.CK;
+        char* img = isy ? yimg : ximg;
+        *reinterpret_cast<uint4*>(img + r * cols * 2 + ((c ^ gw_swz(r, cols)) << 4)) = v[b];
+      }
     }
     __syncthreads();
-    for (int i = tid; i < WB * (XL + YL) / 2; i += NT) {  // logical images, 2 channels per step
-      const bool isx = i < WB * XL / 2;
-      const int ii = isx ? i : i - WB * XL / 2;
-      const int half = (isx ? XL : YL) / 2;
-      const int r = ii / half, l = (ii - r * half) * 2;
-      const u16* src = isx ? xraw + r * XR : yraw + r * YR;
-      const int C = isx ? p.Cin : p.Cout, sg = isx ? p.in_sg : p.out_sg;
-      const uint32_t lo = src[perm_pos(l, C, sg)], hi = src[perm_pos(l + 1, C, sg)];
-      *reinterpret_cast<uint32_t*>((isx ? xl + r * XP : yl + r * YPp) + l) = lo | (hi << 16);
-    }
-    __syncthreads();
-    if (active) {
-      const int nr = min(WB, rend - t0);
-      for (int r = 0; r < nr; ++r) {
-        const uint2 xv = *reinterpret_cast<const uint2*>(xl + r * XP + g * p.Cg + k0);
-        const uint2 yv = *reinterpret_cast<const uint2*>(yl + r * YPp + g * p.Og + j0);
-        const float xf[4] = {bf2f(xv.x & 0xffff), bf2f(xv.x >> 16), bf2f(xv.y & 0xffff), bf2f(xv.y >> 16)};
-        const float yf[4] = {bf2f(yv.x & 0xffff), bf2f(yv.x >> 16), bf2f(yv.y & 0xffff), bf2f(yv.y >> 16)};
+    if (t + 1 < t1) fetch(t + 1);
 #pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-          for (int b = 0; b < 4; ++b) acc[a][b] = fmaf(yf[a], xf[b], acc[a][b]);
+    for (int f = 0; f < FPW; ++f) {
+      const int fi = fc * 4 * FPW + f * 4 + wid;  // round-robin over the block's 4 waves
+      if (fi < p.nfrag) {                          // wave-uniform
+        const int jf = fi / p.nkf, kf = fi - jf * p.nkf;
+        for (int ks = 0; ks < WT / 32; ++ks) {
+          const bf16x8 a = gw_read(yimg, p.CJ, jf * 16, ks * 32, lane);
+          const bf16x8 b = gw_read(ximg, p.CK, kf * 16, ks * 32, lane);
+          acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[f], 0, 0, 0);
+        }
       }
     }
   }
-  if (!active) return;
+  // acc[f][r] = dW[j = jf*16 + (lane>>4)*4 + r][k = kf*16 + (lane&15)] of group g
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int f = 0; f < FPW; ++f) {
+    const int fi = fc * 4 * FPW + f * 4 + wid;
+    if (fi >= p.nfrag) break;
+    const int jf = fi / p.nkf, kf = fi - jf * p.nkf;
+    const int k = kf * 16 + (lane & 15);
 #pragma unroll
-    for (int b = 0; b < 4; ++b) atomicAdd(p.dw + (int64_t)(g * p.Og + j0 + a) * p.Cg + k0 + b, acc[a][b]);
+    for (int r = 0; r < 4; ++r) {
+      const int j = jf * 16 + (lane >> 4) * 4 + r;
+      if (j < p.Og && k < p.Cg) atomicAdd(p.dw + (int64_t)(g * p.Og + j) * p.Cg + k, acc[f][r]);
+    }
+  }
 }
 }  // namespace
 
 // fwd / dgrad; returns -1 for an unsupported shape (the caller falls back)
-int dv_gconv(const void* x, int ldx, int Cin, int in_sg, const void* w, int Orows, void* y, int ldy, int Cout, int out_sg,
-             int M, int G, int Cg, int Og, int Kp, float* stats, hipStream_t st) {
+int dv_gconv(const void* x, int ldx, int Cin, const int16_t* tin, const void* w, int Orows, void* y, int ldy, int Cout,
+             const int16_t* tout, int M, int G, int Cg, int Og, int Kp, float* stats, hipStream_t st) {
   if (Cin != G * Cg || Cout != G * Og || Kp % 32 || Kp < Cg || ldx % 8 || ldy % 4 || (uintptr_t)x % 16 ||
-      (uintptr_t)w % 16 || r8(Cin) > ldx || (in_sg > 1 && Cin % in_sg) || (out_sg > 1 && Cout % out_sg) || Orows < Og)
+      (uintptr_t)w % 16 || Orows < Og || Cout > 32767 || Cin > 32767)
     return -1;
-  GcParams p{(const u16*)x, ldx, Cin, in_sg, (const u16*)w, Orows, (u16*)y, ldy, Cout, out_sg, M, G, Cg, Og, Kp, stats};
-  const GcLayout L = gc_layout(Cin, G, Cg, Kp, in_sg, Cout);
-  // 64 rows while two blocks fit a CU, else 32 / 16
-  int BM = 64;
-  while (BM > 16 && gc_lds_bytes(L, BM, Cout, stats) > 80 * 1024) BM /= 2;
-  const size_t lds = gc_lds_bytes(L, BM, Cout, stats);
+  int BM = 64;  // two blocks per CU where the tiles allow
+  while (BM > 16 && gc_lds_bytes(BM, G, Kp, Cout, stats) > 80 * 1024) BM /= 2;
+  const size_t lds = gc_lds_bytes(BM, G, Kp, Cout, stats);
   if (lds > 160 * 1024) return -1;
+  GcParams p{(const u16*)x, ldx, Cin, tin, (const u16*)w, Orows, (u16*)y, ldy, Cout, tout, M, G, Cg, Og, Kp, stats,
+             make_fastdiv((uint32_t)(G * Kp / 8)), make_fastdiv((uint32_t)(Kp / 8))};
   const unsigned grid = (unsigned)((M + BM - 1) / BM);
-  static bool attr[3] = {false, false, false};
-#define GC_LAUNCH(B, I)                                                                                        \
-  do {                                                                                                         \
-    if (!attr[I]) {                                                                                            \
-      hipFuncSetAttribute((const void*)gconv_kernel<B>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
-      attr[I] = true;                                                                                          \
-    }                                                                                                          \
-    gconv_kernel<B><<<grid, NT, lds, st>>>(p);                                                                 \
+  const int mode = tin ? GW_GATHER : (Cg % 8 == 0) ? GW_V16 : (Cg % 2 == 0) ? GW_PAIR : GW_GATHER;
+  static bool attr[9] = {};
+#define GC_LAUNCH(B, MD, I)                                                                                         \
+  do {                                                                                                              \
+    if (!attr[I]) {                                                                                                 \
+      hipFuncSetAttribute((const void*)gconv_kernel<B, MD>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+      attr[I] = true;                                                                                               \
+    }                                                                                                               \
+    gconv_kernel<B, MD><<<grid, NT, lds, st>>>(p);                                                                  \
   } while (0)
-  if (BM == 64) GC_LAUNCH(64, 0);
-  else if (BM == 32) GC_LAUNCH(32, 1);
-  else GC_LAUNCH(16, 2);
+#define GC_BM(MD, I0)                  \
+  if (BM == 64) GC_LAUNCH(64, MD, I0);  \
+  else if (BM == 32) GC_LAUNCH(32, MD, I0 + 1); \
+  else GC_LAUNCH(16, MD, I0 + 2);
+  if (mode == GW_V16) { GC_BM(GW_V16, 0) }
+  else if (mode == GW_PAIR) { GC_BM(GW_PAIR, 3) }
+  else { GC_BM(GW_GATHER, 6) }
+#undef GC_BM
 #undef GC_LAUNCH
   return 0;
 }
 
-int dv_gconv_wgrad(const void* x, int ldx, int Cin, int in_sg, const void* dy, int ldy, int Cout, int out_sg, float* dw,
+int dv_gconv_wgrad(const void* x, int ldx, const int16_t* tin, const void* dy, int ldy, const int16_t* tout, float* dw,
                    int M, int G, int Cg, int Og, hipStream_t st) {
-  if (Cin != G * Cg || Cout != G * Og || Cg % 4 || Og % 4 || ldx % 8 || ldy % 8 || (uintptr_t)x % 16 ||
-      (uintptr_t)dy % 16 || r8(Cin) > ldx || r8(Cout) > ldy)
-    return -1;
-  auto lds_of = [&](int wb) { return (size_t)wb * ((r8(Cin) + 8) + (r8(Cout) + 8) + (G * Cg + 4) + (G * Og + 4)) * 2; };
-  int WB = 64;
-  while (WB > 16 && lds_of(WB) > 80 * 1024) WB /= 2;
-  const size_t lds = lds_of(WB);
-  if (lds > 160 * 1024) return -1;
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)gconv_wgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
+  if ((uintptr_t)x % 16 || (uintptr_t)dy % 16 || ldx % 8 || ldy % 8) return -1;
+  GwParams p{};
+  p.x = (const u16*)x; p.ldx = ldx; p.tin = tin; p.dy = (const u16*)dy; p.ldy = ldy; p.tout = tout; p.dw = dw;
+  p.M = M; p.G = G; p.Cg = Cg; p.Og = Og;
+  // image widths: 64 columns, or a multiple of 128 (the XOR key stays inside 16-chunk blocks)
+  auto width = [](int c) { return c <= 64 ? 64 : (c + 127) / 128 * 128; };
+  p.CJ = width(Og); p.CK = width(Cg);
+  p.nkf = (Cg + 15) / 16;
+  p.nfrag = ((Og + 15) / 16) * p.nkf;
+  p.fchunks = (p.nfrag + 4 * FPW - 1) / (4 * FPW);
+  auto mode_of = [](const int16_t* tab, int nch, int G_) {
+    if (tab) return (int)GW_GATHER;
+    if ((nch & 7) == 0) return (int)GW_V16;  // base = g * nch stays 8-aligned
+    if ((nch & 1) == 0) return (int)GW_PAIR;
+    (void)G_;
+    return (int)GW_GATHER;
+  };
+  const int my = mode_of(tout, Og, G), mx = mode_of(tin, Cg, G);
+  const int maxp = 8;
+  p.WT = 64;
+  while (p.WT > 32 && p.WT * (p.CJ + p.CK) / 8 > maxp * NT) p.WT /= 2;
+  if (p.WT * (p.CJ + p.CK) / 8 > maxp * NT) return -1;
+  const size_t lds = (size_t)p.WT * (p.CJ + p.CK) * 2 + (size_t)(Og + Cg) * 2;
+  // split the pixels so that ~1024 blocks run (each adds its tile into dW once: the atomic
+  // traffic is blocks x outputs per block, 16 fragments = 16 KB)
+  const int ntiles = (M + p.WT - 1) / p.WT;
+  const int cols = G * p.fchunks;
+  const int rchunks = std::max(1, std::min(ntiles, 1024 / cols));
+  p.tiles_per_block = (ntiles + rchunks - 1) / rchunks;
+  const int gx = (ntiles + p.tiles_per_block - 1) / p.tiles_per_block;
+  const dim3 grid((unsigned)gx, (unsigned)cols);
+#define GW_CASE(A, B, P)                                                                                          \
+  if (my == A && mx == B) {                                                                                       \
+    gconv_wgrad_kernel<A, B, P><<<grid, NT, lds, st>>>(p);                                                        \
+    return 0;                                                                                                     \
   }
-  const int items = G * (Og / 4) * (Cg / 4);
-  const int ichunks = (items + NT - 1) / NT;
-  // ~1024 blocks in all, >= 4 row tiles per block (the 16 atomics per thread amortised)
-  int64_t rchunks = std::max<int64_t>(1, 1024 / ichunks);
-  int64_t rpb = (M + rchunks - 1) / rchunks;
-  rpb = std::max<int64_t>(4 * WB, (rpb + WB - 1) / WB * WB);
-  rchunks = (M + rpb - 1) / rpb;
-  GwParams p{(const u16*)x, ldx, Cin, in_sg, (const u16*)dy, ldy, Cout, out_sg, dw, M, G, Cg, Og, (int)rpb, WB};
-  gconv_wgrad_kernel<<<dim3((unsigned)rchunks, (unsigned)ichunks), NT, lds, st>>>(p);
-  return 0;
+  GW_CASE(GW_V16, GW_V16, 8) GW_CASE(GW_V16, GW_PAIR, 8) GW_CASE(GW_PAIR, GW_V16, 8) GW_CASE(GW_PAIR, GW_PAIR, 8)
+  GW_CASE(GW_GATHER, GW_V16, 8) GW_CASE(GW_GATHER, GW_PAIR, 8) GW_CASE(GW_V16, GW_GATHER, 8)
+  GW_CASE(GW_PAIR, GW_GATHER, 8) GW_CASE(GW_GATHER, GW_GATHER, 8)
+#undef GW_CASE
+  return -1;
 }

@@ -70,10 +70,11 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st);  // 0 ok, 1 ok but BN sta
 void dv_conv_fwd_variant(int v);  // 0 = heuristic tile choice; others: benchmarking override
 int dv_conv_wgrad(const ConvWgradArgs& a, hipStream_t st);
 // grouped 1x1 conv with small unaligned groups and a fused channel shuffle (csrc/gconv.hip):
-// forward / dgrad (weights [G][Orows][Kp] bf16) and the fp32 weight gradient (accumulated)
-int dv_gconv(const void* x, int ldx, int Cin, int in_sg, const void* w, int Orows, void* y, int ldy, int Cout, int out_sg,
-             int M, int G, int Cg, int Og, int Kp, float* stats, hipStream_t st);
-int dv_gconv_wgrad(const void* x, int ldx, int Cin, int in_sg, const void* dy, int ldy, int Cout, int out_sg, float* dw,
+// forward / dgrad (weights [G][Orows][Kp] bf16) and the fp32 weight gradient (accumulated);
+// tin / tout: logical -> stored channel tables (int16, nullptr = identity)
+int dv_gconv(const void* x, int ldx, int Cin, const int16_t* tin, const void* w, int Orows, void* y, int ldy, int Cout,
+             const int16_t* tout, int M, int G, int Cg, int Og, int Kp, float* stats, hipStream_t st);
+int dv_gconv_wgrad(const void* x, int ldx, const int16_t* tin, const void* dy, int ldy, const int16_t* tout, float* dw,
                    int M, int G, int Cg, int Og, hipStream_t st);
 void dv_conv_wgrad_tuning(int variant, int split_pct);  // benchmarking override (0, 100 = heuristic)
 int dv_conv_wgrad_splits(const ConvWgradArgs& a);

@@ -626,6 +626,22 @@ def _gconv_ok(x, weight, bias, stride, padding, dilation, groups, act, join=None
             and C == Cg * groups and O % groups == 0 and Cg % 4 == 0 and (O // groups) % 4 == 0 and x.dim() == 4)
 
 
+_PERM = {}
+
+
+def _shuffle_table(C, sg, device):
+    """int16 logical -> stored channel table of the ShuffleNet shuffle (None = identity)."""
+    if not sg or sg <= 1:
+        return None
+    key = (C, sg, str(device))
+    t = _PERM.get(key)
+    if t is None:
+        l = torch.arange(C)
+        cpg = C // sg
+        t = _PERM[key] = ((l % cpg) * sg + l // cpg).to(torch.int16).to(device)
+    return t
+
+
 class _GConvFn(torch.autograd.Function):
     """Grouped 1x1 conv (+ fused output channel shuffle, + BN statistics) on csrc/gconv.hip."""
 
@@ -640,7 +656,8 @@ class _GConvFn(torch.autograd.Function):
         stats = None
         if want_stats:
             stats = stats_buf if stats_buf is not None else torch.zeros((STAT_ROWS, O), dtype=F32, device=x.device)
-        lib().gconv(ptr(x), ld_of(x), C, 0, ptr(wk), Og, ptr(y), ld_of(y), O, int(shuffle), N * H * W, G, Cg, Og, Kp,
+        tab = _shuffle_table(O, shuffle, x.device)
+        lib().gconv(ptr(x), ld_of(x), C, 0, ptr(wk), Og, ptr(y), ld_of(y), O, ptr(tab), N * H * W, G, Cg, Og, Kp,
                     ptr(stats), stream_handle())
         ctx.save_for_backward(x, weight)
         ctx.cfg = (G, int(shuffle))
@@ -667,13 +684,13 @@ class _GConvFn(torch.autograd.Function):
             Kp = (Og + 31) // 32 * 32
             wt = _prep_weight(weight, G, Kp, mode=1)  # [G][Cg][Kp]: per-group transpose
             dx = empty_nhwc(N, C, H, W, x.device)
-            lib().gconv(ptr(dy), ld_of(dy), O, sg, ptr(wt), Cg, ptr(dx), ld_of(dx), C, 0, N * H * W, G, Og, Cg, Kp, 0,
-                        stream_handle())
+            lib().gconv(ptr(dy), ld_of(dy), O, ptr(_shuffle_table(O, sg, x.device)), ptr(wt), Cg, ptr(dx), ld_of(dx), C,
+                        0, N * H * W, G, Og, Cg, Kp, 0, stream_handle())
         if ctx.needs_input_grad[1]:
             sink = grad_sink(weight)
             acc = sink if sink is not None else torch.zeros(weight.shape, dtype=F32, device=x.device)
-            lib().gconv_wgrad(ptr(x), ld_of(x), C, 0, ptr(dy), ld_of(dy), O, sg, ptr(acc), N * H * W, G, Cg, Og,
-                              stream_handle())
+            lib().gconv_wgrad(ptr(x), ld_of(x), 0, ptr(dy), ld_of(dy), ptr(_shuffle_table(O, sg, x.device)), ptr(acc),
+                              N * H * W, G, Cg, Og, stream_handle())
             dw = None if sink is not None else acc
         return dx, dw, None, None, None, None
 
