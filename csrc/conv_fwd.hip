@@ -102,23 +102,30 @@ constexpr int stage_bytes() { return (BM_ + BN_) * BK_ * 2; }
 
 // BatchNorm-backward reduction terms of 8 stored gradient values `o` (bf16, exactly what the
 // unfused bn_bwd_reduce pass would read back) at element offset `off` of the BN input / mask:
-// dz = act'(z) * dout, sum dz and sum dz * (x - mean) * invstd (csrc/bn.hip bn_bwd_reduce_kernel).
-DV_DEVICE void bn_bwd_accum(const FwdParams& p, const uint4& o, const uint4& xr, uint32_t mb, float* bs, float* bq,
-                            const float* bmu, const float* bis, const float* bms, const float* bmh) {
+// dz = act'(z) * dout, sum dz and sum dz * (x - mean) (csrc/bn.hip bn_bwd_reduce_kernel; the
+// invstd factor is applied once per channel after the loop). Element pairs run as packed fp32
+// (v_pk_add / v_pk_fma: half the VALU issue of the scalar form in an epilogue-bound kernel).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+DV_DEVICE f32x2 bf2x(uint32_t w) { return f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)}; }
+DV_DEVICE void bn_bwd_accum(const FwdParams& p, const uint4& o, const uint4& xr, uint32_t mb, f32x2* bs, f32x2* bq,
+                            const f32x2* bmu, const f32x2* bms, const f32x2* bmh) {
   const uint32_t dw[4] = {o.x, o.y, o.z, o.w}, xw[4] = {xr.x, xr.y, xr.z, xr.w};
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const float d = bf2f((u16)(dw[e >> 1] >> ((e & 1) * 16)));
-    const float x = bf2f((u16)(xw[e >> 1] >> ((e & 1) * 16)));
-    float dz = d;
+  for (int e = 0; e < 4; ++e) {
+    const f32x2 d = bf2x(dw[e]), x = bf2x(xw[e]);
+    f32x2 dz = d;
     if (p.bnmode == 3) {
-      dz = ((mb >> e) & 1u) ? d : (p.bnact == 2 ? d * p.bnslope : 0.f);
+      const f32x2 neg = p.bnact == 2 ? d * p.bnslope : f32x2{0.f, 0.f};
+      dz.x = ((mb >> (2 * e)) & 1u) ? d.x : neg.x;
+      dz.y = ((mb >> (2 * e + 1)) & 1u) ? d.y : neg.y;
     } else if (p.bnmode == 2) {
-      const float z = fmaf(x, bms[e], bmh[e]);
-      dz = z > 0.f ? d : (p.bnact == 2 ? d * p.bnslope : 0.f);
+      const f32x2 z = x * bms[e] + bmh[e];
+      const f32x2 neg = p.bnact == 2 ? d * p.bnslope : f32x2{0.f, 0.f};
+      dz.x = z.x > 0.f ? d.x : neg.x;
+      dz.y = z.y > 0.f ? d.y : neg.y;
     }
     bs[e] += dz;
-    bq[e] += dz * (x - bmu[e]) * bis[e];
+    bq[e] = __builtin_elementwise_fma(dz, x - bmu[e], bq[e]);
   }
 }
 
@@ -361,17 +368,16 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
 #pragma unroll
     for (int r = 0; r < 4; ++r) { bsum[j][r] = 0.f; bsq[j][r] = 0.f; }
   // BNR: this lane's 8 channels are fixed over the store loop (rows it*8 + lane/8)
-  float bs[8], bq[8], bmu[8], bis[8], bms[8], bmh[8];
+  f32x2 bs2[4], bq2[4], bmu2[4], bms2[4], bmh2[4];
   if constexpr (BNR) {
     const int nb = nw0 + (lane & 7) * 8;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      bs[e] = 0.f; bq[e] = 0.f;
-      const bool ok = nb + e < p.N;
-      bms[e] = ok ? p.bnprm[nb + e] : 0.f;
-      bmh[e] = ok ? p.bnprm[p.N + nb + e] : 0.f;
-      bmu[e] = ok ? p.bnprm[2 * p.N + nb + e] : 0.f;
-      bis[e] = ok ? p.bnprm[3 * p.N + nb + e] : 0.f;
+    for (int e = 0; e < 4; ++e) {
+      bs2[e] = f32x2{0.f, 0.f}; bq2[e] = f32x2{0.f, 0.f};
+      const bool ok0 = nb + 2 * e < p.N, ok1 = nb + 2 * e + 1 < p.N;
+      bms2[e] = f32x2{ok0 ? p.bnprm[nb + 2 * e] : 0.f, ok1 ? p.bnprm[nb + 2 * e + 1] : 0.f};
+      bmh2[e] = f32x2{ok0 ? p.bnprm[p.N + nb + 2 * e] : 0.f, ok1 ? p.bnprm[p.N + nb + 2 * e + 1] : 0.f};
+      bmu2[e] = f32x2{ok0 ? p.bnprm[2 * p.N + nb + 2 * e] : 0.f, ok1 ? p.bnprm[2 * p.N + nb + 2 * e + 1] : 0.f};
     }
   }
   u16* st = reinterpret_cast<u16*>(smem + wid * EPI_WAVE_BYTES);
@@ -481,18 +487,21 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
       if constexpr (RES) {  // residual-gradient join: dX += stashed gradient (fused instead of an add pass)
         const u16* rp = p.res + yoff;
         if (vec) {
-          uint4 a = *reinterpret_cast<const uint4*>(src), b = pf_res[it];
-          const u16* av = reinterpret_cast<const u16*>(&a);
-          const u16* bw = reinterpret_cast<const u16*>(&b);
-          uint4 o;
-          uint32_t* ov = reinterpret_cast<uint32_t*>(&o);
+          const uint4 a = *reinterpret_cast<const uint4*>(src), b = pf_res[it];
+          const uint32_t aw[4] = {a.x, a.y, a.z, a.w}, bw[4] = {b.x, b.y, b.z, b.w};
+          uint32_t ov[4];
           const uint32_t rmb = pf_rmb[it];
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            ov[e] = pack2bf(bf2f(av[2 * e]) + masked_res(bf2f(bw[2 * e]), rmb, 2 * e, p.resact, p.resslope),
-                            bf2f(av[2 * e + 1]) + masked_res(bf2f(bw[2 * e + 1]), rmb, 2 * e + 1, p.resact, p.resslope));
+          for (int e = 0; e < 4; ++e) {  // packed fp32 pairs: act'(res) * res + conv result
+            const f32x2 r = bf2x(bw[e]);
+            const f32x2 neg = p.resact == 2 ? r * p.resslope : f32x2{0.f, 0.f};
+            const f32x2 m = f32x2{((rmb >> (2 * e)) & 1u) ? r.x : neg.x, ((rmb >> (2 * e + 1)) & 1u) ? r.y : neg.y};
+            const f32x2 t = bf2x(aw[e]) + m;
+            ov[e] = pack2bf(t.x, t.y);
+          }
+          const uint4 o = uint4{ov[0], ov[1], ov[2], ov[3]};
           *reinterpret_cast<uint4*>(dst) = o;
-          if constexpr (BNR) bn_bwd_accum(p, o, pf_x[it], pf_mb[it], bs, bq, bmu, bis, bms, bmh);
+          if constexpr (BNR) bn_bwd_accum(p, o, pf_x[it], pf_mb[it], bs2, bq2, bmu2, bms2, bmh2);
         } else {
           const uint32_t rmb = pf_rmb[it];
 #pragma unroll
@@ -502,7 +511,7 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
       } else if (vec) {
         const uint4 o = *reinterpret_cast<const uint4*>(src);
         *reinterpret_cast<uint4*>(dst) = o;
-        if constexpr (BNR) bn_bwd_accum(p, o, pf_x[it], pf_mb[it], bs, bq, bmu, bis, bms, bmh);
+        if constexpr (BNR) bn_bwd_accum(p, o, pf_x[it], pf_mb[it], bs2, bq2, bmu2, bms2, bmh2);
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e) if (n + e < p.N) dst[e] = src[e];
@@ -540,6 +549,17 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
   if constexpr (BNR) {
     // lanes sharing (lane & 7) hold partials of the same 8 channels: butterfly over lane bits 3-5,
     // then the WM waves of one channel column meet in LDS; one coalesced atomic row per block
+    float bs[8], bq[8];
+    {
+      const int nb = nw0 + (lane & 7) * 8;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {  // sum dz*(x - mean) -> sum dz*xhat: one invstd per channel
+        const float i0 = nb + 2 * e < p.N ? p.bnprm[3 * p.N + nb + 2 * e] : 0.f;
+        const float i1 = nb + 2 * e + 1 < p.N ? p.bnprm[3 * p.N + nb + 2 * e + 1] : 0.f;
+        bs[2 * e] = bs2[e].x; bs[2 * e + 1] = bs2[e].y;
+        bq[2 * e] = bq2[e].x * i0; bq[2 * e + 1] = bq2[e].y * i1;
+      }
+    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
 #pragma unroll

@@ -40,6 +40,13 @@ def init_distributed(backend: str | None = None, timeout_s: int = 600, force: bo
         kw = dict(backend=be, timeout=datetime.timedelta(seconds=timeout_s))
         if be == "nccl":
             kw["device_id"] = device
+            # RCCL kernels on a high-priority HIP stream: the bucket all-reduces overlap a
+            # backward pass that keeps every CU busy, and win the dispatch arbitration against
+            # it. DV_COMM_PRIORITY=0 reverts to a normal-priority stream.
+            if os.environ.get("DV_COMM_PRIORITY", "1") != "0":
+                opts = dist.ProcessGroupNCCL.Options()
+                opts.is_high_priority_stream = True
+                kw["pg_options"] = opts
         dist.init_process_group(**kw)
     return world, rank, local, device
 
