@@ -62,6 +62,7 @@ PYBIND11_MODULE(_C, m) {
      py::arg("reflect") = 0, py::arg("ksplit") = 1, py::arg("ypart") = 0, py::arg("zfill") = 0);
   m.def("conv_fwd_variant", [](int v) { dv_conv_fwd_variant(v); });
   m.def("bn_tuning", [](int blocks, int unroll) { dv_bn_tuning(blocks, unroll); });
+  m.def("bn_apply_tuning", [](int blocks, int unroll) { dv_bn_apply_tuning(blocks, unroll); });
   m.def("dw_variant", [](int v) { dv_dw_variant(v); });
   m.def("set_sync_check", [](bool on) { g_sync_check = on; });
   m.def("sync_check", []() { return g_sync_check; });

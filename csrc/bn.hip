@@ -212,7 +212,7 @@ struct RowTile {
 };
 
 // ---- out = act(x*scale + shift (+res)) ----
-template <int VEC, bool MB, bool RBN = false>
+template <int VEC, bool MB, bool RBN = false, int UNR = 2>
 __global__ __launch_bounds__(NT) void bn_apply_kernel(const u16* __restrict__ x, const u16* __restrict__ res,
                                                         u16* __restrict__ out, int64_t rows, int C, int64_t rows_per_block,
                                                         const float* __restrict__ scale, const float* __restrict__ shift,
@@ -229,7 +229,7 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const u16* __restrict__ x,
       // residual BN: z = x*sc + res*rs + (sf + rshift): one shift per channel
       if constexpr (RBN) { rs[k] = rscale[g * VEC + k]; sf[k] += rshift[g * VEC + k]; }
     }
-#pragma unroll 2
+#pragma unroll UNR
     for (int64_t r = r0 + t.lane_r; r < r1; r += t.rpi) {
       const int64_t o = r * C + g * VEC;
       float v[VEC], rv[VEC];
@@ -320,7 +320,7 @@ __global__ void bn_bwd_finalize_kernel(float* __restrict__ acc, int C, double co
 // same input (e.g. a pre-activation block's residual path, models/hourglass.py) summed in this pass
 // instead of a separate add; it may alias dx (each element is read before it is written by the
 // same thread), hence no __restrict__ on the two.
-template <int VEC, int MM>
+template <int VEC, int MM, int UNR = 2>
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const u16* __restrict__ dout, const u16* __restrict__ out,
                                                             const u16* __restrict__ x, u16* dx, u16* __restrict__ dres,
                                                             int64_t rows, int C, int64_t rows_per_block, const float* __restrict__ kA,
@@ -338,7 +338,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const u16* __restrict_
       ms[k] = MM == MM_X ? mscale[g * VEC + k] : 0.f;
       mh[k] = MM == MM_X ? mshift[g * VEC + k] : 0.f;
     }
-#pragma unroll 2
+#pragma unroll UNR
     for (int64_t r = r0 + t.lane_r; r < r1; r += t.rpi) {
       const int64_t o = r * C + g * VEC;
       float d[VEC], ov[VEC], xv[VEC], rr[VEC], av[VEC];
@@ -405,10 +405,13 @@ inline dim3 reduce_grid(int64_t rows, int C) {
   const int64_t g = std::min<int64_t>(std::max<int64_t>(target, 1), std::max<int64_t>(1, rows / 32));
   return dim3((unsigned)g, (unsigned)slabs);
 }
-// rows per block for the row-tiled apply passes: ~4096 blocks, a multiple of rows/iteration
+// rows per block for the row-tiled apply passes: ~g_apply_blocks blocks (8192), a multiple of
+// rows/iteration; g_apply_unroll: rows in flight per thread (benchmarking override, dv_bn_apply_tuning)
+int g_apply_blocks = 8192;  // tools/bn_apply_bench.py: 8192 beat 4096 by 3-6 % on every ResNet-50 shape
+int g_apply_unroll = 2;
 inline int64_t apply_rows_per_block(int64_t rows, int C, int v) {
   const int cg = C / v, tpr = cg < NT ? cg : NT, rpi = NT / tpr;
-  int64_t rpb = (rows + 4095) / 4096;
+  int64_t rpb = (rows + g_apply_blocks - 1) / g_apply_blocks;
   rpb = ((rpb + rpi - 1) / rpi) * rpi;
   return std::max<int64_t>(rpb, rpi);
 }
@@ -425,6 +428,11 @@ inline int64_t apply_rows_per_block(int64_t rows, int C, int v) {
 void dv_bn_tuning(int reduce_blocks, int reduce_unroll) {
   g_reduce_blocks = reduce_blocks > 0 ? reduce_blocks : 1024;
   g_reduce_unroll = reduce_unroll == 4 ? 4 : 2;
+}
+
+void dv_bn_apply_tuning(int blocks, int unroll) {
+  g_apply_blocks = blocks > 0 ? blocks : 8192;
+  g_apply_unroll = unroll == 4 ? 4 : 2;
 }
 
 void dv_bn_stats(const void* x, int64_t rows, int C, float* acc, hipStream_t st) {
@@ -467,6 +475,11 @@ void dv_bn_apply(const void* x, const void* res, void* out, int64_t n, int C, co
   const int64_t rpb = apply_rows_per_block(rows, C, v);
   const int g = (int)((rows + rpb - 1) / rpb);
 #define AP_ARGS <<<g, NT, 0, st>>>((const u16*)x, (const u16*)res, (u16*)out, rows, C, rpb, scale, shift, act, slope, (uint8_t*)mask, rscale, rshift)
+  if (g_apply_unroll == 4 && mask && v == 8) {
+    if (res && rscale && rshift) bn_apply_kernel<8, true, true, 4> AP_ARGS;
+    else bn_apply_kernel<8, true, false, 4> AP_ARGS;
+    return;
+  }
   if (res && rscale && rshift) {
     if (mask && v == 8) bn_apply_kernel<8, true, true> AP_ARGS;
     else if (v == 8) bn_apply_kernel<8, false, true> AP_ARGS;
@@ -547,6 +560,12 @@ void dv_bn_bwd_apply(const void* dout, const void* out, const void* x, void* dx,
   const int64_t rows = n / C;
   const int64_t rpb = apply_rows_per_block(rows, C, v);
   const int g = (int)((rows + rpb - 1) / rpb);
+  if (act && mask_bits && v == 8 && g_apply_unroll == 4) {
+    bn_bwd_apply_kernel<8, MM_BITS, 4><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, (u16*)dx,
+                                                           (u16*)dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope,
+                                                           (const u16*)addend);
+    return;
+  }
   if (act && mask_bits && v == 8) {
     bn_bwd_apply_kernel<8, MM_BITS><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, (u16*)dx,
                                                         (u16*)dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope,

@@ -296,6 +296,203 @@ __global__ __launch_bounds__(NT, OCC) void dw_wgrad_kernel(const u16* __restrict
   for (int e = threadIdx.x; e < sw * KS * KS; e += NT) atomicAdd(dst + e, red[e]);
 }
 
+
+// ---------------------------------------------------------------- small planes (<= 14x14 outputs)
+// One block = one image x 64 channels x the WHOLE output plane. The input window the plane needs
+// ((P-1)*sh + KS rows x (Q-1)*SW + KS columns, zero outside the image) is staged once in LDS with
+// 16-B loads issued all at once; every tap is then an LDS read. The strip kernels above re-read
+// each input pixel ~4.5x through L1/L2 and, on 14x14 / 7x7 layers, ran at 1.2-2 TB/s
+// (profiles/dw_bench_r2.txt). Thread = 8 channels (cg = tid % 8) x output pixels pl, pl + 32, ...
+constexpr int PL_CH = 64;              // channels per block
+constexpr int PL_LANES = NT / 8;       // pixel lanes
+constexpr int PLANE_MAX_OUT = 196;     // 14 x 14
+inline int plane_win(int P, int s, int KS) { return (P - 1) * s + KS; }
+inline size_t plane_lds(int P, int Q, int sh, int sw, int KS) {
+  return (size_t)plane_win(P, sh, KS) * plane_win(Q, sw, KS) * PL_CH * 2;
+}
+
+template <int KS>
+DV_DEVICE void plane_stage(const u16* __restrict__ x, const DwGeo& g, int n, int c0, u16* win, int WR, int WC) {
+  const int total = WR * WC * 8;  // 16-B pieces
+  for (int base = threadIdx.x; base < total; base += 8 * NT) {
+    uint4 v[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {  // all loads in flight before the LDS writes
+      const int i = min(base + b * NT, total - 1);
+      const int pix = i >> 3, cg = i & 7;
+      const int wr = pix / WC, wc = pix - wr * WC;
+      const int h = wr - g.ph, w = wc - g.pw;
+      const bool ok = h >= 0 && h < g.H && w >= 0 && w < g.W;
+      const u16* src = ok ? x + (((int64_t)n * g.H + h) * g.W + w) * g.ldx + c0 + cg * 8
+                          : reinterpret_cast<const u16*>(dv_zero_page);
+      v[b] = *reinterpret_cast<const uint4*>(src);
+    }
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const int i = base + b * NT;
+      if (i < total) *reinterpret_cast<uint4*>(win + (int64_t)(i >> 3) * PL_CH + (i & 7) * 8) = v[b];
+    }
+  }
+}
+
+template <int KS, int SW, bool FLIP>
+__global__ __launch_bounds__(NT) void dw_plane_fwd_kernel(const u16* __restrict__ x, const float* __restrict__ w,
+                                                          const float* __restrict__ bias, u16* __restrict__ y, DwGeo g,
+                                                          int act, float slope, float* __restrict__ stats) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  u16* win = reinterpret_cast<u16*>(smem);
+  const int slabs = g.C / PL_CH;
+  const int n = blockIdx.x / slabs, c0 = (blockIdx.x - n * slabs) * PL_CH;
+  const int WR = (g.P - 1) * g.sh + KS, WC = (g.Q - 1) * SW + KS;
+  const int cg = threadIdx.x & 7, pl = threadIdx.x >> 3;
+  const int c = c0 + cg * 8;
+  float wr[KS * KS][8], bv[8], ssum[8], ssq[8], kq[8];
+#pragma unroll
+  for (int tp = 0; tp < KS * KS; ++tp)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) wr[tp][k] = w[(c + k) * KS * KS + (FLIP ? KS * KS - 1 - tp : tp)];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    bv[k] = bias ? bias[c + k] : 0.f;
+    ssum[k] = 0.f; ssq[k] = 0.f;
+    kq[k] = stats ? stat_shift(stats, g.C)[c + k] : 0.f;
+  }
+  plane_stage<KS>(x, g, n, c0, win, WR, WC);
+  __syncthreads();
+  const int npix = g.P * g.Q;
+  for (int o = pl; o < npix; o += PL_LANES) {
+    const int p = o / g.Q, q = o - p * g.Q;
+    float acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = bv[k];
+#pragma unroll
+    for (int r = 0; r < KS; ++r)
+#pragma unroll
+      for (int s2 = 0; s2 < KS; ++s2) {
+        float v[8];
+        ld8(win + ((p * g.sh + r) * WC + q * SW + s2) * PL_CH + cg * 8, v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] = fmaf(v[k], wr[r * KS + s2][k], acc[k]);
+      }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float v = acc[k];
+      if (act == 1) v = fmaxf(v, 0.f);
+      else if (act == 2) v = v > 0.f ? v : v * slope;
+      acc[k] = v;
+      const float d = v - kq[k];
+      ssum[k] += d; ssq[k] = fmaf(d, d, ssq[k]);
+    }
+    st8(y + ((int64_t)n * npix + o) * g.ldy + c, acc);
+  }
+  if (!stats) return;
+  // shifted BN partial statistics: the 32 pixel lanes of each channel meet in LDS (the window
+  // is no longer read), one coalesced atomic row per block
+  __syncthreads();
+  float* sh = reinterpret_cast<float*>(smem);  // [2][PL_LANES][PL_CH]
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    sh[pl * PL_CH + cg * 8 + k] = ssum[k];
+    sh[PL_LANES * PL_CH + pl * PL_CH + cg * 8 + k] = ssq[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * PL_CH) {
+    const int which = threadIdx.x / PL_CH, ch = threadIdx.x % PL_CH;
+    float t = 0.f;
+    for (int l = 0; l < PL_LANES; ++l) t += sh[which * PL_LANES * PL_CH + l * PL_CH + ch];
+    atomicAdd(stats + (int64_t)(blockIdx.x % DV_STAT_SHARDS) * 2 * g.C + which * g.C + c0 + ch, t);
+  }
+}
+
+// dw[c][r][s] += sum over the images of this block and the output plane of
+//                dy[n][p][q][c] * x[n][p*sh - ph + r][q*SW - pw + s][c]
+template <int KS, int SW>
+__global__ __launch_bounds__(NT) void dw_plane_wgrad_kernel(const u16* __restrict__ x, const u16* __restrict__ dy,
+                                                            float* __restrict__ dw, DwGeo g, int imgs_per_block) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  u16* win = reinterpret_cast<u16*>(smem);
+  const int slabs = g.C / PL_CH;
+  const int nb = blockIdx.x / slabs, c0 = (blockIdx.x - nb * slabs) * PL_CH;
+  const int WR = (g.P - 1) * g.sh + KS, WC = (g.Q - 1) * SW + KS;
+  const int cg = threadIdx.x & 7, pl = threadIdx.x >> 3;
+  const int c = c0 + cg * 8;
+  const int npix = g.P * g.Q;
+  float acc[KS * KS][8];
+#pragma unroll
+  for (int tp = 0; tp < KS * KS; ++tp)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[tp][k] = 0.f;
+  const int n0 = nb * imgs_per_block, n1 = min(g.N, n0 + imgs_per_block);
+  for (int n = n0; n < n1; ++n) {
+    __syncthreads();  // the previous image's window is no longer read
+    plane_stage<KS>(x, g, n, c0, win, WR, WC);
+    __syncthreads();
+    for (int o = pl; o < npix; o += PL_LANES) {
+      const int p = o / g.Q, q = o - p * g.Q;
+      float d[8];
+      ld8(dy + ((int64_t)n * npix + o) * g.ldy + c, d);
+#pragma unroll
+      for (int r = 0; r < KS; ++r)
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2) {
+          float v[8];
+          ld8(win + ((p * g.sh + r) * WC + q * SW + s2) * PL_CH + cg * 8, v);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[r * KS + s2][k] = fmaf(d[k], v[k], acc[r * KS + s2][k]);
+        }
+    }
+  }
+  // the 8 pixel lanes of a wave (lane bits 3-5) by butterfly, then the 4 waves in LDS
+#pragma unroll
+  for (int tp = 0; tp < KS * KS; ++tp)
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int off = 8; off < 64; off <<= 1) acc[tp][k] += __shfl_xor(acc[tp][k], off, 64);
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);  // [4 waves][KS*KS][PL_CH]
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane < 8) {
+#pragma unroll
+    for (int tp = 0; tp < KS * KS; ++tp)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[(wv * KS * KS + tp) * PL_CH + cg * 8 + k] = acc[tp][k];
+  }
+  __syncthreads();
+  // dw is [C][KS*KS]: this slab's block of PL_CH * KS*KS floats is contiguous
+  for (int e = threadIdx.x; e < PL_CH * KS * KS; e += NT) {
+    const int ch = e / (KS * KS), tp = e - ch * (KS * KS);
+    float t = 0.f;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) t += red[(v * KS * KS + tp) * PL_CH + ch];
+    atomicAdd(dw + (int64_t)(c0 + ch) * KS * KS + tp, t);
+  }
+}
+
+template <int KS, int SW, bool FLIP>
+bool plane_fwd(const void* x, const float* w, const float* bias, void* y, const DwGeo& g, int act, float slope,
+               float* stats, hipStream_t st) {
+  if constexpr (KS > 3) return false;  // the 5x5 / 7x7 filters' registers do not fit this layout
+  const size_t lds = plane_lds(g.P, g.Q, g.sh, SW, KS);
+  const size_t need = std::max(lds, stats ? (size_t)2 * PL_LANES * PL_CH * 4 : (size_t)0);
+  if (g.C % PL_CH || g.P * g.Q > PLANE_MAX_OUT || need > 64 * 1024 || g.sh != SW) return false;
+  dw_plane_fwd_kernel<KS, SW, FLIP><<<g.N * (g.C / PL_CH), NT, need, st>>>((const u16*)x, w, bias, (u16*)y, g, act,
+                                                                              slope, stats);
+  return true;
+}
+template <int KS, int SW>
+bool plane_wgrad(const void* x, const void* dy, float* dw, const DwGeo& g, hipStream_t st) {
+  if constexpr (KS > 3) return false;
+  const size_t lds = std::max(plane_lds(g.P, g.Q, g.sh, SW, KS), (size_t)4 * KS * KS * PL_CH * 4);
+  if (g.C % PL_CH || g.P * g.Q > PLANE_MAX_OUT || lds > 64 * 1024 || g.sh != SW) return false;
+  const int slabs = g.C / PL_CH;
+  // ~512 blocks: each adds its 64 x KS*KS tile into dw once
+  const int ipb = std::max(1, (g.N * slabs + 511) / 512);
+  const int nblk = (g.N + ipb - 1) / ipb;
+  dw_plane_wgrad_kernel<KS, SW><<<nblk * slabs, NT, lds, st>>>((const u16*)x, (const u16*)dy, dw, g, ipb);
+  return true;
+}
+
 int64_t per_block(int64_t nstrips, int rpi, int slabs, int64_t target_blocks) {
   // ~target blocks in total over the slabs, a whole number of strip passes per block
   int64_t spb = std::max<int64_t>(rpi, (nstrips * slabs + target_blocks - 1) / target_blocks);
@@ -332,6 +529,9 @@ void fwd_variants(const void* x, const float* w, const float* bias, void* y, con
       default: break;
     }
   }
+  // the whole-plane forward measured no faster on 14x14 and slower on 7x7 outputs than the strip
+  // kernel (profiles/dw_bench_r3.txt): benchmark variant 51 only
+  if (g_dw_variant == 51 && plane_fwd<KS, SW, FLIP>(x, w, bias, y, g, act, slope, stats, st)) return;
   fwd_launch<KS, SW, FLIP, 4, 1>(x, w, bias, y, g, act, slope, stats, 4096, st);
 }
 template <int KS, int SW, int QT, int OCC>
@@ -360,6 +560,7 @@ void wgrad_variants(const void* x, const void* dy, float* dw, const DwGeo& g, hi
       default: break;
     }
   }
+  if (g_dw_variant != 50 && !dv_deterministic() && plane_wgrad<KS, SW>(x, dy, dw, g, st)) return;
   wgrad_launch<KS, SW, 4, 1>(x, dy, dw, g, 512, st);
 }
 template <int KS, int QT, int OCC>

@@ -90,6 +90,7 @@ int dv_conv_stats_tiles(int Nb, int P, int Q);
 
 // ---- batchnorm (bn.hip) ----
 void dv_bn_tuning(int reduce_blocks, int reduce_unroll);  // benchmarking override (1024, 2 = default)
+void dv_bn_apply_tuning(int blocks, int unroll);          // apply passes: benchmarking override (4096, 2)
 void dv_bn_stats(const void* x, int64_t rows, int C, float* acc, hipStream_t st);
 void dv_bn_finalize(float* acc, int C, double count, float eps, float momentum, const float* gamma,
                     const float* beta, float* rm, float* rv, float* save_mean, float* save_invstd, float* scale,
