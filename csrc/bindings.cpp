@@ -176,6 +176,20 @@ PYBIND11_MODULE(_C, m) {
   m.def("add", [](uptr a, uptr b, uptr y, int64_t n, float alpha, float beta, int act, float slope, uptr st) { dv_add(CP(a), CP(b), P(y), n, alpha, beta, act, slope, ST(st)); check_last("add"); });
   m.def("dropout", [](uptr x, uptr y, int64_t n, float p, uint64_t seed, uptr st) { dv_dropout(CP(x), P(y), n, p, seed, ST(st)); check_last("dropout"); });
   m.def("wprep", [](uptr w, uptr out, int G, int Og, int Ig, int R, int S, int Ipad, int mode, int Sp, uptr st) { dv_wprep(CFP(w), P(out), G, Og, Ig, R, S, Ipad, mode, Sp, ST(st)); check_last("wprep"); });
+  m.def("stem_fwd", [](uptr xp, uptr w, uptr y, uptr bias, uptr stats, int act, float slope, int N, int Hp, int Wp,
+                       int P_, int Q, int R, int Sp, int K, int sh, int sw, uptr st) {
+    const int r = dv_stem_fwd(CP(xp), CP(w), P(y), CFP(bias), FP(stats), act, slope, N, Hp, Wp, P_, Q, R, Sp, K, sh, sw,
+                              ST(st));
+    if (r == 0) check_last("stem_fwd");
+    return r;
+  });
+  m.def("stem_wgrad", [](uptr xp, uptr dy, int ldy, uptr dw, int N, int C, int S, int Hp, int Wp, int P_, int Q, int R,
+                         int Sp, int K, int sh, int sw, uptr st) {
+    const int r = dv_stem_wgrad(CP(xp), CP(dy), ldy, FP(dw), N, C, S, Hp, Wp, P_, Q, R, Sp, K, sh, sw, ST(st));
+    if (r == 0) check_last("stem_wgrad");
+    return r;
+  });
+  m.def("stem_tuning", [](int blocks, int wg_blocks) { dv_stem_tuning(blocks, wg_blocks); });
   m.def("stem_pack", [](uptr x, int is_f32, uptr y, int N, int C, int H, int W, int Hp, int Wp, int pt, int pl, uptr st,
                         int reflect) {
     dv_stem_pack(CP(x), is_f32, P(y), N, C, H, W, Hp, Wp, pt, pl, reflect, ST(st)); check_last("stem_pack");

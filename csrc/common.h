@@ -27,8 +27,12 @@ DV_DEVICE u16 f2bf(float f) {
   __bf16 b = (__bf16)f;  // hipcc emits v_cvt_pk_bf16_f32 at -O3 (RNE, NaN-safe)
   return __builtin_bit_cast(u16, b);
 }
+// one v_cvt_pk_bf16_f32 (the scalar-pair form f2bf(a) | f2bf(b) << 16 was sometimes emitted as
+// two packed converts plus and/or/sdwa re-shuffles)
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
 DV_DEVICE uint32_t pack2bf(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a, b}, bf16x2_t));
 }
 
 // ---- wave / block reductions (wave64) ----

@@ -149,6 +149,12 @@ int dv_nhwc_copy(const void* src, int lds, void* dst, int ldd, int64_t rows, int
 // reflects onto (h, w) (the interior one plus up to three mirrored border positions)
 void dv_reflect_pad_bwd(const void* dxp, void* dx, int N, int H, int W, int C, int ldp, int ld, int ph, int pw,
                         hipStream_t st);
+// dedicated 7x7 / 64-channel stem kernels on the tap-packed image (csrc/stem.hip); -1 = not covered
+int dv_stem_fwd(const void* xp, const void* w, void* y, const float* bias, float* stats, int act, float slope, int N,
+                int Hp, int Wp, int P, int Q, int R, int Sp, int K, int sh, int sw, hipStream_t st);
+int dv_stem_wgrad(const void* xp, const void* dy, int ldy, float* dw, int N, int C, int S, int Hp, int Wp, int P, int Q,
+                  int R, int Sp, int K, int sh, int sw, hipStream_t st);
+void dv_stem_tuning(int blocks, int wg_blocks);  // benchmarking override of the target grids (0 = default)
 void dv_stem_pack(const void* x, int x_is_f32, void* y, int N, int C, int H, int W, int Hp, int Wp, int pt, int pl,
                   int reflect, hipStream_t st);
 void dv_wgrad_unprep(float* src, float* dst, int G, int Og, int Ig, int R, int S, int Ipad, float alpha,

@@ -419,6 +419,10 @@ class _ConvFn(torch.autograd.Function):
 # stride of 4), so K = R * Sp * 4 (7x7: 224) instead of R * S * 8 with channels padded to 8
 # (392): 1.75x fewer MFMA k-steps and no im2col bounds checks (csrc/conv_fwd.hip packed mode).
 # ---------------------------------------------------------------------------------------
+STEM_KERNELS = True  # 7x7 / 64-channel stems on csrc/stem.hip (else the packed implicit-GEMM path)
+COUNTERS = {"stem_kernel_fwd": 0, "stem_generic_fwd": 0, "stem_kernel_wgrad": 0}
+
+
 def _stem_geometry(x, weight, stride, padding, dilation, groups, extra):
     """(Sp, Hp, Wp, P, Q) when the tap-packed path applies, else None."""
     if groups != 1 or tuple(dilation) != (1, 1) or x.requires_grad or x.dim() != 4 or x.dtype not in (F32, BF16):
@@ -468,8 +472,14 @@ class _StemConvFn(torch.autograd.Function):
         if want_stats:
             stats = stats_buf if stats_buf is not None else torch.zeros((STAT_ROWS, O), dtype=F32, device=x.device)
         b = bias.detach().float().contiguous() if bias is not None else None
-        conv_fwd_raw(xp, wk, y, b, stats, N, Hp, Wp, 4 * Sp, 4, 1, O, P, Q, R, 1, stride, (0, 0), (1, 1), act=act,
-                     slope=slope, tgather=2)
+        r = -1
+        if STEM_KERNELS and act in (0, 1, 2):  # dedicated row-walking 7x7 / 64-channel kernel (csrc/stem.hip)
+            r = lib().stem_fwd(ptr(xp), ptr(wk), ptr(y), ptr(b), ptr(stats), int(act), float(slope), N, Hp, Wp, P, Q,
+                               R, Sp, O, stride[0], stride[1], stream_handle())
+        if r != 0:
+            conv_fwd_raw(xp, wk, y, b, stats, N, Hp, Wp, 4 * Sp, 4, 1, O, P, Q, R, 1, stride, (0, 0), (1, 1), act=act,
+                         slope=slope, tgather=2)
+        COUNTERS["stem_kernel_fwd" if r == 0 else "stem_generic_fwd"] += 1
         ctx.save_for_backward(xp, weight, y if act else None)
         ctx.bias_param = bias  # leaf parameter (not saved): its gradient may sink in place
         ctx.cfg = (stride, act, slope, geo, bias is not None)
@@ -492,6 +502,21 @@ class _StemConvFn(torch.autograd.Function):
         if act:
             dy = act_grad(dy, y, act, slope)
         dw = db = None
+        if ctx.needs_input_grad[1] and STEM_KERNELS and not lib().deterministic():
+            # dedicated kernel: per-block partials reduced straight into the [O][C][R][S] gradient
+            sink = grad_sink(weight)
+            dst = sink if sink is not None else torch.zeros(weight.shape, dtype=F32, device=xp.device)
+            r = lib().stem_wgrad(ptr(xp), ptr(dy), ld_of(dy), ptr(dst), N, I, S, Hp, Wp, P, Q, R, Sp, O, stride[0],
+                                 stride[1], stream_handle())
+            if r == 0:
+                COUNTERS["stem_kernel_wgrad"] += 1
+                if sink is None:
+                    dw = dst
+                if has_bias and ctx.needs_input_grad[2]:
+                    db = _bias_grad(ctx.bias_param, dy)
+                return None, dw, db, None, None, None, None, None, None, None, None
+            if sink is None:
+                del dst
         if ctx.needs_input_grad[1]:
             ws = _wgrad_workspace(O * R * Sp * 4, xp.device)  # [O][R][Sp][4], zero on entry and exit
             lib().conv_wgrad(ptr(xp), ptr(dy), ptr(ws), N, Hp, Wp, 4 * Sp, 4, 1, O, P, Q, ld_of(dy), R, 1, stride[0],

@@ -525,6 +525,75 @@ def test_stem_packed_conv(case):
         assert _rel(b.grad, br.grad) < 3e-2
 
 
+STEM_KERNEL_CASES = [
+    # N, C, H, W, padding, bias, act
+    (3, 3, 64, 64, 3, False, None),            # ResNet / Inception stem geometry (Q = 32)
+    (2, 3, 50, 38, 3, True, "relu"),           # Q = 19: partial 16-pixel fragments, ragged row groups
+    (2, 3, 45, 61, (2, 3, 2, 3), False, "leaky"),  # Keras 'same' 7x7 s2 (Hourglass), odd sizes
+    (5, 1, 30, 30, 3, True, None),             # one input channel, 5 images (several blocks per image)
+]
+
+
+@pytest.mark.parametrize("case", STEM_KERNEL_CASES)
+def test_stem_dedicated_kernel(case):
+    """csrc/stem.hip (7x7, 64 output channels) forward, BN statistics and weight gradient (into a
+    zero and into a live gradient buffer) vs the fp32 torch conv of the same bf16 operands."""
+    from deep_vision_amd import ops as F
+    from deep_vision_amd.ops import conv as C
+
+    N, Cin, H, W, p, has_b, act = case
+    torch.manual_seed(1)
+    x = torch.randn(N, Cin, H, W, device=DEV).bfloat16().float()
+    w = (torch.randn(64, Cin, 7, 7, device=DEV) * 0.1).requires_grad_(True)
+    b = torch.randn(64, device=DEV).requires_grad_(True) if has_b else None
+    n0 = dict(C.COUNTERS)
+    y = F.conv2d(x, w, b, 2, p, act=act, slope=0.1)
+    assert C.COUNTERS["stem_kernel_fwd"] == n0["stem_kernel_fwd"] + 1, "dedicated stem kernel not taken"
+    wr = w.detach().bfloat16().float().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True) if has_b else None
+    xr = TF.pad(x, (p[2], p[3], p[0], p[1])) if isinstance(p, tuple) else x
+    yr = TF.conv2d(xr, wr, br, 2, 0 if isinstance(p, tuple) else p)
+    if act == "relu":
+        yr = TF.relu(yr)
+    elif act == "leaky":
+        yr = TF.leaky_relu(yr, 0.1)
+    assert y.shape == yr.shape
+    assert _rel(y, yr) < 1e-2
+    dy = torch.randn_like(yr).bfloat16().float()
+    y.backward(_nhwc(dy))
+    yr.backward(dy)
+    assert C.COUNTERS["stem_kernel_wgrad"] == n0["stem_kernel_wgrad"] + 1
+    assert _rel(w.grad, wr.grad) < 1e-2
+    # second backward accumulates into the live gradient
+    y2 = F.conv2d(x, w, b, 2, p, act=act, slope=0.1)
+    y2.backward(_nhwc(dy))
+    assert _rel(w.grad, 2 * wr.grad) < 1e-2
+    if has_b:
+        assert _rel(b.grad, 2 * br.grad) < 2e-2
+
+
+def test_stem_dedicated_kernel_stats():
+    """Stem BN statistics from the dedicated kernel's register accumulators (shifted sums)."""
+    from deep_vision_amd import nn
+    from deep_vision_amd import ops as F
+    from deep_vision_amd.ops import conv as C
+
+    conv = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False).to(DEV)
+    bn = nn.BatchNorm2d(64).to(DEV)
+    ref_conv = torch.nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False).to(DEV)
+    ref_conv.weight.data.copy_(conv.weight.data.bfloat16().float())
+    ref_bn = torch.nn.BatchNorm2d(64).to(DEV)
+    n0 = C.COUNTERS["stem_kernel_fwd"]
+    for it in range(3):  # shifted sums: the shift is the previous batch's mean from step 2 on
+        x = (torch.randn(3, 3, 72, 60, device=DEV) * 2 + 5).bfloat16().float()
+        y = F.conv_bn_act(x, conv, bn, "relu")
+        yr = TF.relu(ref_bn(ref_conv(x)))
+        assert _rel(y, yr) < 3e-2, it
+    assert C.COUNTERS["stem_kernel_fwd"] == n0 + 3
+    assert _rel(bn.running_mean, ref_bn.running_mean) < 1e-2
+    assert _rel(bn.running_var, ref_bn.running_var) < 1e-2
+
+
 def test_stem_conv_bn_stats():
     """Stem conv with BatchNorm statistics from the packed kernel's epilogue (ResNet stem)."""
     from deep_vision_amd import nn
