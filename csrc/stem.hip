@@ -30,7 +30,6 @@
 namespace {
 
 constexpr int SR = 7;        // filter rows handled by these kernels (7x7 stems)
-constexpr int NR_F = 32;     // forward ring slots: window sh*(RG-1)+R plus two groups ahead (2*sh*RG)
 constexpr int RG = 4;        // output rows per forward group
 constexpr int NR_W = 16;     // weight-gradient ring slots: R + 3*sh (three output rows ahead)
 constexpr int NDY = 4;       // weight-gradient dY row buffers (three in flight behind the one in use)
@@ -89,42 +88,96 @@ DV_DEVICE void wait_vm() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   __builtin_amdgcn_s_waitcnt((N & 0xF) | (0x7 << 4) | (0xF << 8) | ((N >> 4) << 14));
 }
-// vmcnt(n) for a wave-uniform runtime n, rounded DOWN to a multiple of 4 (waiting for more is
-// always safe); n >= 64 waits to 60
+// exact vmcnt(n) for a wave-uniform runtime n (a jump table of immediates); n >= 63 waits to 62
 DV_DEVICE void wait_vm_dyn(int n) {
-  switch (n >> 2) {
+  switch (n) {
     case 0: wait_vm<0>(); break;
-    case 1: wait_vm<4>(); break;
-    case 2: wait_vm<8>(); break;
-    case 3: wait_vm<12>(); break;
-    case 4: wait_vm<16>(); break;
-    case 5: wait_vm<20>(); break;
-    case 6: wait_vm<24>(); break;
-    case 7: wait_vm<28>(); break;
-    case 8: wait_vm<32>(); break;
-    case 9: wait_vm<36>(); break;
-    case 10: wait_vm<40>(); break;
-    case 11: wait_vm<44>(); break;
-    case 12: wait_vm<48>(); break;
-    case 13: wait_vm<52>(); break;
-    case 14: wait_vm<56>(); break;
-    default: wait_vm<60>(); break;
+    case 1: wait_vm<1>(); break;
+    case 2: wait_vm<2>(); break;
+    case 3: wait_vm<3>(); break;
+    case 4: wait_vm<4>(); break;
+    case 5: wait_vm<5>(); break;
+    case 6: wait_vm<6>(); break;
+    case 7: wait_vm<7>(); break;
+    case 8: wait_vm<8>(); break;
+    case 9: wait_vm<9>(); break;
+    case 10: wait_vm<10>(); break;
+    case 11: wait_vm<11>(); break;
+    case 12: wait_vm<12>(); break;
+    case 13: wait_vm<13>(); break;
+    case 14: wait_vm<14>(); break;
+    case 15: wait_vm<15>(); break;
+    case 16: wait_vm<16>(); break;
+    case 17: wait_vm<17>(); break;
+    case 18: wait_vm<18>(); break;
+    case 19: wait_vm<19>(); break;
+    case 20: wait_vm<20>(); break;
+    case 21: wait_vm<21>(); break;
+    case 22: wait_vm<22>(); break;
+    case 23: wait_vm<23>(); break;
+    case 24: wait_vm<24>(); break;
+    case 25: wait_vm<25>(); break;
+    case 26: wait_vm<26>(); break;
+    case 27: wait_vm<27>(); break;
+    case 28: wait_vm<28>(); break;
+    case 29: wait_vm<29>(); break;
+    case 30: wait_vm<30>(); break;
+    case 31: wait_vm<31>(); break;
+    case 32: wait_vm<32>(); break;
+    case 33: wait_vm<33>(); break;
+    case 34: wait_vm<34>(); break;
+    case 35: wait_vm<35>(); break;
+    case 36: wait_vm<36>(); break;
+    case 37: wait_vm<37>(); break;
+    case 38: wait_vm<38>(); break;
+    case 39: wait_vm<39>(); break;
+    case 40: wait_vm<40>(); break;
+    case 41: wait_vm<41>(); break;
+    case 42: wait_vm<42>(); break;
+    case 43: wait_vm<43>(); break;
+    case 44: wait_vm<44>(); break;
+    case 45: wait_vm<45>(); break;
+    case 46: wait_vm<46>(); break;
+    case 47: wait_vm<47>(); break;
+    case 48: wait_vm<48>(); break;
+    case 49: wait_vm<49>(); break;
+    case 50: wait_vm<50>(); break;
+    case 51: wait_vm<51>(); break;
+    case 52: wait_vm<52>(); break;
+    case 53: wait_vm<53>(); break;
+    case 54: wait_vm<54>(); break;
+    case 55: wait_vm<55>(); break;
+    case 56: wait_vm<56>(); break;
+    case 57: wait_vm<57>(); break;
+    case 58: wait_vm<58>(); break;
+    case 59: wait_vm<59>(); break;
+    case 60: wait_vm<60>(); break;
+    case 61: wait_vm<61>(); break;
+    case 62: wait_vm<62>(); break;
+    default: wait_vm<62>(); break;
   }
 }
 
 enum { SE_STATS = 0, SE_FULL = 1 };
 
 // ---------------------------------------------------------------- forward
-// FULLQ: Q % 16 == 0 (every 16-pixel fragment lies inside its output row: no lane masking)
-template <int EPI, bool FULLQ>
+// Stride-2 stems (ResNet / Inception / Hourglass). A group of RG output rows reads a window of
+// FWIN = 2*(RG-1) + 7 input rows; each group's window is loaded whole into one of NWB buffers
+// (two groups ahead of the compute) at a compile-time row pitch ROWB, so a fragment's 7
+// filter-row reads are one VGPR base + immediate offsets. FULLQ: Q % 16 == 0 (no lane masking).
+constexpr int FWIN = 2 * (RG - 1) + SR;
+constexpr int NWB = 3;
+template <int EPI, bool FULLQ, int ROWB>
 __global__ __launch_bounds__(256, 2) void stem_fwd_kernel(StemParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int SW = 2, FSTRIDE = 128 * SW, WBYTES = FWIN * ROWB;
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int img = blockIdx.x / p.chunks, chunk = blockIdx.x - img * p.chunks;
   const int p0 = chunk * p.rpb, p1 = min(p.P, p0 + p.rpb);
-  const uint32_t ring = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem));
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem));
   const char* xim = reinterpret_cast<const char*>(p.x) + (int64_t)img * p.Hp * p.rowbytes;
+  const void* zpage = dv_zero_page;
 
   // weights as A-fragments: lane holds W[n = 16j + (lane&15)][k = 32r + 8(lane>>4) .. +7]
   bf16x8 wf[4][SR];
@@ -146,38 +199,56 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_kernel(StemParams p) {
       s1[j][e] = 0.f; s2[j][e] = 0.f;
     }
 
-  const int win = p.sh * (RG - 1) + SR;  // input rows of one group's window
+  // window of the group starting at output row pg -> buffer gi % NWB (piece t to wave t % 4)
+  auto load_win = [&](int pg, int gi) {
+    const uint32_t base = lds0 + (uint32_t)((gi % NWB) * WBYTES);
+    int t = 0, n = 0;
+    for (int rr = 0; rr < FWIN; ++rr) {
+      const int row = 2 * pg + rr;
+      for (int pc = 0; pc < p.ipr; ++pc, ++t) {
+        if ((t & 3) != wid) continue;
+        const int off = pc * 1024 + lane * 16;
+        const bool ok = row < p.Hp && off < p.rowbytes;
+        glds16(ok ? (const void*)(xim + (int64_t)row * p.rowbytes + off) : zpage, base + rr * ROWB + pc * 1024);
+        ++n;
+      }
+    }
+    return n;
+  };
+
   const int QF = (p.Q + 15) >> 4;
-  // lane-constant parts of the addresses: pixel (lane&15) of a fragment, chunk 2*(lane>>4) of its
-  // filter-row slice; output channel group 4*(lane>>4) of pixel (lane&15)
-  const int colb0 = 8 * p.sw * (lane & 15) + 16 * (lane >> 4);
-  const int fstride = 128 * p.sw;         // LDS bytes between consecutive 16-pixel fragments
-  const int yoff = (lane & 15) * OC + 4 * (lane >> 4);
-  // pipeline: the rows of group g+2 are issued while group g computes; before group g every
-  // vector-memory op this wave issued in the previous iteration (group g+1's rows, group g-1's
-  // output stores) may stay in flight -- the counted vmcnt retires exactly group g's rows
-  load_rows<NR_F, 4>(p, xim, ring, p.sh * p0, win, wid, lane);
-  if (p0 + RG < p1) load_rows<NR_F, 4>(p, xim, ring, p.sh * p0 + win, p.sh * RG, wid, lane);
+  const int colb0 = 8 * SW * (lane & 15) + 16 * (lane >> 4);  // pixel (lane&15), chunk 2*(lane>>4)
+  const int yoff = (lane & 15) * OC + 4 * (lane >> 4);       // channel group 4*(lane>>4) of that pixel
+  // pipeline: group g+2's window is issued while group g computes; before group g every
+  // vector-memory op this wave issued in the previous iteration (group g+1's window, group g-1's
+  // output stores) may stay in flight -- the exact counted vmcnt retires group g's window
+  load_win(p0, 0);
+  if (p0 + RG < p1) load_win(p0 + RG, 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   int pend = 0;
-  for (int pg = p0; pg < p1; pg += RG) {
+  for (int pg = p0, gi = 0; pg < p1; pg += RG, ++gi) {
     wait_vm_dyn(pend);
     __syncthreads();
     pend = 0;
-    if (pg + 2 * RG < p1) pend = load_rows<NR_F, 4>(p, xim, ring, p.sh * (pg + RG) + win, p.sh * RG, wid, lane);
+    if (pg + 2 * RG < p1) pend = load_win(pg + 2 * RG, gi + 2);
     const int nf = min(RG, p1 - pg) * QF;
     const int myf = wid < nf ? (nf - wid + 3) / 4 : 0;  // fragments wid, wid+4, ...
     pend += 4 * myf;                                    // 4 output stores per fragment
+    const char* win = smem + (gi % NWB) * WBYTES + colb0;
     int pl = 0, qf = wid;
     while (qf >= QF) { qf -= QF; ++pl; }
-    for (int i = 0; i < myf; ++i) {
-      const unsigned rb = (unsigned)(p.sh * (pg + pl));
-      int colb = colb0 + qf * fstride;
-      if constexpr (!FULLQ) colb = min(colb, colb0 - 8 * p.sw * (lane & 15) + 8 * p.sw * (p.Q - 1));
-      bf16x8 xf[SR];
+    // the 7 filter-row operands of fragment (pl, qf)
+    auto rd = [&](int pl_, int qf_, bf16x8* xf) {
+      int cb = 2 * pl_ * ROWB + qf_ * FSTRIDE;
+      if constexpr (!FULLQ) cb = min(cb, 2 * pl_ * ROWB + 8 * SW * (p.Q - 1 - (lane & 15)));
+      const char* xr = win + cb;
 #pragma unroll
-      for (int r = 0; r < SR; ++r)
-        xf[r] = *reinterpret_cast<const bf16x8*>(smem + ((rb + r) % NR_F) * p.rowb + colb);
+      for (int r = 0; r < SR; ++r) xf[r] = *reinterpret_cast<const bf16x8*>(xr + r * ROWB);
+    };
+    // software-pipelined: the next fragment's LDS reads are issued before this one's epilogue
+    bf16x8 xf[SR];
+    if (myf > 0) rd(pl, qf, xf);
+    for (int i = 0; i < myf; ++i) {
       f32x4 acc[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -186,9 +257,13 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_kernel(StemParams p) {
       for (int r = 1; r < SR; ++r)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][r], xf[r], acc[j], 0, 0, 0);
+      const int cpl = pl, cqf = qf;
+      qf += 4;
+      while (qf >= QF) { qf -= QF; ++pl; }
+      if (i + 1 < myf) rd(pl, qf, xf);
       // D[n][q]: lane holds channels 16j + 4(lane>>4) + e of pixel q
-      const bool valid = FULLQ || qf * 16 + (lane & 15) < p.Q;
-      u16* dst = p.y + (((int64_t)img * p.P + pg + pl) * p.Q + qf * 16) * OC + yoff;
+      const bool valid = FULLQ || cqf * 16 + (lane & 15) < p.Q;
+      u16* dst = p.y + (((int64_t)img * p.P + pg + cpl) * p.Q + cqf * 16) * OC + yoff;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float v[4];
@@ -207,8 +282,6 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_kernel(StemParams p) {
         uint2 pk; pk.x = pack2bf(v[0], v[1]); pk.y = pack2bf(v[2], v[3]);
         if (valid) *reinterpret_cast<uint2*>(dst + 16 * j) = pk;
       }
-      qf += 4;
-      while (qf >= QF) { qf -= QF; ++pl; }
     }
   }
   if (!st) return;
@@ -398,14 +471,15 @@ bool stem_setup(StemParams& p, int N, int Hp, int Wp, int P, int Q, int sh, int 
   return true;
 }
 
-template <int EPI, bool FULLQ>
-void launch_fwd(const StemParams& p, dim3 grid, size_t lds, hipStream_t st) {
+template <int EPI, bool FULLQ, int ROWB>
+void launch_fwd(const StemParams& p, dim3 grid, hipStream_t st) {
+  constexpr int lds = NWB * FWIN * ROWB;  // 78 KB at ROWB 2048: two blocks per CU
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)stem_fwd_kernel<EPI, FULLQ>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    (void)hipFuncSetAttribute((const void*)stem_fwd_kernel<EPI, FULLQ, ROWB>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  stem_fwd_kernel<EPI, FULLQ><<<grid, 256, lds, st>>>(p);
+  stem_fwd_kernel<EPI, FULLQ, ROWB><<<grid, 256, lds, st>>>(p);
 }
 
 template <bool FULLQ>
@@ -427,23 +501,22 @@ void dv_stem_tuning(int blocks, int wg_blocks) {
 
 int dv_stem_fwd(const void* xp, const void* w, void* y, const float* bias, float* stats, int act, float slope, int N,
                 int Hp, int Wp, int P, int Q, int R, int Sp, int K, int sh, int sw, hipStream_t st) {
-  if (R != SR || Sp != 8 || K != OC) return -1;
+  if (R != SR || Sp != 8 || K != OC || sh != 2 || sw != 2) return -1;
   StemParams p{};
   if (!stem_setup(p, N, Hp, Wp, P, Q, sh, sw, g_stem_blocks)) return -1;
+  if (p.rowbytes > 3072) return -1;
   p.rpb = (p.rpb + RG - 1) / RG * RG;  // whole groups
   p.chunks = (P + p.rpb - 1) / p.rpb;
   p.x = (const u16*)xp; p.w = (const u16*)w; p.y = (u16*)y; p.bias = bias; p.stats = stats;
   p.act = act; p.slope = slope;
-  const size_t lds = (size_t)NR_F * p.rowb;
-  if (lds > 150 * 1024) return -1;
-  const bool full = bias || act;
+  const bool full = bias || act, fq = Q % 16 == 0;
   const dim3 grid(N * p.chunks);
-  if (full) {
-    if (Q % 16 == 0) launch_fwd<SE_FULL, true>(p, grid, lds, st);
-    else launch_fwd<SE_FULL, false>(p, grid, lds, st);
+  if (p.rowbytes <= 2048) {
+    if (full) { if (fq) launch_fwd<SE_FULL, true, 2048>(p, grid, st); else launch_fwd<SE_FULL, false, 2048>(p, grid, st); }
+    else { if (fq) launch_fwd<SE_STATS, true, 2048>(p, grid, st); else launch_fwd<SE_STATS, false, 2048>(p, grid, st); }
   } else {
-    if (Q % 16 == 0) launch_fwd<SE_STATS, true>(p, grid, lds, st);
-    else launch_fwd<SE_STATS, false>(p, grid, lds, st);
+    if (full) { if (fq) launch_fwd<SE_FULL, true, 3072>(p, grid, st); else launch_fwd<SE_FULL, false, 3072>(p, grid, st); }
+    else { if (fq) launch_fwd<SE_STATS, true, 3072>(p, grid, st); else launch_fwd<SE_STATS, false, 3072>(p, grid, st); }
   }
   return 0;
 }
@@ -455,7 +528,8 @@ int dv_stem_wgrad(const void* xp, const void* dy, int ldy, float* dw, int N, int
   if (!stem_setup(p, N, Hp, Wp, P, Q, sh, sw, g_stem_wg_blocks)) return -1;
   p.x = (const u16*)xp; p.dy = (const u16*)dy;
   const int QS = (Q + 15) / 16;
-  const size_t lds = (size_t)NR_W * p.rowb + NDY * (size_t)QS * 16 * 128;
+  // staging (input ring + dY buffers), at least the end-of-kernel parity reduction [4][2][2][16][64] f32
+  const size_t lds = std::max((size_t)NR_W * p.rowb + NDY * (size_t)QS * 16 * 128, (size_t)4 * 2 * 2 * 16 * 64 * 4);
   if (lds > 150 * 1024) return -1;
   const int nblk = N * p.chunks;
   const size_t slab_elems = (size_t)nblk * OC * SR * 32;
