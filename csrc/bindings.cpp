@@ -254,11 +254,16 @@ PYBIND11_MODULE(_C, m) {
     check_last("dw_fwd");
   });
   m.def("dw_dgrad", [](uptr dy, uptr w, uptr dx, int N, int H, int W, int C, int ldx, int P_, int Q, int ldy, int K, int sh,
-                       int sw, int ph, int pw, uptr st) {
-    if (dv_dw_dgrad(CP(dy), CFP(w), P(dx), N, H, W, C, ldx, P_, Q, ldy, K, sh, sw, ph, pw, ST(st)))
+                       int sw, int ph, int pw, uptr st, uptr bnx, uptr bnprm, uptr bnacc, int bnmode, int bnact,
+                       float bnslope) {
+    if (dv_dw_dgrad(CP(dy), CFP(w), P(dx), N, H, W, C, ldx, P_, Q, ldy, K, sh, sw, ph, pw, ST(st), CP(bnx), CFP(bnprm),
+                    FP(bnacc), bnmode, bnact, bnslope))
       throw std::runtime_error("dw_dgrad: unsupported shape");
     check_last("dw_dgrad");
-  });
+  }, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("ldx"),
+     py::arg("P"), py::arg("Q"), py::arg("ldy"), py::arg("K"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
+     py::arg("st"), py::arg("bnx") = 0, py::arg("bnprm") = 0, py::arg("bnacc") = 0, py::arg("bnmode") = 0,
+     py::arg("bnact") = 0, py::arg("bnslope") = 0.f);
   m.def("dw_wgrad", [](uptr x, uptr dy, uptr dw, int N, int H, int W, int C, int ldx, int P_, int Q, int ldy, int K, int sh,
                        int sw, int ph, int pw, int accumulate, uptr st) {
     if (dv_dw_wgrad(CP(x), CP(dy), FP(dw), N, H, W, C, ldx, P_, Q, ldy, K, sh, sw, ph, pw, accumulate, ST(st)))

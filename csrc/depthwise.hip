@@ -37,7 +37,89 @@ DV_DEVICE void st8(u16* p, const float* v) {
 
 struct DwGeo {
   int N, H, W, C, ldx, P, Q, ldy, sh, sw, ph, pw;
+  FastDiv fd_strips, fd_rows;  // strip decode: strip -> (row index, strip in row) -> (image, row)
 };
+
+// Packed-fp32 forms (v_pk_fma_f32 / v_pk_add_f32: two channels per VALU instruction; the strip
+// kernels are VALU-issue-bound -- 1,760 VALU per wave for 128 outputs on the 112x112x32 forward
+// before, profiles/pmc_dw_*): a 16-B bf16 vector unpacks to 4 channel pairs
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+DV_DEVICE void ld8p(const u16* p, f32x2* v) {
+  const uint4 r = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = f32x2{__uint_as_float(w[i] << 16), __uint_as_float(w[i] & 0xffff0000u)};
+}
+DV_DEVICE void st8p(u16* p, const f32x2* v) {
+  uint4 r; r.x = pack2bf(v[0].x, v[0].y); r.y = pack2bf(v[1].x, v[1].y); r.z = pack2bf(v[2].x, v[2].y); r.w = pack2bf(v[3].x, v[3].y);
+  *reinterpret_cast<uint4*>(p) = r;
+}
+DV_DEVICE f32x2 pfma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// Fused BatchNorm-backward reduction in a depthwise dgrad epilogue (the dgrad output is the
+// incoming gradient of the BatchNorm that feeds this depthwise conv, MobileNet's pw -> BN -> ReLU
+// -> dw): sum dz and sum dz*(x - mean) of the STORED bf16 gradient, dz = act'(x*scale + shift)*d
+// (mode 2) or d (mode 1) -- what csrc/bn.hip bn_bwd_reduce would read back -- into the BN's
+// [SHARDS][2][C] accumulator (the invstd factor is applied once per channel at the end).
+struct DwBnr {
+  const u16* x;       // BN input, dense NHWC like dx
+  const float* prm;   // [4][C]: scale, shift, mean, invstd
+  float* acc;         // [SHARDS][2][C]
+  int mode, act;      // mode 1: no activation, 2: mask recomputed from x
+  float slope;
+};
+struct DwBnrLane {  // this thread's 8 channels
+  f32x2 ms[4], mh[4], mu[4], s[4], q[4];
+  DV_DEVICE void init(const DwBnr& b, int C, int c0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = c0 + 2 * k;
+      ms[k] = f32x2{b.prm[c], b.prm[c + 1]};
+      mh[k] = f32x2{b.prm[C + c], b.prm[C + c + 1]};
+      mu[k] = f32x2{b.prm[2 * C + c], b.prm[2 * C + c + 1]};
+      s[k] = f32x2{0.f, 0.f}; q[k] = f32x2{0.f, 0.f};
+    }
+  }
+  // v: the 8 fp32 gradient values about to be stored; xr: the BN input at the same element
+  // offset, loaded when the strip started (a load issued here would stall every strip on a
+  // full memory round trip)
+  DV_DEVICE void add(const DwBnr& b, const f32x2* v, const uint4& xr) {
+    f32x2 xv[4];
+    const uint32_t w[4] = {xr.x, xr.y, xr.z, xr.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xv[i] = f32x2{__uint_as_float(w[i] << 16), __uint_as_float(w[i] & 0xffff0000u)};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f32x2 d{bf2f(f2bf(v[k].x)), bf2f(f2bf(v[k].y))};  // the bf16 value the store writes
+      if (b.mode == 2) {
+        const f32x2 z = pfma(xv[k], ms[k], mh[k]);
+        const f32x2 neg = b.act == 2 ? d * b.slope : f32x2{0.f, 0.f};
+        d.x = z.x > 0.f ? d.x : neg.x;
+        d.y = z.y > 0.f ? d.y : neg.y;
+      }
+      s[k] += d;
+      q[k] = pfma(d, xv[k] - mu[k], q[k]);
+    }
+  }
+};
+// block-wide: [NT][8] lanes -> per-channel sums of the slab -> one coalesced atomic row per block
+DV_DEVICE void bnr_commit(const DwBnr& b, const DwBnrLane& l, int C, int tpr, int rpi, float* sh0, float* sh1) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    sh0[threadIdx.x * 8 + 2 * k] = l.s[k].x; sh0[threadIdx.x * 8 + 2 * k + 1] = l.s[k].y;
+    sh1[threadIdx.x * 8 + 2 * k] = l.q[k].x; sh1[threadIdx.x * 8 + 2 * k + 1] = l.q[k].y;
+  }
+  __syncthreads();
+  const int sw = tpr * 8;
+  float* a = b.acc + (int64_t)(blockIdx.x % DV_STAT_SHARDS) * 2 * C;
+  const int cbase = (int)blockIdx.y * SLAB * 8;
+  for (int ch = threadIdx.x; ch < sw; ch += NT) {
+    float s1v = 0.f, s2v = 0.f;
+    for (int rr = 0; rr < rpi; ++rr) { s1v += sh0[rr * sw + ch]; s2v += sh1[rr * sw + ch]; }
+    atomicAdd(a + cbase + ch, s1v);
+    atomicAdd(a + C + cbase + ch, s2v * b.prm[3 * C + cbase + ch]);  // sum dz*(x-mean) * invstd
+  }
+}
 
 // thread -> (channel group, strip lane) inside the block's slab
 struct DwTile {
@@ -56,39 +138,56 @@ struct DwTile {
 // ---------------------------------------------------------------- forward (and stride-1 dgrad)
 // FLIP: correlate with the spatially flipped filter (dgrad of a stride-1 conv); then the caller
 // passes the flipped padding KS-1-p and the output grid is the input grid.
-template <int KS, int SW, int QT, bool FLIP, int OCC = 1>
+template <int KS, int SW, int QT, bool FLIP, int OCC = 1, bool BNR = false>
 __global__ __launch_bounds__(NT, OCC) void dw_fwd_kernel(const u16* __restrict__ x, const float* __restrict__ w,
                                                       const float* __restrict__ bias, u16* __restrict__ y, DwGeo g,
                                                       int act, float slope, float* __restrict__ stats,
-                                                      int64_t strips_per_block) {
+                                                      int strips_per_block, DwBnr bnr) {
   __shared__ float sh[2][NT * 8];
   DwTile t(g.C);
+  DwBnrLane bl;
+  if constexpr (BNR) bl.init(bnr, g.C, t.c0);
   constexpr int NCOL = (QT - 1) * SW + KS;
-  float wr[KS * KS][8];
+  f32x2 wr[KS * KS][4];
 #pragma unroll
   for (int tp = 0; tp < KS * KS; ++tp)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) wr[tp][k] = w[(t.c0 + k) * KS * KS + (FLIP ? KS * KS - 1 - tp : tp)];
-  float bv[8], ssum[8], ssq[8], kq[8];
+    for (int k = 0; k < 4; ++k) {
+      const int wt = FLIP ? KS * KS - 1 - tp : tp;
+      wr[tp][k] = f32x2{w[(t.c0 + 2 * k) * KS * KS + wt], w[(t.c0 + 2 * k + 1) * KS * KS + wt]};
+    }
+  f32x2 bv[4], ssum[4], ssq[4], nkq[4];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    bv[k] = bias ? bias[t.c0 + k] : 0.f; ssum[k] = 0.f; ssq[k] = 0.f;
-    kq[k] = stats ? stat_shift(stats, g.C)[t.c0 + k] : 0.f;  // shifted statistics (bn.hip)
+  for (int k = 0; k < 4; ++k) {
+    bv[k] = bias ? f32x2{bias[t.c0 + 2 * k], bias[t.c0 + 2 * k + 1]} : f32x2{0.f, 0.f};
+    ssum[k] = f32x2{0.f, 0.f}; ssq[k] = f32x2{0.f, 0.f};
+    // shifted statistics (bn.hip): sums of (v - K)
+    nkq[k] = stats ? -f32x2{stat_shift(stats, g.C)[t.c0 + 2 * k], stat_shift(stats, g.C)[t.c0 + 2 * k + 1]}
+                   : f32x2{0.f, 0.f};
   }
   const int qstrips = (g.Q + QT - 1) / QT;
-  const int64_t nstrips = (int64_t)g.N * g.P * qstrips;
-  const int64_t s0 = (int64_t)blockIdx.x * strips_per_block, s1 = min(nstrips, s0 + strips_per_block);
+  const int nstrips = g.N * g.P * qstrips;
+  const int s0 = blockIdx.x * strips_per_block, s1 = min(nstrips, s0 + strips_per_block);
   if (t.active()) {
-    for (int64_t s = s0 + t.lane_r; s < s1; s += t.rpi) {
-      const int qs = (int)(s % qstrips);
-      const int64_t np = s / qstrips;
-      const int p = (int)(np % g.P), n = (int)(np / g.P);
+    for (int s = s0 + t.lane_r; s < s1; s += t.rpi) {
+      const int np = (int)fdiv((uint32_t)s, g.fd_strips);
+      const int qs = s - np * qstrips;
+      const int n = (int)fdiv((uint32_t)np, g.fd_rows);
+      const int p = np - n * g.P;
       const int q0 = qs * QT;
-      float acc[QT][8];
+      uint4 bx[BNR ? QT : 1];
+      if constexpr (BNR) {
+#pragma unroll
+        for (int i = 0; i < QT; ++i) {
+          const int qq = min(q0 + i, g.Q - 1);
+          bx[i] = *reinterpret_cast<const uint4*>(bnr.x + (((int64_t)n * g.P + p) * g.Q + qq) * g.ldy + t.c0);
+        }
+      }
+      f32x2 acc[QT][4];
 #pragma unroll
       for (int i = 0; i < QT; ++i)
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc[i][k] = bv[k];
+        for (int k = 0; k < 4; ++k) acc[i][k] = bv[k];
       // every load is unconditional: out-of-image taps read the zero page (a branch around a
       // load makes hipcc wait for it on the spot -- one serial HBM round trip per tap)
 #pragma unroll
@@ -101,14 +200,14 @@ __global__ __launch_bounds__(NT, OCC) void dw_fwd_kernel(const u16* __restrict__
         for (int j = 0; j < NCOL; ++j) {
           const int ww = wbase + j;
           const bool ok = hv && ww >= 0 && ww < g.W;
-          float v[8];
-          ld8(ok ? xrow + (int64_t)ww * g.ldx : reinterpret_cast<const u16*>(dv_zero_page), v);
+          f32x2 v[4];
+          ld8p(ok ? xrow + (int64_t)ww * g.ldx : reinterpret_cast<const u16*>(dv_zero_page), v);
 #pragma unroll
           for (int i = 0; i < QT; ++i) {
             const int sx = j - i * SW;  // compile-time
             if (sx >= 0 && sx < KS) {
 #pragma unroll
-              for (int k = 0; k < 8; ++k) acc[i][k] = fmaf(v[k], wr[r * KS + sx][k], acc[i][k]);
+              for (int k = 0; k < 4; ++k) acc[i][k] = pfma(v[k], wr[r * KS + sx][k], acc[i][k]);
             }
           }
         }
@@ -118,21 +217,30 @@ __global__ __launch_bounds__(NT, OCC) void dw_fwd_kernel(const u16* __restrict__
         const int q = q0 + i;
         if (q >= g.Q) continue;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          float v = acc[i][k];
-          if (act == 1) v = fmaxf(v, 0.f);
-          else if (act == 2) v = v > 0.f ? v : v * slope;
+        for (int k = 0; k < 4; ++k) {
+          f32x2 v = acc[i][k];
+          if (act == 1) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); }
+          else if (act == 2) { v.x = v.x > 0.f ? v.x : v.x * slope; v.y = v.y > 0.f ? v.y : v.y * slope; }
           acc[i][k] = v;
-          const float d = v - kq[k];
-          ssum[k] += d; ssq[k] = fmaf(d, d, ssq[k]);
+          const f32x2 d = v + nkq[k];
+          ssum[k] += d; ssq[k] = pfma(d, d, ssq[k]);
         }
-        st8(y + (((int64_t)n * g.P + p) * g.Q + q) * g.ldy + t.c0, acc[i]);
+        const int64_t off = (((int64_t)n * g.P + p) * g.Q + q) * g.ldy + t.c0;
+        st8p(y + off, acc[i]);
+        if constexpr (BNR) bl.add(bnr, acc[i], bx[i]);
       }
     }
   }
+  if constexpr (BNR) {
+    bnr_commit(bnr, bl, g.C, t.tpr, t.rpi, sh[0], sh[1]);
+    return;
+  }
   if (stats) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { sh[0][threadIdx.x * 8 + k] = ssum[k]; sh[1][threadIdx.x * 8 + k] = ssq[k]; }
+    for (int k = 0; k < 4; ++k) {
+      sh[0][threadIdx.x * 8 + 2 * k] = ssum[k].x; sh[0][threadIdx.x * 8 + 2 * k + 1] = ssum[k].y;
+      sh[1][threadIdx.x * 8 + 2 * k] = ssq[k].x; sh[1][threadIdx.x * 8 + 2 * k + 1] = ssq[k].y;
+    }
     __syncthreads();
     const int sw = t.tpr * 8;  // slab width in channels; sh is [strip lane][slab channel]
     float* a = stats + (int64_t)(blockIdx.x % DV_STAT_SHARDS) * 2 * g.C;
@@ -155,52 +263,65 @@ __global__ __launch_bounds__(NT, OCC) void dw_fwd_kernel(const u16* __restrict__
 // even; relative to qb = floor((B - (KS-1)) / 2) that column is
 //   j = ((PAR + i - s) >> 1) - ((PAR - KS + 1) >> 1)      (compile-time for a fixed PAR)
 template <int KS, int QT, int PAR>
-DV_DEVICE void dgrad2_row(const u16* __restrict__ dyrow, bool rv, int w0, const DwGeo& g, const float (*wr)[8],
-                          int r, float (*acc)[8]) {
+DV_DEVICE void dgrad2_row(const u16* __restrict__ dyrow, bool rv, int w0, const DwGeo& g, const f32x2 (*wr)[4],
+                          int r, f32x2 (*acc)[4]) {
   const int qb = (w0 + g.pw - (KS - 1)) >> 1;  // arithmetic shift: floor for negatives too
   constexpr int J0 = (PAR - KS + 1) >> 1;
   constexpr int NQ = ((PAR + QT - 1) >> 1) - J0 + 1;
 #pragma unroll
   for (int j = 0; j < NQ; ++j) {
     const int q = qb + j;
-    float v[8];
-    ld8(rv && q >= 0 && q < g.Q ? dyrow + (int64_t)q * g.ldy : reinterpret_cast<const u16*>(dv_zero_page), v);
+    f32x2 v[4];
+    ld8p(rv && q >= 0 && q < g.Q ? dyrow + (int64_t)q * g.ldy : reinterpret_cast<const u16*>(dv_zero_page), v);
 #pragma unroll
     for (int i = 0; i < QT; ++i)
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         if (((PAR + i - s) & 1) == 0 && ((PAR + i - s) >> 1) - J0 == j) {
 #pragma unroll
-          for (int k = 0; k < 8; ++k) acc[i][k] = fmaf(v[k], wr[r * KS + s][k], acc[i][k]);
+          for (int k = 0; k < 4; ++k) acc[i][k] = pfma(v[k], wr[r * KS + s][k], acc[i][k]);
         }
       }
   }
 }
 
-template <int KS, int QT, int OCC = 1>
+template <int KS, int QT, int OCC = 1, bool BNR = false>
 __global__ __launch_bounds__(NT, OCC) void dw_dgrad2_kernel(const u16* __restrict__ dy, const float* __restrict__ w,
-                                                         u16* __restrict__ dx, DwGeo g, int64_t strips_per_block) {
+                                                         u16* __restrict__ dx, DwGeo g, int strips_per_block, DwBnr bnr) {
+  __shared__ float sh[BNR ? 2 : 1][BNR ? NT * 8 : 1];
   DwTile t(g.C);
-  if (!t.active()) return;
-  float wr[KS * KS][8];
+  DwBnrLane bl;
+  if constexpr (BNR) bl.init(bnr, g.C, t.c0);
+  if (!t.active()) {
+    if constexpr (BNR) bnr_commit(bnr, bl, g.C, t.tpr, t.rpi, sh[0], sh[1]);  // zero partials, joins the barrier
+    return;
+  }
+  f32x2 wr[KS * KS][4];
 #pragma unroll
   for (int tp = 0; tp < KS * KS; ++tp)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) wr[tp][k] = w[(t.c0 + k) * KS * KS + tp];
+    for (int k = 0; k < 4; ++k) wr[tp][k] = f32x2{w[(t.c0 + 2 * k) * KS * KS + tp], w[(t.c0 + 2 * k + 1) * KS * KS + tp]};
   const int wstrips = (g.W + QT - 1) / QT;
-  const int64_t nstrips = (int64_t)g.N * g.H * wstrips;
-  const int64_t s0 = (int64_t)blockIdx.x * strips_per_block, s1 = min(nstrips, s0 + strips_per_block);
+  const int nstrips = g.N * g.H * wstrips;
+  const int s0 = blockIdx.x * strips_per_block, s1 = min(nstrips, s0 + strips_per_block);
   const int par = g.pw & 1;  // parity of w0 + pw (w0 is a multiple of the even QT)
-  for (int64_t s = s0 + t.lane_r; s < s1; s += t.rpi) {
-    const int ws = (int)(s % wstrips);
-    const int64_t nh = s / wstrips;
-    const int h = (int)(nh % g.H), n = (int)(nh / g.H);
+  for (int s = s0 + t.lane_r; s < s1; s += t.rpi) {
+    const int nh = (int)fdiv((uint32_t)s, g.fd_strips);
+    const int ws = s - nh * wstrips;
+    const int n = (int)fdiv((uint32_t)nh, g.fd_rows);
+    const int h = nh - n * g.H;
     const int w0 = ws * QT;
-    float acc[QT][8];
+    uint4 bx[BNR ? QT : 1];
+    if constexpr (BNR) {
+#pragma unroll
+      for (int i = 0; i < QT; ++i)
+        bx[i] = *reinterpret_cast<const uint4*>(bnr.x + (((int64_t)n * g.H + h) * g.W + min(w0 + i, g.W - 1)) * g.ldx + t.c0);
+    }
+    f32x2 acc[QT][4];
 #pragma unroll
     for (int i = 0; i < QT; ++i)
 #pragma unroll
-      for (int k = 0; k < 8; ++k) acc[i][k] = 0.f;
+      for (int k = 0; k < 4; ++k) acc[i][k] = f32x2{0.f, 0.f};
 #pragma unroll
     for (int r = 0; r < KS; ++r) {
       const int hn = h + g.ph - r;
@@ -212,39 +333,45 @@ __global__ __launch_bounds__(NT, OCC) void dw_dgrad2_kernel(const u16* __restric
     }
 #pragma unroll
     for (int i = 0; i < QT; ++i)
-      if (w0 + i < g.W) st8(dx + (((int64_t)n * g.H + h) * g.W + w0 + i) * g.ldx + t.c0, acc[i]);
+      if (w0 + i < g.W) {
+        const int64_t off = (((int64_t)n * g.H + h) * g.W + w0 + i) * g.ldx + t.c0;
+        st8p(dx + off, acc[i]);
+        if constexpr (BNR) bl.add(bnr, acc[i], bx[i]);
+      }
   }
+  if constexpr (BNR) bnr_commit(bnr, bl, g.C, t.tpr, t.rpi, sh[0], sh[1]);
 }
 
 // ---------------------------------------------------------------- wgrad
 // dw[c][r][s] += sum_{n,p,q} dy[n][p][q][c] * x[n][p*sh-ph+r][q*SW-pw+s][c]
 template <int KS, int SW, int QT, int OCC = 1>
 __global__ __launch_bounds__(NT, OCC) void dw_wgrad_kernel(const u16* __restrict__ x, const u16* __restrict__ dy,
-                                                        float* __restrict__ dw, DwGeo g, int64_t strips_per_block,
+                                                        float* __restrict__ dw, DwGeo g, int strips_per_block,
                                                         float* __restrict__ slabs) {
   __shared__ float sh[NT * 8];
   __shared__ float red[SLAB * 8 * KS * KS];
   DwTile t(g.C);
   constexpr int NCOL = (QT - 1) * SW + KS;
-  float acc[KS * KS][8];
+  f32x2 acc2[KS * KS][4];
 #pragma unroll
   for (int tp = 0; tp < KS * KS; ++tp)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) acc[tp][k] = 0.f;
+    for (int k = 0; k < 4; ++k) acc2[tp][k] = f32x2{0.f, 0.f};
   const int qstrips = (g.Q + QT - 1) / QT;
-  const int64_t nstrips = (int64_t)g.N * g.P * qstrips;
-  const int64_t s0 = (int64_t)blockIdx.x * strips_per_block, s1 = min(nstrips, s0 + strips_per_block);
+  const int nstrips = g.N * g.P * qstrips;
+  const int s0 = blockIdx.x * strips_per_block, s1 = min(nstrips, s0 + strips_per_block);
   if (t.active()) {
-    for (int64_t s = s0 + t.lane_r; s < s1; s += t.rpi) {
-      const int qs = (int)(s % qstrips);
-      const int64_t np = s / qstrips;
-      const int p = (int)(np % g.P), n = (int)(np / g.P);
+    for (int s = s0 + t.lane_r; s < s1; s += t.rpi) {
+      const int np = (int)fdiv((uint32_t)s, g.fd_strips);
+      const int qs = s - np * qstrips;
+      const int n = (int)fdiv((uint32_t)np, g.fd_rows);
+      const int p = np - n * g.P;
       const int q0 = qs * QT;
-      float d[QT][8];
+      f32x2 d[QT][4];
 #pragma unroll
       for (int i = 0; i < QT; ++i)
-        ld8(q0 + i < g.Q ? dy + (((int64_t)n * g.P + p) * g.Q + q0 + i) * g.ldy + t.c0
-                         : reinterpret_cast<const u16*>(dv_zero_page), d[i]);
+        ld8p(q0 + i < g.Q ? dy + (((int64_t)n * g.P + p) * g.Q + q0 + i) * g.ldy + t.c0
+                          : reinterpret_cast<const u16*>(dv_zero_page), d[i]);
 #pragma unroll
       for (int r = 0; r < KS; ++r) {
         const int h = p * g.sh - g.ph + r;
@@ -255,20 +382,25 @@ __global__ __launch_bounds__(NT, OCC) void dw_wgrad_kernel(const u16* __restrict
         for (int j = 0; j < NCOL; ++j) {
           const int ww = wbase + j;
           const bool ok = hv && ww >= 0 && ww < g.W;
-          float v[8];
-          ld8(ok ? xrow + (int64_t)ww * g.ldx : reinterpret_cast<const u16*>(dv_zero_page), v);
+          f32x2 v[4];
+          ld8p(ok ? xrow + (int64_t)ww * g.ldx : reinterpret_cast<const u16*>(dv_zero_page), v);
 #pragma unroll
           for (int i = 0; i < QT; ++i) {
             const int sx = j - i * SW;
             if (sx >= 0 && sx < KS) {
 #pragma unroll
-              for (int k = 0; k < 8; ++k) acc[r * KS + sx][k] = fmaf(d[i][k], v[k], acc[r * KS + sx][k]);
+              for (int k = 0; k < 4; ++k) acc2[r * KS + sx][k] = pfma(d[i][k], v[k], acc2[r * KS + sx][k]);
             }
           }
         }
       }
     }
   }
+  float acc[KS * KS][8];
+#pragma unroll
+  for (int tp = 0; tp < KS * KS; ++tp)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { acc[tp][2 * k] = acc2[tp][k].x; acc[tp][2 * k + 1] = acc2[tp][k].y; }
   // per tap: strip lanes -> LDS -> per-channel sums into red[channel][tap]
   const int sw = t.tpr * 8;
 #pragma unroll
@@ -498,6 +630,12 @@ int64_t per_block(int64_t nstrips, int rpi, int slabs, int64_t target_blocks) {
   int64_t spb = std::max<int64_t>(rpi, (nstrips * slabs + target_blocks - 1) / target_blocks);
   return (spb + rpi - 1) / rpi * rpi;
 }
+// strip decode divisors of a launch: strips per row (rows = images x rows per image)
+inline DwGeo with_strips(DwGeo g, int strips_per_row, int rows_per_img) {
+  g.fd_strips = make_fastdiv((uint32_t)strips_per_row);
+  g.fd_rows = make_fastdiv((uint32_t)rows_per_img);
+  return g;
+}
 inline int slabs_of(int C) { return (C / 8 + SLAB - 1) / SLAB; }
 inline int rpi_of(int C) {
   const int cgn = C / 8, tpr = cgn < SLAB ? cgn : SLAB;
@@ -509,16 +647,23 @@ int g_dw_variant = 0;
 
 template <int KS, int SW, bool FLIP, int QT, int OCC>
 void fwd_launch(const void* x, const float* w, const float* bias, void* y, const DwGeo& g, int act, float slope,
-                float* stats, int target, hipStream_t st) {
+                float* stats, int target, hipStream_t st, const DwBnr* bnr = nullptr) {
   const int slabs = slabs_of(g.C), rpi = rpi_of(g.C);
   const int64_t nstrips = (int64_t)g.N * g.P * ((g.Q + QT - 1) / QT);
   const int64_t spb = per_block(nstrips, rpi, slabs, target);
   const dim3 grid((unsigned)((nstrips + spb - 1) / spb), (unsigned)slabs);
-  dw_fwd_kernel<KS, SW, QT, FLIP, OCC><<<grid, NT, 0, st>>>((const u16*)x, w, bias, (u16*)y, g, act, slope, stats, spb);
+  const DwGeo gs = with_strips(g, (g.Q + QT - 1) / QT, g.P);
+  if (bnr)
+    dw_fwd_kernel<KS, SW, QT, FLIP, OCC, true><<<grid, NT, 0, st>>>((const u16*)x, w, bias, (u16*)y, gs, act, slope,
+                                                                     stats, (int)spb, *bnr);
+  else
+    dw_fwd_kernel<KS, SW, QT, FLIP, OCC><<<grid, NT, 0, st>>>((const u16*)x, w, bias, (u16*)y, gs, act, slope, stats,
+                                                             (int)spb, DwBnr{});
 }
 template <int KS, int SW, bool FLIP>
 void fwd_variants(const void* x, const float* w, const float* bias, void* y, const DwGeo& g, int act, float slope,
-                  float* stats, hipStream_t st) {
+                  float* stats, hipStream_t st, const DwBnr* bnr = nullptr) {
+  if (bnr) return fwd_launch<KS, SW, FLIP, 4, 1>(x, w, bias, y, g, act, slope, stats, 4096, st, bnr);
   if constexpr (KS == 3) {
     switch (g_dw_variant) {
       case 1: return fwd_launch<KS, SW, FLIP, 4, 4>(x, w, bias, y, g, act, slope, stats, 8192, st);
@@ -545,7 +690,8 @@ void wgrad_launch(const void* x, const void* dy, float* dw, const DwGeo& g, int 
   float* ws = nullptr;
   const int64_t n = (int64_t)g.C * KS * KS;
   if (dv_deterministic()) ws = dv_slab_workspace((size_t)grid.x * n, st);
-  dw_wgrad_kernel<KS, SW, QT, OCC><<<grid, NT, 0, st>>>((const u16*)x, (const u16*)dy, dw, g, spb, ws);
+  dw_wgrad_kernel<KS, SW, QT, OCC><<<grid, NT, 0, st>>>((const u16*)x, (const u16*)dy, dw,
+                                                        with_strips(g, (g.Q + QT - 1) / QT, g.P), (int)spb, ws);
   if (ws) dv_slab_reduce(ws, dw, n, (int)grid.x, 1, st);
 }
 template <int KS, int SW>
@@ -564,15 +710,21 @@ void wgrad_variants(const void* x, const void* dy, float* dw, const DwGeo& g, hi
   wgrad_launch<KS, SW, 4, 1>(x, dy, dw, g, 512, st);
 }
 template <int KS, int QT, int OCC>
-void dgrad2_launch(const void* dy, const float* w, void* dx, const DwGeo& g, int target, hipStream_t st) {
+void dgrad2_launch(const void* dy, const float* w, void* dx, const DwGeo& g, int target, hipStream_t st,
+                   const DwBnr* bnr = nullptr) {
   const int slabs = slabs_of(g.C), rpi = rpi_of(g.C);
   const int64_t nstrips = (int64_t)g.N * g.H * ((g.W + QT - 1) / QT);
   const int64_t spb = per_block(nstrips, rpi, slabs, target);
   const dim3 grid((unsigned)((nstrips + spb - 1) / spb), (unsigned)slabs);
-  dw_dgrad2_kernel<KS, QT, OCC><<<grid, NT, 0, st>>>((const u16*)dy, w, (u16*)dx, g, spb);
+  const DwGeo gs = with_strips(g, (g.W + QT - 1) / QT, g.H);
+  if (bnr)
+    dw_dgrad2_kernel<KS, QT, OCC, true><<<grid, NT, 0, st>>>((const u16*)dy, w, (u16*)dx, gs, (int)spb, *bnr);
+  else
+    dw_dgrad2_kernel<KS, QT, OCC><<<grid, NT, 0, st>>>((const u16*)dy, w, (u16*)dx, gs, (int)spb, DwBnr{});
 }
 template <int KS>
-void dgrad2_variants(const void* dy, const float* w, void* dx, const DwGeo& g, hipStream_t st) {
+void dgrad2_variants(const void* dy, const float* w, void* dx, const DwGeo& g, hipStream_t st, const DwBnr* bnr = nullptr) {
+  if (bnr) return dgrad2_launch<KS, 4, 2>(dy, w, dx, g, 8192, st, bnr);  // 8-pixel strips + BN state: 256 VGPRs
   if constexpr (KS == 3) {
     switch (g_dw_variant) {
       case 1: return dgrad2_launch<KS, 4, 4>(dy, w, dx, g, 8192, st);
@@ -606,7 +758,7 @@ void dv_dw_variant(int v) { g_dw_variant = v; }
 int dv_dw_fwd(const void* x, const float* w, const float* bias, void* y, int N, int H, int W, int C, int ldx, int P,
               int Q, int ldy, int K, int sh, int sw, int ph, int pw, int act, float slope, float* stats, hipStream_t st) {
   if (!dw_shape_ok(C, ldx, ldy) || (sw != 1 && sw != 2)) return -1;
-  DwGeo g{N, H, W, C, ldx, P, Q, ldy, sh, sw, ph, pw};
+  DwGeo g{N, H, W, C, ldx, P, Q, ldy, sh, sw, ph, pw, {}, {}};
   if (sw == 1) {
     DW_KS(K, (fwd_variants<KS, 1, false>(x, w, bias, y, g, act, slope, stats, st)))
   } else {
@@ -616,24 +768,29 @@ int dv_dw_fwd(const void* x, const float* w, const float* bias, void* y, int N, 
 }
 
 int dv_dw_dgrad(const void* dy, const float* w, void* dx, int N, int H, int W, int C, int ldx, int P, int Q, int ldy,
-                int K, int sh, int sw, int ph, int pw, hipStream_t st) {
+                int K, int sh, int sw, int ph, int pw, hipStream_t st, const void* bnx, const float* bnprm, float* bnacc,
+                int bnmode, int bnact, float bnslope) {
   if (!dw_shape_ok(C, ldx, ldy)) return -1;
+  // fused BN-backward reduction: dense dx and BN input (element offsets shared), modes 1 / 2
+  DwBnr b{(const u16*)bnx, bnprm, bnacc, bnmode, bnact, bnslope};
+  const DwBnr* bp = (bnmode == 1 || bnmode == 2) && bnx && bnprm && bnacc && ldx == C ? &b : nullptr;
+  if (bnmode && !bp) return -1;
   if (sh == 1 && sw == 1) {
     // correlation of dY with the flipped filter, padding K-1-p, output grid = input grid
-    DwGeo g{N, P, Q, C, ldy, H, W, ldx, 1, 1, K - 1 - ph, K - 1 - pw};
-    DW_KS(K, (fwd_variants<KS, 1, true>(dy, w, nullptr, dx, g, 0, 0.f, nullptr, st)))
+    DwGeo g{N, P, Q, C, ldy, H, W, ldx, 1, 1, K - 1 - ph, K - 1 - pw, {}, {}};
+    DW_KS(K, (fwd_variants<KS, 1, true>(dy, w, nullptr, dx, g, 0, 0.f, nullptr, st, bp)))
     return 0;
   }
   if (sh != 2 || sw != 2) return -1;
-  DwGeo g{N, H, W, C, ldx, P, Q, ldy, sh, sw, ph, pw};
-  DW_KS(K, (dgrad2_variants<KS>(dy, w, dx, g, st)))
+  DwGeo g{N, H, W, C, ldx, P, Q, ldy, sh, sw, ph, pw, {}, {}};
+  DW_KS(K, (dgrad2_variants<KS>(dy, w, dx, g, st, bp)))
   return 0;
 }
 
 int dv_dw_wgrad(const void* x, const void* dy, float* dw, int N, int H, int W, int C, int ldx, int P, int Q, int ldy,
                 int K, int sh, int sw, int ph, int pw, int accumulate, hipStream_t st) {
   if (!dw_shape_ok(C, ldx, ldy) || (sw != 1 && sw != 2)) return -1;
-  DwGeo g{N, H, W, C, ldx, P, Q, ldy, sh, sw, ph, pw};
+  DwGeo g{N, H, W, C, ldx, P, Q, ldy, sh, sw, ph, pw, {}, {}};
   if (!accumulate) (void)hipMemsetAsync(dw, 0, (size_t)C * K * K * sizeof(float), st);
   if (sw == 1) {
     DW_KS(K, (wgrad_variants<KS, 1>(x, dy, dw, g, st)))

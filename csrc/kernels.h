@@ -177,8 +177,11 @@ void dv_sumsq(const float* x, int64_t n, float* out, hipStream_t st);
 void dv_dw_variant(int v);  // benchmarking override of strip length / occupancy (0 = heuristic)
 int dv_dw_fwd(const void* x, const float* w, const float* bias, void* y, int N, int H, int W, int C, int ldx, int P,
               int Q, int ldy, int K, int sh, int sw, int ph, int pw, int act, float slope, float* stats, hipStream_t st);
+// bnmode 1 / 2: also reduce the BatchNorm-backward sums of dx (dx is that BN's output gradient)
+// into bnacc, as the MFMA dgrad epilogues do (see ConvFwdArgs); -1 when the fusion cannot apply
 int dv_dw_dgrad(const void* dy, const float* w, void* dx, int N, int H, int W, int C, int ldx, int P, int Q, int ldy,
-                int K, int sh, int sw, int ph, int pw, hipStream_t st);
+                int K, int sh, int sw, int ph, int pw, hipStream_t st, const void* bnx = nullptr,
+                const float* bnprm = nullptr, float* bnacc = nullptr, int bnmode = 0, int bnact = 0, float bnslope = 0.f);
 int dv_dw_wgrad(const void* x, const void* dy, float* dw, int N, int H, int W, int C, int ldx, int P, int Q, int ldy,
                 int K, int sh, int sw, int ph, int pw, int accumulate, hipStream_t st);
 

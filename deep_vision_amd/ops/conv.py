@@ -946,6 +946,13 @@ class _DWConvFn(torch.autograd.Function):
         ctx.save_for_backward(x, weight, y if act else None)
         ctx.bias_param = bias  # leaf parameter (not saved): its gradient may sink in place
         ctx.cfg = (stride, padding, act, slope, bias is not None)
+        # x is a BatchNorm output (MobileNet: pw -> BN -> ReLU -> dw): its backward reduction is
+        # folded into this dgrad's epilogue (modes 1 / 2: no mask bits), cf. _ConvFn
+        # (stride 1 only: the stride-2 dgrad writes 4x the pixels it reads, and reading the BN input
+        # there as well cost as much as the separate reduce pass it saved, profiles/dw_bench_r3b.txt)
+        bnref = getattr(x, "_dv_bnref", None)
+        ctx.bnref = (bnref if (bnref is not None and bnref.mode in (1, 2) and ld_of(x) == C and tuple(stride) == (1, 1))
+                     else None)
         ctx.set_materialize_grads(False)
         if want_stats:
             ctx.mark_non_differentiable(stats)
@@ -968,8 +975,15 @@ class _DWConvFn(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = empty_nhwc(N, C, H, W, x.device)
+            br = ctx.bnref
+            bn = {}
+            if br is not None:
+                bn = dict(bnx=ptr(br.x), bnprm=ptr(br.prm), bnacc=ptr(br.acc), bnmode=br.mode, bnact=br.act,
+                          bnslope=float(br.slope))
             lib().dw_dgrad(ptr(dy), ptr(w), ptr(dx), N, H, W, C, ld_of(dx), P, Q, ld_of(dy), K, stride[0], stride[1],
-                           padding[0], padding[1], stream_handle())
+                           padding[0], padding[1], stream_handle(), **bn)
+            if br is not None:
+                br.mark_fused(dx)
         if ctx.needs_input_grad[1]:
             sink = grad_sink(weight)
             buf = sink if sink is not None else torch.empty_like(w)

@@ -150,3 +150,68 @@ def test_depthwise_mobilenet_production_shape(C, HW, s):
     yr.backward(dy)
     assert _rel(x.grad, xr.grad) < 3e-2
     assert _rel(w.grad, wr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("s,act", [(1, "relu"), (2, "relu"), (1, None), (2, "leaky")])
+def test_depthwise_dgrad_fuses_bn_backward(s, act):
+    """pw conv -> BN -> act -> dw conv (MobileNet block): the BN's backward reduction runs in the
+    depthwise dgrad epilogue (csrc/depthwise.hip DwBnr) instead of a bn_bwd_reduce pass. The
+    gradients equal the unfused native chain (same bf16 tensors, tight) and the fp32 torch chain
+    (loose: ReLU masks of bf16 vs fp32 pre-activations differ near zero)."""
+    from deep_vision_amd import nn
+    from deep_vision_amd import ops as F
+    from deep_vision_amd.ops import bn as B
+
+    torch.manual_seed(7 + s)
+    C = 64
+    pw = nn.Conv2d(32, C, 1, bias=False).to(DEV)
+    bn = nn.BatchNorm2d(C).to(DEV)
+    dw = nn.Conv2d(C, C, 3, stride=s, padding=1, groups=C, bias=False).to(DEV)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    x32 = torch.randn(4, 32, 28, 28, device=DEV).bfloat16().float()
+    dy = None
+
+    def run(fuse):
+        nonlocal dy
+        B.FUSE_BWD_STATS = fuse
+        try:
+            for p in (pw.weight, bn.weight, bn.bias, dw.weight):
+                p.grad = None
+            x = _nhwc(x32).requires_grad_(True)
+            n0 = B.COUNTERS["bwd_reduce_fused"]
+            y = dw(F.conv_bn_act(x, pw, bn, act, slope=0.1))
+            if dy is None:
+                dy = torch.randn(y.shape, device=DEV).bfloat16().float()
+            y.backward(_nhwc(dy))
+            return (B.COUNTERS["bwd_reduce_fused"] - n0, y.float(), x.grad.float(), pw.weight.grad.clone(),
+                    bn.weight.grad.clone(), bn.bias.grad.clone(), dw.weight.grad.clone())
+        finally:
+            B.FUSE_BWD_STATS = True
+
+    fused = run(True)
+    plain = run(False)
+    # stride 1 folds the reduction into the dgrad epilogue; stride 2 keeps the reduce pass (and the
+    # fused stride-2 kernel stays exercised through the binding below)
+    assert fused[0] == (1 if s == 1 else 0) and plain[0] == 0, "BN reduction not fused into the depthwise dgrad"
+    for a, b in zip(fused[1:], plain[1:]):
+        assert _rel(a, b) < 2e-3
+    ref = torch.nn.Sequential(torch.nn.Conv2d(32, C, 1, bias=False), torch.nn.BatchNorm2d(C),
+                              torch.nn.ReLU() if act == "relu" else (torch.nn.LeakyReLU(0.1) if act else torch.nn.Identity()),
+                              torch.nn.Conv2d(C, C, 3, stride=s, padding=1, groups=C, bias=False)).to(DEV)
+    with torch.no_grad():
+        ref[0].weight.copy_(pw.weight.bfloat16().float())
+        ref[1].weight.copy_(bn.weight)
+        ref[1].bias.copy_(bn.bias)
+        ref[3].weight.copy_(dw.weight)
+    xr = x32.clone().requires_grad_(True)
+    yr = ref(xr)
+    yr.backward(dy)
+    def nrel(a, b):  # norm-relative: a few flipped ReLU masks move single elements, not the norm
+        return ((a.float() - b.float()).norm() / b.float().norm()).item()
+
+    assert nrel(fused[1], yr) < 2e-2
+    assert nrel(fused[2], xr.grad) < 3e-2
+    assert nrel(fused[4], ref[1].weight.grad) < 3e-2
+    assert nrel(fused[5], ref[1].bias.grad) < 3e-2
