@@ -16,6 +16,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from deep_vision_amd._ext import lib  # noqa: E402
+from deep_vision_amd.ops.bn import STAT_ROWS  # noqa: E402
 from deep_vision_amd.ops.conv import conv_fwd_raw  # noqa: E402
 
 # (Cin, Cout, H, count)
@@ -52,7 +53,7 @@ def main():
         y = torch.empty(M, Cout, device="cuda", dtype=torch.bfloat16)
         dx = torch.empty(M, Cin, device="cuda", dtype=torch.bfloat16)
         wt = w.t().contiguous()
-        stats = torch.zeros(64, 2, Cout, device="cuda")
+        stats = torch.zeros(STAT_ROWS, Cout, device="cuda")  # shard sums + shift row (csrc/kernels.h)
         dw = torch.zeros(Cout, Cin, device="cuda")
 
         def f_nat():
