@@ -136,6 +136,8 @@ def conv_fwd_raw(x, wk, y, bias, stats, N, H, W, Cg, ldx, G, Kout, P, Q, R, S, s
     sh, sw = stride
     ph, pw = padding
     dh, dw = dilation
+    if stats is not None and stats.numel() < STAT_ROWS * G * Kout:  # the kernel reads the shift row
+        raise ValueError(f"conv_fwd_raw: statistics buffer of {stats.numel()} floats < {STAT_ROWS} x {G * Kout}")
     OH, OW, osh, osw, oph, opw = omap if omap is not None else (P, Q, 1, 1, 0, 0)
     bn = {}
     if bnref is not None:
