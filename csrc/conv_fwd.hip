@@ -595,6 +595,245 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Warp-specialised forward (benchmark variants 20-23): 4 loader waves keep an NS-slot LDS ring
+// filled by LDS-DMA, NCW = 4 or 8 consumer waves (64x64 wave tiles) run the MFMAs. Slots change
+// hands through LDS counters -- FULL[s]: loader waves whose pieces of the slot's current fill have
+// landed, FREE[s]: consumer waves that hold the slot's fragments in registers -- so consumers
+// never issue a DMA or wait at a block barrier, and each loader wave keeps RING_LAG fills in
+// flight (counted vmcnt). The block is persistent over output tiles: the ring runs on across tile
+// boundaries, the loaders prefetch the next tile while the consumers store the current one.
+// Scope: KM_FAST loader, identity output map, G == 1, EPI_PLAIN / EPI_STATS.
+constexpr int RING_LAG = 3, RING_BK = 32, RING_EROWS = 16;
+template <int BM_, int BN_>
+constexpr int ring_slot_bytes() { return (BM_ + BN_) * RING_BK * 2; }
+template <int BM_, int BN_>
+constexpr int ring_ncw() { return (BM_ / 64) * (BN_ / 64); }
+template <int BM_, int BN_>
+constexpr int ring_stage_bytes() { return ring_ncw<BM_, BN_>() * RING_EROWS * EPI_PITCH * 2; }
+template <int BM_, int BN_>
+constexpr int ring_ns() {
+  const int n = (150 * 1024 - ring_stage_bytes<BM_, BN_>()) / ring_slot_bytes<BM_, BN_>();
+  return n > 6 ? 6 : n;
+}
+template <int BM_, int BN_>
+constexpr int ring_lds_bytes() { return ring_ns<BM_, BN_>() * ring_slot_bytes<BM_, BN_>() + ring_stage_bytes<BM_, BN_>(); }
+
+// LDS-DMA of one 1-KB wave piece from inline asm (M0 set and restored in the statement): hipcc does
+// not track it, so it neither waits for it before the FULL publish nor before unrelated LDS work
+DV_DEVICE void glds16_asm(const void* src, uint32_t dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(__builtin_amdgcn_readfirstlane(dst))
+               : "memory");
+}
+// wait until an LDS counter reaches `target`; a guard bounds the spin so a broken handshake ends
+// the kernel with wrong numbers instead of hanging the GPU
+DV_DEVICE void ring_wait(volatile int* c, int target) {
+  for (int guard = 0; *c < target && guard < (1 << 24); ++guard) {
+  }
+}
+
+template <int BM_, int BN_, int EPI>
+__global__ __launch_bounds__(64 * (4 + ring_ncw<BM_, BN_>()), 1) void conv_ring_kernel(FwdParams p) {
+  constexpr int WN = BN_ / 64, WM = BM_ / 64, NCW = WM * WN, NS = ring_ns<BM_, BN_>();
+  static_assert(NCW == 4 || NCW == 8, "4 or 8 consumer waves of 64x64");
+  static_assert(NS > RING_LAG, "ring deeper than the loader lag");
+  constexpr int BK_ = RING_BK, CH = BK_ / 8, RPI = 64 / CH;  // 16 rows of 64 B per 1-KB DMA
+  constexpr int MI = BM_ / RPI / 4, NI = BN_ / RPI / 4;        // DMAs per loader wave per fill
+  constexpr int IPL = MI + NI;
+  constexpr int SLOT = ring_slot_bytes<BM_, BN_>();
+  __shared__ int ring_full[NS], ring_free[NS];
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (threadIdx.x < NS) { ring_full[threadIdx.x] = 0; ring_free[threadIdx.x] = 0; }
+  __syncthreads();
+  const int tiles_m = (p.M + BM_ - 1) / BM_, tiles_n = (p.N + BN_ - 1) / BN_;
+  const int ntiles = tiles_m * tiles_n;
+  const int nt = (p.K + BK_ - 1) / BK_;  // K-tiles per output tile (Cg % 64 == 0: one tap each)
+
+  if (wid >= NCW) {
+    // ---------------------------------- loader waves ----------------------------------
+    const int lw = wid - NCW;
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem));
+    const char* zero = dv_zero_page;
+    int fill = 0;
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+      const int tn = tile % tiles_n, tm = tile / tiles_n;
+      const int m0 = tm * BM_, n0 = tn * BN_;
+      const u16* wrow[NI];
+      bool wok[NI];
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int row = (lw * NI + j) * RPI + lane / CH;
+        const int lc = (lane % CH) ^ kc_swz<BK_>(row);
+        const int n = n0 + row;
+        wok[j] = n < p.N;
+        wrow[j] = p.w + (int64_t)(wok[j] ? n : 0) * p.K + lc * 8;
+      }
+      const u16* xrow[MI];
+      uint32_t tapmask[MI];
+#pragma unroll
+      for (int j = 0; j < MI; ++j) {
+        const int row = (lw * MI + j) * RPI + lane / CH;
+        const int lc = (lane % CH) ^ kc_swz<BK_>(row);
+        const int m = m0 + row;
+        const bool ok = m < p.M;
+        const int mm = ok ? m : 0;
+        const int img = (int)fdiv((uint32_t)mm, p.div_pq), rem = mm - img * (p.P * p.Q);
+        const int pp = (int)fdiv((uint32_t)rem, p.div_q), qq = rem - pp * p.Q;
+        const int hb = pp * p.sh - p.ph, wb = qq * p.sw - p.pw;
+        uint32_t mk = 0;
+        for (int r = 0; r < p.R; ++r) { const int h = hb + r * p.dh; mk |= (uint32_t)(h >= 0 && h < p.Hin) << r; }
+        for (int s2 = 0; s2 < p.S; ++s2) { const int w = wb + s2 * p.dw; mk |= (uint32_t)(w >= 0 && w < p.Win) << (16 + s2); }
+        tapmask[j] = ok ? mk : 0u;
+        xrow[j] = p.x + ((int64_t)img * p.Hin * p.Win + (int64_t)hb * p.Win + wb) * p.ldx + lc * 8;
+      }
+      int t_r = 0, t_s = 0, t_c = 0;
+      for (int kt = 0; kt < nt; ++kt, ++fill) {
+        const int s = fill % NS, k = fill / NS;
+        if (k > 0) ring_wait(&ring_free[s], NCW * k);  // every consumer holds the slot's last fill in registers
+        const uint32_t img_n = lds0 + s * SLOT, img_m = img_n + BN_ * BK_ * 2;
+        const int k0 = kt * BK_;
+#pragma unroll
+        for (int j = 0; j < NI; ++j) glds16_asm(wok[j] ? (const void*)(wrow[j] + k0) : (const void*)zero, img_n + (lw * NI + j) * 1024);
+        const int64_t koff = ((int64_t)(t_r * p.dh) * p.Win + t_s * p.dw) * p.ldx + t_c;
+#pragma unroll
+        for (int j = 0; j < MI; ++j) {
+          const bool ok = (tapmask[j] >> t_r) & (tapmask[j] >> (16 + t_s)) & 1u;
+          glds16_asm(ok ? (const void*)(xrow[j] + koff) : (const void*)zero, img_m + (lw * MI + j) * 1024);
+        }
+        t_c += BK_;
+        if (t_c >= p.Cg) { t_c = 0; if (++t_s == p.S) { t_s = 0; ++t_r; } }
+        if (fill >= RING_LAG) {  // fill - LAG has landed (this wave's part): publish it
+          wait_vm<IPL * RING_LAG>();
+          if (lane == 0) atomicAdd(&ring_full[(fill - RING_LAG) % NS], 1);
+        }
+      }
+    }
+    // drain: publish the last LAG fills in order
+    const int last = fill;
+#pragma unroll
+    for (int d = RING_LAG; d >= 1; --d) {
+      const int f = last - d;
+      if (f < 0) continue;
+      if (d == 3) wait_vm<IPL * 2>();
+      else if (d == 2) wait_vm<IPL>();
+      else wait_vm<0>();
+      if (lane == 0) atomicAdd(&ring_full[f % NS], 1);
+    }
+    return;
+  }
+
+  // ---------------------------------- consumer waves ----------------------------------
+  const int wave_m = wid / WN, wave_n = wid % WN;
+  u16* st = reinterpret_cast<u16*>(smem + NS * SLOT + wid * RING_EROWS * EPI_PITCH * 2);
+  int fill = 0;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int tn = tile % tiles_n, tm = tile / tiles_n;
+    const int m0 = tm * BM_, n0 = tn * BN_;
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // software-pipelined: fill t+1's fragment reads are in flight during fill t's MFMAs
+    bf16x8 fa[4], fb[4];
+    auto rd = [&](int f, bf16x8* a_, bf16x8* b_) {
+      const int s = f % NS, k = f / NS;
+      ring_wait(&ring_full[s], 4 * (k + 1));
+      const char* img_n = smem + s * SLOT;
+      const char* img_m = img_n + BN_ * BK_ * 2;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a_[j] = read_kc<BK_>(img_n, wave_n * 64 + j * 16 + (lane & 15), lane >> 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) b_[i] = read_kc<BK_>(img_m, wave_m * 64 + i * 16 + (lane & 15), lane >> 4);
+    };
+    auto release = [&](int f) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) atomicAdd(&ring_free[f % NS], 1);  // fragments in registers: the slot may refill
+    };
+    rd(fill, fa, fb);
+    release(fill);
+    for (int kt = 0; kt < nt; ++kt, ++fill) {
+      bf16x8 na[4], nb[4];
+      if (kt + 1 < nt) rd(fill + 1, na, nb);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[j], fb[i], acc[j][i], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + 1 < nt) {
+        release(fill + 1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { fa[j] = na[j]; fb[j] = nb[j]; }
+      }
+    }
+    // epilogue (identity map): statistics of the fp32 results; the bf16 tile goes out through this
+    // wave's private 16-row LDS staging in 4 passes, as 16-B pieces of whole NHWC rows
+    const int nw0 = n0 + wave_n * 64, mw0 = m0 + wave_m * 64;
+    float bsum[4][4], bsq[4][4], kq[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = nw0 + j * 16 + (lane >> 4) * 4 + r;
+        kq[j][r] = (EPI == EPI_STATS && n < p.N) ? stat_shift(p.stats, p.N)[n] : 0.f;
+        bsum[j][r] = 0.f; bsq[j][r] = 0.f;
+      }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool mv = mw0 + i * 16 + (lane & 15) < p.M;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc[j][i][r];
+          if constexpr (EPI == EPI_STATS) {
+            if (mv) { const float d = v[r] - kq[j][r]; bsum[j][r] += d; bsq[j][r] = fmaf(d, d, bsq[j][r]); }
+          }
+        }
+        uint2 pk; pk.x = pack2bf(v[0], v[1]); pk.y = pack2bf(v[2], v[3]);
+        *reinterpret_cast<uint2*>(st + (lane & 15) * EPI_PITCH + j * 16 + (lane >> 4) * 4) = pk;
+      }
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        const int rl = it * 8 + (lane >> 3), ch = (lane & 7) * 8;
+        const int m = mw0 + i * 16 + rl, n = nw0 + ch;
+        const uint4 o = *reinterpret_cast<const uint4*>(st + rl * EPI_PITCH + ch);
+        if (m < p.M && n < p.N) *reinterpret_cast<uint4*>(p.y + (int64_t)m * p.ldy + n) = o;
+      }
+    }
+    if constexpr (EPI == EPI_STATS) {
+      float* a = p.stats + (int64_t)(tm % DV_STAT_SHARDS) * 2 * p.N;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float s1 = row16_sum(bsum[j][r]), s2 = row16_sum(bsq[j][r]);
+          const int n = nw0 + j * 16 + (lane >> 4) * 4 + r;
+          if ((lane & 15) == 0 && n < p.N) { atomicAdd(a + n, s1); atomicAdd(a + p.N + n, s2); }
+        }
+    }
+  }
+}
+
+template <int BM_, int BN_, int EPI>
+void launch_ring(const FwdParams& p, hipStream_t st) {
+  constexpr int lds = ring_lds_bytes<BM_, BN_>();
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv_ring_kernel<BM_, BN_, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr = true;
+  }
+  const int ntiles = ((p.M + BM_ - 1) / BM_) * ((p.N + BN_ - 1) / BN_);
+  conv_ring_kernel<BM_, BN_, EPI><<<dim3(std::min(ntiles, 256)), dim3(64 * (4 + ring_ncw<BM_, BN_>())), lds, st>>>(p);
+}
+
 int g_last_ksplit = 1;  // splits actually launched by the last split-K launch (finalize pass)
 
 // the epilogue staging tile and the statistics scratch reuse the (drained) operand stages
@@ -860,6 +1099,19 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
     return bn_status;
   }
   if (p.Cg % 8 != 0 || p.ldx % 8 != 0) return -1;
+  // warp-specialised ring (benchmark variants 20: 128x128, 21: 256x64, 22: 256x128, 23: 128x256)
+  if (g_fwd_variant >= 20 && g_fwd_variant <= 23 && !a.tgather && p.Cg % 64 == 0 && p.R <= 16 && p.S <= 16 &&
+      !p.reflect && p.G == 1 && p.identity_map && !p.bias && !p.act && !p.res && !p.bnmode && !p.ypart && !p.zfill &&
+      (p.N % 8) == 0 && (p.ldy % 8) == 0) {
+    const bool sts = p.stats != nullptr;
+    switch (g_fwd_variant) {
+      case 20: if (sts) launch_ring<128, 128, EPI_STATS>(p, st); else launch_ring<128, 128, EPI_PLAIN>(p, st); break;
+      case 21: if (sts) launch_ring<256, 64, EPI_STATS>(p, st); else launch_ring<256, 64, EPI_PLAIN>(p, st); break;
+      case 22: if (sts) launch_ring<256, 128, EPI_STATS>(p, st); else launch_ring<256, 128, EPI_PLAIN>(p, st); break;
+      default: if (sts) launch_ring<128, 256, EPI_STATS>(p, st); else launch_ring<128, 256, EPI_PLAIN>(p, st); break;
+    }
+    return 0;
+  }
   // the fast loader needs every K-tile inside one filter tap: Cg % 64 == 0 covers both BKs
   if (a.tgather) dispatch_tile<KM_TGATHER>(p, st);
   else if (p.Cg % 64 == 0 && p.R <= 16 && p.S <= 16 && !p.reflect) dispatch_tile<KM_FAST>(p, st);
