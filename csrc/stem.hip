@@ -333,6 +333,10 @@ __global__ __launch_bounds__(512, 1) void stem_wgrad_kernel(StemParams p) {
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int img = blockIdx.x / p.chunks, chunk = blockIdx.x - img * p.chunks;
   const int p0 = chunk * p.rpb, p1 = min(p.P, p0 + p.rpb);
+  if (p0 >= p1) {  // never launched so (stem_blocks_ok); keep the slab row defined regardless
+    for (int e = threadIdx.x; e < OC * SR * 32; e += blockDim.x) p.slab[(int64_t)blockIdx.x * OC * SR * 32 + e] = 0.f;
+    return;
+  }
   const int QS = (p.Q + 15) >> 4;           // 16-pixel MFMA k-steps per output row
   const int dyb = QS * 16 * 128;             // bytes of one staged dY row
   const uint32_t ring = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(smem));
@@ -468,8 +472,11 @@ bool stem_setup(StemParams& p, int N, int Hp, int Wp, int P, int Q, int sh, int 
   if (sh < 1 || sh > 4 || (sw & 1) || sw * (Q - 1) + 8 > Wp || Hp < (P - 1) * sh + SR) return false;
   p.chunks = std::max(1, std::min(P, (target + N - 1) / N));
   p.rpb = (P + p.chunks - 1) / p.chunks;
+  p.chunks = (P + p.rpb - 1) / p.rpb;  // every block owns >= 1 output row (chunks * rpb may not overshoot P by a row)
   return true;
 }
+// block b of image b / chunks owns output rows [c * rpb, min(P, (c + 1) * rpb)): non-empty for every c
+inline bool stem_blocks_ok(const StemParams& p) { return p.rpb >= 1 && (p.chunks - 1) * p.rpb < p.P; }
 
 template <int EPI, bool FULLQ, int ROWB>
 void launch_fwd(const StemParams& p, dim3 grid, hipStream_t st) {
@@ -507,6 +514,7 @@ int dv_stem_fwd(const void* xp, const void* w, void* y, const float* bias, float
   if (p.rowbytes > 3072) return -1;
   p.rpb = (p.rpb + RG - 1) / RG * RG;  // whole groups
   p.chunks = (P + p.rpb - 1) / p.rpb;
+  if (!stem_blocks_ok(p)) return -1;
   p.x = (const u16*)xp; p.w = (const u16*)w; p.y = (u16*)y; p.bias = bias; p.stats = stats;
   p.act = act; p.slope = slope;
   const bool full = bias || act, fq = Q % 16 == 0;
@@ -526,6 +534,7 @@ int dv_stem_wgrad(const void* xp, const void* dy, int ldy, float* dw, int N, int
   if (R != SR || Sp != 8 || K != OC || ldy != OC || C > 4 || S > 8) return -1;
   StemParams p{};
   if (!stem_setup(p, N, Hp, Wp, P, Q, sh, sw, g_stem_wg_blocks)) return -1;
+  if (!stem_blocks_ok(p)) return -1;
   p.x = (const u16*)xp; p.dy = (const u16*)dy;
   const int QS = (Q + 15) / 16;
   // staging (input ring + dY buffers), at least the end-of-kernel parity reduction [4][2][2][16][64] f32

@@ -863,6 +863,7 @@ class _LinearFn(torch.autograd.Function):
                      slope=slope, ldy=Op, ksplit=gemm_ksplit(N, O, Kp))
         y = y_full if Op == O else y_full[:, :O]
         ctx.save_for_backward(x, weight, bias, y if act else None)
+        ctx.bias_param = bias  # leaf parameter (not saved): its gradient may sink in place
         ctx.cfg = (act, slope, bias is not None, Kp, Op)
         return y
 
@@ -897,11 +898,16 @@ class _LinearFn(torch.autograd.Function):
             else:
                 dw = buf
         if has_bias and ctx.needs_input_grad[2]:
-            db = dy.float().sum(0)
-            sink = grad_sink(bias)
-            if sink is not None:
-                sink.add_(db)
-                db = None
+            # native per-column sum of the bf16 rows, added straight into the live gradient buffer
+            # when there is one (instead of a bf16->fp32 copy + reduce + autograd add)
+            sink = grad_sink(ctx.bias_param)
+            key = (str(dy.device), Op)
+            acc = _CSUM_WS.get(key)
+            if acc is None:
+                acc = _CSUM_WS[key] = torch.zeros((STAT_ROWS, Op), dtype=F32, device=dy.device)
+            dst = sink if sink is not None else torch.empty(O, dtype=F32, device=dy.device)
+            lib().channel_sum(ptr(dy), N, Op, O, ptr(acc), ptr(dst), int(sink is not None), stream_handle())
+            db = None if sink is not None else dst
         return dx, dw, db, None, None
 
 

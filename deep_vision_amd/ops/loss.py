@@ -21,12 +21,14 @@ class _XentFn(torch.autograd.Function):
         lib().softmax_xent(ptr(logits), int(logits.dtype == BF16), ptr(labels), B, C, ptr(lr), ptr(grad), 1.0 / B,
                            float(label_smoothing), stream_handle())
         ctx.save_for_backward(grad)
-        return lr.sum() / B
+        return lr.mean()  # one reduction launch (sum and scale fused)
 
     @staticmethod
     def backward(ctx, go):
         (grad,) = ctx.saved_tensors
-        g = grad if go is None else grad * go.to(grad.dtype)
+        # the saved gradient is this node's private buffer: scale it in place (one launch, no dtype
+        # conversion of the upstream scalar)
+        g = grad if go is None else grad.mul_(go)
         return g, None, None
 
 
