@@ -43,11 +43,12 @@ PYBIND11_MODULE(_C, m) {
                        int Kout, int P_, int Q, int R, int S, int sh, int sw, int ph, int pw, int dh, int dw, int tgather,
                        int OH, int OW, int osh, int osw, int oph, int opw, int ldy, int act, float slope, uptr res,
                        uptr st, uptr bnx, uptr bnbits, uptr bnprm, uptr bnacc, int bnmode, int bnact, float bnslope,
-                       uptr resbits, int resact, float resslope, int reflect, int ksplit, uptr ypart, int zfill) {
+                       uptr resbits, int resact, float resslope, int reflect, int ksplit, uptr ypart, int zfill,
+                       uptr bnx2, uptr bnprm2, uptr bnacc2) {
     ConvFwdArgs a{CP(x), CP(w), P(y), CFP(bias), FP(stats), Nb, H, W, Cg, ldx, G, Kout, P_, Q, R, S, sh, sw, ph, pw,
                   dh, dw, tgather, OH, OW, osh, osw, oph, opw, ldy, act, slope, CP(res),
                   CP(bnx), CP(bnbits), CFP(bnprm), FP(bnacc), bnmode, bnact, bnslope, CP(resbits), resact, resslope,
-                  reflect, ksplit, FP(ypart), zfill};
+                  reflect, ksplit, FP(ypart), zfill, CP(bnx2), CFP(bnprm2), FP(bnacc2)};
     int r = dv_conv_fwd(a, ST(st));
     if (r < 0) throw std::runtime_error("conv_fwd: unsupported geometry (channels must be a multiple of 8)");
     check_last("conv_fwd");
@@ -59,7 +60,8 @@ PYBIND11_MODULE(_C, m) {
      py::arg("ldy"), py::arg("act"), py::arg("slope"), py::arg("res"), py::arg("st"), py::arg("bnx") = 0,
      py::arg("bnbits") = 0, py::arg("bnprm") = 0, py::arg("bnacc") = 0, py::arg("bnmode") = 0, py::arg("bnact") = 0,
      py::arg("bnslope") = 0.f, py::arg("resbits") = 0, py::arg("resact") = 0, py::arg("resslope") = 0.f,
-     py::arg("reflect") = 0, py::arg("ksplit") = 1, py::arg("ypart") = 0, py::arg("zfill") = 0);
+     py::arg("reflect") = 0, py::arg("ksplit") = 1, py::arg("ypart") = 0, py::arg("zfill") = 0, py::arg("bnx2") = 0,
+     py::arg("bnprm2") = 0, py::arg("bnacc2") = 0);
   m.def("conv_fwd_variant", [](int v) { dv_conv_fwd_variant(v); });
   m.def("bn_tuning", [](int blocks, int unroll) { dv_bn_tuning(blocks, unroll); });
   m.def("bn_apply_tuning", [](int blocks, int unroll) { dv_bn_apply_tuning(blocks, unroll); });
@@ -125,6 +127,12 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("dout"), py::arg("out"), py::arg("x"), py::arg("dx"), py::arg("dres"), py::arg("n"), py::arg("C"), py::arg("kA"),
      py::arg("kB"), py::arg("kC"), py::arg("mscale"), py::arg("mshift"), py::arg("act"), py::arg("slope"),
      py::arg("mask_bits"), py::arg("st"), py::arg("addend") = 0);
+  m.def("bn_bwd_apply_dual", [](uptr dout, uptr bits, uptr x, uptr x2, uptr dx, uptr dx2, int64_t n, int C, uptr k,
+                                uptr k2, int act, float slope, uptr st) {
+    if (C % 8 || n % C) throw std::runtime_error("bn_bwd_apply_dual: channels must be a multiple of 8");
+    dv_bn_bwd_apply_dual(CP(dout), CP(bits), CP(x), CP(x2), P(dx), P(dx2), n, C, CFP(k), CFP(k2), act, slope, ST(st));
+    check_last("bn_bwd_apply_dual");
+  });
   m.def("bn_bwd_eval", [](uptr dout, uptr out, uptr dx, uptr dres, int64_t n, int C, uptr scale, int act, float slope, uptr st) {
     dv_bn_bwd_eval(CP(dout), CP(out), P(dx), P(dres), n, C, CFP(scale), act, slope, ST(st)); check_last("bn_bwd_eval");
   });

@@ -221,6 +221,7 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const u16* __restrict__ x,
   RowTile t(C, VEC);
   if (t.lane_r >= t.rpi) return;
   const int64_t r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
+  const bool pack4 = MB && (t.cg & 3) == 0;  // C % 32 == 0: whole 4-lane groups share a row
   for (int g = t.lane_c; g < t.cg; g += t.tpr) {
     float sc[VEC], sf[VEC], rs[VEC];
 #pragma unroll
@@ -245,7 +246,19 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const u16* __restrict__ x,
         v[k] = act_fwd(z, act, slope);
       }
       VecIO<VEC>::store(out + o, v);
-      if constexpr (MB) mask[o >> 3] = (uint8_t)bits;  // activation mask, 1 bit per element (VEC == 8)
+      if constexpr (MB) {  // activation mask, 1 bit per element (VEC == 8)
+        if (pack4) {
+          // 4 consecutive channel groups (one aligned 4-lane group: same row, all active or all
+          // not) merge their bytes and one lane stores the 32-bit word: a quarter of the store
+          // instructions of byte-wide stores, 4-B instead of 1-B pieces
+          uint32_t w = bits << (8 * (t.lane_c & 3));
+          w |= __shfl_xor(w, 1, 64);
+          w |= __shfl_xor(w, 2, 64);
+          if ((t.lane_c & 3) == 0) *reinterpret_cast<uint32_t*>(mask + (o >> 3)) = w;
+        } else {
+          mask[o >> 3] = (uint8_t)bits;
+        }
+      }
     }
   }
 }
@@ -364,6 +377,48 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const u16* __restrict_
   }
 }
 
+// The two BatchNorms of a residual block's output join out = act(bn(x) + bn2(x2)) (the projection
+// BN folded into the block's last pass, bn_apply_kernel RBN) share dz = act'(z) * dout: one pass
+// reads dout, the mask bits, x and x2 once and writes both input gradients (two separate apply
+// passes read dout and the bits twice). k / k2: [3][C] = kA, kB, kC of each BN.
+template <int UNR = 2>
+__global__ __launch_bounds__(NT) void bn_bwd_apply_dual_kernel(const u16* __restrict__ dout, const uint8_t* __restrict__ bits,
+                                                                 const u16* __restrict__ x, const u16* __restrict__ x2,
+                                                                 u16* __restrict__ dx, u16* __restrict__ dx2, int64_t rows, int C,
+                                                                 int64_t rows_per_block, const float* __restrict__ k,
+                                                                 const float* __restrict__ k2, int act, float slope) {
+  constexpr int VEC = 8;
+  RowTile t(C, VEC);
+  if (t.lane_r >= t.rpi) return;
+  const int64_t r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
+  for (int g = t.lane_c; g < t.cg; g += t.tpr) {
+    float a[VEC], b[VEC], cc[VEC], a2[VEC], b2[VEC], c2[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      const int c = g * VEC + e;
+      a[e] = k[c]; b[e] = k[C + c]; cc[e] = k[2 * C + c];
+      a2[e] = k2[c]; b2[e] = k2[C + c]; c2[e] = k2[2 * C + c];
+    }
+#pragma unroll UNR
+    for (int64_t r = r0 + t.lane_r; r < r1; r += t.rpi) {
+      const int64_t o = r * C + g * VEC;
+      float d[VEC], xv[VEC], xv2[VEC];
+      VecIO<VEC>::load(dout + o, d);
+      VecIO<VEC>::load(x + o, xv);
+      VecIO<VEC>::load(x2 + o, xv2);
+      const uint32_t mb = bits[o >> 3];
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        const float dz = ((mb >> e) & 1u) ? d[e] : (act == 2 ? d[e] * slope : 0.f);
+        xv[e] = fmaf(a[e], dz, fmaf(b[e], xv[e], cc[e]));
+        xv2[e] = fmaf(a2[e], dz, fmaf(b2[e], xv2[e], c2[e]));
+      }
+      VecIO<VEC>::store(dx + o, xv);
+      VecIO<VEC>::store(dx2 + o, xv2);
+    }
+  }
+}
+
 // eval-mode / frozen-stat backward: dx = scale * dz
 template <int VEC>
 __global__ __launch_bounds__(NT) void bn_bwd_eval_kernel(const u16* __restrict__ dout, const u16* __restrict__ out,
@@ -405,13 +460,16 @@ inline dim3 reduce_grid(int64_t rows, int C) {
   const int64_t g = std::min<int64_t>(std::max<int64_t>(target, 1), std::max<int64_t>(1, rows / 32));
   return dim3((unsigned)g, (unsigned)slabs);
 }
-// rows per block for the row-tiled apply passes: ~g_apply_blocks blocks (8192), a multiple of
-// rows/iteration; g_apply_unroll: rows in flight per thread (benchmarking override, dv_bn_apply_tuning)
-int g_apply_blocks = 8192;  // tools/bn_apply_bench.py: 8192 beat 4096 by 3-6 % on every ResNet-50 shape
+// rows per block for the row-tiled apply passes: ~16384 blocks for tensors of >= 40M elements,
+// ~8192 below (tools/bn_apply_bench.py, profiles/bn_apply_bench.txt: 16384 is 3-10 % faster from
+// 1024@14 up, 8192 wins at 2048@7), a multiple of rows/iteration; g_apply_blocks / g_apply_unroll:
+// benchmarking overrides (dv_bn_apply_tuning; 0 = this heuristic)
+int g_apply_blocks = 0;
 int g_apply_unroll = 2;
 inline int64_t apply_rows_per_block(int64_t rows, int C, int v) {
   const int cg = C / v, tpr = cg < NT ? cg : NT, rpi = NT / tpr;
-  int64_t rpb = (rows + g_apply_blocks - 1) / g_apply_blocks;
+  const int64_t blocks = g_apply_blocks > 0 ? g_apply_blocks : (rows * C >= (int64_t)40 << 20 ? 16384 : 8192);
+  int64_t rpb = (rows + blocks - 1) / blocks;
   rpb = ((rpb + rpi - 1) / rpi) * rpi;
   return std::max<int64_t>(rpb, rpi);
 }
@@ -431,7 +489,7 @@ void dv_bn_tuning(int reduce_blocks, int reduce_unroll) {
 }
 
 void dv_bn_apply_tuning(int blocks, int unroll) {
-  g_apply_blocks = blocks > 0 ? blocks : 8192;
+  g_apply_blocks = blocks > 0 ? blocks : 0;
   g_apply_unroll = unroll == 4 ? 4 : 2;
 }
 
@@ -575,6 +633,15 @@ void dv_bn_bwd_apply(const void* dout, const void* out, const void* x, void* dx,
   if (!act) bwd_apply_launch<MM_NONE>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, addend, st);
   else if (out) bwd_apply_launch<MM_OUT>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, addend, st);
   else bwd_apply_launch<MM_X>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, addend, st);
+}
+
+void dv_bn_bwd_apply_dual(const void* dout, const void* bits, const void* x, const void* x2, void* dx, void* dx2,
+                          int64_t n, int C, const float* k, const float* k2, int act, float slope, hipStream_t st) {
+  const int64_t rows = n / C;
+  const int64_t rpb = apply_rows_per_block(rows, C, 8);
+  const int g = (int)((rows + rpb - 1) / rpb);
+  bn_bwd_apply_dual_kernel<><<<g, NT, 0, st>>>((const u16*)dout, (const uint8_t*)bits, (const u16*)x, (const u16*)x2,
+                                               (u16*)dx, (u16*)dx2, rows, C, rpb, k, k2, act, slope);
 }
 
 void dv_bn_bwd_eval(const void* dout, const void* out, void* dx, void* dres, int64_t n, int C, const float* scale,

@@ -35,9 +35,10 @@ template <int BM_, int BN_, int WMT = 64>
 constexpr int n_waves() { return (BM_ / WMT) * (BN_ / 64); }
 template <int BM_, int BN_, int WMT = 64>
 constexpr int epi_bytes() { return n_waves<BM_, BN_, WMT>() * EPI_WAVE_BYTES; }
-// statistics scratch behind the staged tile: [WM][BN][2] (fwd BN stats) or [waves][64][2] (BNR)
+// statistics scratch behind the staged tile: [WM][BN][2] (fwd BN stats) or [waves][64][3] (BNR:
+// sum dz, sum dz*xhat and the dual BN's sum dz*xhat2)
 template <int BM_, int BN_, int WMT = 64>
-constexpr int stat_bytes() { return n_waves<BM_, BN_, WMT>() * 64 * 2 * 4; }
+constexpr int stat_bytes() { return n_waves<BM_, BN_, WMT>() * 64 * 3 * 4; }
 
 enum { KM_FAST = 0, KM_GENERIC = 1, KM_TGATHER = 2 };
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_LEAKY = 2 };
@@ -69,6 +70,9 @@ struct FwdParams {
   int ksplit, kt_per;      // split-K: K-tiles [split*kt_per, +kt_per) per block (kernels.h)
   float* ypart;            // split-K fp32 slabs [ksplit][M][N] (single group)
   int zfill;               // strided scatter output: also zero the untouched sibling pixels (kernels.h)
+  const u16* bnx2;         // BNR: second BatchNorm fed by the same dz (kernels.h ConvFwdArgs), or nullptr
+  const float* bnprm2;
+  float* bnacc2;
 };
 
 // ReflectionPad2d index map (pad < n): -1 -> 1, n -> n - 2
@@ -107,9 +111,15 @@ constexpr int stage_bytes() { return (BM_ + BN_) * BK_ * 2; }
 // (v_pk_add / v_pk_fma: half the VALU issue of the scalar form in an epilogue-bound kernel).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 DV_DEVICE f32x2 bf2x(uint32_t w) { return f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)}; }
+// DUAL: a second BatchNorm on the same dz (mode 3 only) adds its own sum dz*(x2 - mean2) into bq2
+// (its sum dz is the first one's).
+template <bool DUAL = false>
 DV_DEVICE void bn_bwd_accum(const FwdParams& p, const uint4& o, const uint4& xr, uint32_t mb, f32x2* bs, f32x2* bq,
-                            const f32x2* bmu, const f32x2* bms, const f32x2* bmh) {
+                            const f32x2* bmu, const f32x2* bms, const f32x2* bmh, const uint4* xr2 = nullptr,
+                            f32x2* bq2 = nullptr, const f32x2* bmu2 = nullptr) {
   const uint32_t dw[4] = {o.x, o.y, o.z, o.w}, xw[4] = {xr.x, xr.y, xr.z, xr.w};
+  uint32_t xw2[4] = {0u, 0u, 0u, 0u};
+  if constexpr (DUAL) { xw2[0] = xr2->x; xw2[1] = xr2->y; xw2[2] = xr2->z; xw2[3] = xr2->w; }
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const f32x2 d = bf2x(dw[e]), x = bf2x(xw[e]);
@@ -126,6 +136,7 @@ DV_DEVICE void bn_bwd_accum(const FwdParams& p, const uint4& o, const uint4& xr,
     }
     bs[e] += dz;
     bq[e] = __builtin_elementwise_fma(dz, x - bmu[e], bq[e]);
+    if constexpr (DUAL) bq2[e] = __builtin_elementwise_fma(dz, bf2x(xw2[e]) - bmu2[e], bq2[e]);
   }
 }
 
@@ -146,7 +157,7 @@ enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_FULL = 2 };
 // 256 threads (4 waves: one per SIMD, two blocks per CU) or 512 threads (8 waves: two per SIMD
 // from one block, whose deep LDS ring then holds one CU); __launch_bounds__' second argument is
 // waves per SIMD, so both forms get up to 256 VGPRs.
-template <int BM_, int BN_, int BK_, int KMODE, bool RES, int STAGES, bool BNR = false, int EPI = EPI_FULL,
+template <int BM_, int BN_, int BK_, int KMODE, bool RES, int STAGES, int BNR = 0, int EPI = EPI_FULL,
           int WMT = 64>
 __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_kernel(FwdParams p) {
   constexpr int WN = BN_ / 64, WM = BM_ / WMT;
@@ -368,13 +379,17 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
 #pragma unroll
     for (int r = 0; r < 4; ++r) { bsum[j][r] = 0.f; bsq[j][r] = 0.f; }
   // BNR: this lane's 8 channels are fixed over the store loop (rows it*8 + lane/8)
-  f32x2 bs2[4], bq2[4], bmu2[4], bms2[4], bmh2[4];
+  // dual: a second BatchNorm on the same dz (kernels.h ConvFwdArgs bnx2): its sum dz*(x2 - mean2)
+  f32x2 bs2[4], bq2[4], bmu2[4], bms2[4], bmh2[4], dq2[4], dmu2[4];
+  constexpr bool dual = BNR == 2;  // compile-time: the single-BN forms keep their registers
   if constexpr (BNR) {
     const int nb = nw0 + (lane & 7) * 8;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      bs2[e] = f32x2{0.f, 0.f}; bq2[e] = f32x2{0.f, 0.f};
+      bs2[e] = f32x2{0.f, 0.f}; bq2[e] = f32x2{0.f, 0.f}; dq2[e] = f32x2{0.f, 0.f};
       const bool ok0 = nb + 2 * e < p.N, ok1 = nb + 2 * e + 1 < p.N;
+      dmu2[e] = f32x2{(dual && ok0) ? p.bnprm2[2 * p.N + nb + 2 * e] : 0.f,
+                      (dual && ok1) ? p.bnprm2[2 * p.N + nb + 2 * e + 1] : 0.f};
       bms2[e] = f32x2{ok0 ? p.bnprm[nb + 2 * e] : 0.f, ok1 ? p.bnprm[nb + 2 * e + 1] : 0.f};
       bmh2[e] = f32x2{ok0 ? p.bnprm[p.N + nb + 2 * e] : 0.f, ok1 ? p.bnprm[p.N + nb + 2 * e + 1] : 0.f};
       bmu2[e] = f32x2{ok0 ? p.bnprm[2 * p.N + nb + 2 * e] : 0.f, ok1 ? p.bnprm[2 * p.N + nb + 2 * e + 1] : 0.f};
@@ -422,7 +437,7 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
     // input and mask) for all 8 row groups now: issued in the loop they would each wait behind the
     // previous iteration's stores (one vmcnt queue for loads and stores), 8 serial round trips.
     int64_t pf_off[PF ? 8 : 1];
-    uint4 pf_res[RES ? 8 : 1], pf_x[BNR ? 8 : 1];
+    uint4 pf_res[RES ? 8 : 1], pf_x[BNR ? 8 : 1], pf_x2[dual ? 8 : 1];
     uint32_t pf_mb[BNR ? 8 : 1], pf_rmb[RES ? 8 : 1];
     if constexpr (PF) {
 #pragma unroll
@@ -449,6 +464,7 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
         if constexpr (BNR) {
           pf_x[it] = ld ? *reinterpret_cast<const uint4*>(p.bnx + off) : uint4{0u, 0u, 0u, 0u};
           pf_mb[it] = (ld && p.bnmode == 3) ? (uint32_t)p.bnbits[off >> 3] : 0u;
+          if constexpr (dual) pf_x2[it] = ld ? *reinterpret_cast<const uint4*>(p.bnx2 + off) : uint4{0u, 0u, 0u, 0u};
         }
       }
     }
@@ -501,7 +517,10 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
           }
           const uint4 o = uint4{ov[0], ov[1], ov[2], ov[3]};
           *reinterpret_cast<uint4*>(dst) = o;
-          if constexpr (BNR) bn_bwd_accum(p, o, pf_x[it], pf_mb[it], bs2, bq2, bmu2, bms2, bmh2);
+          if constexpr (BNR) {
+            if constexpr (dual) bn_bwd_accum<true>(p, o, pf_x[it], pf_mb[it], bs2, bq2, bmu2, bms2, bmh2, &pf_x2[it], dq2, dmu2);
+            else bn_bwd_accum(p, o, pf_x[it], pf_mb[it], bs2, bq2, bmu2, bms2, bmh2);
+          }
         } else {
           const uint32_t rmb = pf_rmb[it];
 #pragma unroll
@@ -511,7 +530,10 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
       } else if (vec) {
         const uint4 o = *reinterpret_cast<const uint4*>(src);
         *reinterpret_cast<uint4*>(dst) = o;
-        if constexpr (BNR) bn_bwd_accum(p, o, pf_x[it], pf_mb[it], bs2, bq2, bmu2, bms2, bmh2);
+        if constexpr (BNR) {
+          if constexpr (dual) bn_bwd_accum<true>(p, o, pf_x[it], pf_mb[it], bs2, bq2, bmu2, bms2, bmh2, &pf_x2[it], dq2, dmu2);
+          else bn_bwd_accum(p, o, pf_x[it], pf_mb[it], bs2, bq2, bmu2, bms2, bmh2);
+        }
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e) if (n + e < p.N) dst[e] = src[e];
@@ -549,15 +571,18 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
   if constexpr (BNR) {
     // lanes sharing (lane & 7) hold partials of the same 8 channels: butterfly over lane bits 3-5,
     // then the WM waves of one channel column meet in LDS; one coalesced atomic row per block
-    float bs[8], bq[8];
+    float bs[8], bq[8], bd[8];
     {
       const int nb = nw0 + (lane & 7) * 8;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {  // sum dz*(x - mean) -> sum dz*xhat: one invstd per channel
         const float i0 = nb + 2 * e < p.N ? p.bnprm[3 * p.N + nb + 2 * e] : 0.f;
         const float i1 = nb + 2 * e + 1 < p.N ? p.bnprm[3 * p.N + nb + 2 * e + 1] : 0.f;
+        const float j0 = (dual && nb + 2 * e < p.N) ? p.bnprm2[3 * p.N + nb + 2 * e] : 0.f;
+        const float j1 = (dual && nb + 2 * e + 1 < p.N) ? p.bnprm2[3 * p.N + nb + 2 * e + 1] : 0.f;
         bs[2 * e] = bs2[e].x; bs[2 * e + 1] = bs2[e].y;
         bq[2 * e] = bq2[e].x * i0; bq[2 * e + 1] = bq2[e].y * i1;
+        bd[2 * e] = dq2[e].x * j0; bd[2 * e + 1] = dq2[e].y * j1;
       }
     }
 #pragma unroll
@@ -566,30 +591,39 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
       for (int off = 8; off < 64; off <<= 1) {
         bs[e] += __shfl_xor(bs[e], off, 64);
         bq[e] += __shfl_xor(bq[e], off, 64);
+        if constexpr (dual) bd[e] += __shfl_xor(bd[e], off, 64);
       }
     }
-    float* sh = reinterpret_cast<float*>(smem + EPI_BYTES);  // [waves][64 channels][2]
+    float* sh = reinterpret_cast<float*>(smem + EPI_BYTES);  // [waves][64 channels][3]
     if (lane < 8) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        sh[(wid * 64 + lane * 8 + e) * 2 + 0] = bs[e];
-        sh[(wid * 64 + lane * 8 + e) * 2 + 1] = bq[e];
+        sh[(wid * 64 + lane * 8 + e) * 3 + 0] = bs[e];
+        sh[(wid * 64 + lane * 8 + e) * 3 + 1] = bq[e];
+        sh[(wid * 64 + lane * 8 + e) * 3 + 2] = bd[e];
       }
     }
     __syncthreads();
     if (threadIdx.x < BN_) {
       const int nl = threadIdx.x, n = n0 + nl;
       if (n < p.N) {
-        float s1 = 0.f, s2 = 0.f;
+        float s1 = 0.f, s2 = 0.f, s3 = 0.f;
 #pragma unroll
         for (int wm = 0; wm < WM; ++wm) {
           const int w = wm * WN + nl / 64;
-          s1 += sh[(w * 64 + (nl & 63)) * 2];
-          s2 += sh[(w * 64 + (nl & 63)) * 2 + 1];
+          s1 += sh[(w * 64 + (nl & 63)) * 3];
+          s2 += sh[(w * 64 + (nl & 63)) * 3 + 1];
+          s3 += sh[(w * 64 + (nl & 63)) * 3 + 2];
         }
-        float* a = p.bnacc + (int64_t)(tm % DV_STAT_SHARDS) * 2 * p.N;
+        const int64_t shard = (int64_t)(tm % DV_STAT_SHARDS) * 2 * p.N;
+        float* a = p.bnacc + shard;
         atomicAdd(a + n, s1);
         atomicAdd(a + p.N + n, s2);
+        if constexpr (dual) {  // the same dz: the second BN's sum dz is s1
+          float* a2 = p.bnacc2 + shard;
+          atomicAdd(a2 + n, s1);
+          atomicAdd(a2 + p.N + n, s3);
+        }
       }
     }
   }
@@ -843,7 +877,7 @@ constexpr int lds_bytes(int stages) {
   return stages * stage_bytes<BM_, BN_, BK_>() > epi ? stages * stage_bytes<BM_, BN_, BK_>() : epi;
 }
 
-template <int BM_, int BN_, int BK_, int KMODE, bool RES, int STAGES, bool BNR = false, int EPI = EPI_FULL,
+template <int BM_, int BN_, int BK_, int KMODE, bool RES, int STAGES, int BNR = 0, int EPI = EPI_FULL,
           int WMT = 64>
 void launch_fwd(const FwdParams& p, hipStream_t st) {
   static bool attr = false;
@@ -885,7 +919,7 @@ bool big_tile_ok(const FwdParams& p) {
   return tiles >= 192 || g_fwd_variant == 100;  // 100: tests force it at small shapes
 }
 
-template <int KMODE, bool RES, bool BNR, int EPI>
+template <int KMODE, bool RES, int BNR, int EPI>
 void launch_heuristic(const FwdParams& p, hipStream_t st) {
   if (KMODE == KM_FAST) {
     if (big_tile_ok<KMODE>(p)) { launch_fwd<256, 256, 64, KMODE, RES, 2, BNR, EPI, 128>(p, st); return; }
@@ -902,10 +936,10 @@ void launch_heuristic(const FwdParams& p, hipStream_t st) {
   else launch_fwd<128, 128, 64, KMODE, RES, 2, BNR, EPI>(p, st);
 }
 
-template <int KMODE, bool RES, bool BNR = false>
+template <int KMODE, bool RES, int BNR = 0>
 void dispatch_res(const FwdParams& p, hipStream_t st) {
   if constexpr (BNR) {  // fused BN-backward statistics (dgrads, KM_FAST only): plain epilogue
-    launch_heuristic<KMODE, RES, true, EPI_PLAIN>(p, st);
+    launch_heuristic<KMODE, RES, BNR, EPI_PLAIN>(p, st);
     return;
   }
   if constexpr (KMODE == KM_FAST) {
@@ -922,17 +956,17 @@ void dispatch_res(const FwdParams& p, hipStream_t st) {
       // 8-wave tiles (one 512-thread block per CU, deep LDS-DMA ring)
       case 10: return launch_fwd<256, 128, 64, KMODE, RES, 3>(p, st);
       // 128-row wave tiles (a wave = 128 pixels x 64 channels)
-      case 12: return launch_fwd<256, 128, 64, KMODE, RES, 2, false, EPI_FULL, 128>(p, st);  // 4 waves
-      case 14: return launch_fwd<256, 256, 64, KMODE, RES, 2, false, EPI_FULL, 128>(p, st);  // 8 waves
+      case 12: return launch_fwd<256, 128, 64, KMODE, RES, 2, 0, EPI_FULL, 128>(p, st);  // 4 waves
+      case 14: return launch_fwd<256, 256, 64, KMODE, RES, 2, 0, EPI_FULL, 128>(p, st);  // 8 waves
       default: break;
     }
     const bool full = p.bias || p.act || p.ypart;  // split-K slabs are written by the FULL form
-    if (!full && !p.stats) launch_heuristic<KMODE, RES, false, EPI_PLAIN>(p, st);
-    else if (!full) launch_heuristic<KMODE, RES, false, EPI_STATS>(p, st);
-    else launch_heuristic<KMODE, RES, false, EPI_FULL>(p, st);
+    if (!full && !p.stats) launch_heuristic<KMODE, RES, 0, EPI_PLAIN>(p, st);
+    else if (!full) launch_heuristic<KMODE, RES, 0, EPI_STATS>(p, st);
+    else launch_heuristic<KMODE, RES, 0, EPI_FULL>(p, st);
     return;
   }
-  launch_heuristic<KMODE, RES, false, EPI_FULL>(p, st);
+  launch_heuristic<KMODE, RES, 0, EPI_FULL>(p, st);
 }
 
 template <int KMODE>
@@ -940,9 +974,14 @@ void dispatch_tile(const FwdParams& p, hipStream_t st) {
   // in-place gradient accumulation / fused BN statistics epilogues are compile-time: no cost
   // for the others
   if constexpr (KMODE == KM_FAST) {
-    if (p.bnmode) {
-      if (p.res) dispatch_res<KMODE, true, true>(p, st);
-      else dispatch_res<KMODE, false, true>(p, st);
+    if (p.bnmode) {  // BNR 2: a second BatchNorm on the same dz (projection-block join, bnx2)
+      if (p.bnx2) {
+        if (p.res) dispatch_res<KMODE, true, 2>(p, st);
+        else dispatch_res<KMODE, false, 2>(p, st);
+      } else {
+        if (p.res) dispatch_res<KMODE, true, 1>(p, st);
+        else dispatch_res<KMODE, false, 1>(p, st);
+      }
       return;
     }
   }
@@ -1026,6 +1065,7 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
   p.identity_map = (a.OH == a.P && a.OW == a.Q && a.osh == 1 && a.osw == 1 && a.oph == 0 && a.opw == 0);
   p.bnx = (const u16*)a.bnx; p.bnbits = (const uint8_t*)a.bnbits; p.bnprm = a.bnprm; p.bnacc = a.bnacc;
   p.bnmode = a.bnmode; p.bnact = a.bnact; p.bnslope = a.bnslope;
+  p.bnx2 = (const u16*)a.bnx2; p.bnprm2 = a.bnprm2; p.bnacc2 = a.bnacc2;
   p.resbits = (const uint8_t*)a.resbits; p.resact = a.resact; p.resslope = a.resslope;
   p.reflect = a.reflect;
   p.ksplit = 1; p.kt_per = 1 << 30; p.ypart = nullptr;
@@ -1063,9 +1103,10 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
     const bool map_ok = p.identity_map || (a.oph == 0 && a.opw == 0 && !p.zfill);
     const bool ok = a.tgather == 0 && map_ok && p.G == 1 && (p.N & 7) == 0 && p.ldy == p.N &&
                     p.Cg % 64 == 0 && p.ldx % 8 == 0 && p.R <= 16 && p.S <= 16 && p.bnx && p.bnprm && p.bnacc &&
-                    (p.bnmode != 3 || p.bnbits);
+                    (p.bnmode != 3 || p.bnbits) && (!p.bnx2 || (p.bnmode == 3 && p.bnprm2 && p.bnacc2));
     if (!ok) { p.bnmode = 0; bn_status = 1; }
   }
+  if (!p.bnmode) p.bnx2 = nullptr;
   p.div_pq = make_fastdiv((uint32_t)(a.P * a.Q));
   p.div_q = make_fastdiv((uint32_t)a.Q);
   if (a.tgather == 2) {

@@ -51,6 +51,12 @@ struct ConvFwdArgs {
   // also zeroes the (osh x osw) - 1 output pixels its tap never reaches, so the output needs no
   // separate zero fill (1x1 stride-s dgrad: every pixel of the input grid is written once)
   int zfill = 0;
+  // optional second BatchNorm fed by the same dz (a residual block's projection-shortcut BN folded
+  // into the block's last BN pass: both see act'(z) * dout with the bnmode-3 mask): its input,
+  // [4][C] parameters and accumulator. The sum dz is shared, the sum dz*xhat is its own.
+  const void* bnx2 = nullptr;
+  const float* bnprm2 = nullptr;
+  float* bnacc2 = nullptr;
 };
 
 struct ConvWgradArgs {
@@ -109,6 +115,10 @@ void dv_bn_bwd_finalize(float* acc, int C, double count, const float* gamma, con
 void dv_bn_bwd_apply(const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t n, int C,
                      const float* kA, const float* kB, const float* kC, const float* mscale, const float* mshift, int act,
                      float slope, int mask_bits, const void* addend, hipStream_t st);
+// both BatchNorms of a residual block's output join (main + folded projection BN, one mask):
+// dz = act'(z)*dout from the mask bits, dx = kA*dz + kB*x + kC, dx2 = kA2*dz + kB2*x2 + kC2
+void dv_bn_bwd_apply_dual(const void* dout, const void* bits, const void* x, const void* x2, void* dx, void* dx2,
+                          int64_t n, int C, const float* k, const float* k2, int act, float slope, hipStream_t st);
 void dv_bn_bwd_eval(const void* dout, const void* out, void* dx, void* dres, int64_t n, int C, const float* scale,
                     int act, float slope, hipStream_t st);
 

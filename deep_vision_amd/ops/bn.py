@@ -26,7 +26,8 @@ STAT_ROWS = 2 * STAT_SHARDS + 1  # forward statistics: shard sums + the shift ro
 FUSE_BWD_STATS = True  # fold the backward reduction into the consumer conv's dgrad epilogue
 LAZY_SHORTCUT = True   # identity-shortcut gradient masked inside the consumer's dgrad epilogue
 FOLD_RESIDUAL_BN = True  # projection-shortcut BN applied inside the block's last BN pass
-COUNTERS = {"bwd_reduce_fused": 0, "bwd_reduce_pass": 0, "shortcut_lazy": 0}
+DUAL_BWD = True  # ...and its backward: reduction in the consumer dgrad's epilogue, one dual apply pass
+COUNTERS = {"bwd_reduce_fused": 0, "bwd_reduce_pass": 0, "shortcut_lazy": 0, "dual_apply": 0, "dual_fused": 0}
 
 
 class BNRef:
@@ -35,12 +36,15 @@ class BNRef:
     statistics. Attached to the BN output tensor (``_dv_bnref``); the conv records the gradient
     tensor it produced, and the BN backward uses the fused sums only if the gradient it receives
     IS that tensor (same storage, untouched version, a single fusion) -- otherwise it zeroes the
-    accumulator and runs its own reduce pass."""
+    accumulator and runs its own reduce pass.
+    ``x2, prm2, acc2``: a residual block's projection BN folded into this pass (mode 3, the same
+    dz): the epilogue reduces it too (sum dz shared, its own sum dz*xhat2)."""
 
-    __slots__ = ("x", "bits", "prm", "mode", "act", "slope", "acc", "fused", "nfused")
+    __slots__ = ("x", "bits", "prm", "mode", "act", "slope", "acc", "fused", "nfused", "x2", "prm2", "acc2")
 
-    def __init__(self, x, bits, prm, mode, act, slope, acc):
+    def __init__(self, x, bits, prm, mode, act, slope, acc, x2=None, prm2=None, acc2=None):
         self.x, self.bits, self.prm, self.mode, self.act, self.slope, self.acc = x, bits, prm, mode, act, slope, acc
+        self.x2, self.prm2, self.acc2 = (x2, prm2, acc2) if mode == 3 and x2 is not None else (None, None, None)
         self.fused = None
         self.nfused = 0
 
@@ -55,6 +59,8 @@ class BNRef:
         ok = self.nfused == 1 and self.fused == (dout.data_ptr(), dout._version, tuple(dout.shape), dout.stride())
         if not ok:
             self.acc.zero_()  # partial / foreign sums
+            if self.acc2 is not None:
+                self.acc2.zero_()
         self.fused = None
         self.nfused = 0
         return ok
@@ -124,7 +130,8 @@ class _BNActFn(torch.autograd.Function):
         ctx.bnref = None
         if refbox is not None and training and ws_bwd is not None and C % 8 == 0 and (not act or bits or residual is None):
             mode = 3 if bits else (2 if act else 1)
-            ctx.bnref = BNRef(x, mask if bits else None, prm, mode, act, slope, ws_bwd)
+            dual = (residual, rprm, r_cfg[3]) if (rprm is not None and DUAL_BWD) else (None, None, None)
+            ctx.bnref = BNRef(x, mask if bits else None, prm, mode, act, slope, ws_bwd, *dual)
             refbox.append(ctx.bnref)
         return out
 
@@ -135,6 +142,7 @@ class _BNActFn(torch.autograd.Function):
         scale, shift, mean, invstd = prm[0], prm[1], prm[2], prm[3]
         N, C, H, W = x.shape
         fused = ctx.bnref is not None and ctx.bnref.take(dout)
+        fused2 = fused and ctx.bnref.x2 is not None  # the folded projection BN's sums came along
         dout = grad_nhwc(dout)
         if ld_of(dout) != C:
             dout = dout.contiguous(memory_format=torch.channels_last)
@@ -175,18 +183,29 @@ class _BNActFn(torch.autograd.Function):
             L.bn_bwd_finalize(ptr(acc), C, float(rows), ptr(weight.detach() if weight is not None else None), ptr(mean),
                               ptr(invstd), ptr(sg if direct else dgamma), ptr(sb if direct else dbeta), int(direct),
                               ptr(coef[0]), ptr(coef[1]), ptr(coef[2]), st)
-        if training:
+        # residual join with the projection BN folded in: both input gradients from one pass
+        dual = (DUAL_BWD and training and rprm is not None and ctx.bits and not fold_x and ctx.needs_input_grad[6]
+                and dout.is_contiguous(memory_format=torch.channels_last))
+        if training and not dual:
             L.bn_bwd_apply(ptr(dout), ptr(out), ptr(x), ptr(dx), ptr(dres), x.numel(), C, ptr(coef[0]), ptr(coef[1]),
                            ptr(coef[2]), ptr(scale), ptr(shift), act, float(slope), int(ctx.bits), st,
                            addend=ptr(xg) if fold_x else 0)
-        else:
+        elif not training:
             if act and out is None:  # eval backward needs the mask: rebuild the output
                 out = torch.empty_like(x)
                 L.bn_apply(ptr(x), 0, ptr(out), x.numel(), C, ptr(scale), ptr(shift), act, float(slope), 0, st)
             L.bn_bwd_eval(ptr(dout), ptr(out), ptr(dx), ptr(dres), x.numel(), C, ptr(scale), act, float(slope), st)
         r_dgamma = r_dbeta = None
-        if rprm is not None:
-            dres, r_dgamma, r_dbeta = _residual_bn_backward(ctx, dout, out, r_x, rprm, r_weight, r_bias, act, slope)
+        if dual:
+            COUNTERS["dual_apply"] += 1
+            COUNTERS["dual_fused"] += int(fused2)
+            coef_r, r_dgamma, r_dbeta = _residual_bn_coef(ctx, dout, out, r_x, rprm, r_weight, r_bias, act, slope, fused2)
+            dres = torch.empty_like(r_x)
+            L.bn_bwd_apply_dual(ptr(dout), ptr(out), ptr(x), ptr(r_x), ptr(dx), ptr(dres), x.numel(), C, ptr(coef),
+                                ptr(coef_r), act, float(slope), st)
+        elif rprm is not None:
+            dres, r_dgamma, r_dbeta = _residual_bn_backward(ctx, dout, out, r_x, rprm, r_weight, r_bias, act, slope,
+                                                            fused2)
         if lazy:
             from .conv import MaskedGrad
 
@@ -200,17 +219,19 @@ class _BNActFn(torch.autograd.Function):
                 None, r_dgamma, r_dbeta, None, None, None, None)
 
 
-def _residual_bn_backward(ctx, dout, bits, r_x, rprm, r_weight, r_bias, act, slope):
-    """Backward of the folded residual BatchNorm: dz = act'(z)*dout from the mask bits (never
-    materialised), its reduction against xhat_r, then d(r_x) = kA*dz + kB*r_x + kC."""
+def _residual_bn_coef(ctx, dout, bits, r_x, rprm, r_weight, r_bias, act, slope, fused):
+    """Folded residual BatchNorm, backward statistics: dz = act'(z)*dout from the mask bits (never
+    materialised) reduced against xhat_r -- unless the consumer dgrad's epilogue already did
+    (``fused``) -- then dgamma_r / dbeta_r and the coefficients of d(r_x) = kA*dz + kB*r_x + kC."""
     L = lib()
     st = stream_handle()
     N, C, H, W = r_x.shape
     rows = N * H * W
     mbits = int(bits is not None and ctx.bits)
     acc = ctx.r_ws_bwd
-    L.bn_bwd_reduce(ptr(dout), ptr(bits), ptr(r_x), rows, C, ptr(rprm[2]), ptr(rprm[3]), 0, 0, act, float(slope), ptr(acc),
-                    mbits, st)
+    if not fused:
+        L.bn_bwd_reduce(ptr(dout), ptr(bits), ptr(r_x), rows, C, ptr(rprm[2]), ptr(rprm[3]), 0, 0, act, float(slope),
+                        ptr(acc), mbits, st)
     sg = grad_sink(r_weight) if ctx.needs_input_grad[17] else None
     sb = grad_sink(r_bias) if ctx.needs_input_grad[18] else None
     direct = sg is not None and sb is not None
@@ -222,6 +243,17 @@ def _residual_bn_backward(ctx, dout, bits, r_x, rprm, r_weight, r_bias, act, slo
     L.bn_bwd_finalize(ptr(acc), C, float(rows), ptr(r_weight.detach()), ptr(rprm[2]), ptr(rprm[3]),
                       ptr(sg if direct else dgamma), ptr(sb if direct else dbeta), int(direct), ptr(coef[0]), ptr(coef[1]),
                       ptr(coef[2]), st)
+    return coef, dgamma, dbeta
+
+
+def _residual_bn_backward(ctx, dout, bits, r_x, rprm, r_weight, r_bias, act, slope, fused=False):
+    """Backward of the folded residual BatchNorm on its own: statistics (_residual_bn_coef), then
+    d(r_x) = kA*dz + kB*r_x + kC in a separate apply pass."""
+    L = lib()
+    st = stream_handle()
+    C = r_x.shape[1]
+    mbits = int(bits is not None and ctx.bits)
+    coef, dgamma, dbeta = _residual_bn_coef(ctx, dout, bits, r_x, rprm, r_weight, r_bias, act, slope, fused)
     dr = torch.empty_like(r_x)
     L.bn_bwd_apply(ptr(dout), ptr(bits), ptr(r_x), ptr(dr), 0, r_x.numel(), C, ptr(coef[0]), ptr(coef[1]), ptr(coef[2]),
                    0, 0, act, float(slope), mbits, st)

@@ -143,6 +143,8 @@ def conv_fwd_raw(x, wk, y, bias, stats, N, H, W, Cg, ldx, G, Kout, P, Q, R, S, s
     if bnref is not None:
         bn = dict(bnx=ptr(bnref.x), bnbits=ptr(bnref.bits), bnprm=ptr(bnref.prm), bnacc=ptr(bnref.acc),
                   bnmode=bnref.mode, bnact=bnref.act, bnslope=float(bnref.slope))
+        if bnref.x2 is not None:  # the folded projection BN of the same residual join (same dz)
+            bn.update(bnx2=ptr(bnref.x2), bnprm2=ptr(bnref.prm2), bnacc2=ptr(bnref.acc2))
     if resmask is not None:
         bn.update(resbits=ptr(resmask[0]), resact=int(resmask[1]), resslope=float(resmask[2]))
     if reflect:

@@ -494,3 +494,62 @@ def test_projection_bn_folded_into_block_apply(stride):
         assert torch.allclose(bn_n.running_mean, bn_r.running_mean, atol=2e-3, rtol=2e-2)
         assert torch.allclose(bn_n.running_var, bn_r.running_var, atol=2e-3, rtol=2e-2)
         assert int(bn_n.num_batches_tracked) == int(bn_r.num_batches_tracked) == 1
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_projection_bn_dual_backward(stride):
+    """Projection block followed by an identity block: the next block's conv1 dgrad epilogue reduces
+    BOTH BatchNorms of the projection block's output join (bn3 and the folded shortcut BN share
+    dz = act'(z)*dout; csrc/conv_fwd.hip BNR dual), and one dual apply pass writes both input
+    gradients (csrc/bn.hip bn_bwd_apply_dual_kernel). Gradients equal the two-pass path within its
+    run-to-run noise and track a torch fp32 run of the same blocks."""
+    from deep_vision_amd.models.resnet import BottleneckBlock
+    from deep_vision_amd.ops import bn as B
+    from deep_vision_amd.ops.common import set_backend
+
+    torch.manual_seed(0)
+    base = torch.nn.Sequential(BottleneckBlock(64, 64, 256, stride=stride, downsample=True),
+                               BottleneckBlock(256, 64, 256)).to(DEV)
+    x32 = torch.randn(8, 64, 28, 28, device=DEV).bfloat16().float()
+    g = torch.randn(8, 256, 28 // stride, 28 // stride, device=DEV)
+    runs = {}
+    for key in ("a", "b", "dual", "torch"):
+        blk = copy.deepcopy(base)
+        B.DUAL_BWD = key == "dual"
+        set_backend("torch" if key == "torch" else "native")
+        c0 = dict(B.COUNTERS)
+        try:
+            if key == "torch":
+                x = x32.clone().requires_grad_(True)
+                y = blk(x)
+                y.backward(g)
+            else:
+                x = x32.to(torch.bfloat16).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+                y = blk(x)
+                y.backward(g.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+            torch.cuda.synchronize()
+        finally:
+            B.DUAL_BWD = True
+            set_backend("native")
+        if key != "torch":
+            n_dual = B.COUNTERS["dual_apply"] - c0["dual_apply"]
+            n_fused = B.COUNTERS["dual_fused"] - c0["dual_fused"]
+            assert (n_dual, n_fused) == ((1, 1) if key == "dual" else (0, 0)), (key, n_dual, n_fused)
+        blk.state_dict()  # flushes the lazily counted num_batches_tracked
+        vec = torch.cat([x.grad.float().flatten()] + [p.grad.flatten() for p in blk.parameters()])
+        runs[key] = (y.detach().float(), vec, blk)
+    noise = _cos(runs["a"][1], runs["b"][1])
+    assert _cos(runs["dual"][1], runs["a"][1]) > min(noise, 0.99999) - 5e-4, (noise, _cos(runs["dual"][1], runs["a"][1]))
+    assert _cos(runs["dual"][1], runs["torch"][1]) > 0.99
+    # the shortcut BN's own parameter gradients (the sums the epilogue produced): as close to the
+    # two-pass path as that path is to itself, and as close to torch fp32 as the two-pass path is
+    bns = {k: runs[k][2][0].projection[1] for k in runs}
+    for name in ("weight", "bias"):
+        gd, ga, gb, gt = (getattr(bns[k], name).grad for k in ("dual", "a", "b", "torch"))
+        assert _cos(gd, ga) > min(_cos(ga, gb), 0.9999) - 1e-3, (name, _cos(gd, ga), _cos(ga, gb))
+        assert _cos(gd, gt) > _cos(ga, gt) - 2e-3, (name, _cos(gd, gt), _cos(ga, gt))
+    bf, bt = runs["dual"][2][0], runs["torch"][2][0]
+    for bn_n, bn_r in ((bf.bn3, bt.bn3), (bf.projection[1], bt.projection[1])):
+        assert torch.allclose(bn_n.running_mean, bn_r.running_mean, atol=2e-3, rtol=2e-2)
+        assert torch.allclose(bn_n.running_var, bn_r.running_var, atol=2e-3, rtol=2e-2)
+        assert int(bn_n.num_batches_tracked) == int(bn_r.num_batches_tracked) == 1
