@@ -131,11 +131,17 @@ __global__ __launch_bounds__((64 * wg_waves<BM_, BN_, WMT>()), 2) void conv_wgra
     mok[j] = m < p.M;
     mrow[j] = p.dy + (int64_t)row * p.ldm + (int64_t)grp * p.M + (mok[j] ? m : 0);
   }
-  // ---- N operand (im2col X): fixed column chunk (r, s, c), pixel decode walked per tile ----
-  int n_r[NI], n_s[NI], n_c[NI];
-  bool nok[NI];
-  int w_img[NI], w_p[NI], w_q[NI];
-  const u16* nrow[NI];  // PLAIN: pointer at (pixel row, channel)
+  // ---- N operand (im2col X): fixed column chunk (r, s, c) per lane, the pixel walked per tile ----
+  // Multiply-free walk, 4 registers per DMA instruction: the tap pointer itself (x at the pixel's
+  // window origin + the tap offset), hw = p*sh << 16 | q*sw and the tap's (r*dh - ph, s*dw - pw)
+  // as two int16 (a column past N gets an always-out-of-image row offset). A tile step adds
+  // wave-uniform deltas and carries q -> p -> image. (The per-tile decode with 64-bit multiplies
+  // ran ~12 VALU per MFMA: the kernel was VALU-bound.)
+  const u16* nptr[NI];   // PLAIN: pointer at (pixel row, channel); im2col: the tap pointer
+  uint32_t w_hw[NI], n_tap[NI];
+  bool nok[NI];          // PLAIN only
+  const int64_t ldx = p.ldx, SWL = (int64_t)p.sw * ldx, SHL = (int64_t)p.sh * p.Win * ldx;
+  const int64_t IMGL = (int64_t)p.Hin * p.Win * ldx;
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
     const int row = (wid * NI + j) * NRPI + lane / NCH;
@@ -144,21 +150,29 @@ __global__ __launch_bounds__((64 * wg_waves<BM_, BN_, WMT>()), 2) void conv_wgra
     nok[j] = n < p.N;
     const int nn = nok[j] ? n : 0;
     if (PLAIN) {
-      n_c[j] = nn;
-      nrow[j] = p.x + (int64_t)row * p.ldx + goff_x + nn;
+      nptr[j] = p.x + (int64_t)row * p.ldx + goff_x + nn;
     } else {
       const int rs = (int)fdiv((uint32_t)nn, p.div_cg);
-      n_c[j] = nn - rs * p.Cg;
-      n_r[j] = (int)fdiv((uint32_t)rs, p.div_s);
-      n_s[j] = rs - n_r[j] * p.S;
+      const int c = nn - rs * p.Cg;
+      const int r = (int)fdiv((uint32_t)rs, p.div_s), sc = rs - r * p.S;
+      const int hr = nok[j] ? r * p.dh - p.ph : -32768, wr = sc * p.dw_ - p.pw;
+      n_tap[j] = ((uint32_t)hr << 16) | ((uint32_t)wr & 0xffffu);
       const int pix = kt0 * BK + row;
-      w_img[j] = (int)fdiv((uint32_t)pix, p.div_pq);
-      const int rem = pix - w_img[j] * p.P * p.Q;
-      w_p[j] = (int)fdiv((uint32_t)rem, p.div_q);
-      w_q[j] = rem - w_p[j] * p.Q;
+      const int img = (int)fdiv((uint32_t)pix, p.div_pq);
+      const int rem = pix - img * p.P * p.Q;
+      const int pp = (int)fdiv((uint32_t)rem, p.div_q);
+      const int hb = pp * p.sh, wb = (rem - pp * p.Q) * p.sw;
+      w_hw[j] = ((uint32_t)hb << 16) | (uint32_t)wb;
+      nptr[j] = p.x + (int64_t)img * IMGL + ((int64_t)(hb + hr) * p.Win + (wb + wr)) * ldx + goff_x + c;
     }
   }
+  // per-tile deltas (BK pixels) and the carries, all wave-uniform
   const int d_q = BK % p.Q, d_p = (BK / p.Q) % p.P, d_img = BK / (p.P * p.Q);
+  const uint32_t dhw = ((uint32_t)(d_p * p.sh) << 16) + (uint32_t)(d_q * p.sw);
+  const uint32_t Qsw = p.Q * p.sw, Psh = p.P * p.sh;
+  const uint32_t cq_hw = ((uint32_t)p.sh << 16) - Qsw, cp_hw = Psh << 16;
+  const int64_t dpo = (int64_t)d_q * SWL + (int64_t)d_p * SHL + (int64_t)d_img * IMGL;
+  const int64_t cq = SHL - (int64_t)p.Q * SWL, cp = IMGL - (int64_t)p.P * SHL;
 
   auto stage = [&](int kt, int buf) {
     char* img_m = smem + buf * STAGE;
@@ -176,16 +190,20 @@ __global__ __launch_bounds__((64 * wg_waves<BM_, BN_, WMT>()), 2) void conv_wgra
       const int row = (wid * NI + j) * NRPI + lane / NCH;
       const void* src = zero;
       if (PLAIN) {
-        if (nok[j] && k0 + row < p.K) src = nrow[j] + (int64_t)k0 * p.ldx;
+        if (nok[j] && k0 + row < p.K) src = nptr[j] + (int64_t)k0 * p.ldx;
       } else {
-        int h = w_p[j] * p.sh - p.ph + n_r[j] * p.dh;
-        int w = w_q[j] * p.sw - p.pw + n_s[j] * p.dw_;
-        if (p.reflect) {
-          h = h < 0 ? -h : (h >= p.Hin ? 2 * p.Hin - 2 - h : h);
-          w = w < 0 ? -w : (w >= p.Win ? 2 * p.Win - 2 - w : w);
+        const int hr = (int)n_tap[j] >> 16, wr = (int)(n_tap[j] << 16) >> 16;
+        int h = (int)(w_hw[j] >> 16) + hr, w = (int)(w_hw[j] & 0xffffu) + wr;
+        const u16* a = nptr[j];
+        if (p.reflect) {  // wave-uniform: ReflectionPad2d-fused layers re-aim out-of-image taps
+          const int h2 = h < 0 ? -h : (h >= p.Hin ? 2 * p.Hin - 2 - h : h);
+          const int w2 = w < 0 ? -w : (w >= p.Win ? 2 * p.Win - 2 - w : w);
+          a += ((int64_t)(h2 - h) * p.Win + (w2 - w)) * ldx;
+          h = hr == -32768 ? -1 : h2;
+          w = w2;
         }
-        if (nok[j] && k0 + row < p.K && (unsigned)h < (unsigned)p.Hin && (unsigned)w < (unsigned)p.Win)
-          src = p.x + (((int64_t)w_img[j] * p.Hin + h) * p.Win + w) * p.ldx + goff_x + n_c[j];
+        const bool ok = k0 + row < p.K && (unsigned)h < (unsigned)p.Hin && (unsigned)w < (unsigned)p.Win;
+        src = ok ? (const void*)a : src;
       }
       glds16(src, lds0 + buf * STAGE + MBYTES + (wid * NI + j) * 1024);
     }
@@ -194,10 +212,12 @@ __global__ __launch_bounds__((64 * wg_waves<BM_, BN_, WMT>()), 2) void conv_wgra
     if (!PLAIN) {
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        int q = w_q[j] + d_q, pp = w_p[j] + d_p, im = w_img[j] + d_img;
-        if (q >= p.Q) { q -= p.Q; ++pp; }
-        if (pp >= p.P) { pp -= p.P; ++im; }
-        w_q[j] = q; w_p[j] = pp; w_img[j] = im;
+        uint32_t hw = w_hw[j] + dhw;
+        int64_t d = dpo;
+        if ((hw & 0xffffu) >= Qsw) { hw += cq_hw; d += cq; }
+        if ((hw >> 16) >= Psh) { hw -= cp_hw; d += cp; }
+        w_hw[j] = hw;
+        nptr[j] += d;
       }
     }
   };
