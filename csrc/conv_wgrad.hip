@@ -232,7 +232,11 @@ __global__ __launch_bounds__((64 * wg_waves<BM_, BN_, WMT>()), 2) void conv_wgra
   // scheduler recycled one fragment register per 4 MFMAs and waited on each re-read, exposing
   // the LDS latency every 4 MFMAs; here it is exposed once per tile, the in-order LDS returns
   // release the MFMAs as they arrive
+  // a wave whose 64 columns all lie past N (the last N tile of 3x3 x 64: N = 576 on 256-wide
+  // tiles) skips its fragment reads and MFMAs: its SIMD time goes to the co-resident waves
+  const bool live = n0 + wave_n * 64 < p.N;
   auto compute = [&](int buf) {
+    if (!live) return;
     const char* img_m = smem + buf * STAGE;
     const char* img_n = img_m + MBYTES;
     constexpr int KK = BK / 32;
