@@ -407,6 +407,37 @@ __global__ void slab_reduce_kernel(const float* __restrict__ ws, float* __restri
   }
 }
 
+// the same sum over 16-B vectors, the splits spread over SG thread groups (each walks its
+// splits s = g, g + SG, ... with four loads in flight, added in order) and the SG partials
+// combined in fixed order: 4 x the memory parallelism of the per-element serial chain above,
+// still reproducible bit for bit. n % 4 == 0, 16-B aligned ws / dst.
+constexpr int SLAB_SG = 4;
+__global__ __launch_bounds__(256) void slab_reduce4_kernel(const float4* __restrict__ ws, float4* __restrict__ dst,
+                                                          int64_t n4, int splits, int accumulate) {
+  __shared__ float4 part[SLAB_SG][64];
+  const int tx = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + tx;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto add = [](float4& a, const float4& b) { a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w; };
+  if (i < n4) {
+    int sp = g;
+    for (; sp + 3 * SLAB_SG < splits; sp += 4 * SLAB_SG) {
+      const float4 v0 = ws[(int64_t)sp * n4 + i], v1 = ws[(int64_t)(sp + SLAB_SG) * n4 + i];
+      const float4 v2 = ws[(int64_t)(sp + 2 * SLAB_SG) * n4 + i], v3 = ws[(int64_t)(sp + 3 * SLAB_SG) * n4 + i];
+      add(acc, v0); add(acc, v1); add(acc, v2); add(acc, v3);
+    }
+    for (; sp < splits; sp += SLAB_SG) add(acc, ws[(int64_t)sp * n4 + i]);
+  }
+  part[g][tx] = acc;
+  __syncthreads();
+  if (g == 0 && i < n4) {
+    float4 t = accumulate ? dst[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int q = 0; q < SLAB_SG; ++q) add(t, part[q][tx]);
+    dst[i] = t;
+  }
+}
+
 int g_deterministic = [] {
   const char* v = std::getenv("DV_DETERMINISTIC");
   return (v && v[0] && v[0] != '0') ? 1 : 0;
@@ -430,9 +461,24 @@ float* dv_slab_workspace(size_t elems, hipStream_t st) {
 }
 
 void dv_slab_reduce(const float* ws, float* dst, int64_t n, int splits, int accumulate, hipStream_t st) {
+  if (n % 4 == 0 && ((uintptr_t)ws & 15) == 0 && ((uintptr_t)dst & 15) == 0) {
+    const int64_t n4 = n / 4;
+    slab_reduce4_kernel<<<(unsigned)((n4 + 63) / 64), 256, 0, st>>>((const float4*)ws, (float4*)dst, n4, splits,
+                                                                     accumulate);
+    return;
+  }
   const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
   slab_reduce_kernel<<<grid, 256, 0, st>>>(ws, dst, n, splits, accumulate);
 }
+
+// split-K partials through plain-stored fp32 slabs + one ordered reduce pass instead of float
+// atomics into dw (atomic adds run at ~1.3 TB/s chip-wide and land at the end of the grid, where
+// every block reaches its epilogue together); 1 = slabs (DV_WG_SLAB=1 / conv_wgrad_slab), 0 = atomics
+int g_wg_slab = [] {
+  const char* v = std::getenv("DV_WG_SLAB");
+  return (v && v[0] == '1') ? 1 : 0;
+}();
+void dv_conv_wgrad_slab(int on) { g_wg_slab = on; }
 
 int dv_conv_wgrad_splits(const ConvWgradArgs& a) {
   const int M = a.Kout, N = a.R * a.S * a.Cg, K = a.Nb * a.P * a.Q;
@@ -502,13 +548,15 @@ int dv_conv_wgrad(const ConvWgradArgs& a, hipStream_t st) {
   if (p.reflect && (p.ph >= p.Hin || p.pw >= p.Win || p.ph < 0 || p.pw < 0)) return -1;
   if (p.oirs_ig > p.Cg) return -1;
   const size_t out_elems = (size_t)p.G * p.M * (p.oirs_ig > 0 ? (size_t)p.oirs_ig * p.R * p.S : (size_t)p.N);
-  const bool det = g_deterministic && p.splits > 1;
+  // deterministic mode, and by default every split-K launch: each split stores its partial tile
+  // into its own slab (every valid element of dW is written once per split: no memset), the
+  // slabs are summed in a fixed order afterwards -- no atomics, reproducible bits
+  bool det = (g_deterministic || g_wg_slab) && p.splits > 1;
+  if (det && !dv_slab_workspace((size_t)p.splits * out_elems, st)) {
+    if (g_deterministic) return -1;
+    det = false;  // no room for the slabs: atomics
+  }
   if (det) {
-    // every split stores its partial tile (all tile elements, masked rows included) into its own
-    // slab; the slabs are summed in split order afterwards: no atomics, reproducible bits
-    const size_t need = (size_t)p.splits * out_elems;
-    if (!dv_slab_workspace(need, st)) return -1;
-    (void)hipMemsetAsync(g_slab_ws, 0, need * sizeof(float), st);
     p.dw = g_slab_ws;
     p.slab = (int64_t)out_elems;
     p.atomic_out = 0;

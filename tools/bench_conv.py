@@ -77,7 +77,7 @@ def run(name, H, Cin, Cout, k, s, N, variants, iters):
     return res
 
 
-def run_wgrad(name, H, Cin, Cout, k, s, N, variants, iters, split_pcts=(100,)):
+def run_wgrad(name, H, Cin, Cout, k, s, N, variants, iters, split_pcts=(100,), slabs=(1,)):
     """dW of the forward conv (Cin -> Cout): the wgrad kernel with M = Cout, N = k*k*Cin."""
     pad = k // 2
     P = (H + 2 * pad - k) // s + 1
@@ -87,9 +87,10 @@ def run_wgrad(name, H, Cin, Cout, k, s, N, variants, iters, split_pcts=(100,)):
     flops = 2.0 * N * P * P * Cout * Cin * k * k
     ref = None
     res = {}
-    for v in variants:
-        for sp in split_pcts:
+    for v, sp, sl in [(v, sp, sl) for v in variants for sp in split_pcts for sl in slabs]:
+        if True:
             lib().conv_wgrad_tuning(v, sp)
+            lib().conv_wgrad_slab(bool(sl))
 
             def go():
                 return lib().conv_wgrad(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), N, H, H, Cin, Cin, 1, Cout, P, P,
@@ -109,10 +110,11 @@ def run_wgrad(name, H, Cin, Cout, k, s, N, variants, iters, split_pcts=(100,)):
             e1.record()
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / iters
-            res[f"{v}/{sp}"] = (us, err)
-            print(f"wg {name:22s} v{v} split{sp:4d}% ({splits:3d})  {us:8.1f} us  {flops / us / 1e6:7.1f} TF/s  relerr {err:.3g}",
-                  flush=True)
+            res[f"{v}/{sp}/{sl}"] = (us, err)
+            print(f"wg {name:22s} v{v} split{sp:4d}% ({splits:3d}) {'slab' if sl else 'atom'} {us:8.1f} us  "
+                  f"{flops / us / 1e6:7.1f} TF/s  relerr {err:.3g}", flush=True)
     lib().conv_wgrad_tuning(0, 100)
+    lib().conv_wgrad_slab(False)
     return res
 
 
@@ -124,6 +126,7 @@ def main():
     ap.add_argument("--out")
     ap.add_argument("--wgrad", action="store_true")
     ap.add_argument("--splits", default="100")
+    ap.add_argument("--slab", default="1", help="wgrad split-K combine: 1 = ordered slabs, 0 = atomics (e.g. 1,0)")
     ap.add_argument("--layers", default="", help="comma-separated layer names (default: all)")
     ap.add_argument("--set", default="resnet50", choices=["resnet50", "hourglass"])
     a = ap.parse_args()
@@ -135,7 +138,8 @@ def main():
             continue
         if a.wgrad:
             if not L[0].startswith("dg_"):
-                out[L[0]] = run_wgrad(*L, a.batch, vs, a.iters, [int(x) for x in a.splits.split(",")])
+                out[L[0]] = run_wgrad(*L, a.batch, vs, a.iters, [int(x) for x in a.splits.split(",")],
+                                      [int(x) for x in a.slab.split(",")])
         else:
             out[L[0]] = run(*L, a.batch, vs, a.iters)
     if a.out:
