@@ -71,7 +71,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_deterministic", [](bool on) { dv_set_deterministic(on ? 1 : 0); });
   m.def("deterministic", []() { return dv_deterministic() != 0; });
   m.def("conv_wgrad_tuning", [](int v, int split_pct) { dv_conv_wgrad_tuning(v, split_pct); });
-  m.def("conv_wgrad_slab", [](bool on) { dv_conv_wgrad_slab(on ? 1 : 0); });
+  m.def("conv_wgrad_slab", [](int mode) { dv_conv_wgrad_slab(mode); });
   // host-side split-K heuristic of conv_wgrad (no GPU work): tests pin the grid sizing
   m.def("conv_wgrad_splits", [](int Nb, int H, int W, int Cg, int Kout, int P_, int Q, int R, int S, int sh, int sw,
                                 int ph, int pw) {

@@ -473,10 +473,15 @@ void dv_slab_reduce(const float* ws, float* dst, int64_t n, int splits, int accu
 
 // split-K partials through plain-stored fp32 slabs + one ordered reduce pass instead of float
 // atomics into dw (atomic adds run at ~1.3 TB/s chip-wide and land at the end of the grid, where
-// every block reaches its epilogue together); 1 = slabs (DV_WG_SLAB=1 / conv_wgrad_slab), 0 = atomics
+// every block reaches its epilogue together). -1 (default): slabs up to SLAB_MAX_SPLITS splits --
+// the slab bytes grow with the split count and the reduce pass reads them all: slabs won 5-10 %
+// on the 6-56-split layers (1x1 at 14x14 / 7x7, 3x3 at 28x28 / 14x14) and lost 4-8 % on the
+// 96-392-split 56x56 / 28x28 1x1 layers (profiles/wgbench_slab.txt); 1 / 0 (DV_WG_SLAB,
+// conv_wgrad_slab): always slabs / always atomics
+constexpr int SLAB_MAX_SPLITS = 64;
 int g_wg_slab = [] {
   const char* v = std::getenv("DV_WG_SLAB");
-  return (v && v[0] == '1') ? 1 : 0;
+  return (v && (v[0] == '0' || v[0] == '1')) ? v[0] - '0' : -1;
 }();
 void dv_conv_wgrad_slab(int on) { g_wg_slab = on; }
 
@@ -551,7 +556,8 @@ int dv_conv_wgrad(const ConvWgradArgs& a, hipStream_t st) {
   // deterministic mode, and by default every split-K launch: each split stores its partial tile
   // into its own slab (every valid element of dW is written once per split: no memset), the
   // slabs are summed in a fixed order afterwards -- no atomics, reproducible bits
-  bool det = (g_deterministic || g_wg_slab) && p.splits > 1;
+  const bool slab = g_wg_slab == 1 || (g_wg_slab < 0 && p.splits <= SLAB_MAX_SPLITS);
+  bool det = (g_deterministic || slab) && p.splits > 1;
   if (det && !dv_slab_workspace((size_t)p.splits * out_elems, st)) {
     if (g_deterministic) return -1;
     det = false;  // no room for the slabs: atomics

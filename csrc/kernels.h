@@ -83,7 +83,7 @@ int dv_gconv(const void* x, int ldx, int Cin, const int16_t* tin, const void* w,
 int dv_gconv_wgrad(const void* x, int ldx, const int16_t* tin, const void* dy, int ldy, const int16_t* tout, float* dw,
                    int M, int G, int Cg, int Og, hipStream_t st);
 void dv_conv_wgrad_tuning(int variant, int split_pct);  // benchmarking override (0, 100 = heuristic)
-void dv_conv_wgrad_slab(int on);  // split-K partials via ordered fp32 slabs (1, default) or float atomics (0)
+void dv_conv_wgrad_slab(int on);  // split-K combine: -1 auto (slabs up to 64 splits), 1 ordered fp32 slabs, 0 float atomics
 int dv_conv_wgrad_splits(const ConvWgradArgs& a);
 // deterministic mode: split-K weight gradients go through per-split fp32 slabs reduced in a
 // fixed order instead of atomics (bitwise-reproducible dW)

@@ -90,7 +90,7 @@ def run_wgrad(name, H, Cin, Cout, k, s, N, variants, iters, split_pcts=(100,), s
     for v, sp, sl in [(v, sp, sl) for v in variants for sp in split_pcts for sl in slabs]:
         if True:
             lib().conv_wgrad_tuning(v, sp)
-            lib().conv_wgrad_slab(bool(sl))
+            lib().conv_wgrad_slab(int(sl))
 
             def go():
                 return lib().conv_wgrad(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), N, H, H, Cin, Cin, 1, Cout, P, P,
@@ -111,10 +111,10 @@ def run_wgrad(name, H, Cin, Cout, k, s, N, variants, iters, split_pcts=(100,), s
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / iters
             res[f"{v}/{sp}/{sl}"] = (us, err)
-            print(f"wg {name:22s} v{v} split{sp:4d}% ({splits:3d}) {'slab' if sl else 'atom'} {us:8.1f} us  "
+            print(f"wg {name:22s} v{v} split{sp:4d}% ({splits:3d}) { {1: 'slab', 0: 'atom'}.get(sl, 'auto') } {us:8.1f} us  "
                   f"{flops / us / 1e6:7.1f} TF/s  relerr {err:.3g}", flush=True)
     lib().conv_wgrad_tuning(0, 100)
-    lib().conv_wgrad_slab(False)
+    lib().conv_wgrad_slab(-1)
     return res
 
 
@@ -126,7 +126,7 @@ def main():
     ap.add_argument("--out")
     ap.add_argument("--wgrad", action="store_true")
     ap.add_argument("--splits", default="100")
-    ap.add_argument("--slab", default="1", help="wgrad split-K combine: 1 = ordered slabs, 0 = atomics (e.g. 1,0)")
+    ap.add_argument("--slab", default="1", help="wgrad split-K combine: 1 = ordered slabs, 0 = atomics, -1 = heuristic (e.g. 1,0)")
     ap.add_argument("--layers", default="", help="comma-separated layer names (default: all)")
     ap.add_argument("--set", default="resnet50", choices=["resnet50", "hourglass"])
     a = ap.parse_args()
