@@ -27,8 +27,9 @@ Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--model
 
 Reported besides the contract fields: ``per_gpu`` images/s, ``comm_exposed_ms`` (compute-stream
 time blocked on the gradient all-reduces per step, HIP events around DataParallel.finish) and
-``vs_same_box_miopen`` (ratio to the PyTorch/MIOpen eager run on the same MI355X,
-profiles/bench_resnet50_1gpu_torch_miopen.json, scaled by N). ``vs_baseline`` divides by the
+``vs_same_box_miopen`` (ratio to the PyTorch/MIOpen eager run on the same MI355X, read from the
+record ``bench.py --backend torch --write-comparator`` measured, profiles/bench_<model>_1gpu_torch_miopen.json,
+scaled by N; the file is named in ``vs_same_box_miopen_src``). ``vs_baseline`` divides by the
 BASELINE.md proxy (~376 img/s per 8-GPU node, fp32 K80-era); it is NOT a like-for-like ratio.
 """
 from __future__ import annotations
@@ -41,8 +42,34 @@ import time
 # Reference-derived comparators, images/sec per node:
 #   ResNet-50-equivalent proxy ~376 (8 GPUs), YOLOv3 ~179 (8x V100), LeNet-5 PT ~906.
 BASELINES = {"resnet50": 376.0, "yolov3": 179.0, "lenet5": 906.0}
-# same-box PyTorch-ROCm eager (MIOpen) images/s per GPU, profiles/bench_resnet50_1gpu_torch_miopen.json
-SAME_BOX_MIOPEN = {"resnet50": 6724.58}  # 20-step run, round 3
+PROFILES = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.abspath(__file__)), "profiles")
+
+
+def comparator_path(model):
+    """The same-box PyTorch-ROCm eager (MIOpen) record of ``model`` on one GPU: written by
+    ``bench.py --backend torch --model M`` (the measured run, not a constant), read by the native
+    arm for ``vs_same_box_miopen``."""
+    import os
+
+    return os.path.join(PROFILES, f"bench_{model}_1gpu_torch_miopen.json")
+
+
+def same_box_miopen(model):
+    """(per-GPU images/s, source file) of the measured MIOpen arm, or (None, None)."""
+    import os
+
+    path = comparator_path(model)
+    if not os.path.exists(path):
+        return None, None
+    try:
+        with open(path) as f:
+            rec = json.loads(f.read().strip().splitlines()[-1])
+        if rec.get("config", {}).get("backend") != "torch" or not rec.get("per_gpu"):
+            return None, None
+        return float(rec["per_gpu"]), os.path.relpath(path, os.path.dirname(PROFILES))
+    except (OSError, ValueError, KeyError, IndexError):
+        return None, None
+
 RESNET_METRIC = "images/sec (whole node), ResNet-50 224x224 bf16 at 1/2/4/8 MI355X"
 
 # model -> (per-GPU batch, image size, optimizer name, optimizer kwargs, family)
@@ -141,6 +168,9 @@ def main():
     ap.add_argument("--model", default="resnet50", choices=sorted(SPECS))
     ap.add_argument("--backend", default="native", choices=["native", "torch"],
                     help="torch = PyTorch/MIOpen reference path (for comparison only)")
+    ap.add_argument("--write-comparator", action="store_true",
+                    help="with --backend torch: record this run as the same-box comparator of the native arm "
+                         "(profiles/bench_<model>_1gpu_torch_miopen.json)")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"],
                     help="gradient all-reduce wire format (fp32 master gradients either way)")
@@ -234,8 +264,25 @@ def main():
             raise SystemExit("[bench] --graph needs the native GPU path")
         from deep_vision_amd.train.graph import CapturedStep
 
+        opt.use_device_guard(True)  # the trainers' captured step: non-finite skip decided on the device
         cap = CapturedStep(step, opt, model=model, warmup=2)  # 2 eager side-stream steps, then capture
         step = cap  # noqa: F811 - replays from here on
+
+    # multi-rank runs: every step's GPU completion is watched (a dead / wedged peer ends the rank
+    # instead of hanging the job; captured all-reduces run without RCCL's own async error handling)
+    cwd = None
+    if cuda and is_dist():
+        from deep_vision_amd.parallel.watchdog import CommWatchdog
+
+        cwd = CommWatchdog().start()
+        inner = step
+
+        def step():  # noqa: F811
+            out = inner()
+            ev = torch.cuda.Event()
+            ev.record()
+            cwd.track("bench step", ev)
+            return out
 
     for _ in range(args.warmup):
         loss = step()
@@ -266,6 +313,7 @@ def main():
         comm_ms = float(t.item())
     if rank == 0:
         base = BASELINES.get(args.model)
+        miopen, miopen_src = same_box_miopen(args.model)
         if args.model == "resnet50":
             metric = RESNET_METRIC
         else:
@@ -283,8 +331,9 @@ def main():
             "vs_baseline": round(imgs / base, 3) if base else None,
             "vs_baseline_basis": ("BASELINE.md reference proxy: images/s of a whole 8-GPU K80-era fp32 node "
                                   "(not like-for-like; see vs_same_box_miopen)") if base else None,
-            "vs_same_box_miopen": (round(imgs / (SAME_BOX_MIOPEN[args.model] * world), 3)
-                                   if args.model in SAME_BOX_MIOPEN and cuda and args.backend == "native" else None),
+            "vs_same_box_miopen": (round(imgs / (miopen * world), 3)
+                                   if miopen and cuda and args.backend == "native" else None),
+            "vs_same_box_miopen_src": miopen_src if (miopen and cuda and args.backend == "native") else None,
             "per_gpu": round(imgs / max(1, world), 2),
             "comm_exposed_ms": round(comm_ms, 3),
             "dtype": "bf16" if cuda else "fp32",
@@ -306,6 +355,11 @@ def main():
             },
         }
         print(json.dumps(rec), flush=True)
+        if args.backend == "torch" and cuda and world == 1 and args.steps >= 10 and args.write_comparator:
+            with open(comparator_path(args.model), "w") as f:  # the measured comparator of the native arm
+                f.write(json.dumps(rec) + "\n")
+    if cwd is not None:
+        cwd.stop()
     if is_dist():
         dist.destroy_process_group()
 

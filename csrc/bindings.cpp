@@ -225,23 +225,29 @@ PYBIND11_MODULE(_C, m) {
     check_last("softmax_xent");
   });
   m.def("sgd", [](uptr p, uptr g, uptr buf, int64_t n, float lr, float mom, float damp, float wd, int nesterov, int first,
-                  float gscale, uptr st, uptr hp) {
-    dv_sgd(FP(p), CFP(g), FP(buf), n, lr, mom, damp, wd, nesterov, first, gscale, CFP(hp), ST(st)); check_last("sgd");
+                  float gscale, uptr st, uptr hp, uptr skip) {
+    dv_sgd(FP(p), CFP(g), FP(buf), n, lr, mom, damp, wd, nesterov, first, gscale, CFP(hp), ST(st), CFP(skip)); check_last("sgd");
   }, py::arg("p"), py::arg("g"), py::arg("buf"), py::arg("n"), py::arg("lr"), py::arg("mom"), py::arg("damp"), py::arg("wd"),
-     py::arg("nesterov"), py::arg("first"), py::arg("gscale"), py::arg("st"), py::arg("hp") = 0);
+     py::arg("nesterov"), py::arg("first"), py::arg("gscale"), py::arg("st"), py::arg("hp") = 0, py::arg("skip") = 0);
   m.def("adam", [](uptr p, uptr g, uptr mm, uptr v, int64_t n, float lr, float b1, float b2, float eps, float wd, int decoupled,
-                   float bc1, float bc2, float gscale, uptr st, uptr hp) {
-    dv_adam(FP(p), CFP(g), FP(mm), FP(v), n, lr, b1, b2, eps, wd, decoupled, bc1, bc2, gscale, CFP(hp), ST(st)); check_last("adam");
+                   float bc1, float bc2, float gscale, uptr st, uptr hp, uptr skip) {
+    dv_adam(FP(p), CFP(g), FP(mm), FP(v), n, lr, b1, b2, eps, wd, decoupled, bc1, bc2, gscale, CFP(hp), ST(st), CFP(skip));
+    check_last("adam");
   }, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("n"), py::arg("lr"), py::arg("b1"), py::arg("b2"),
      py::arg("eps"), py::arg("wd"), py::arg("decoupled"), py::arg("bc1"), py::arg("bc2"), py::arg("gscale"), py::arg("st"),
-     py::arg("hp") = 0);
+     py::arg("hp") = 0, py::arg("skip") = 0);
   m.def("rmsprop", [](uptr p, uptr g, uptr sq, uptr mom, uptr gavg, int64_t n, float lr, float alpha, float eps, float wd,
-                      float momentum, int centered, float gscale, uptr st, uptr hp) {
-    dv_rmsprop(FP(p), CFP(g), FP(sq), FP(mom), FP(gavg), n, lr, alpha, eps, wd, momentum, centered, gscale, CFP(hp), ST(st));
+                      float momentum, int centered, float gscale, uptr st, uptr hp, uptr skip) {
+    dv_rmsprop(FP(p), CFP(g), FP(sq), FP(mom), FP(gavg), n, lr, alpha, eps, wd, momentum, centered, gscale, CFP(hp), ST(st),
+               CFP(skip));
     check_last("rmsprop");
   }, py::arg("p"), py::arg("g"), py::arg("sq"), py::arg("mom"), py::arg("gavg"), py::arg("n"), py::arg("lr"), py::arg("alpha"),
      py::arg("eps"), py::arg("wd"), py::arg("momentum"), py::arg("centered"), py::arg("gscale"), py::arg("st"),
-     py::arg("hp") = 0);
+     py::arg("hp") = 0, py::arg("skip") = 0);
+  m.def("nonfinite_check", [](uptr g, int64_t n, uptr guard, uptr st) {
+    dv_nonfinite_check(CFP(g), n, FP(guard), ST(st)); check_last("nonfinite_check");
+  });
+  m.def("nonfinite_tally", [](uptr guard, uptr st) { dv_nonfinite_tally(FP(guard), ST(st)); check_last("nonfinite_tally"); });
   m.def("gconv", [](uptr x, int ldx, int Cin, uptr tin, uptr w, int Orows, uptr y, int ldy, int Cout, uptr tout, int M,
                     int G, int Cg, int Og, int Kp, uptr stats, uptr st) {
     if (dv_gconv(CP(x), ldx, Cin, reinterpret_cast<const int16_t*>(tin), CP(w), Orows, P(y), ldy, Cout,

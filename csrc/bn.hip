@@ -177,12 +177,16 @@ __global__ void bn_finalize_kernel(float* __restrict__ acc, int C, double count,
   const double mean = (double)*shiftp + dm;
   double var = q / count - dm * dm;
   if (var < 0) var = 0;
-  *shiftp = (float)mean;  // the next batch's shift
+  // the next batch's shift; a non-finite batch (skipped by the trainer's NaN guard) must not
+  // poison every later batch's statistics through it: reset to 0 (the unshifted sums)
+  *shiftp = isfinite(mean) ? (float)mean : 0.f;
   const float invstd = (float)(1.0 / sqrt(var + (double)eps));
   const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
   save_mean[c] = (float)mean; save_invstd[c] = invstd;
   scale[c] = g * invstd; shift[c] = b - (float)mean * g * invstd;
-  if (running_mean) {
+  // a non-finite batch (the step the non-finite guard skips) leaves the running statistics as they
+  // were, so evaluation after a skipped step is not poisoned either
+  if (running_mean && isfinite(mean) && isfinite(var)) {
     const double unb = count > 1 ? var * count / (count - 1) : var;
     running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
     running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;

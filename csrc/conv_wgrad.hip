@@ -16,6 +16,7 @@
 // Tile variants (4 waves of 64x64): 128x128, and 64x256 for 64-output-channel layers.
 // A plain-row fast path serves 1x1 / stride-1 / pad-0 convs and Linear (no spatial decode).
 #include <cstdlib>
+#include <vector>
 
 #include "common.h"
 #include "kernels.h"
@@ -450,12 +451,23 @@ size_t g_slab_elems = 0;
 void dv_set_deterministic(int on) { g_deterministic = on; }
 int dv_deterministic() { return g_deterministic; }
 
+// Grow-only: a HIP graph captured earlier keeps the pointer it was recorded with, so a buffer
+// is never freed once handed out -- a larger request retires it (kept alive for the process)
+// and allocates 1.5x the request, so a model's warm-up converges in a few steps. During a
+// stream capture the buffer cannot grow (hipMalloc / a retire would change what the graph
+// holds mid-capture): nullptr, and the caller falls back to atomics (or fails in
+// deterministic mode).
+std::vector<float*> g_slab_retired;
 float* dv_slab_workspace(size_t elems, hipStream_t st) {
   if (elems > g_slab_elems) {
-    (void)hipStreamSynchronize(st);
-    if (g_slab_ws) (void)hipFree(g_slab_ws);
-    if (hipMalloc(&g_slab_ws, elems * sizeof(float)) != hipSuccess) { g_slab_ws = nullptr; g_slab_elems = 0; return nullptr; }
-    g_slab_elems = elems;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return nullptr;
+    const size_t want = elems + elems / 2;
+    float* fresh = nullptr;
+    if (hipMalloc(&fresh, want * sizeof(float)) != hipSuccess) return nullptr;
+    if (g_slab_ws) g_slab_retired.push_back(g_slab_ws);
+    g_slab_ws = fresh;
+    g_slab_elems = want;
   }
   return g_slab_ws;
 }

@@ -177,11 +177,15 @@ void dv_f32_to_bf16(const float* x, void* y, int64_t n, hipStream_t st);
 void dv_softmax_xent(const void* logits, int is_bf16, const int64_t* labels, int rows, int C, float* loss_rows, void* grad,
                      float grad_scale, float label_smoothing, hipStream_t st);
 void dv_sgd(float* p, const float* g, float* buf, int64_t n, float lr, float momentum, float dampening, float wd,
-            int nesterov, int first, float gscale, const float* hp, hipStream_t st);
+            int nesterov, int first, float gscale, const float* hp, hipStream_t st, const float* skip = nullptr);
 void dv_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps, float wd,
-             int decoupled, float bc1, float bc2, float gscale, const float* hp, hipStream_t st);
+             int decoupled, float bc1, float bc2, float gscale, const float* hp, hipStream_t st,
+             const float* skip = nullptr);
 void dv_rmsprop(float* p, const float* g, float* sq, float* mom, float* gavg, int64_t n, float lr, float alpha, float eps,
-                float wd, float momentum, int centered, float gscale, const float* hp, hipStream_t st);
+                float wd, float momentum, int centered, float gscale, const float* hp, hipStream_t st,
+                const float* skip = nullptr);
+void dv_nonfinite_check(const float* g, int64_t n, float* guard, hipStream_t st);
+void dv_nonfinite_tally(float* guard, hipStream_t st);
 void dv_sumsq(const float* x, int64_t n, float* out, hipStream_t st);
 
 // ---- depthwise conv (depthwise.hip) ----

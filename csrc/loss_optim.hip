@@ -71,7 +71,9 @@ __global__ __launch_bounds__(NT) void softmax_xent_kernel(const void* __restrict
 // captured optimizer step follows LR schedules / Adam bias correction without re-capture
 __global__ __launch_bounds__(NT) void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ buf,
                                                    int64_t n, float lr, float momentum, float dampening, float wd,
-                                                   int nesterov, int first, float gscale, const float* __restrict__ hp) {
+                                                   int nesterov, int first, float gscale, const float* __restrict__ hp,
+                                                   const float* __restrict__ skip) {
+  if (skip && *skip != 0.f) return;  // device non-finite guard: the step is a no-op
   if (hp) lr = hp[0];
   for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
     const float pv = p[i];
@@ -88,7 +90,8 @@ __global__ __launch_bounds__(NT) void sgd_kernel(float* __restrict__ p, const fl
 __global__ __launch_bounds__(NT) void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                                                     float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps,
                                                     float wd, int decoupled, float bc1, float bc2, float gscale,
-                                                    const float* __restrict__ hp) {
+                                                    const float* __restrict__ hp, const float* __restrict__ skip) {
+  if (skip && *skip != 0.f) return;
   if (hp) { lr = hp[0]; bc1 = hp[1]; bc2 = hp[2]; }
   for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
     float pv = p[i];
@@ -105,7 +108,8 @@ __global__ __launch_bounds__(NT) void adam_kernel(float* __restrict__ p, const f
 __global__ __launch_bounds__(NT) void rmsprop_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ sq,
                                                        float* __restrict__ mom, float* __restrict__ gavg, int64_t n, float lr,
                                                        float alpha, float eps, float wd, float momentum, int centered, float gscale,
-                                                       const float* __restrict__ hp) {
+                                                       const float* __restrict__ hp, const float* __restrict__ skip) {
+  if (skip && *skip != 0.f) return;
   if (hp) lr = hp[0];
   for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
     const float pv = p[i];
@@ -129,6 +133,38 @@ __global__ __launch_bounds__(NT) void sumsq_kernel(const float* __restrict__ x, 
   if (threadIdx.x == 0) atomicAdd(out, s);
 }
 
+// Device-side non-finite guard (graph-captured steps: no host sync). guard = [flag, skipped total,
+// consecutive skips, last step's flag]. nonfinite_check ORs "any non-finite gradient" into flag
+// (every finder stores the same 1.0: plain vector stores, no atomics); the optimizer kernels
+// read flag and skip the whole update; nonfinite_tally, the step's last launch, folds flag into
+// the counters and re-arms it for the next step. In a data-parallel step the checked buffer is
+// the all-reduced gradient, identical on every rank, so every rank skips or steps together.
+template <bool V4>
+__global__ __launch_bounds__(NT) void nonfinite_check_kernel(const float* __restrict__ g, int64_t n,
+                                                               float* __restrict__ guard) {
+  bool bad = false;
+  if constexpr (V4) {  // 16-B aligned buffer: float4 body + scalar tail
+    const int64_t n4 = n >> 2;
+    const float4* g4 = reinterpret_cast<const float4*>(g);
+    for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n4; i += (int64_t)gridDim.x * NT) {
+      const float4 v = g4[i];
+      bad |= !(isfinite(v.x) && isfinite(v.y) && isfinite(v.z) && isfinite(v.w));
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) bad |= !isfinite(g[n4 * 4 + threadIdx.x]);
+  } else {
+    for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) bad |= !isfinite(g[i]);
+  }
+  if (__syncthreads_or(bad) && threadIdx.x == 0) guard[0] = 1.f;
+}
+
+__global__ void nonfinite_tally_kernel(float* __restrict__ guard) {
+  const float f = guard[0] != 0.f ? 1.f : 0.f;
+  guard[1] += f;
+  guard[2] = f != 0.f ? guard[2] + 1.f : 0.f;
+  guard[3] = f;
+  guard[0] = 0.f;
+}
+
 inline int grid_for(int64_t n) {
   int64_t g = (n + NT - 1) / NT;
   return (int)std::min<int64_t>(std::max<int64_t>(g, 1), 256 * 8);
@@ -141,17 +177,23 @@ void dv_softmax_xent(const void* logits, int is_bf16, const int64_t* labels, int
   else softmax_xent_kernel<false><<<rows, NT, 0, st>>>(logits, labels, C, loss_rows, grad, grad_scale, label_smoothing);
 }
 void dv_sgd(float* p, const float* g, float* buf, int64_t n, float lr, float momentum, float dampening, float wd,
-            int nesterov, int first, float gscale, const float* hp, hipStream_t st) {
-  sgd_kernel<<<grid_for(n), NT, 0, st>>>(p, g, buf, n, lr, momentum, dampening, wd, nesterov, first, gscale, hp);
+            int nesterov, int first, float gscale, const float* hp, hipStream_t st, const float* skip) {
+  sgd_kernel<<<grid_for(n), NT, 0, st>>>(p, g, buf, n, lr, momentum, dampening, wd, nesterov, first, gscale, hp, skip);
 }
 void dv_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps, float wd,
-             int decoupled, float bc1, float bc2, float gscale, const float* hp, hipStream_t st) {
-  adam_kernel<<<grid_for(n), NT, 0, st>>>(p, g, m, v, n, lr, b1, b2, eps, wd, decoupled, bc1, bc2, gscale, hp);
+             int decoupled, float bc1, float bc2, float gscale, const float* hp, hipStream_t st, const float* skip) {
+  adam_kernel<<<grid_for(n), NT, 0, st>>>(p, g, m, v, n, lr, b1, b2, eps, wd, decoupled, bc1, bc2, gscale, hp, skip);
 }
 void dv_rmsprop(float* p, const float* g, float* sq, float* mom, float* gavg, int64_t n, float lr, float alpha, float eps,
-                float wd, float momentum, int centered, float gscale, const float* hp, hipStream_t st) {
-  rmsprop_kernel<<<grid_for(n), NT, 0, st>>>(p, g, sq, mom, gavg, n, lr, alpha, eps, wd, momentum, centered, gscale, hp);
+                float wd, float momentum, int centered, float gscale, const float* hp, hipStream_t st, const float* skip) {
+  rmsprop_kernel<<<grid_for(n), NT, 0, st>>>(p, g, sq, mom, gavg, n, lr, alpha, eps, wd, momentum, centered, gscale, hp,
+                                             skip);
 }
+void dv_nonfinite_check(const float* g, int64_t n, float* guard, hipStream_t st) {
+  if (((uintptr_t)g & 15) == 0) nonfinite_check_kernel<true><<<std::min(grid_for((n + 3) / 4), 1024), NT, 0, st>>>(g, n, guard);
+  else nonfinite_check_kernel<false><<<std::min(grid_for(n), 1024), NT, 0, st>>>(g, n, guard);
+}
+void dv_nonfinite_tally(float* guard, hipStream_t st) { nonfinite_tally_kernel<<<1, 1, 0, st>>>(guard); }
 void dv_sumsq(const float* x, int64_t n, float* out, hipStream_t st) {
   sumsq_kernel<<<std::min(grid_for(n), 1024), NT, 0, st>>>(x, n, out);
 }

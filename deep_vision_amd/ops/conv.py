@@ -558,11 +558,12 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=
             return _gconv(x, weight, groups, shuffle, want_stats, stats_buf)
         from .concat import channel_shuffle
 
-        r = conv2d(x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats, stats_buf, join,
+        # no statistics from the inner conv: they would land in the BN's workspace in the
+        # unshuffled channel order, and the BN takes its own pass over the shuffled output
+        y = conv2d(x, weight, bias, stride, padding, dilation, groups, act, slope, False, None, join,
                    join_role, pad_mode, out, residual, residual_join)
-        if want_stats:  # the statistics were taken in the unshuffled order: recompute downstream
-            return channel_shuffle(r[0], shuffle), None
-        return channel_shuffle(r, shuffle)
+        y = channel_shuffle(y, shuffle)
+        return (y, None) if want_stats else y
     if residual is not None and (act or want_stats or out is not None or not native(x)):
         y = conv2d(x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats, stats_buf, join,
                    join_role, pad_mode, out)

@@ -26,10 +26,12 @@ class _XentFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, go):
         (grad,) = ctx.saved_tensors
-        # the saved gradient is this node's private buffer: scale it in place (one launch, no dtype
-        # conversion of the upstream scalar)
-        g = grad if go is None else grad.mul_(go)
-        return g, None, None
+        if go is None:
+            return grad, None, None
+        # out of place: the saved buffer stays the unscaled gradient, so a second backward through
+        # a retained graph scales the same values again (an in-place mul_ would have returned
+        # grad*go1*go2); the (B, classes) product is one small launch either way
+        return grad * go, None, None
 
 
 def cross_entropy(logits, labels, label_smoothing=0.0):

@@ -14,6 +14,12 @@ leaves its peers blocked inside an RCCL all-reduce forever; this module bounds t
 * Exceptions raised inside a guard by the backend (RCCL async errors surfaced by
   ``TORCH_NCCL_ASYNC_ERROR_HANDLING``, gloo "connection closed by peer") are reported and turned
   into ``os._exit(EXIT_COMM_ERROR)`` for the same reason.
+* ``CommWatchdog.track(name, event)`` watches GPU-side completion instead of a host region: the
+  caller records an event after the work it enqueued (a HIP-graph replay of a data-parallel step,
+  whose captured RCCL all-reduces run with ProcessGroupNCCL's async error handling off, or an
+  eager step whose ``work.wait()`` only made the compute stream wait). The thread polls
+  ``event.query()``; an event not complete ``timeout`` seconds after it was recorded ends the
+  process the same way. A dead or wedged peer therefore ends the job in graph mode too.
 * ``install_backend_error_handling()`` sets the RCCL env knobs that make the process group
   surface async errors and abort the communicator instead of hanging (must run before the
   process group is created).
@@ -46,6 +52,7 @@ class CommWatchdog:
         self.on_timeout = on_timeout
         self.poll = poll if poll is not None else max(0.05, min(2.0, self.timeout / 10))
         self._open = {}  # token -> (name, start)
+        self._events = []  # (name, event, recorded-at), oldest first
         self._lock = threading.Lock()
         self._next = 0
         self._stop = threading.Event()
@@ -76,6 +83,35 @@ class CommWatchdog:
         finally:
             with self._lock:
                 self._open.pop(tok, None)
+
+    def track(self, name: str, event) -> None:
+        """Watch ``event`` (anything with ``query() -> bool``, e.g. a torch.cuda.Event recorded
+        after a graph replay): the process ends if it has not completed ``timeout`` s from now."""
+        if self.timeout <= 0:
+            return
+        with self._lock:
+            self._events.append((name, event, time.monotonic()))
+
+    def pending(self) -> int:
+        with self._lock:
+            return len(self._events)
+
+    def _check_events(self, now):
+        """Drop completed events (in order); return the oldest incomplete one past the deadline."""
+        while True:
+            with self._lock:
+                if not self._events:
+                    return None
+                name, ev, t0 = self._events[0]
+            try:
+                done = bool(ev.query())
+            except Exception as e:  # a failed stream (aborted communicator): report it as a comm error
+                return name, t0, f"{type(e).__name__}: {e}"
+            if not done:
+                return (name, t0, None) if now - t0 > self.timeout else None
+            with self._lock:
+                if self._events and self._events[0][1] is ev:
+                    self._events.pop(0)
 
     @staticmethod
     def _is_comm_error(e: BaseException) -> bool:
@@ -114,4 +150,13 @@ class CommWatchdog:
                 name, t0 = min(stale, key=lambda v: v[1])
                 self._abort(EXIT_COMM_TIMEOUT, f"collective region '{name}' open for {now - t0:.1f}s "
                                                f"(> {self.timeout:.0f}s)")
+                return
+            late = self._check_events(now)
+            if late is not None:
+                name, t0, err = late
+                if err is not None:
+                    self._abort(EXIT_COMM_ERROR, f"GPU work '{name}' failed: {err}")
+                else:
+                    self._abort(EXIT_COMM_TIMEOUT, f"GPU work '{name}' not complete {now - t0:.1f}s after it was "
+                                                   f"enqueued (> {self.timeout:.0f}s)")
                 return

@@ -67,8 +67,10 @@ class Engine:
         # then tears the job down) instead of blocking the whole job forever
         self.comm_watchdog = CommWatchdog().start() if self.world > 1 else None
         self.step_count = 0
-        # HIP-graph replay of the whole step (train/graph.py), data-parallel all-reduces included;
-        # the non-finite skip and fault injection need the eager step and are off in this mode
+        # HIP-graph replay of the whole step (train/graph.py), data-parallel all-reduces included.
+        # In this mode the non-finite skip is decided on the device inside the captured step
+        # (optimizer.use_device_guard), and every replay is tracked by the comm watchdog through an
+        # event recorded after it (CommWatchdog.track). Host-side fault injection needs the eager step.
         self.graph = bool(graph) and self.device.type == "cuda"
         if graph and not self.graph:
             self.log("[dv] --graph needs a GPU: running eagerly")
@@ -126,7 +128,29 @@ class Engine:
             self.log(f"[dv] non-finite loss/gradients at step {s}: step skipped ({self.guard.skipped} so far)")
         if self.watchdog is not None:
             self.watchdog.beat()
+        self._track_gpu("step")
         return ok
+
+    def _track_gpu(self, name):
+        """GPU-side completion of the step just enqueued, watched by the comm watchdog: an RCCL
+        all-reduce that never completes (dead / wedged peer) ends this rank even though the host
+        only enqueued it (eager ``work.wait()`` is a stream wait; graph replays are one launch)."""
+        if self.comm_watchdog is not None and self.device.type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record()
+            self.comm_watchdog.track(f"{name} {self.step_count}", ev)
+
+    def _check_device_guard(self, optimizer):
+        """Graph mode: read the device non-finite counters at the guard cadence (one sync)."""
+        if not hasattr(optimizer, "device_guard_counts") or not self.guard.should_check(self.step_count):
+            return
+        skipped, consecutive, _ = optimizer.device_guard_counts()
+        if skipped > self.guard.skipped:
+            self.log(f"[dv] non-finite gradients: {skipped - self.guard.skipped} captured step(s) skipped on the device "
+                     f"by step {self.step_count} ({skipped} so far)")
+            self.guard.skipped = skipped
+        if consecutive >= self.guard.max_consecutive:
+            raise FloatingPointError(f"{consecutive} consecutive non-finite steps")
 
     def train_step(self, model, optimizer, forward_loss, *inputs):
         """One optimisation step: ``forward_loss(*inputs) -> (loss, extra)``, backward, all-reduce,
@@ -145,11 +169,15 @@ class Engine:
         key = (id(model), id(optimizer), getattr(forward_loss, "__code__", forward_loss))
         g = self._graphed.get(key)
         if g is None:
+            if hasattr(optimizer, "use_device_guard") and self.guard.every > 0:
+                optimizer.use_device_guard(True)  # captured with the step: skip decided on the device
             g = self._graphed[key] = GraphedTrainStep(model, optimizer, forward_loss, eager)
         before = self.step_count
         out = g(*inputs)
         if self.step_count == before:  # replay / capture: backward_step (which counts) did not run
             self.step_count += 1
+            self._track_gpu("graph replay")
+        self._check_device_guard(optimizer)
         return out
 
     def reduce_sum(self, values):

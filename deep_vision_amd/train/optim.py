@@ -173,6 +173,35 @@ class _FlatOptimizer(torch.optim.Optimizer):
         hp = f.get("hp")
         return 0 if hp is None else ptr(hp)
 
+    # ---------------- device-side non-finite guard (HIP-graph replay) ----------------
+    def use_device_guard(self, on: bool = True):
+        """Skip-step on non-finite gradients decided ON THE DEVICE (csrc/loss_optim.hip
+        nonfinite_check / nonfinite_tally): every step checks the flat gradients, the update
+        kernels become no-ops when any is Inf/NaN, and device counters record the skips -- no host
+        synchronisation, so it works inside a captured step. The guard
+        tensor [flag, skipped, consecutive, last] is allocated once and never replaced (graphs
+        bake its pointer in). In a data-parallel step the checked gradients are the all-reduced
+        ones, identical on every rank: the ranks skip together without an extra collective."""
+        self._dguard_on = bool(on)
+        if on and getattr(self, "_dguard", None) is None:
+            dev = next((f["param"].device for f in self._flat if f is not None), None)
+            if dev is not None and dev.type == "cuda":
+                self._dguard = torch.zeros(4, dtype=torch.float32, device=dev)
+
+    def _guard_active(self):
+        return getattr(self, "_dguard_on", False) and getattr(self, "_dguard", None) is not None
+
+    def _skip_ptr(self):
+        return ptr(self._dguard) if self._guard_active() else 0
+
+    def device_guard_counts(self):
+        """(steps skipped so far, current run of consecutive skips, last step skipped) -- one
+        device->host read; call at the logging cadence."""
+        if getattr(self, "_dguard", None) is None:
+            return 0, 0, False
+        v = self._dguard.tolist()
+        return int(v[1]), int(v[2]), bool(v[3])
+
     def param_views(self):
         return [v for f in self._flat if f for v in f["views"]]
 
@@ -223,6 +252,12 @@ class _FlatOptimizer(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         self._check_binding()
+        guard = self._guard_active()
+        if guard:  # flag any non-finite gradient of any group before the first update launch
+            for group, f in zip(self.param_groups, self._flat):
+                if f is not None:
+                    self._sync_grads(group, f)
+                    lib().nonfinite_check(ptr(f["grad"]), f["grad"].numel(), ptr(self._dguard), stream_handle())
         for group, f in zip(self.param_groups, self._flat):
             if f is None:
                 continue
@@ -235,6 +270,8 @@ class _FlatOptimizer(torch.optim.Optimizer):
             for off, n in segs:
                 self._update(group, f, off, n, grad_scale)
             f["first"] = False
+        if guard:
+            lib().nonfinite_tally(ptr(self._dguard), stream_handle())  # counters; re-arms the flag
         if any(f is not None and f["param"].is_cuda for f in self._flat):
             from ..ops import wcache
 
@@ -308,7 +345,7 @@ class FusedSGD(_FlatOptimizer):
         if p.is_cuda:
             lib().sgd(ptr(p), ptr(gr), ptr(buf), n, float(g["lr"]), float(g["momentum"]), float(g["dampening"]),
                       float(g["weight_decay"]), int(g["nesterov"]), int(f["first"]), float(gs), stream_handle(),
-                      hp=self._hp_ptr(f))
+                      hp=self._hp_ptr(f), skip=self._skip_ptr())
             return
         d = gr * gs + g["weight_decay"] * p
         if g["momentum"] != 0:
@@ -340,7 +377,7 @@ class FusedAdam(_FlatOptimizer):
         if p.is_cuda:
             lib().adam(ptr(p), ptr(gr), ptr(m), ptr(v), n, float(g["lr"]), float(b1), float(b2), float(g["eps"]),
                        float(g["weight_decay"]), int(g["decoupled"]), float(bc1), float(bc2), float(gs), stream_handle(),
-                       hp=self._hp_ptr(f))
+                       hp=self._hp_ptr(f), skip=self._skip_ptr())
             return
         grad = gr * gs
         if g["decoupled"]:
@@ -369,7 +406,7 @@ class FusedRMSprop(_FlatOptimizer):
         if p.is_cuda:
             lib().rmsprop(ptr(p), ptr(gr), ptr(sq), ptr(mom), ptr(ga), n, float(g["lr"]), float(g["alpha"]),
                           float(g["eps"]), float(g["weight_decay"]), float(g["momentum"]), int(g["centered"]), float(gs),
-                          stream_handle(), hp=self._hp_ptr(f))
+                          stream_handle(), hp=self._hp_ptr(f), skip=self._skip_ptr())
             return
         grad = gr * gs + g["weight_decay"] * p
         sq.mul_(g["alpha"]).addcmul_(grad, grad, value=1 - g["alpha"])

@@ -92,3 +92,25 @@ def test_depthwise_epilogue_stats_offset(offset):
         # emulate the finalize: re-zero the shards, next shift = this batch mean
         st[:128].zero_()
         st[128].copy_(mean.float())
+
+
+def test_nonfinite_batch_does_not_poison_shift():
+    """the finalize stores each batch mean as the next batch's shift. A batch with an
+    Inf/NaN must not leave a non-finite shift behind: the following finite batch's statistics
+    (and so training after a skipped step) must be exact again."""
+    from deep_vision_amd import nn
+
+    torch.manual_seed(3)
+    C = 64
+    bn = nn.BatchNorm2d(C, momentum=1.0).to(DEV)
+    bad = torch.randn(8, C, 12, 12, device=DEV)
+    bad[0, 3, 0, 0] = float("inf")
+    bad[1, 7, 2, 2] = float("nan")
+    bn(_nhwc(bad))
+    torch.cuda.synchronize()
+    x = _nhwc(5 + torch.randn(8, C, 12, 12, device=DEV))
+    y = bn(x)
+    torch.cuda.synchronize()
+    assert torch.isfinite(bn.running_mean).all() and torch.isfinite(bn.running_var).all()
+    assert torch.isfinite(y.float()).all()
+    _check(bn, x.double(), 1, 5.0)

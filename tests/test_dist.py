@@ -355,3 +355,84 @@ def test_nan_skip_decision_identical_across_ranks():
         assert p.exitcode == 0
     assert res[0][0] == res[1][0] == [True, False, True, True]
     assert (res[0][1] == res[1][1]).all()  # replicas still identical after the skipped step
+
+
+class _NeverDone:
+    """Stands in for a torch.cuda.Event recorded after a replay whose all-reduce never completes."""
+
+    def query(self):
+        return False
+
+
+class _DoneAfter:
+    def __init__(self, n):
+        self.n = n
+
+    def query(self):
+        self.n -= 1
+        return self.n < 0
+
+
+def test_comm_watchdog_event_deadline_hook():
+    """GPU work tracked by event (graph replays) that never completes fires
+    the watchdog with EXIT_COMM_TIMEOUT; completed events are dropped in order."""
+    import time
+
+    from deep_vision_amd.parallel.watchdog import EXIT_COMM_TIMEOUT, CommWatchdog
+
+    fired = []
+    wd = CommWatchdog(timeout=0.3, poll=0.05, on_timeout=lambda c, why: fired.append((c, why)))
+    wd.track("done soon", _DoneAfter(2))
+    wd.start()
+    time.sleep(0.5)
+    assert not fired and wd.pending() == 0
+    wd.track("graph replay 7", _NeverDone())
+    t0 = time.time()
+    while not fired and time.time() - t0 < 5:
+        time.sleep(0.05)
+    wd.stop()
+    assert fired and fired[0][0] == EXIT_COMM_TIMEOUT and "graph replay 7" in fired[0][1]
+
+
+def test_comm_watchdog_event_deadline_exits_process():
+    """Without a hook the rank ends itself with os._exit(EXIT_COMM_TIMEOUT) -- no Python cleanup
+    that could block on a wedged communicator."""
+    import subprocess
+    import sys
+    import time
+
+    from deep_vision_amd.parallel.watchdog import EXIT_COMM_TIMEOUT
+
+    code = ("import time, sys; sys.path.insert(0, %r)\n"
+            "from deep_vision_amd.parallel.watchdog import CommWatchdog\n"
+            "class E:\n    def query(self): return False\n"
+            "wd = CommWatchdog(timeout=0.5, poll=0.05).start()\n"
+            "wd.track('graph replay 3', E())\n"
+            "time.sleep(30)\n") % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    t0 = time.time()
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == EXIT_COMM_TIMEOUT, (r.returncode, r.stderr[-500:])
+    assert time.time() - t0 < 20
+    assert "graph replay 3" in r.stderr
+
+
+def test_comm_watchdog_event_error_is_comm_error():
+    from deep_vision_amd.parallel.watchdog import EXIT_COMM_ERROR, CommWatchdog
+
+    class Boom:
+        def query(self):
+            raise RuntimeError("HIP error: the launch failed")
+
+    fired = []
+    wd = CommWatchdog(timeout=60, poll=0.05, on_timeout=lambda c, why: fired.append((c, why)))
+    wd.track("step 1", Boom())
+    late = wd._check_events(0.0)
+    assert late is not None and "launch failed" in late[2]
+    wd.start()
+    import time
+
+    t0 = time.time()
+    while not fired and time.time() - t0 < 5:
+        time.sleep(0.05)
+    wd.stop()
+    assert fired and fired[0][0] == EXIT_COMM_ERROR

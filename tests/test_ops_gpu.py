@@ -195,6 +195,23 @@ def test_gap_linear_xent():
     assert _rel(b.grad, br.grad) < 5e-2
 
 
+def test_xent_retain_graph_twice():
+    """a second backward through a retained graph gets the same (scaled) gradient."""
+    from deep_vision_amd import ops as F
+
+    logits = torch.randn(16, 100, device=DEV).requires_grad_(True)
+    lab = torch.randint(0, 100, (16,), device=DEV)
+    loss = F.cross_entropy(logits, lab)
+    (loss * 3).backward(retain_graph=True)
+    g1 = logits.grad.clone()
+    logits.grad = None
+    (loss * 3).backward()
+    lr =logits.detach().clone().requires_grad_(True)
+    (TF.cross_entropy(lr, lab) * 3).backward()
+    assert _rel(g1, lr.grad) < 1e-3
+    assert _rel(logits.grad, lr.grad) < 1e-3
+
+
 def test_linear_odd_sizes():
     from deep_vision_amd import ops as F
 
