@@ -73,7 +73,30 @@ struct FwdParams {
   const u16* bnx2;         // BNR: second BatchNorm fed by the same dz (kernels.h ConvFwdArgs), or nullptr
   const float* bnprm2;
   float* bnacc2;
+  // A-operand transform (template AT; kernels.h ConvFwdArgs at_*)
+  const u16* at_x;
+  const u16* at_r;
+  const uint8_t* at_bits_in;
+  uint8_t* at_bits_out;
+  u16* at_side;
+  const float* at_c[5];
+  int at_act; float at_slope;
 };
+
+// A-operand transforms (compile time). The A tile is staged through registers: global loads of
+// the source rows, the per-element BatchNorm form, ds_write into the same swizzled LDS image the
+// LDS-DMA path would have produced. Only 1x1 / stride-1 / unpadded single-group convs and dgrads:
+// A row m is source row m (dense, ld = ldx).
+//   AT_BN   a = act(x*c0 + c1)                        (BN -> act feeding the conv)
+//   AT_JOIN a = act(x*c0 + (c1 + c3) + r*c2)           (residual join, r the identity (c2 = 1, c3 = 0)
+//                                                       or a second BN's input; + mask bits)
+//   AT_BWDB a = c0*dz + c1*x + c2, dz = bit ? r : slope*r / 0  (BN backward, stored mask bits)
+//   AT_BWDX a = c0*dz + c1*x + c2, dz = act'(x*c3 + c4) * r    (BN backward, mask recomputed)
+enum { AT_NONE = 0, AT_BN = 1, AT_JOIN = 2, AT_BWDB = 3, AT_BWDX = 4 };
+template <int AT>
+constexpr int at_ncoef() { return AT == AT_BN ? 2 : AT == AT_JOIN ? 4 : AT == AT_BWDB ? 3 : AT == AT_BWDX ? 5 : 0; }
+template <int AT>
+constexpr bool at_has_r() { return AT >= AT_JOIN; }
 
 // ReflectionPad2d index map (pad < n): -1 -> 1, n -> n - 2
 DV_DEVICE int reflect_idx(int i, int n) {
@@ -158,7 +181,7 @@ enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_FULL = 2 };
 // from one block, whose deep LDS ring then holds one CU); __launch_bounds__' second argument is
 // waves per SIMD, so both forms get up to 256 VGPRs.
 template <int BM_, int BN_, int BK_, int KMODE, bool RES, int STAGES, int BNR = 0, int EPI = EPI_FULL,
-          int WMT = 64>
+          int WMT = 64, int AT = AT_NONE>
 __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_kernel(FwdParams p) {
   constexpr int WN = BN_ / 64, WM = BM_ / WMT;
   constexpr int NW = WN * WM;
@@ -247,7 +270,9 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
       const bool ok = wok[j] && (KMODE == KM_FAST || k0 + lc * 8 < p.K);
       glds16(ok ? (const void*)(wrow[j] + k0) : (const void*)zero, img_n + (wid * NI + j) * 1024);
     }
-    if (KMODE == KM_FAST) {
+    if constexpr (AT != AT_NONE) {
+      // A comes through registers (aload / acommit below)
+    } else if (KMODE == KM_FAST) {
       const int64_t koff = ((int64_t)(t_r * p.dh) * p.Win + t_s * p.dw) * p.ldx + t_c;
       const int sh_r = t_r, sh_s = 16 + t_s;
 #pragma unroll
@@ -312,7 +337,117 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
           acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[j], fb[i], acc[j][i], 0, 0, 0);
     }
   };
-  if constexpr (STAGES == 2) {
+  // ---------------- register-staged A operand (AT) ----------------
+  // thread -> (chunk column a_c, rows a_r0 + i*ARP): a thread's 8 channels are the same for all of
+  // its rows, so one set of coefficients per K-tile (read from the LDS copy staged at entry)
+  constexpr int ACH = BK_ / 8, ARP = (64 * NW) / ACH;
+  constexpr int AI = AT != AT_NONE ? BM_ / ARP : 1;
+  constexpr int NCO = at_ncoef<AT>();
+  static_assert(AT == AT_NONE || (ARP * ACH == 64 * NW && AI * ARP == BM_), "A staging rows must split evenly");
+  static_assert(AT == AT_NONE || STAGES == 2, "register-staged A runs on the double buffer");
+  const int a_c = threadIdx.x % ACH, a_r0 = threadIdx.x / ACH;
+  uint4 ax[AI], ar[AI];
+  uint32_t abits[AI];
+  float* coef = reinterpret_cast<float*>(smem + STAGES * STAGE);  // [NCO][K]
+  // column-tile 0 of each M-panel materialises the transformed operand (side output)
+  const bool a_side = AT != AT_NONE && tn == 0 && split == 0 && grp == 0;
+  auto aload = [&](int kt) {
+    const int64_t k = (int64_t)kt * BK_ + a_c * 8;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      // rows past M read row M-1 (valid memory, results never stored): no branch around the load
+      const int m = min(m0 + a_r0 + i * ARP, p.M - 1);
+      const int64_t off = (int64_t)m * p.ldx + k;
+      ax[i] = *reinterpret_cast<const uint4*>(p.at_x + off);
+      if constexpr (at_has_r<AT>()) ar[i] = *reinterpret_cast<const uint4*>(p.at_r + off);
+      if constexpr (AT == AT_BWDB) abits[i] = p.at_bits_in[off >> 3];
+    }
+  };
+  auto acommit = [&](int kt, int buf) {
+    char* img_m = smem + buf * STAGE + BN_ * BK_ * 2;
+    const int kc = kt * BK_ + a_c * 8;
+    f32x2 cf[NCO > 0 ? NCO : 1][4];
+#pragma unroll
+    for (int j = 0; j < NCO; ++j) {
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(coef + j * p.K + kc);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(coef + j * p.K + kc + 4);
+      cf[j][0] = f32x2{lo[0], lo[1]}; cf[j][1] = f32x2{lo[2], lo[3]};
+      cf[j][2] = f32x2{hi[0], hi[1]}; cf[j][3] = f32x2{hi[2], hi[3]};
+    }
+    if constexpr (AT == AT_JOIN) {  // one shift per channel: c1 + c3 (bn_apply_kernel RBN order)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) cf[1][e] += cf[3][e];
+    }
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int row = a_r0 + i * ARP;
+      const uint32_t xw[4] = {ax[i].x, ax[i].y, ax[i].z, ax[i].w};
+      uint32_t rw[4] = {0u, 0u, 0u, 0u};
+      if constexpr (at_has_r<AT>()) { rw[0] = ar[i].x; rw[1] = ar[i].y; rw[2] = ar[i].z; rw[3] = ar[i].w; }
+      uint32_t ow[4], mb = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const f32x2 x = bf2x(xw[e]);
+        f32x2 v;
+        if constexpr (AT == AT_BN || AT == AT_JOIN) {
+          f32x2 z = __builtin_elementwise_fma(x, cf[0][e], cf[1][e]);
+          if constexpr (AT == AT_JOIN) z = __builtin_elementwise_fma(bf2x(rw[e]), cf[2][e], z);
+          mb |= (z.x > 0.f ? 1u : 0u) << (2 * e);
+          mb |= (z.y > 0.f ? 1u : 0u) << (2 * e + 1);
+          if (p.at_act == ACT_RELU) { v.x = fmaxf(z.x, 0.f); v.y = fmaxf(z.y, 0.f); }
+          else if (p.at_act == ACT_LEAKY) { v.x = z.x > 0.f ? z.x : z.x * p.at_slope; v.y = z.y > 0.f ? z.y : z.y * p.at_slope; }
+          else v = z;
+        } else {
+          const f32x2 d = bf2x(rw[e]);
+          const f32x2 neg = p.at_act == ACT_LEAKY ? d * p.at_slope : f32x2{0.f, 0.f};
+          f32x2 dz = d;
+          if constexpr (AT == AT_BWDB) {
+            dz.x = ((abits[i] >> (2 * e)) & 1u) ? d.x : neg.x;
+            dz.y = ((abits[i] >> (2 * e + 1)) & 1u) ? d.y : neg.y;
+          } else if (p.at_act) {
+            const f32x2 z = __builtin_elementwise_fma(x, cf[3][e], cf[4][e]);
+            dz.x = z.x > 0.f ? d.x : neg.x;
+            dz.y = z.y > 0.f ? d.y : neg.y;
+          }
+          v = __builtin_elementwise_fma(cf[0][e], dz, __builtin_elementwise_fma(cf[1][e], x, cf[2][e]));
+        }
+        ow[e] = pack2bf(v.x, v.y);
+      }
+      const uint4 o = uint4{ow[0], ow[1], ow[2], ow[3]};
+      *reinterpret_cast<uint4*>(img_m + row * (BK_ * 2) + ((a_c ^ kc_swz<BK_>(row)) << 4)) = o;
+      const int m = m0 + row;
+      if (a_side && m < p.M) {
+        const int64_t off = (int64_t)m * p.ldx + kc;
+        if (p.at_side) *reinterpret_cast<uint4*>(p.at_side + off) = o;
+        if constexpr (AT == AT_BN || AT == AT_JOIN) {
+          if (p.at_bits_out) p.at_bits_out[off >> 3] = (uint8_t)mb;
+        }
+      }
+    }
+  };
+
+  if constexpr (AT != AT_NONE) {
+    // coefficient vectors -> LDS once per block (behind the operand stages)
+#pragma unroll
+    for (int j = 0; j < NCO; ++j)
+      for (int k = threadIdx.x * 4; k < p.K; k += 64 * NW * 4)
+        *reinterpret_cast<f32x4*>(coef + j * p.K + k) = *reinterpret_cast<const f32x4*>(p.at_c[j] + k);
+    aload(kt0);
+    stage(kt0, 0);
+    advance();
+    __syncthreads();  // coefficients visible
+    acommit(kt0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int t = 0; t < nt; ++t) {
+      const int cur = t & 1;
+      if (t + 1 < nt) { aload(kt0 + t + 1); stage(kt0 + t + 1, cur ^ 1); advance(); }
+      compute(cur);
+      if (t + 1 < nt) acommit(kt0 + t + 1, cur ^ 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else if constexpr (STAGES == 2) {
     // double buffer, one barrier per K-tile: the DMA of tile t+1 overlaps the MFMAs of tile t
     stage(kt0, 0);
     advance();
@@ -877,13 +1012,23 @@ constexpr int lds_bytes(int stages) {
   return stages * stage_bytes<BM_, BN_, BK_>() > epi ? stages * stage_bytes<BM_, BN_, BK_>() : epi;
 }
 
+// dynamic LDS of an A-transform launch: the operand stages, then the [NCO][K] coefficients
+template <int BM_, int BN_, int BK_, int WMT, int AT>
+size_t at_lds_bytes(int K) {
+  const size_t a = (size_t)2 * stage_bytes<BM_, BN_, BK_>() + (size_t)at_ncoef<AT>() * K * 4;
+  const size_t b = lds_bytes<BM_, BN_, BK_, WMT>(2);
+  return a > b ? a : b;
+}
+constexpr size_t LDS_MAX = 160 * 1024;
+
 template <int BM_, int BN_, int BK_, int KMODE, bool RES, int STAGES, int BNR = 0, int EPI = EPI_FULL,
-          int WMT = 64>
+          int WMT = 64, int AT = AT_NONE>
 void launch_fwd(const FwdParams& p, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES, BNR, EPI, WMT>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes<BM_, BN_, BK_, WMT>(STAGES));
+    hipFuncSetAttribute((const void*)conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES, BNR, EPI, WMT, AT>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize,
+                        AT != AT_NONE ? (int)LDS_MAX : lds_bytes<BM_, BN_, BK_, WMT>(STAGES));
     attr = true;
   }
   FwdParams q = p;
@@ -892,9 +1037,10 @@ void launch_fwd(const FwdParams& p, hipStream_t st) {
   q.kt_per = (nt_all + q.ksplit - 1) / q.ksplit;
   q.ksplit = (nt_all + q.kt_per - 1) / q.kt_per;  // no empty splits
   const int nt = q.kt_per;
-  const size_t lds = lds_bytes<BM_, BN_, BK_, WMT>(nt < STAGES ? nt : STAGES);
+  const size_t lds = AT != AT_NONE ? at_lds_bytes<BM_, BN_, BK_, WMT, AT>(p.K)
+                                   : lds_bytes<BM_, BN_, BK_, WMT>(nt < STAGES ? nt : STAGES);
   const int blocks = ((p.M + BM_ - 1) / BM_) * ((p.N + BN_ - 1) / BN_) * p.G * q.ksplit;
-  conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES, BNR, EPI, WMT>
+  conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES, BNR, EPI, WMT, AT>
       <<<dim3(blocks), dim3(64 * n_waves<BM_, BN_, WMT>()), lds, st>>>(q);
   if (p.ypart) g_last_ksplit = q.ksplit;
 }
@@ -967,6 +1113,44 @@ void dispatch_res(const FwdParams& p, hipStream_t st) {
     return;
   }
   launch_heuristic<KMODE, RES, 0, EPI_FULL>(p, st);
+}
+
+// A-transform launches (csrc kernels.h ConvFwdArgs at_*): the heuristic's tile set on the
+// double buffer; the 8-wave 256x256 tile only when its 128 KB of stages leave room for the
+// coefficients
+template <int AT, bool RES, int BNR, int EPI>
+void launch_at(const FwdParams& p, hipStream_t st) {
+  if (big_tile_ok<KM_FAST>(p) && at_lds_bytes<256, 256, 64, 128, AT>(p.K) <= LDS_MAX)
+    launch_fwd<256, 256, 64, KM_FAST, RES, 2, BNR, EPI, 128, AT>(p, st);
+  else if (p.N <= 64) launch_fwd<256, 64, 32, KM_FAST, RES, 2, BNR, EPI, 64, AT>(p, st);
+  else if (p.K > 64 && p.K < 2048) launch_fwd<128, 128, 32, KM_FAST, RES, 2, BNR, EPI, 64, AT>(p, st);
+  else launch_fwd<128, 128, 64, KM_FAST, RES, 2, BNR, EPI, 64, AT>(p, st);
+}
+
+template <int AT, bool RES, int BNR>
+void dispatch_at_epi(const FwdParams& p, hipStream_t st) {
+  if constexpr (AT == AT_BWDB || AT == AT_BWDX || BNR) {
+    launch_at<AT, RES, BNR, EPI_PLAIN>(p, st);  // dgrads: plain store (+ fused BN-backward sums)
+  } else {
+    const bool full = p.bias || p.act;
+    if (full) launch_at<AT, RES, 0, EPI_FULL>(p, st);
+    else if (p.stats) launch_at<AT, RES, 0, EPI_STATS>(p, st);
+    else launch_at<AT, RES, 0, EPI_PLAIN>(p, st);
+  }
+}
+
+template <int AT>
+void dispatch_at(const FwdParams& p, hipStream_t st) {
+  const int bnr = p.bnmode ? (p.bnx2 ? 2 : 1) : 0;
+  if (p.res) {
+    if (bnr == 2) dispatch_at_epi<AT, true, 2>(p, st);
+    else if (bnr == 1) dispatch_at_epi<AT, true, 1>(p, st);
+    else dispatch_at_epi<AT, true, 0>(p, st);
+  } else {
+    if (bnr == 2) dispatch_at_epi<AT, false, 2>(p, st);
+    else if (bnr == 1) dispatch_at_epi<AT, false, 1>(p, st);
+    else dispatch_at_epi<AT, false, 0>(p, st);
+  }
 }
 
 template <int KMODE>
@@ -1069,6 +1253,10 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
   p.resbits = (const uint8_t*)a.resbits; p.resact = a.resact; p.resslope = a.resslope;
   p.reflect = a.reflect;
   p.ksplit = 1; p.kt_per = 1 << 30; p.ypart = nullptr;
+  p.at_x = (const u16*)a.at_x; p.at_r = (const u16*)a.at_r; p.at_bits_in = (const uint8_t*)a.at_bits_in;
+  p.at_bits_out = (uint8_t*)a.at_bits_out; p.at_side = (u16*)a.at_side;
+  for (int j = 0; j < 5; ++j) p.at_c[j] = a.at_c[j];
+  p.at_act = a.at_act; p.at_slope = a.at_slope;
   // zero-filling scatter: plain epilogue, no residual, a strided map with no offset whose
   // siblings tile the output grid (OH <= P*osh, OW <= Q*osw), vector stores
   p.zfill = a.zfill;
@@ -1140,6 +1328,25 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
     return bn_status;
   }
   if (p.Cg % 8 != 0 || p.ldx % 8 != 0) return -1;
+  if (a.at) {
+    // A-transform: every A row is one dense source row (1x1, stride 1, no padding, one group, the
+    // fast loader's whole K-tiles), no split-K; the coefficient vectors must all be present
+    const bool geo = a.R == 1 && a.S == 1 && a.sh == 1 && a.sw == 1 && a.ph == 0 && a.pw == 0 && a.H == a.P &&
+                     a.W == a.Q && a.G == 1 && !a.tgather && !a.reflect && !p.ypart && !p.zfill && p.Cg % 64 == 0 &&
+                     a.at_x && (a.at < AT_JOIN || a.at_r) && (a.at != AT_BWDB || a.at_bits_in);
+    int nco = a.at == AT_BN ? 2 : a.at == AT_JOIN ? 4 : a.at == AT_BWDB ? 3 : a.at == AT_BWDX ? 5 : -1;
+    bool cok = nco > 0;
+    for (int j = 0; j < nco && cok; ++j) cok = a.at_c[j] != nullptr && ((uintptr_t)a.at_c[j] & 15) == 0;
+    // the 128x128 / 256x64 tiles' stages (<= 64 KB) plus the coefficients must fit one block's LDS
+    if (!geo || !cok || (size_t)65536 + (size_t)nco * p.K * 4 > LDS_MAX) return -1;
+    switch (a.at) {
+      case AT_BN: dispatch_at<AT_BN>(p, st); break;
+      case AT_JOIN: dispatch_at<AT_JOIN>(p, st); break;
+      case AT_BWDB: dispatch_at<AT_BWDB>(p, st); break;
+      default: dispatch_at<AT_BWDX>(p, st); break;
+    }
+    return bn_status;
+  }
   // warp-specialised ring (benchmark variants 20: 128x128, 21: 256x64, 22: 256x128, 23: 128x256)
   if (g_fwd_variant >= 20 && g_fwd_variant <= 23 && !a.tgather && p.Cg % 64 == 0 && p.R <= 16 && p.S <= 16 &&
       !p.reflect && p.G == 1 && p.identity_map && !p.bias && !p.act && !p.res && !p.bnmode && !p.ypart && !p.zfill &&
