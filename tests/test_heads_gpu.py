@@ -199,8 +199,8 @@ def _compare_model(make, inputs, loss_fn, out_cos=0.99, grad_cos=0.97, train=Tru
 
     Eval mode: direct thresholds. Train mode: random-init nets with batch-statistics BN at
     small batch amplify *any* bf16 rounding (PyTorch's own autocast-bf16 path reaches only
-    ~0.2-0.4 median gradient cosine to fp32 on ResNet-50 / MobileNet there, see
-    tools/debug_gradcmp.py), so the native path is held to the torch-bf16 baseline instead."""
+    ~0.2-0.4 median gradient cosine to fp32 on ResNet-50 / MobileNet there, measured with a
+    one-off comparison script in round 3), so the native path is held to the torch-bf16 baseline."""
     m, out = _run_variant(make, inputs, loss_fn, train, "native")
     ref, out_r = _run_variant(make, inputs, loss_fn, train, "fp32")
     base = _run_variant(make, inputs, loss_fn, train, "bf16") if train else None

@@ -191,3 +191,22 @@ def test_entry_point_cli(tmp_path):
                        env=env, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "Validation Top 1 acc" in r.stdout and any(f.startswith("lenet5-") for f in os.listdir(tmp_path))
+
+
+@pytest.mark.parametrize("fam,target,model", [("ResNet/pytorch", "train_resnet50", "resnet50"),
+                                              ("ResNet/tensorflow", "train_resnet152", "resnet152"),
+                                              ("AlexNet/tensorflow", "train_alexnet2", "alexnet2"),
+                                              ("LeNet/tensorflow", "train_lenet5", "lenet5")])
+def test_family_makefile_targets(fam, target, model):
+    """The reference's run UX (R/<Family>/<fw>/Makefile): `make train_<model>` starts a nohup'ed
+    train.py -m <model> writing <model>-<time>.log (dry run: the command line only)."""
+    import os
+    import shutil
+    import subprocess
+
+    if shutil.which("make") is None:
+        pytest.skip("make not installed")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run(["make", "-n", "-C", os.path.join(root, fam), target], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert f"train.py -m {model}" in r.stdout and "nohup" in r.stdout and f"{model}-" in r.stdout
