@@ -208,6 +208,11 @@ PYBIND11_MODULE(_C, m) {
     return r;
   });
   m.def("stem_tuning", [](int blocks, int wg_blocks) { dv_stem_tuning(blocks, wg_blocks); });
+  m.def("u8_normalize", [](uptr x, uptr flip, uptr y, int N, int C, int H, int W, float scale, std::vector<float> mean,
+                           std::vector<float> sd, uptr st) {
+    if (C < 1 || C > 3 || (int)mean.size() < C || (int)sd.size() < C) throw std::runtime_error("u8_normalize: 1-3 channels");
+    dv_u8_normalize(CP(x), CP(flip), P(y), N, C, H, W, scale, mean.data(), sd.data(), ST(st)); check_last("u8_normalize");
+  });
   m.def("stem_pack", [](uptr x, int is_f32, uptr y, int N, int C, int H, int W, int Hp, int Wp, int pt, int pl, uptr st,
                         int reflect) {
     dv_stem_pack(CP(x), is_f32, P(y), N, C, H, W, Hp, Wp, pt, pl, reflect, ST(st)); check_last("stem_pack");

@@ -311,6 +311,41 @@ __global__ void stem_pack_kernel(const T* __restrict__ x, u16* __restrict__ y, i
   }
 }
 
+// Input pipeline, device side (data/device_input.py): uint8 HWC crops as the loader workers ship
+// them (a quarter of the fp32 CHW bytes over PCIe) -> normalised bf16 NCHW network input:
+// y[n][c][h][w] = (x[n][h][w'][c] * scale - mean[c]) / std[c], w' = W-1-w for flipped samples.
+// One thread per output pixel quad (4 consecutive w of one (n, c, h)): 8-B stores.
+__global__ void u8_normalize_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ flip,
+                                    u16* __restrict__ y, int N, int C, int H, int W, float scale, float m0, float m1,
+                                    float m2, float is0, float is1, float is2) {
+  const int WQ = (W + 3) / 4;
+  const int64_t total = (int64_t)N * C * H * WQ;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int wq = (int)(t % WQ);
+    int64_t r = t / WQ;
+    const int h = (int)(r % H); r /= H;
+    const int c = (int)(r % C);
+    const int64_t n = r / C;
+    const bool f = flip && flip[n];
+    const float m = c == 0 ? m0 : (c == 1 ? m1 : m2), is = c == 0 ? is0 : (c == 1 ? is1 : is2);
+    const uint8_t* row = x + ((n * H + h) * (int64_t)W) * C + c;
+    u16 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int w = wq * 4 + k;
+      const int ws = f ? W - 1 - w : w;
+      v[k] = w < W ? f2bf(((float)row[(int64_t)ws * C] * scale - m) * is) : (u16)0;
+    }
+    u16* out = y + ((n * C + c) * (int64_t)H + h) * W + wq * 4;
+    if ((W & 3) == 0) {
+      uint2 pk; pk.x = v[0] | ((uint32_t)v[1] << 16); pk.y = v[2] | ((uint32_t)v[3] << 16);
+      *reinterpret_cast<uint2*>(out) = pk;
+    } else {
+      for (int k = 0; k < 4 && wq * 4 + k < W; ++k) out[k] = v[k];
+    }
+  }
+}
+
 // NHWC channel-slice copy / gather: dst[row][c] = src[row][idx ? idx[c] : c] for c < C.
 // Contiguous copies (concat into a channel slice) move 16-B vectors; gathers (channel shuffle
 // and its inverse) read 2-B elements through the index table.
@@ -436,6 +471,14 @@ void dv_wgrad_unprep(float* src, float* dst, int G, int Og, int Ig, int R, int S
   }
   wgrad_unprep_kernel<<<grid_for(total), NT, 0, st>>>(src, dst, G, Og, Ig, R, S, Ipad, alpha, accumulate, zero_src);
 }
+void dv_u8_normalize(const void* x, const void* flip, void* y, int N, int C, int H, int W, float scale, const float* mean,
+                     const float* std_, hipStream_t st) {
+  const int64_t total = (int64_t)N * C * H * ((W + 3) / 4);
+  u8_normalize_kernel<<<grid_for(total), NT, 0, st>>>((const uint8_t*)x, (const uint8_t*)flip, (u16*)y, N, C, H, W, scale,
+                                                     mean[0], C > 1 ? mean[1] : 0.f, C > 2 ? mean[2] : 0.f, 1.f / std_[0],
+                                                     C > 1 ? 1.f / std_[1] : 1.f, C > 2 ? 1.f / std_[2] : 1.f);
+}
+
 void dv_to_nhwc(const void* x, int x_is_f32, void* y, int N, int C, int H, int W, int Cp, hipStream_t st) {
   const int64_t total = (int64_t)N * H * W * (Cp / 8);
   if (x_is_f32) to_nhwc_kernel<float><<<grid_for(total), NT, 0, st>>>((const float*)x, (u16*)y, N, C, H, W, Cp);

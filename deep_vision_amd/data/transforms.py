@@ -147,13 +147,38 @@ class ColorJitter:
         return {**sample, "image": np.asarray(image)}
 
 
-def imagenet_train_transform():
-    """R/ResNet/pytorch/train.py:315-324."""
+class ToUint8:
+    """Final step of the device-normalised pipeline (data/device_input.py): the HWC uint8 crop
+    as a tensor (grayscale expanded to 3 channels) plus the horizontal-flip draw, which the device
+    kernel applies together with ToTensor + Normalize. 150 KB per 224x224 image instead of 602."""
+
+    def __init__(self, flip_p=0.0):
+        self.flip_p = flip_p
+
+    def __call__(self, sample):
+        image = sample["image"]
+        if image.ndim == 2:
+            image = np.stack((image,) * 3, axis=-1)
+        flip = self.flip_p > 0 and random.random() < self.flip_p
+        image = np.ascontiguousarray(image)
+        if not image.flags.writeable:  # PIL-backed arrays are read-only
+            image = image.copy()
+        return {**sample, "image": torch.from_numpy(image), "flip": flip}
+
+
+def imagenet_train_transform(device_normalize=False):
+    """R/ResNet/pytorch/train.py:315-324. ``device_normalize``: stop at the uint8 crop + flip
+    draw; flip, ToTensor and Normalize run on the GPU (data.device_input)."""
+    if device_normalize:
+        return Compose([Rescale(256), RandomCrop(224), ColorJitter(brightness=0.2, contrast=0.2, saturation=0.2, hue=0),
+                        ToUint8(flip_p=0.5)])
     return Compose([Rescale(256), RandomHorizontalFlip(0.5), RandomCrop(224),
                     ColorJitter(brightness=0.2, contrast=0.2, saturation=0.2, hue=0), ToTensor(),
                     Normalize(IMAGENET_MEAN, IMAGENET_STD)])
 
 
-def imagenet_val_transform():
+def imagenet_val_transform(device_normalize=False):
     """R/ResNet/pytorch/train.py:326-331."""
+    if device_normalize:
+        return Compose([Rescale(256), CenterCrop(224), ToUint8()])
     return Compose([Rescale(256), CenterCrop(224), ToTensor(), Normalize(IMAGENET_MEAN, IMAGENET_STD)])

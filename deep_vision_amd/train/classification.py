@@ -27,6 +27,7 @@ from .. import ops as F
 from ..config import TrainConfig, get_config
 from ..data import transforms as T
 from ..data.datasets import ImageNet2012Dataset, MnistDataset, SyntheticClassification
+from ..data.device_input import batch_images
 from ..data.loader import DevicePrefetcher, make_loader, set_epoch
 from ..utils.tensorboard import SummaryWriter
 from . import checkpoint as C
@@ -88,8 +89,9 @@ def build_datasets(cfg: TrainConfig, data_dir=None, synthetic=False, synthetic_s
         if not os.path.isfile(labels):
             labels = None  # the packaged ImageNet-2012 synset list (data.imagenet_meta)
         if os.path.isdir(tr):
-            return (ImageNet2012Dataset(tr, labels, T.imagenet_train_transform()),
-                    ImageNet2012Dataset(va, labels, T.imagenet_val_transform()))
+            dn = bool(cfg.extras.get("device_normalize", True))  # uint8 crops, normalised on the GPU
+            return (ImageNet2012Dataset(tr, labels, T.imagenet_train_transform(device_normalize=dn)),
+                    ImageNet2012Dataset(va, labels, T.imagenet_val_transform(device_normalize=dn)))
     return (SyntheticClassification(synthetic_size, cfg.input_shape, nc, key, seed=1),
             SyntheticClassification(max(64, synthetic_size // 4), cfg.input_shape, nc, key, seed=2))
 
@@ -118,7 +120,7 @@ def train(loader, net, optimizer, epoch, loggers, eng: Engine, cfg: TrainConfig,
     for batch_i, data in enumerate(loader):
         if max_steps is not None and batch_i >= max_steps:
             break
-        image = data["image"].to(eng.device, non_blocking=True)
+        image = batch_images(data, eng.device)
         target = data[key].to(eng.device, dtype=torch.long, non_blocking=True)
         with eng.timer.step(samples=image.shape[0]):
             lr = C.get_lr(optimizer)
@@ -193,7 +195,7 @@ def validate(loader, net, epoch, loggers, eng: Engine, cfg: TrainConfig, max_ste
         for batch_i, data in enumerate(loader):
             if max_steps is not None and batch_i >= max_steps:
                 break
-            image = data["image"].to(eng.device, non_blocking=True)
+            image = batch_images(data, eng.device)
             target = data[key].to(eng.device, dtype=torch.long, non_blocking=True)
             out = net(image)
             out = out[0] if isinstance(out, tuple) else out

@@ -237,3 +237,30 @@ def test_celeba_split_and_val_flatten(tmp_path):
     assert flatten_imagenet_val(str(val), str(labels), str(tmp_path / "vf")) == 2
     assert sorted(os.listdir(tmp_path / "vf")) == ["n01751748_ILSVRC2012_val_00000001.JPEG",
                                                    "n09193705_ILSVRC2012_val_00000002.JPEG"]
+
+
+def test_uint8_pipeline_matches_float_pipeline():
+    """workers ship uint8 HWC crops + a flip draw; flip / ToTensor / Normalize
+    on the device (here the CPU arm of data.device_input) equal the reference float pipeline."""
+    import random as pyrandom
+
+    import numpy as np
+
+    from deep_vision_amd.data import transforms as T
+    from deep_vision_amd.data.device_input import normalize_u8
+
+    rng = np.random.RandomState(0)
+    img = rng.randint(0, 256, (300, 420, 3), dtype=np.uint8)
+    ref_t = T.Compose([T.Rescale(256), T.CenterCrop(224), T.ToTensor(), T.Normalize(T.IMAGENET_MEAN, T.IMAGENET_STD)])
+    u8_t = T.Compose([T.Rescale(256), T.CenterCrop(224), T.ToUint8(flip_p=1.0)])
+    ref = ref_t({"image": img, "annotation": 3})["image"]
+    s = u8_t({"image": img, "annotation": 3})
+    assert s["image"].dtype == torch.uint8 and tuple(s["image"].shape) == (224, 224, 3) and s["flip"]
+    assert s["image"].numel() * s["image"].element_size() * 4 == ref.numel() * ref.element_size()  # 4x fewer bytes
+    batch = torch.utils.data.default_collate([s, {**s, "flip": False}])
+    out = normalize_u8(batch["image"], batch["flip"])
+    assert torch.allclose(out[0], ref.flip(2), atol=1e-4)
+    assert torch.allclose(out[1], ref, atol=1e-4)
+    pyrandom.seed(0)
+    tr = T.imagenet_train_transform(device_normalize=True)({"image": img, "annotation": 1})
+    assert tr["image"].dtype == torch.uint8 and isinstance(tr["flip"], bool)

@@ -702,3 +702,16 @@ def test_reflect_pad_fused_conv(case):
         assert _rel(x.grad, xr.grad) < 3e-2
     if has_b:
         assert _rel(b.grad, br.grad) < 3e-2
+
+
+@pytest.mark.parametrize("W", [224, 30])
+def test_u8_normalize_kernel(W):
+    """csrc u8_normalize: uint8 HWC crops + flip flags -> bf16 NCHW, vs the fp32 torch form."""
+    from deep_vision_amd.data.device_input import normalize_u8
+
+    x = torch.randint(0, 256, (5, 17, W, 3), dtype=torch.uint8)
+    flip = torch.tensor([1, 0, 1, 1, 0], dtype=torch.bool)
+    ref = normalize_u8(x, flip)
+    out = normalize_u8(x.to(DEV), flip.to(DEV))
+    assert out.dtype == torch.bfloat16 and tuple(out.shape) == (5, 3, 17, W)
+    assert torch.allclose(out.float().cpu(), ref, rtol=1e-2, atol=1e-2)
