@@ -481,7 +481,9 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
     bool cok = nco > 0;
     for (int j = 0; j < nco && cok; ++j) cok = a.at_c[j] != nullptr && ((uintptr_t)a.at_c[j] & 15) == 0;
     // the 128x128 / 256x64 tiles' stages (<= 64 KB) plus the coefficients must fit one block's LDS
-    if (!geo || !cok || (size_t)65536 + (size_t)nco * p.K * 4 > LDS_MAX) return -1;
+    // the widest A-transform stage set: 3 x 256x64x32 stages with dout + bits (about 122 KB)
+    if (!geo || !cok || (size_t)3 * 41984 + (size_t)nco * p.K * 4 > LDS_MAX) return -1;
+    p.x = p.at_x;  // the LDS-DMA loader stages the raw BN input; the transform runs per fragment
     dv_conv_fwd_at(p, a.at, st);
     return bn_status;
   }

@@ -141,6 +141,12 @@ DV_DEVICE bf16x8 read_kc(const char* img, int row, int chunk) {
 
 template <int BM_, int BN_, int BK_>
 constexpr int stage_bytes() { return (BM_ + BN_) * BK_ * 2; }
+// an A-transform stage also holds the raw second source (residual / dout, same image layout as
+// the A operand) and, for AT_BWDB, the tile's mask bits ([BM_][BK_/8] bytes, row-major)
+template <int BM_, int BN_, int BK_, int AT>
+constexpr int at_stage_bytes() {
+  return stage_bytes<BM_, BN_, BK_>() + (AT >= AT_JOIN ? BM_ * BK_ * 2 : 0) + (AT == AT_BWDB ? BM_ * BK_ / 8 : 0);
+}
 
 // BatchNorm-backward reduction terms of 8 stored gradient values `o` (bf16, exactly what the
 // unfused bn_bwd_reduce pass would read back) at element offset `off` of the BN input / mask:
@@ -211,7 +217,15 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
   constexpr int NI = BN_ / RPI / NW;   // N-operand DMA instructions per wave per K-tile
   static_assert(MI * RPI * NW == BM_ && NI * RPI * NW == BN_, "loader rows must split evenly over the waves");
   constexpr int KK = BK_ / 32;         // 32-deep MFMA steps per K-tile
-  constexpr int STAGE = stage_bytes<BM_, BN_, BK_>();
+  constexpr int STAGE = at_stage_bytes<BM_, BN_, BK_, AT>();
+  constexpr int NCO = at_ncoef<AT>();
+  // AT: second-source DMAs (MI per wave) and the tile's mask bits as 4-byte-per-lane DMAs (the
+  // sub-dword LDS-DMA forms do not pack lanes at their own width): NBW waves issue one each --
+  // all of them on the 256x64 tile, whose 3-deep ring counts them per wave (IPT)
+  constexpr int NBW = AT == AT_BWDB ? BM_ * BK_ / 8 / 256 : 0;
+  static_assert(AT != AT_BWDB || (NBW >= 1 && NBW <= NW && (STAGES == 2 || NBW == NW)), "mask-bit DMA split");
+  static_assert(AT == AT_NONE || (BK_ == 32 && KMODE == KM_FAST), "A-transform: BK 32 on the fast loader");
+  constexpr int IPT = MI + NI + (AT >= AT_JOIN ? MI : 0) + (AT == AT_BWDB ? 1 : 0);  // DMAs per wave per tile
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -285,15 +299,31 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
       const bool ok = wok[j] && (KMODE == KM_FAST || k0 + lc * 8 < p.K);
       glds16(ok ? (const void*)(wrow[j] + k0) : (const void*)zero, img_n + (wid * NI + j) * 1024);
     }
-    if constexpr (AT != AT_NONE) {
-      // A comes through registers (aload / acommit below)
-    } else if (KMODE == KM_FAST) {
+    if (KMODE == KM_FAST) {
       const int64_t koff = ((int64_t)(t_r * p.dh) * p.Win + t_s * p.dw) * p.ldx + t_c;
       const int sh_r = t_r, sh_s = 16 + t_s;
 #pragma unroll
       for (int j = 0; j < MI; ++j) {
         const bool ok = (tapmask[j] >> sh_r) & (tapmask[j] >> sh_s) & 1u;
         glds16(ok ? (const void*)(xrow[j] + koff) : (const void*)zero, img_m + (wid * MI + j) * 1024);
+      }
+      if constexpr (AT >= AT_JOIN) {  // raw residual / dout rows into the second image, same layout
+        char* img_r = img_m + BM_ * BK_ * 2;
+#pragma unroll
+        for (int j = 0; j < MI; ++j) {
+          const bool ok = (tapmask[j] >> sh_r) & (tapmask[j] >> sh_s) & 1u;
+          glds16(ok ? (const void*)(p.at_r + (xrow[j] - p.x) + koff) : (const void*)zero, img_r + (wid * MI + j) * 1024);
+        }
+      }
+      if constexpr (AT == AT_BWDB) {  // mask bits of the tile: [BM_][BK_/8] bytes, 4 per lane
+        if (wid < NBW) {
+          char* img_b = img_m + 2 * BM_ * BK_ * 2;
+          const int off = (wid * 64 + lane) * 4, row = off / (BK_ / 8), byte = off % (BK_ / 8);
+          const int m = m0 + row;
+          const void* src =
+              m < p.M ? (const void*)(p.at_bits_in + (((int64_t)m * p.ldx + t_c) >> 3) + byte) : (const void*)zero;
+          __builtin_amdgcn_global_load_lds(GLB_PTR(src), LDS_PTR(img_b + wid * 256), 4, 0, 0);
+        }
       }
     } else {
 #pragma unroll
@@ -333,7 +363,60 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
 #pragma unroll
     for (int b = 0; b < FM; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](int buf) {
+  float* coef = reinterpret_cast<float*>(smem + STAGES * STAGE);  // AT: [NCO][K] per-channel coefficients
+  // AT side output: the waves of output-column tile 0 (wave_n 0) store each transformed A element once
+  const bool a_side = AT != AT_NONE && tn == 0 && split == 0 && grp == 0 && wave_n == 0;
+  // A-transform of one fragment (8 consecutive channels of one pixel row) in registers, right before
+  // its MFMAs: the BN / join / BN-backward expression of kernels.h ConvFwdArgs at_*
+  auto at_fragment = [&](bf16x8& f, const char* img_m, int row, int chunk, int kt, const f32x2 (*cf)[4]) {
+    const uint4 xv = __builtin_bit_cast(uint4, f);
+    uint4 rv = uint4{0u, 0u, 0u, 0u};
+    uint32_t mbits = 0;
+    if constexpr (AT >= AT_JOIN)
+      rv = *reinterpret_cast<const uint4*>(img_m + BM_ * BK_ * 2 + row * (BK_ * 2) + ((chunk ^ kc_swz<BK_>(row)) << 4));
+    if constexpr (AT == AT_BWDB) mbits = *reinterpret_cast<const uint8_t*>(img_m + 2 * BM_ * BK_ * 2 + row * (BK_ / 8) + chunk);
+    const uint32_t xw[4] = {xv.x, xv.y, xv.z, xv.w}, rw[4] = {rv.x, rv.y, rv.z, rv.w};
+    uint32_t ow[4], mb = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const f32x2 x = bf2x(xw[e]);
+      f32x2 v;
+      if constexpr (AT == AT_BN || AT == AT_JOIN) {
+        f32x2 z = __builtin_elementwise_fma(x, cf[0][e], cf[1][e]);
+        if constexpr (AT == AT_JOIN) z = __builtin_elementwise_fma(bf2x(rw[e]), cf[2][e], z);
+        mb |= (z.x > 0.f ? 1u : 0u) << (2 * e);
+        mb |= (z.y > 0.f ? 1u : 0u) << (2 * e + 1);
+        if (p.at_act == ACT_RELU) { v.x = fmaxf(z.x, 0.f); v.y = fmaxf(z.y, 0.f); }
+        else if (p.at_act == ACT_LEAKY) { v.x = z.x > 0.f ? z.x : z.x * p.at_slope; v.y = z.y > 0.f ? z.y : z.y * p.at_slope; }
+        else v = z;
+      } else {
+        const f32x2 d = bf2x(rw[e]);
+        const f32x2 neg = p.at_act == ACT_LEAKY ? d * p.at_slope : f32x2{0.f, 0.f};
+        f32x2 dz = d;
+        if constexpr (AT == AT_BWDB) {
+          dz.x = ((mbits >> (2 * e)) & 1u) ? d.x : neg.x;
+          dz.y = ((mbits >> (2 * e + 1)) & 1u) ? d.y : neg.y;
+        } else if (p.at_act) {
+          const f32x2 z = __builtin_elementwise_fma(x, cf[3][e], cf[4][e]);
+          dz.x = z.x > 0.f ? d.x : neg.x;
+          dz.y = z.y > 0.f ? d.y : neg.y;
+        }
+        v = __builtin_elementwise_fma(cf[0][e], dz, __builtin_elementwise_fma(cf[1][e], x, cf[2][e]));
+      }
+      ow[e] = pack2bf(v.x, v.y);
+    }
+    const uint4 o = uint4{ow[0], ow[1], ow[2], ow[3]};
+    f = __builtin_bit_cast(bf16x8, o);
+    const int m = m0 + row;
+    if (a_side && m < p.M) {
+      const int64_t off = (int64_t)m * p.ldx + kt * BK_ + chunk * 8;
+      *reinterpret_cast<uint4*>(p.at_side + off) = o;
+      if constexpr (AT == AT_BN || AT == AT_JOIN) {
+        if (p.at_bits_out) p.at_bits_out[off >> 3] = (uint8_t)mb;
+      }
+    }
+  };
+  auto compute = [&](int buf, int kt) {
     const char* img_n = smem + buf * STAGE;
     const char* img_m = img_n + BN_ * BK_ * 2;
 #pragma unroll
@@ -345,6 +428,24 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
 #pragma unroll
       for (int i = 0; i < FM; ++i)
         fb[i] = read_kc<BK_>(img_m, wave_m * WMT + i * 16 + (lane & 15), kk * 4 + (lane >> 4));
+      if constexpr (AT != AT_NONE) {
+        const int chunk = kk * 4 + (lane >> 4);
+        const int kc = kt * BK_ + chunk * 8;
+        f32x2 cf[NCO > 0 ? NCO : 1][4];
+#pragma unroll
+        for (int j = 0; j < NCO; ++j) {
+          const f32x4 lo = *reinterpret_cast<const f32x4*>(coef + j * p.K + kc);
+          const f32x4 hi = *reinterpret_cast<const f32x4*>(coef + j * p.K + kc + 4);
+          cf[j][0] = f32x2{lo[0], lo[1]}; cf[j][1] = f32x2{lo[2], lo[3]};
+          cf[j][2] = f32x2{hi[0], hi[1]}; cf[j][3] = f32x2{hi[2], hi[3]};
+        }
+        if constexpr (AT == AT_JOIN) {  // one shift per channel: c1 + c3 (bn_apply_kernel RBN order)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) cf[1][e] += cf[3][e];
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i) at_fragment(fb[i], img_m, wave_m * WMT + i * 16 + (lane & 15), chunk, kt, cf);
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -352,117 +453,15 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
           acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[j], fb[i], acc[j][i], 0, 0, 0);
     }
   };
-  // ---------------- register-staged A operand (AT) ----------------
-  // thread -> (chunk column a_c, rows a_r0 + i*ARP): a thread's 8 channels are the same for all of
-  // its rows, so one set of coefficients per K-tile (read from the LDS copy staged at entry)
-  constexpr int ACH = BK_ / 8, ARP = (64 * NW) / ACH;
-  constexpr int AI = AT != AT_NONE ? BM_ / ARP : 1;
-  constexpr int NCO = at_ncoef<AT>();
-  static_assert(AT == AT_NONE || (ARP * ACH == 64 * NW && AI * ARP == BM_), "A staging rows must split evenly");
-  static_assert(AT == AT_NONE || STAGES == 2, "register-staged A runs on the double buffer");
-  const int a_c = threadIdx.x % ACH, a_r0 = threadIdx.x / ACH;
-  uint4 ax[AI], ar[AI];
-  uint32_t abits[AI];
-  float* coef = reinterpret_cast<float*>(smem + STAGES * STAGE);  // [NCO][K]
-  // column-tile 0 of each M-panel materialises the transformed operand (side output)
-  const bool a_side = AT != AT_NONE && tn == 0 && split == 0 && grp == 0;
-  auto aload = [&](int kt) {
-    const int64_t k = (int64_t)kt * BK_ + a_c * 8;
-#pragma unroll
-    for (int i = 0; i < AI; ++i) {
-      // rows past M read row M-1 (valid memory, results never stored): no branch around the load
-      const int m = min(m0 + a_r0 + i * ARP, p.M - 1);
-      const int64_t off = (int64_t)m * p.ldx + k;
-      ax[i] = *reinterpret_cast<const uint4*>(p.at_x + off);
-      if constexpr (at_has_r<AT>()) ar[i] = *reinterpret_cast<const uint4*>(p.at_r + off);
-      if constexpr (AT == AT_BWDB) abits[i] = p.at_bits_in[off >> 3];
-    }
-  };
-  auto acommit = [&](int kt, int buf) {
-    char* img_m = smem + buf * STAGE + BN_ * BK_ * 2;
-    const int kc = kt * BK_ + a_c * 8;
-    f32x2 cf[NCO > 0 ? NCO : 1][4];
-#pragma unroll
-    for (int j = 0; j < NCO; ++j) {
-      const f32x4 lo = *reinterpret_cast<const f32x4*>(coef + j * p.K + kc);
-      const f32x4 hi = *reinterpret_cast<const f32x4*>(coef + j * p.K + kc + 4);
-      cf[j][0] = f32x2{lo[0], lo[1]}; cf[j][1] = f32x2{lo[2], lo[3]};
-      cf[j][2] = f32x2{hi[0], hi[1]}; cf[j][3] = f32x2{hi[2], hi[3]};
-    }
-    if constexpr (AT == AT_JOIN) {  // one shift per channel: c1 + c3 (bn_apply_kernel RBN order)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) cf[1][e] += cf[3][e];
-    }
-#pragma unroll
-    for (int i = 0; i < AI; ++i) {
-      const int row = a_r0 + i * ARP;
-      const uint32_t xw[4] = {ax[i].x, ax[i].y, ax[i].z, ax[i].w};
-      uint32_t rw[4] = {0u, 0u, 0u, 0u};
-      if constexpr (at_has_r<AT>()) { rw[0] = ar[i].x; rw[1] = ar[i].y; rw[2] = ar[i].z; rw[3] = ar[i].w; }
-      uint32_t ow[4], mb = 0;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const f32x2 x = bf2x(xw[e]);
-        f32x2 v;
-        if constexpr (AT == AT_BN || AT == AT_JOIN) {
-          f32x2 z = __builtin_elementwise_fma(x, cf[0][e], cf[1][e]);
-          if constexpr (AT == AT_JOIN) z = __builtin_elementwise_fma(bf2x(rw[e]), cf[2][e], z);
-          mb |= (z.x > 0.f ? 1u : 0u) << (2 * e);
-          mb |= (z.y > 0.f ? 1u : 0u) << (2 * e + 1);
-          if (p.at_act == ACT_RELU) { v.x = fmaxf(z.x, 0.f); v.y = fmaxf(z.y, 0.f); }
-          else if (p.at_act == ACT_LEAKY) { v.x = z.x > 0.f ? z.x : z.x * p.at_slope; v.y = z.y > 0.f ? z.y : z.y * p.at_slope; }
-          else v = z;
-        } else {
-          const f32x2 d = bf2x(rw[e]);
-          const f32x2 neg = p.at_act == ACT_LEAKY ? d * p.at_slope : f32x2{0.f, 0.f};
-          f32x2 dz = d;
-          if constexpr (AT == AT_BWDB) {
-            dz.x = ((abits[i] >> (2 * e)) & 1u) ? d.x : neg.x;
-            dz.y = ((abits[i] >> (2 * e + 1)) & 1u) ? d.y : neg.y;
-          } else if (p.at_act) {
-            const f32x2 z = __builtin_elementwise_fma(x, cf[3][e], cf[4][e]);
-            dz.x = z.x > 0.f ? d.x : neg.x;
-            dz.y = z.y > 0.f ? d.y : neg.y;
-          }
-          v = __builtin_elementwise_fma(cf[0][e], dz, __builtin_elementwise_fma(cf[1][e], x, cf[2][e]));
-        }
-        ow[e] = pack2bf(v.x, v.y);
-      }
-      const uint4 o = uint4{ow[0], ow[1], ow[2], ow[3]};
-      *reinterpret_cast<uint4*>(img_m + row * (BK_ * 2) + ((a_c ^ kc_swz<BK_>(row)) << 4)) = o;
-      const int m = m0 + row;
-      if (a_side && m < p.M) {
-        const int64_t off = (int64_t)m * p.ldx + kc;
-        if (p.at_side) *reinterpret_cast<uint4*>(p.at_side + off) = o;
-        if constexpr (AT == AT_BN || AT == AT_JOIN) {
-          if (p.at_bits_out) p.at_bits_out[off >> 3] = (uint8_t)mb;
-        }
-      }
-    }
-  };
-
   if constexpr (AT != AT_NONE) {
-    // coefficient vectors -> LDS once per block (behind the operand stages)
+    // coefficient vectors -> LDS once per block (behind the operand stages); the first barrier of
+    // the K loop orders them before any read
 #pragma unroll
     for (int j = 0; j < NCO; ++j)
       for (int k = threadIdx.x * 4; k < p.K; k += 64 * NW * 4)
         *reinterpret_cast<f32x4*>(coef + j * p.K + k) = *reinterpret_cast<const f32x4*>(p.at_c[j] + k);
-    aload(kt0);
-    stage(kt0, 0);
-    advance();
-    __syncthreads();  // coefficients visible
-    acommit(kt0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int t = 0; t < nt; ++t) {
-      const int cur = t & 1;
-      if (t + 1 < nt) { aload(kt0 + t + 1); stage(kt0 + t + 1, cur ^ 1); advance(); }
-      compute(cur);
-      if (t + 1 < nt) acommit(kt0 + t + 1, cur ^ 1);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-  } else if constexpr (STAGES == 2) {
+  }
+  if constexpr (STAGES == 2) {
     // double buffer, one barrier per K-tile: the DMA of tile t+1 overlaps the MFMAs of tile t
     stage(kt0, 0);
     advance();
@@ -471,7 +470,7 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
     for (int t = 0; t < nt; ++t) {
       const int cur = t & 1;
       if (t + 1 < nt) { stage(kt0 + t + 1, cur ^ 1); advance(); }
-      compute(cur);
+      compute(cur, kt0 + t);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
@@ -479,7 +478,6 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
     // STAGES-deep ring: STAGES-2 tiles stay in flight across each barrier. A counted vmcnt
     // retires only tile t's DMAs (IPT per wave per tile, issued in order) and the raw s_barrier
     // does not drain the younger ones (__syncthreads() would emit vmcnt(0)).
-    constexpr int IPT = MI + NI;
 #pragma unroll
     for (int s = 0; s < STAGES - 1; ++s)
       if (s < nt) { stage(kt0 + s, s); advance(); }
@@ -492,7 +490,7 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       if (t + STAGES - 1 < nt) { stage(kt0 + t + STAGES - 1, nxt); advance(); }
-      compute(cur);
+      compute(cur, kt0 + t);
       cur = cur + 1 == STAGES ? 0 : cur + 1;
       nxt = nxt + 1 == STAGES ? 0 : nxt + 1;
     }
@@ -786,11 +784,11 @@ constexpr int lds_bytes(int stages) {
   return stages * stage_bytes<BM_, BN_, BK_>() > epi ? stages * stage_bytes<BM_, BN_, BK_>() : epi;
 }
 
-// dynamic LDS of an A-transform launch: the operand stages, then the [NCO][K] coefficients
+// dynamic LDS of an A-transform launch: the (wider) operand stages, then the [NCO][K] coefficients
 template <int BM_, int BN_, int BK_, int WMT, int AT>
-size_t at_lds_bytes(int K) {
-  const size_t a = (size_t)2 * stage_bytes<BM_, BN_, BK_>() + (size_t)at_ncoef<AT>() * K * 4;
-  const size_t b = lds_bytes<BM_, BN_, BK_, WMT>(2);
+size_t at_lds_bytes(int K, int stages) {
+  const size_t a = (size_t)stages * at_stage_bytes<BM_, BN_, BK_, AT>() + (size_t)at_ncoef<AT>() * K * 4;
+  const size_t b = lds_bytes<BM_, BN_, BK_, WMT>(stages);
   return a > b ? a : b;
 }
 constexpr size_t LDS_MAX = 160 * 1024;
@@ -811,7 +809,7 @@ void launch_fwd(const FwdParams& p, hipStream_t st) {
   q.kt_per = (nt_all + q.ksplit - 1) / q.ksplit;
   q.ksplit = (nt_all + q.kt_per - 1) / q.kt_per;  // no empty splits
   const int nt = q.kt_per;
-  const size_t lds = AT != AT_NONE ? at_lds_bytes<BM_, BN_, BK_, WMT, AT>(p.K)
+  const size_t lds = AT != AT_NONE ? at_lds_bytes<BM_, BN_, BK_, WMT, AT>(p.K, STAGES)
                                    : lds_bytes<BM_, BN_, BK_, WMT>(nt < STAGES ? nt : STAGES);
   const int blocks = ((p.M + BM_ - 1) / BM_) * ((p.N + BN_ - 1) / BN_) * p.G * q.ksplit;
   conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES, BNR, EPI, WMT, AT>
@@ -837,16 +835,18 @@ bool big_tile_ok(const FwdParams& p) {
   return tiles >= 192 || dv_g_fwd_variant == 100;  // 100: tests force it at small shapes
 }
 
-// A-transform launches (csrc kernels.h ConvFwdArgs at_*): the heuristic's tile set on the
-// double buffer; the 8-wave 256x256 tile only when its 128 KB of stages leave room for the
-// coefficients
+// A-transform launches (csrc kernels.h ConvFwdArgs at_*): the transform runs on each A fragment
+// right before its MFMAs, so the tiles whose A fragments are read by one wave column (256x64,
+// N <= 64) or two (128x128) keep it cheap; BK 32, the heuristic's LDS-DMA pipeline (the 3-deep
+// ring on the short-K 64-channel layers)
 template <int AT, bool RES, int BNR, int EPI>
 void launch_at(const FwdParams& p, hipStream_t st) {
-  if (big_tile_ok<KM_FAST>(p) && at_lds_bytes<256, 256, 64, 128, AT>(p.K) <= LDS_MAX)
-    launch_fwd<256, 256, 64, KM_FAST, RES, 2, BNR, EPI, 128, AT>(p, st);
-  else if (p.N <= 64) launch_fwd<256, 64, 32, KM_FAST, RES, 2, BNR, EPI, 64, AT>(p, st);
-  else if (p.K > 64 && p.K < 2048) launch_fwd<128, 128, 32, KM_FAST, RES, 2, BNR, EPI, 64, AT>(p, st);
-  else launch_fwd<128, 128, 64, KM_FAST, RES, 2, BNR, EPI, 64, AT>(p, st);
+  if (p.N <= 64) {
+    if (p.K <= 256) launch_fwd<256, 64, 32, KM_FAST, RES, 3, BNR, EPI, 64, AT>(p, st);
+    else launch_fwd<256, 64, 32, KM_FAST, RES, 2, BNR, EPI, 64, AT>(p, st);
+  } else {
+    launch_fwd<128, 128, 32, KM_FAST, RES, 2, BNR, EPI, 64, AT>(p, st);
+  }
 }
 
 template <int AT, bool RES, int BNR>

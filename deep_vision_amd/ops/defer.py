@@ -1,5 +1,5 @@
 """Deferred BatchNorm applies: the elementwise BN pass folded into the operand load of the 1x1
-conv that consumes its result (csrc/conv_fwd.hip ``AT_*`` register-staged A operand).
+conv that consumes its result (csrc/conv_fwd_core.h ``AT_*`` A-operand transforms).
 
 A training BatchNorm cannot be applied in its producer's epilogue (the batch statistics are
 complete only when the producer has finished), so the unfused graph spends one full read + write
@@ -27,7 +27,14 @@ Hand-off rules (every path is safe without the fusion):
     1x1 conv created in the same fused op (ops.bn.conv_bn_act), so that conv's backward is the
     tensor's only consumer.
 
-``DV_DEFER=0`` (or ``ENABLED``) turns the whole mechanism off (A/B benchmarking, debugging).
+OFF BY DEFAULT (``DV_DEFER=1`` / ``ENABLED = True`` turns it on): measured on ResNet-50 at batch
+256 it loses (profiles/defer_experiment.txt). The separate apply passes already stream at
+5-6 TB/s, the best case saves only the consumer's re-read (13 vs 17 tensor-widths of traffic on a
+stage-1 join), and both kernel forms tried cost more than that: staging A through registers
+breaks the LDS-DMA pipeline (latency-bound K loop), and a per-fragment transform on top of the
+DMA pipeline repeats the transform in every output-column tile and wave column and widens the
+stages to one block per CU. The kernels are exact (bitwise equal to the unfused step,
+tests/test_defer_gpu.py) and stay available for A/B runs.
 """
 from __future__ import annotations
 
@@ -38,7 +45,7 @@ import torch
 from .common import F32, lib, ptr, stream_handle
 
 AT_BN, AT_JOIN, AT_BWDB, AT_BWDX = 1, 2, 3, 4
-ENABLED = os.environ.get("DV_DEFER", "1") not in ("0", "off")
+ENABLED = os.environ.get("DV_DEFER", "0") not in ("0", "off", "")
 COUNTERS = {"fwd_fused": 0, "fwd_materialized": 0, "bwd_fused": 0, "bwd_materialized": 0}
 
 _ONES = {}
