@@ -28,6 +28,10 @@ Design (MI355X-first, not a translation of DataParallel / MirroredStrategy):
     parameters: Inception aux heads in eval, Hourglass dead convs) and makes the compute stream
     wait on every outstanding all-reduce; with ``timing=True`` a HIP event pair around that wait
     measures the *exposed* communication time (``comm_stats['exposed_ms']``);
+  * ``record_issue=True`` (overlap evidence, tests/test_ddp_gpu.py): every bucket issue records
+    where it came from (a backward hook or ``finish``) and a HIP event at that point of the
+    compute stream; ``finish`` records the end of backward, so ``issue_report()`` gives, per
+    bucket, how much backward compute was still queued behind its all-reduce;
   * the 1/world averaging is fused into the optimizer kernel (``grad_scale``) — no extra pass;
   * BatchNorm statistics stay per replica (reference semantics, no SyncBN); initial parameters
     and buffers are broadcast from rank 0.
@@ -64,8 +68,11 @@ class _Bucket:
 class DataParallel(torch.nn.Module):
     def __init__(self, module: torch.nn.Module, bucket_mb: float = 32.0, broadcast: bool = True,
                  process_group=None, comm=None, comm_dtype: torch.dtype = torch.float32, timing: bool = False,
-                 always_reduce: bool = False, tail_mb: float = 4.0):
+                 always_reduce: bool = False, tail_mb: float = 4.0, record_issue: bool = False):
         super().__init__()
+        self.record_issue = record_issue
+        self.issue_log = []  # this step's [(bucket index, 'hook' | 'finish', event | None)]
+        self.bwd_end = None
         self.module = module
         self.pg = process_group
         self.comm = comm  # optional injected communicator (tests): callable(tensor) -> None (sum in place)
@@ -129,6 +136,8 @@ class DataParallel(torch.nn.Module):
             b.work = None
             b.issued = False
         self._done = set()
+        self.issue_log = []
+        self.bwd_end = None
 
     def _make_hook(self, p):
         pid = id(p)
@@ -144,15 +153,21 @@ class DataParallel(torch.nn.Module):
             b = self.buckets[bi]
             b.pending -= 1
             if b.pending == 0 and not b.issued:
-                self._issue(b)
+                self._issue(b, "hook")
 
         return hook
 
     # ------------------------------------------------------------------ communication
-    def _issue(self, b: _Bucket):
+    def _issue(self, b: _Bucket, where: str = "finish"):
         t = self.gflat[b.start:b.end]
         b.issued = True
         self.comm_stats["allreduce_calls"] += 1
+        if self.record_issue:
+            ev = None
+            if t.is_cuda and not torch.cuda.is_current_stream_capturing():
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+            self.issue_log.append((self.buckets.index(b), where, ev))
         if self.comm is not None:
             self.comm_stats["allreduce_bytes"] += t.numel() * 4
             self.comm(t)
@@ -189,9 +204,12 @@ class DataParallel(torch.nn.Module):
         """Issue incomplete buckets and make the current stream wait for all reductions."""
         if not self.reduce or not self._sync_enabled:
             return
+        if self.record_issue and self.gflat.is_cuda and not torch.cuda.is_current_stream_capturing():
+            self.bwd_end = torch.cuda.Event(enable_timing=True)
+            self.bwd_end.record()
         for b in self.buckets:
             if not b.issued:
-                self._issue(b)
+                self._issue(b, "finish")
         ev = None
         if self.timing and not torch.cuda.is_current_stream_capturing():
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -206,6 +224,17 @@ class DataParallel(torch.nn.Module):
         if ev is not None:
             ev[1].record()
             self.comm_stats["exposed_ms"].append(ev)
+
+    def issue_report(self):
+        """[(bucket, 'hook' | 'finish', MB, ms of backward compute queued after the issue)] of the
+        last step (record_issue=True; synchronises)."""
+        torch.cuda.synchronize()
+        out = []
+        for bi, where, ev in self.issue_log:
+            b = self.buckets[bi]
+            ms = ev.elapsed_time(self.bwd_end) if (ev is not None and self.bwd_end is not None) else None
+            out.append((bi, where, (b.end - b.start) * 4 / 2 ** 20, ms))
+        return out
 
     def exposed_comm_ms(self, last: int | None = None) -> float:
         """Mean compute-stream time spent waiting on gradient all-reduces (synchronises)."""

@@ -239,3 +239,58 @@ def test_rccl_world1_bucket_path(order, comm_dtype):
     err = (d - dref).norm() / dref.norm()
     assert err < (1e-3 if comm_dtype == torch.float32 else 2e-2), float(err)
     assert losses[-1] < losses[0]
+
+
+def _overlap_worker(port, q):
+    """ResNet-50 on the native kernels, world-1 RCCL group, DataParallel forced on: where was each
+    bucket's all-reduce issued, and how much backward compute was still queued behind it."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    import torch.distributed as dist
+
+    from deep_vision_amd import ops as F
+    from deep_vision_amd.models import ResNet50
+    from deep_vision_amd.parallel.ddp import DataParallel
+    from deep_vision_amd.parallel.dist import init_distributed
+    from deep_vision_amd.train.optim import FusedSGD
+
+    init_distributed("nccl", force=True)
+    torch.manual_seed(0)
+    m = ResNet50().cuda()
+    ddp = DataParallel(m, bucket_mb=8, always_reduce=True, record_issue=True)
+    opt = FusedSGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    x = torch.randn(64, 3, 160, 160, device="cuda")
+    y = torch.randint(0, 1000, (64,), device="cuda")
+    for _ in range(3):
+        opt.zero_grad()
+        loss = F.cross_entropy(ddp(x), y)
+        b0 = torch.cuda.Event(enable_timing=True)
+        b0.record()
+        loss.backward()
+        ddp.finish()
+        opt.step(grad_scale=ddp.grad_scale)
+    rep = ddp.issue_report()
+    bwd_ms = b0.elapsed_time(ddp.bwd_end)
+    q.put((rep, bwd_ms, len(ddp.buckets)))
+    dist.destroy_process_group()
+
+
+def test_bucket_allreduce_overlaps_backward():
+    """every bucket's all-reduce is issued from a backward
+    hook, in bucket order, while backward compute is still queued behind it -- not by finish()."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_overlap_worker, args=(_port(), q))
+    p.start()
+    rep, bwd_ms, nb = q.get(timeout=300)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert nb >= 8 and len(rep) == nb
+    assert all(where == "hook" for _, where, _, _ in rep), rep
+    assert [bi for bi, _, _, _ in rep] == list(range(nb)), "buckets issued out of order"
+    queued = [ms for _, _, _, ms in rep]
+    # all but the tail (the stem's gradients, complete at the very end) leave backward compute
+    # behind them; the first bucket is issued in the first half of backward
+    assert all(ms > 0.05 for ms in queued[:-1]), queued
+    assert queued[0] > 0.5 * bwd_ms, (queued[0], bwd_ms)
+    print(f"backward {bwd_ms:.2f} ms; compute queued behind each bucket issue (ms): "
+          + ", ".join(f"{ms:.2f}" for ms in queued))
