@@ -46,11 +46,12 @@ PYBIND11_MODULE(_C, m) {
                        uptr resbits, int resact, float resslope, int reflect, int ksplit, uptr ypart, int zfill,
                        uptr bnx2, uptr bnprm2, uptr bnacc2, int at, int at_flags, int at_act, float at_slope, uptr at_x,
                        uptr at_r, uptr at_bits_in, uptr at_bits_out, uptr at_side, uptr at_c0, uptr at_c1, uptr at_c2,
-                       uptr at_c3, uptr at_c4) {
+                       uptr at_c3, uptr at_c4, int w_ld, int w_kr, int w_ks) {
     ConvFwdArgs a{CP(x), CP(w), P(y), CFP(bias), FP(stats), Nb, H, W, Cg, ldx, G, Kout, P_, Q, R, S, sh, sw, ph, pw,
                   dh, dw, tgather, OH, OW, osh, osw, oph, opw, ldy, act, slope, CP(res),
                   CP(bnx), CP(bnbits), CFP(bnprm), FP(bnacc), bnmode, bnact, bnslope, CP(resbits), resact, resslope,
                   reflect, ksplit, FP(ypart), zfill, CP(bnx2), CFP(bnprm2), FP(bnacc2)};
+    a.w_ld = w_ld; a.w_kr = w_kr; a.w_ks = w_ks;
     a.at = at; a.at_flags = at_flags; a.at_act = at_act; a.at_slope = at_slope;
     a.at_x = CP(at_x); a.at_r = CP(at_r); a.at_bits_in = CP(at_bits_in); a.at_bits_out = P(at_bits_out);
     a.at_side = P(at_side);
@@ -70,7 +71,7 @@ PYBIND11_MODULE(_C, m) {
      py::arg("bnprm2") = 0, py::arg("bnacc2") = 0, py::arg("at") = 0, py::arg("at_flags") = 0, py::arg("at_act") = 0,
      py::arg("at_slope") = 0.f, py::arg("at_x") = 0, py::arg("at_r") = 0, py::arg("at_bits_in") = 0,
      py::arg("at_bits_out") = 0, py::arg("at_side") = 0, py::arg("at_c0") = 0, py::arg("at_c1") = 0, py::arg("at_c2") = 0,
-     py::arg("at_c3") = 0, py::arg("at_c4") = 0);
+     py::arg("at_c3") = 0, py::arg("at_c4") = 0, py::arg("w_ld") = 0, py::arg("w_kr") = 0, py::arg("w_ks") = 0);
   m.def("conv_fwd_variant", [](int v) { dv_conv_fwd_variant(v); });
   m.def("bn_tuning", [](int blocks, int unroll) { dv_bn_tuning(blocks, unroll); });
   m.def("bn_apply_tuning", [](int blocks, int unroll) { dv_bn_apply_tuning(blocks, unroll); });

@@ -395,6 +395,9 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
   p.bnx2 = (const u16*)a.bnx2; p.bnprm2 = a.bnprm2; p.bnacc2 = a.bnacc2;
   p.resbits = (const uint8_t*)a.resbits; p.resact = a.resact; p.resslope = a.resslope;
   p.reflect = a.reflect;
+  p.wld = a.w_ld ? a.w_ld : p.K;
+  p.wkr = a.w_kr ? a.w_kr : a.S * a.Cg;
+  p.wks = a.w_ks ? a.w_ks : a.Cg;
   p.ksplit = 1; p.kt_per = 1 << 30; p.ypart = nullptr;
   p.at_x = (const u16*)a.at_x; p.at_r = (const u16*)a.at_r; p.at_bits_in = (const uint8_t*)a.at_bits_in;
   p.at_bits_out = (uint8_t*)a.at_bits_out; p.at_side = (u16*)a.at_side;
@@ -431,7 +434,8 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
     // identity map, or the strided scatter of a 1x1 stride-s dgrad (no offset): the pixels it does
     // not write hold zero gradient and add nothing to either sum. Not with zfill (its sibling
     // zeroing lives in the non-prefetching store path).
-    const bool map_ok = p.identity_map || (a.oph == 0 && a.opw == 0 && !p.zfill);
+    // (a parity part of a sub-pixel dgrad: offset map, its own disjoint pixels)
+    const bool map_ok = p.identity_map || !p.zfill;
     const bool ok = a.tgather == 0 && map_ok && p.G == 1 && (p.N & 7) == 0 && p.ldy == p.N &&
                     p.Cg % 64 == 0 && p.ldx % 8 == 0 && p.R <= 16 && p.S <= 16 && p.bnx && p.bnprm && p.bnacc &&
                     (p.bnmode != 3 || p.bnbits) && (!p.bnx2 || (p.bnmode == 3 && p.bnprm2 && p.bnacc2));
@@ -500,6 +504,9 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
     }
     return 0;
   }
+  // a strided / offset weight layout is read by the fast loader only
+  const bool fast = !a.tgather && p.Cg % 64 == 0 && p.R <= 16 && p.S <= 16 && !p.reflect;
+  if ((a.w_ld || a.w_kr || a.w_ks) && !fast) return -1;
   // the fast loader needs every K-tile inside one filter tap: Cg % 64 == 0 covers both BKs
   if (a.tgather) dispatch_tile<KM_TGATHER>(p, st);
   else if (p.Cg % 64 == 0 && p.R <= 16 && p.S <= 16 && !p.reflect) dispatch_tile<KM_FAST>(p, st);

@@ -61,6 +61,7 @@ struct FwdParams {
   const u16* bnx2;         // BNR: second BatchNorm fed by the same dz (kernels.h ConvFwdArgs), or nullptr
   const float* bnprm2;
   float* bnacc2;
+  int wld, wkr, wks;  // weight row / tap strides (kernels.h ConvFwdArgs w_ld, w_kr, w_ks)
   // A-operand transform (template AT; kernels.h ConvFwdArgs at_*)
   const u16* at_x;
   const u16* at_r;
@@ -253,7 +254,7 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
     const int lc = (lane % CH) ^ kc_swz<BK_>(row);
     const int n = n0 + row;
     wok[j] = n < p.N;
-    wrow[j] = p.w + ((int64_t)grp * p.N + (wok[j] ? n : 0)) * p.K + lc * 8;
+    wrow[j] = p.w + ((int64_t)grp * p.N + (wok[j] ? n : 0)) * p.wld + lc * 8;
   }
   const u16* xrow[MI];      // KM_FAST: pointer at (pixel origin, channel lc*8)
   uint32_t tapmask[MI];     // KM_FAST: bit r (h valid) | bit 16+s (w valid); 0 for m >= M
@@ -297,7 +298,9 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
       const int row = (wid * NI + j) * RPI + lane / CH;
       const int lc = (lane % CH) ^ kc_swz<BK_>(row);
       const bool ok = wok[j] && (KMODE == KM_FAST || k0 + lc * 8 < p.K);
-      glds16(ok ? (const void*)(wrow[j] + k0) : (const void*)zero, img_n + (wid * NI + j) * 1024);
+      // fast loader: the weight offset of this K-tile's tap (equal to k0 for a whole filter)
+      const int64_t wo = KMODE == KM_FAST ? (int64_t)t_r * p.wkr + t_s * p.wks + t_c : k0;
+      glds16(ok ? (const void*)(wrow[j] + wo) : (const void*)zero, img_n + (wid * NI + j) * 1024);
     }
     if (KMODE == KM_FAST) {
       const int64_t koff = ((int64_t)(t_r * p.dh) * p.Win + t_s * p.dw) * p.ldx + t_c;

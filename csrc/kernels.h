@@ -65,6 +65,10 @@ struct ConvFwdArgs {
   // and writes `a` into the LDS image. Blocks of output-column tile 0 also store `a` (and the
   // forward activation mask bits) to at_side / at_bits_out: the materialised BN output /
   // gradient the rest of the graph reads, written once instead of by a separate apply pass.
+  // weight operand layout (fast loader only): elements between output-channel rows (0 = R*S*Cg)
+  // and between consecutive taps of a row / column (0 = S*Cg / Cg). A tap subset of a larger
+  // filter reads the full cached weight in place: w points at its first tap (sub-pixel dgrad)
+  int w_ld = 0, w_kr = 0, w_ks = 0;
   int at = 0;
   int at_flags = 0;           // at 1: bit0 residual r, bit1 residual BN (c2, c3); at 2: mask mode 1/2/3
   int at_act = 0;

@@ -129,7 +129,7 @@ def conv_ksplit(M, O, K, G=1):
 
 def conv_fwd_raw(x, wk, y, bias, stats, N, H, W, Cg, ldx, G, Kout, P, Q, R, S, stride, padding, dilation,
                  act=0, slope=0.0, tgather=0, omap=None, ldy=None, res=None, bnref=None, resmask=None, reflect=False,
-                 ksplit=1, zfill=0, at=None):
+                 ksplit=1, zfill=0, at=None, wlayout=None):
     """Launch the implicit-GEMM kernel. ``bnref`` (ops.bn.BNRef): also reduce that BatchNorm's
     backward statistics over ``y`` in the epilogue; returns True when that was done.
     ``resmask`` (bits, act, slope): ``res`` is a raw gradient masked by act'() before the add.
@@ -158,6 +158,8 @@ def conv_fwd_raw(x, wk, y, bias, stats, N, H, W, Cg, ldx, G, Kout, P, Q, R, S, s
         bn.update(ksplit=int(ksplit), ypart=ptr(part))
     if at is not None:
         bn.update(at.kernel_args())
+    if wlayout is not None:  # (row stride, tap-row stride, tap stride) of a tap subset read in place
+        bn.update(w_ld=int(wlayout[0]), w_kr=int(wlayout[1]), w_ks=int(wlayout[2]))
     r = lib().conv_fwd(ptr(x), ptr(wk), ptr(y), ptr(bias), ptr(stats), N, H, W, Cg, ldx, G, Kout, P, Q, R, S, sh, sw,
                        ph, pw, dh, dw, tgather, OH, OW, osh, osw, oph, opw, ldy if ldy is not None else ld_of(y), act,
                        float(slope), ptr(res), stream_handle(), **bn)
@@ -235,12 +237,68 @@ def _dgrad(dy, weight, x_shape, Cg_x, G, stride, padding, dilation, device, accu
         if conv_fwd_raw(dy, wd, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, P, Q, 1, 1, (1, 1), (0, 0), (1, 1),
                         omap=(H, W, sh, sw, 0, 0), ldy=G * Cg_x, res=res, zfill=zfill, bnref=fuse, at=at):
             fuse.mark_fused(dX)
+    elif SUBPIXEL_DGRAD and tuple(dilation) == (1, 1) and Cg_dy % 64 == 0 and R <= 16 and S <= 16:
+        _subpixel_dgrad(dy, wd, dX, res, bnref, N, H, W, P, Q, Cg_dy, ldy_in, G, Ig, Cg_x, R, S, stride, padding)
     else:
+        COUNTERS_DGRAD["tgather"] += 1
         conv_fwd_raw(dy, wd, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, H, W, R, S, stride, padding, dilation,
                      tgather=1, ldy=G * Cg_x, res=res)
     if accum is not None and res is None:  # layout mismatch: plain add
         dX = dX[:, : accum.shape[1]] + accum if dX.shape[1] != accum.shape[1] else dX + accum
     return dX
+
+
+# Strided dgrad (and ConvTranspose forward) by output parity: for stride s every output pixel
+# (s*u + a, s*v + b) receives exactly the taps r = a + ph (mod s), s' = b + pw (mod s) -- a dense
+# stride-1 sub-convolution of dY with a (ceil(R/s) x ceil(S/s))-ish tap subset, scattered to the
+# parity's output grid (omap offset (a, b)). The s*s sub-convolutions cover every output pixel
+# once and read the cached full-filter weight in place (strided taps, csrc ConvFwdArgs w_kr/w_ks)
+# on the fast LDS-DMA loader; the one-pass transposed gather they replace tests divisibility per
+# tap and fetches s*s times the taps it uses (YOLOv3's 3x3/2 downsampling dgrads: 290-380 us).
+SUBPIXEL_DGRAD = True
+COUNTERS_DGRAD = {"subpixel": 0, "tgather": 0}
+
+
+def _subpixel_parts(H, W, P, Q, R, S, stride, padding):
+    """[(a, b, r0, s0, Ra, Sb, d_h, d_w, U, V)] per output parity: first tap, tap counts, the tap
+    offsets' max (as negative padding), sub-output extent; parities no tap reaches have Ra or Sb 0."""
+    sh, sw = stride
+    ph, pw = padding
+    parts = []
+    for a in range(min(sh, H)):
+        rs = [r for r in range(R) if (r - a - ph) % sh == 0]
+        U = -(-(H - a) // sh)
+        for b in range(min(sw, W)):
+            ss = [t for t in range(S) if (t - b - pw) % sw == 0]
+            V = -(-(W - b) // sw)
+            dh = (a + ph - rs[0]) // sh if rs else 0
+            dw = (b + pw - ss[0]) // sw if ss else 0
+            parts.append((a, b, rs[0] if rs else 0, ss[0] if ss else 0, len(rs), len(ss), dh, dw, U, V))
+    return parts
+
+
+def _subpixel_dgrad(dy, wd, dX, res, bnref, N, H, W, P, Q, Cg_dy, ldy_in, G, Ig, Cg_x, R, S, stride, padding):
+    sh, sw = stride
+    parts = _subpixel_parts(H, W, P, Q, R, S, stride, padding)
+    live = [p for p in parts if p[4] and p[5] and p[8] > 0 and p[9] > 0]
+    if len(live) < len(parts) and res is None:
+        dX.zero_()  # output parities no tap reaches keep zero gradient
+    # the BatchNorm-backward sums ride on every part (disjoint pixels, together all of them), or
+    # on none: a partial fusion would leave part of the sums in the accumulator
+    fuse = bnref if (bnref is not None and G == 1 and Cg_x == Ig and len(live) == len(parts)) else None
+    ok = []
+    for a, b, r0, s0, ra, sb, dh, dw, U, V in live:
+        # the parity's taps (r0 + sh*i, s0 + sw*j) of the [G][Ig][R][S][Cg_dy] operand, read in place
+        wsub = wd[(r0 * S + s0) * Cg_dy:]
+        COUNTERS_DGRAD["subpixel"] += 1
+        ok.append(conv_fwd_raw(dy, wsub, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, U, V, ra, sb, (1, 1),
+                               (-dh, -dw), (-1, -1), omap=(H, W, sh, sw, a, b), ldy=G * Cg_x, res=res, bnref=fuse,
+                               wlayout=(R * S * Cg_dy, sh * S * Cg_dy, sw * Cg_dy)))
+    if fuse is not None:
+        if all(ok):
+            fuse.mark_fused(dX)
+        elif any(ok):  # mixed acceptance (not expected): drop the partial sums, the BN reduces itself
+            fuse.acc.zero_()
 
 
 class MaskedGrad:

@@ -49,6 +49,13 @@ CONV_CASES = [
     (2, 96, 13, 13, 256, 5, 1, 2, 1),    # 5x5, C % 64 != 0 (generic K decode)
     (2, 128, 8, 8, 128, 3, 1, 1, 2),     # grouped
     (3, 200, 7, 7, 520, 1, 1, 0, 1),     # odd M / N tails
+    # strided dgrads by output parity (ops.conv._subpixel_dgrad): 3x3/2 (YOLOv3, ResNet-34),
+    # odd maps, 4x4/2 (PatchGAN), 5x5/2 pad 2 (DCGAN), 3x3/3
+    (2, 64, 17, 15, 64, 3, 2, 1, 1),
+    (2, 128, 16, 16, 64, 3, 2, 1, 1),
+    (2, 64, 16, 16, 128, 4, 2, 1, 1),
+    (2, 64, 14, 14, 128, 5, 2, 2, 1),
+    (2, 64, 13, 11, 64, 3, 3, 1, 1),
 ]
 
 
@@ -71,6 +78,17 @@ def test_conv_fwd_bwd(case):
     yr.backward(dy32)
     assert _rel(x.grad, xr.grad) < 3e-2
     assert _rel(w.grad, wr.grad) < 3e-2
+
+
+def test_strided_dgrad_takes_subpixel_path():
+    from deep_vision_amd import ops as F
+    from deep_vision_amd.ops import conv as C
+
+    x = _nhwc(torch.randn(2, 64, 17, 15, device=DEV)).requires_grad_(True)
+    w = torch.randn(64, 64, 3, 3, device=DEV) * 0.05
+    n0, t0 = C.COUNTERS_DGRAD["subpixel"], C.COUNTERS_DGRAD["tgather"]
+    F.conv2d(x, w, None, 2, 1).sum().backward()
+    assert C.COUNTERS_DGRAD["subpixel"] - n0 == 4 and C.COUNTERS_DGRAD["tgather"] == t0
 
 
 def test_conv_bias_relu_epilogue():

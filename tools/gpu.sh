@@ -38,6 +38,7 @@ case "$mode" in
     [ -n "$f" ] && python tools/prof_summary.py "$f" 7 "$m bench.py --steps 5 --warmup 2" > gpurun_out/prof_$m.txt 2>&1
     t=$(find gpurun_out/prof_$m -name '*kernel_trace.csv' -print -quit)
     [ -n "$t" ] && python tools/trace_step.py "$t" > gpurun_out/trace_$m.txt 2>&1
+    [ -n "$t" ] && python tools/kernel_census.py "$t" > gpurun_out/census_$m.txt 2>&1
     rm -f "$t"
     cat gpurun_out/prof_$m.txt | cut -c1-160 | sed -n '1,45p' ;;
   pmc)

@@ -18,11 +18,11 @@ def short(n):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("csv")
-    ap.add_argument("--marker", default="sgd_kernel")
+    ap.add_argument("--marker", default="(sgd|adam|rmsprop)_kernel", help="regex of the step-ending kernel")
     ap.add_argument("--which", type=int, default=-1)
     a = ap.parse_args()
     rows = sorted(csv.DictReader(open(a.csv)), key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
+    idx = [i for i, r in enumerate(rows) if re.search(a.marker, r["Kernel_Name"])]
     lo, hi = idx[a.which - 1], idx[a.which]
     busy = idle = 0.0
     for i in range(lo + 1, hi + 1):
