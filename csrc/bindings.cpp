@@ -126,10 +126,12 @@ PYBIND11_MODULE(_C, m) {
     check_last("bn_bwd_reduce");
   });
   m.def("bn_bwd_finalize", [](uptr acc, int C, double count, uptr gamma, uptr mean, uptr invstd, uptr dgamma, uptr dbeta,
-                              int accumulate, uptr kA, uptr kB, uptr kC, uptr st) {
-    dv_bn_bwd_finalize(FP(acc), C, count, CFP(gamma), CFP(mean), CFP(invstd), FP(dgamma), FP(dbeta), accumulate, FP(kA), FP(kB), FP(kC), ST(st));
+                              int accumulate, uptr kA, uptr kB, uptr kC, uptr st, uptr xsum) {
+    dv_bn_bwd_finalize(FP(acc), C, count, CFP(gamma), CFP(mean), CFP(invstd), FP(dgamma), FP(dbeta), accumulate, FP(kA), FP(kB), FP(kC), ST(st),
+                       FP(xsum));
     check_last("bn_bwd_finalize");
-  });
+  }, py::arg("acc"), py::arg("C"), py::arg("count"), py::arg("gamma"), py::arg("mean"), py::arg("invstd"), py::arg("dgamma"),
+     py::arg("dbeta"), py::arg("accumulate"), py::arg("kA"), py::arg("kB"), py::arg("kC"), py::arg("st"), py::arg("xsum") = 0);
   m.def("bn_bwd_apply", [](uptr dout, uptr out, uptr x, uptr dx, uptr dres, int64_t n, int C, uptr kA, uptr kB, uptr kC,
                            uptr mscale, uptr mshift, int act, float slope, int mask_bits, uptr st, uptr addend) {
     dv_bn_bwd_apply(CP(dout), CP(out), CP(x), P(dx), P(dres), n, C, CFP(kA), CFP(kB), CFP(kC), CFP(mscale), CFP(mshift), act, slope,
@@ -234,6 +236,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("to_nhwc", [](uptr x, int is_f32, uptr y, int N, int C, int H, int W, int Cp, uptr st) { dv_to_nhwc(CP(x), is_f32, P(y), N, C, H, W, Cp, ST(st)); check_last("to_nhwc"); });
   m.def("f32_to_bf16", [](uptr x, uptr y, int64_t n, uptr st) { dv_f32_to_bf16(CFP(x), P(y), n, ST(st)); check_last("f32_to_bf16"); });
 
+  m.def("scale_by", [](uptr in, uptr out, int64_t n, int is_bf16, uptr sp, uptr st) {
+    dv_scale_by(CP(in), P(out), n, is_bf16, reinterpret_cast<const float*>(sp), ST(st));
+    check_last("scale_by");
+  });
   m.def("softmax_xent", [](uptr logits, int is_bf16, uptr labels, int rows, int C, uptr loss_rows, uptr grad, float gscale,
                            float ls, uptr st) {
     dv_softmax_xent(CP(logits), is_bf16, reinterpret_cast<const int64_t*>(labels), rows, C, FP(loss_rows), P(grad), gscale, ls, ST(st));

@@ -321,11 +321,11 @@ void dispatch_tile(const FwdParams& p, hipStream_t st) {
 // slabs are summed in split order (bitwise reproducible). Block = 64 column lanes x 4 columns
 // (256 channels) x 4 row lanes walking FR_ROWS rows; statistics meet in LDS, one coalesced atomic
 // row per block into shard blockIdx.y % SHARDS.
-constexpr int FR_ROWS = 64;
+constexpr int FR_ROWS = 64;  // rows per block on large grids; small ones shrink it (dv_conv_fwd)
 __global__ __launch_bounds__(256) void splitk_finalize_kernel(const float* __restrict__ ypart, int ksplit, int M, int N,
                                                               const float* __restrict__ bias, int act, float slope,
                                                               const u16* __restrict__ res, float* __restrict__ stats,
-                                                              u16* __restrict__ y, int ldy) {
+                                                              u16* __restrict__ y, int ldy, int fr) {
   __shared__ float red[2][4][256];
   const int lc = threadIdx.x & 63, lr = threadIdx.x >> 6;
   const int n = blockIdx.x * 256 + lc * 4;
@@ -337,8 +337,8 @@ __global__ __launch_bounds__(256) void splitk_finalize_kernel(const float* __res
     bv[r] = (bias && nv) ? bias[n + r] : 0.f;
     kq[r] = (stats && nv) ? stat_shift(stats, N)[n + r] : 0.f;
   }
-  const int m1 = min(M, (int)(blockIdx.y + 1) * FR_ROWS);
-  for (int m = blockIdx.y * FR_ROWS + lr; nv && m < m1; m += 4) {
+  const int m1 = min(M, (int)(blockIdx.y + 1) * fr);
+  for (int m = blockIdx.y * fr + lr; nv && m < m1; m += 4) {
     f32x4 a = *reinterpret_cast<const f32x4*>(ypart + (int64_t)m * N + n);
     for (int sp = 1; sp < ksplit; ++sp) a += *reinterpret_cast<const f32x4*>(ypart + sp * slab + (int64_t)m * N + n);
     float rv[4] = {0.f, 0.f, 0.f, 0.f};
@@ -512,9 +512,14 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
   else if (p.Cg % 64 == 0 && p.R <= 16 && p.S <= 16 && !p.reflect) dispatch_tile<KM_FAST>(p, st);
   else dispatch_tile<KM_GENERIC>(p, st);
   if (p.ypart) {
-    const dim3 grid((unsigned)((p.N + 255) / 256), (unsigned)((p.M + FR_ROWS - 1) / FR_ROWS));
+    // split-K serves small grids (Hourglass 4x4-16x16 maps): 64-row blocks left 8-32 blocks walking
+    // up to 16 slabs serially (37 us median); shrink the row block until ~512 blocks
+    const int ncb = (p.N + 255) / 256;
+    int fr = (int)(((int64_t)p.M * ncb + 511) / 512);
+    fr = std::max(4, std::min(FR_ROWS, (fr + 3) / 4 * 4));
+    const dim3 grid((unsigned)ncb, (unsigned)((p.M + fr - 1) / fr));
     splitk_finalize_kernel<<<grid, dim3(256), 0, st>>>(p.ypart, dv_g_last_ksplit, p.M, p.N, p.bias, p.act, p.slope,
-                                                       fin_res, fin_stats, p.y, p.ldy);
+                                                       fin_res, fin_stats, p.y, p.ldy, fr);
   }
   return bn_status;
 }

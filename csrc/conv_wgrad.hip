@@ -16,6 +16,7 @@
 // Tile variants (4 waves of 64x64): 128x128, and 64x256 for 64-output-channel layers.
 // A plain-row fast path serves 1x1 / stride-1 / pad-0 convs and Linear (no spatial decode).
 #include <cstdlib>
+#include <unordered_map>
 #include <vector>
 
 #include "common.h"
@@ -443,9 +444,13 @@ int g_deterministic = [] {
   const char* v = std::getenv("DV_DETERMINISTIC");
   return (v && v[0] && v[0] != '0') ? 1 : 0;
 }();
-float* g_slab_ws = nullptr;
-size_t g_slab_elems = 0;
-
+// per-stream slab workspaces: independent branches of a model may run their wgrads concurrently
+// on different streams (models/hourglass.py), each needs its own
+struct SlabWs {
+  float* ptr = nullptr;
+  size_t elems = 0;
+};
+std::unordered_map<hipStream_t, SlabWs> g_slab_ws;
 }  // namespace
 
 void dv_set_deterministic(int on) { g_deterministic = on; }
@@ -459,17 +464,18 @@ int dv_deterministic() { return g_deterministic; }
 // deterministic mode).
 std::vector<float*> g_slab_retired;
 float* dv_slab_workspace(size_t elems, hipStream_t st) {
-  if (elems > g_slab_elems) {
+  SlabWs& w = g_slab_ws[st];
+  if (elems > w.elems) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return nullptr;
     const size_t want = elems + elems / 2;
     float* fresh = nullptr;
     if (hipMalloc(&fresh, want * sizeof(float)) != hipSuccess) return nullptr;
-    if (g_slab_ws) g_slab_retired.push_back(g_slab_ws);
-    g_slab_ws = fresh;
-    g_slab_elems = want;
+    if (w.ptr) g_slab_retired.push_back(w.ptr);
+    w.ptr = fresh;
+    w.elems = want;
   }
-  return g_slab_ws;
+  return w.ptr;
 }
 
 void dv_slab_reduce(const float* ws, float* dst, int64_t n, int splits, int accumulate, hipStream_t st) {
@@ -568,14 +574,18 @@ int dv_conv_wgrad(const ConvWgradArgs& a, hipStream_t st) {
   // deterministic mode, and by default every split-K launch: each split stores its partial tile
   // into its own slab (every valid element of dW is written once per split: no memset), the
   // slabs are summed in a fixed order afterwards -- no atomics, reproducible bits
-  const bool slab = g_wg_slab == 1 || (g_wg_slab < 0 && p.splits <= SLAB_MAX_SPLITS);
+  // tiny accumulating launches (Hourglass 4x4 / 8x8 maps, < 4 GFLOP): the reduce pass's launch
+  // costs more than the atomics it avoids, and accumulating into a zeroed buffer needs no memset
+  const bool tiny = a.accumulate && 2.0 * p.M * (double)p.N * p.K * p.G < 4e9;
+  const bool slab = g_wg_slab == 1 || (g_wg_slab < 0 && p.splits <= SLAB_MAX_SPLITS && !tiny);
   bool det = (g_deterministic || slab) && p.splits > 1;
-  if (det && !dv_slab_workspace((size_t)p.splits * out_elems, st)) {
+  float* slab_ws = det ? dv_slab_workspace((size_t)p.splits * out_elems, st) : nullptr;
+  if (det && !slab_ws) {
     if (g_deterministic) return -1;
     det = false;  // no room for the slabs: atomics
   }
   if (det) {
-    p.dw = g_slab_ws;
+    p.dw = slab_ws;
     p.slab = (int64_t)out_elems;
     p.atomic_out = 0;
     p.accumulate = 0;
@@ -590,7 +600,7 @@ int dv_conv_wgrad(const ConvWgradArgs& a, hipStream_t st) {
   if (plain) dispatch_wg<true>(p, bn, bw, st);
   else dispatch_wg<false>(p, bn, bw, st);
   if (det) {
-    dv_slab_reduce(g_slab_ws, a.dw, (int64_t)out_elems, p.splits, a.accumulate, st);
+    dv_slab_reduce(slab_ws, a.dw, (int64_t)out_elems, p.splits, a.accumulate, st);
   }
   return p.splits;
 }

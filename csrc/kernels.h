@@ -134,7 +134,8 @@ void dv_bn_bwd_reduce(const void* dout, const void* out, const void* x, int64_t 
                       const float* invstd, const float* mscale, const float* mshift, int act, float slope, float* acc,
                       int mask_bits, hipStream_t st);
 void dv_bn_bwd_finalize(float* acc, int C, double count, const float* gamma, const float* mean, const float* invstd,
-                        float* dgamma, float* dbeta, int accumulate, float* kA, float* kB, float* kC, hipStream_t st);
+                        float* dgamma, float* dbeta, int accumulate, float* kA, float* kB, float* kC, hipStream_t st,
+                        float* xsum = nullptr);
 void dv_bn_bwd_apply(const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t n, int C,
                      const float* kA, const float* kB, const float* kC, const float* mscale, const float* mshift, int act,
                      float slope, int mask_bits, const void* addend, hipStream_t st);
@@ -199,6 +200,7 @@ void dv_u8_normalize(const void* x, const void* flip, void* y, int N, int C, int
 void dv_f32_to_bf16(const float* x, void* y, int64_t n, hipStream_t st);
 
 // ---- loss / optimizers (loss_optim.hip) ----
+void dv_scale_by(const void* in, void* out, int64_t n, int is_bf16, const float* s, hipStream_t st);
 void dv_softmax_xent(const void* logits, int is_bf16, const int64_t* labels, int rows, int C, float* loss_rows, void* grad,
                      float grad_scale, float label_smoothing, hipStream_t st);
 void dv_sgd(float* p, const float* g, float* buf, int64_t n, float lr, float momentum, float dampening, float wd,

@@ -176,6 +176,38 @@ void dv_softmax_xent(const void* logits, int is_bf16, const int64_t* labels, int
   if (is_bf16) softmax_xent_kernel<true><<<rows, NT, 0, st>>>(logits, labels, C, loss_rows, grad, grad_scale, label_smoothing);
   else softmax_xent_kernel<false><<<rows, NT, 0, st>>>(logits, labels, C, loss_rows, grad, grad_scale, label_smoothing);
 }
+// out = in * (*s): the cross-entropy backward's upstream-gradient scale, read on the device (no
+// host sync) -- one vectorised launch instead of a broadcasting torch multiply with type promotion
+template <bool BF>
+__global__ __launch_bounds__(NT) void scale_by_kernel(const void* __restrict__ in, void* __restrict__ out, int64_t n,
+                                                      const float* __restrict__ s) {
+  const float k = *s;
+  const int64_t i0 = ((int64_t)blockIdx.x * NT + threadIdx.x) * 8;
+  if (i0 >= n) return;
+  if constexpr (BF) {
+    const u16* a = reinterpret_cast<const u16*>(in) + i0;
+    u16* o = reinterpret_cast<u16*>(out) + i0;
+    if (i0 + 8 <= n) {
+      const uint4 v = *reinterpret_cast<const uint4*>(a);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      uint32_t r[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) r[e] = pack2bf(bf2f(w[e] & 0xffff) * k, bf2f(w[e] >> 16) * k);
+      *reinterpret_cast<uint4*>(o) = uint4{r[0], r[1], r[2], r[3]};
+    } else {
+      for (int64_t i = 0; i < n - i0; ++i) o[i] = f2bf(bf2f(a[i]) * k);
+    }
+  } else {
+    const float* a = reinterpret_cast<const float*>(in) + i0;
+    float* o = reinterpret_cast<float*>(out) + i0;
+    for (int64_t i = 0; i < 8 && i0 + i < n; ++i) o[i] = a[i] * k;
+  }
+}
+void dv_scale_by(const void* in, void* out, int64_t n, int is_bf16, const float* s, hipStream_t st) {
+  const unsigned g = (unsigned)((n + NT * 8 - 1) / (NT * 8));
+  if (is_bf16) scale_by_kernel<true><<<g, NT, 0, st>>>(in, out, n, s);
+  else scale_by_kernel<false><<<g, NT, 0, st>>>(in, out, n, s);
+}
 void dv_sgd(float* p, const float* g, float* buf, int64_t n, float lr, float momentum, float dampening, float wd,
             int nesterov, int first, float gscale, const float* hp, hipStream_t st, const float* skip) {
   sgd_kernel<<<grid_for(n), NT, 0, st>>>(p, g, buf, n, lr, momentum, dampening, wd, nesterov, first, gscale, hp, skip);

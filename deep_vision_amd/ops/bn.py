@@ -76,7 +76,7 @@ class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, stats, weight, bias, running_mean, running_var, residual, training, momentum, eps, act,
                 slope, ws_fwd, ws_bwd, join=None, refbox=None, r_stats=None, r_weight=None, r_bias=None, r_rm=None,
-                r_rv=None, r_cfg=None, xjoin=None, defer_fwd=False, defer_bwd=False):
+                r_rv=None, r_cfg=None, xjoin=None, defer_fwd=False, defer_bwd=False, prod_bias=None):
         # xjoin (conv.GradJoin): another consumer of ``x`` stashes its gradient there (e.g. the
         # identity path of a pre-activation block); the backward apply pass adds it in place
         # r_*: a second, training-mode BatchNorm applied to ``residual`` inside the same pass
@@ -139,6 +139,8 @@ class _BNActFn(torch.autograd.Function):
         ctx.join = join
         ctx.xjoin = xjoin
         ctx.defer_bwd = bool(defer_bwd) and training
+        ctx.has_prod_bias = prod_bias is not None
+        ctx.prod_bias_param = prod_bias  # leaf parameter (not saved): its gradient may sink in place
         ctx.bnref = None
         if refbox is not None and training and ws_bwd is not None and C % 8 == 0 and (not act or bits or residual is None):
             mode = 3 if bits else (2 if act else 1)
@@ -162,6 +164,7 @@ class _BNActFn(torch.autograd.Function):
         st = stream_handle()
         L = lib()
         xg = ctx.xjoin.take() if ctx.xjoin is not None else None
+        pb_sink = pb_grad = None
         if xg is not None and not isinstance(xg, torch.Tensor):
             xg = xg.materialize()
         # the other consumer's gradient is summed inside the apply pass, written over its own buffer
@@ -192,9 +195,17 @@ class _BNActFn(torch.autograd.Function):
                 dgamma = torch.empty(C, dtype=F32, device=dev)
                 dbeta = torch.empty(C, dtype=F32, device=dev)
             coef = torch.empty((3, C), dtype=F32, device=dev)
+            # the producing conv's bias gradient = sum of this BN's input gradient, from the same sums
+            # in the finalize (training statistics, no other gradient folded into dx)
+            if ctx.has_prod_bias and ctx.needs_input_grad[25]:
+                if training and xg is None:
+                    pb_sink = grad_sink(ctx.prod_bias_param)
+                    if pb_sink is None:
+                        pb_grad = torch.zeros(C, dtype=F32, device=dev)
             L.bn_bwd_finalize(ptr(acc), C, float(rows), ptr(weight.detach() if weight is not None else None), ptr(mean),
                               ptr(invstd), ptr(sg if direct else dgamma), ptr(sb if direct else dbeta), int(direct),
-                              ptr(coef[0]), ptr(coef[1]), ptr(coef[2]), st)
+                              ptr(coef[0]), ptr(coef[1]), ptr(coef[2]), st,
+                              xsum=ptr(pb_sink if pb_sink is not None else pb_grad))
         # residual join with the projection BN folded in: both input gradients from one pass
         dual = (DUAL_BWD and training and rprm is not None and ctx.bits and not fold_x and ctx.needs_input_grad[6]
                 and dout.is_contiguous(memory_format=torch.channels_last))
@@ -258,8 +269,13 @@ class _BNActFn(torch.autograd.Function):
             dres = ctx.join.produce(dres)  # folded into the shortcut consumer's dgrad epilogue
         if xg is not None and not fold_x:
             dx = dx + xg
+        if ctx.has_prod_bias and ctx.needs_input_grad[25] and pb_sink is None and pb_grad is None:
+            # eval statistics / a folded second gradient: reduce the final dx explicitly
+            from .conv import _channel_sum
+
+            pb_grad = _channel_sum(dx if dx.shape[1] == C else dx.contiguous(memory_format=torch.channels_last))
         return (dx, None, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None, None, None,
-                None, r_dgamma, r_dbeta, None, None, None, None, None, None)
+                None, r_dgamma, r_dbeta, None, None, None, None, None, None, pb_grad)
 
 
 def _residual_bn_coef(ctx, dout, bits, r_x, rprm, r_weight, r_bias, act, slope, fused):
@@ -469,7 +485,7 @@ def bn_momentum(bn) -> float:
 
 
 def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None, residual_join=None, residual_bn=None,
-                   input_join=None, defer_out=False, defer_bwd=False):
+                   input_join=None, defer_out=False, defer_bwd=False, prod_bias=None):
     """act(BN(x) (+ residual)) with ``bn`` an nn.BatchNorm2d (parameters, buffers, mode).
     ``input_join`` (conv.GradJoin): x's gradient from another consumer, stashed there by its
     producer, is added inside this BN's backward apply pass.
@@ -520,7 +536,7 @@ def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None, residu
         rargs = (None,) * 6
     y = _BNActFn.apply(x, stats, bn.weight, bn.bias, rm, rv, residual, training, mom,
                        bn.eps, ACT_IDS[act], float(slope), ws_fwd, ws_bwd, residual_join, refbox, *rargs, input_join,
-                       bool(defer_out), bool(defer_bwd) and torch.is_grad_enabled())
+                       bool(defer_out), bool(defer_bwd) and torch.is_grad_enabled(), prod_bias)
     if refbox:
         y._dv_bnref = refbox[0]  # read by the consumer conv (ops.conv._ConvFn)
     return y
@@ -579,9 +595,11 @@ def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None, join=None, join
     mode = "zeros"
     if reflect_pad is not None:  # ReflectionPad2d in front of a pad-0 conv: fused into the gather
         pad, mode = reflect_pad, "reflect"
+    bvb = conv.bias is not None and bn.training and not shuffle  # bias gradient from the BN (bn_bwd_finalize xsum)
     r = conv2d(x, conv.weight, conv.bias, conv.stride, pad, conv.dilation, conv.groups, want_stats=want,
-               stats_buf=sbuf, join=join, join_role=join_role, pad_mode=mode, shuffle=shuffle)
+               stats_buf=sbuf, join=join, join_role=join_role, pad_mode=mode, shuffle=shuffle, bias_via_bn=bvb)
     y, stats = r if want else (r, None)
+    prod_bias = conv.bias if (bvb and getattr(y, "_dv_bias_via_bn", False)) else None
     if y.shape[1] % 8 != 0:  # padded view: BN kernels require dense channels
         y = y.contiguous(memory_format=torch.channels_last)
         stats = None
@@ -590,7 +608,7 @@ def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None, join=None, join
     bwd = (not shuffle and reflect_pad is None and y.requires_grad
            and defer.fusable_1x1(y.shape[1], ld_of(y), k[0], k[1], conv.stride, _pad2(pad), dl, conv.groups))
     return batch_norm_act(y, bn, act, slope, residual, stats, residual_join=residual_join, residual_bn=residual_bn,
-                          defer_out=defer_out, defer_bwd=bwd)
+                          defer_out=defer_out, defer_bwd=bwd, prod_bias=prod_bias)
 
 
 def _pad2(p):

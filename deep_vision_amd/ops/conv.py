@@ -86,7 +86,7 @@ def _channel_sum(dy: torch.Tensor, out=None) -> torch.Tensor:
     launches into a self-cleaning per-device workspace. ``out`` (a gradient sink): added into."""
     N, C, H, W = dy.shape
     ld = ld_of(dy)
-    key = (str(dy.device), ld)
+    key = (str(dy.device), ld, stream_handle())  # per stream: concurrent branches (models/hourglass.py)
     acc = _CSUM_WS.get(key)
     if acc is None:
         acc = _CSUM_WS[key] = torch.zeros((STAT_ROWS, ld), dtype=F32, device=dy.device)
@@ -405,7 +405,8 @@ def _wgrad_workspace(numel, device):
 class _ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats, stats_buf=None,
-                extra=(0, 0), join=None, join_role=None, reflect=False, out_box=None, residual=None, residual_join=None):
+                extra=(0, 0), join=None, join_role=None, reflect=False, out_box=None, residual=None, residual_join=None,
+                bias_via_bn=False):
         N, Cx, H, W = x.shape
         O, Ig, R, S = weight.shape
         G = groups
@@ -439,12 +440,16 @@ class _ConvFn(torch.autograd.Function):
         ctx.rjoin = residual_join  # the residual's gradient (= dy) is stashed there for its other consumer
         ctx.save_for_backward(x, weight, y if act else None)
         ctx.bias_param = bias  # leaf parameter (not saved): its gradient may sink in place
-        ctx.cfg = (stride, padding, dilation, G, act, slope, Cg_x, bias is not None)
+        # bias_via_bn: y feeds a training BatchNorm that returns this bias's gradient itself
+        # (ops.bn, from its backward sums: no reduction pass over dy here)
+        ctx.cfg = (stride, padding, dilation, G, act, slope, Cg_x, bias is not None and not bias_via_bn)
         ctx.reflect = reflect
         ctx.join = (join, join_role)
         # the producing BatchNorm of x: its backward statistics can ride on this conv's dgrad
         ctx.bnref = getattr(x, "_dv_bnref", None) if join_role != "producer" else None
         ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics output
+        if bias_via_bn and bias is not None:
+            y._dv_bias_via_bn = True  # the consumer BN owes this bias's gradient (ops.bn.conv_bn_act)
         if want_stats:
             ctx.mark_non_differentiable(stats)
             return y, stats
@@ -460,8 +465,8 @@ class _ConvFn(torch.autograd.Function):
                 g = join.take()  # nothing to add to: hand a stashed shortcut gradient through
                 if isinstance(g, MaskedGrad):
                     g = g.materialize()
-                return (g, None, None) + (None,) * 15
-            return (None,) * 18
+                return (g, None, None) + (None,) * 16
+            return (None,) * 19
         at = defer.take_grad(dy)  # dy = a deferred BN-backward apply (ops.defer): fold or run it first
         if at is not None and (act or ctx.reflect or not ctx.needs_input_grad[0] or G != 1
                                or not defer.fusable_1x1(dy.shape[1], ld_of(dy), *weight.shape[2:], stride, padding,
@@ -494,7 +499,7 @@ class _ConvFn(torch.autograd.Function):
         dres = dy if ctx.has_residual and ctx.needs_input_grad[16] else None  # y = ... + residual
         if dres is not None and ctx.rjoin is not None:
             dres = ctx.rjoin.produce(dres)
-        return dx, dw, db, None, None, None, None, None, None, None, None, None, None, None, None, None, dres, None
+        return dx, dw, db, None, None, None, None, None, None, None, None, None, None, None, None, None, dres, None, None
 
 
 # ---------------------------------------------------------------------------------------
@@ -620,7 +625,7 @@ class _StemConvFn(torch.autograd.Function):
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=None, slope=0.0,
            want_stats=False, stats_buf=None, join=None, join_role=None, pad_mode="zeros", out=None, residual=None,
-           residual_join=None, shuffle=0):
+           residual_join=None, shuffle=0, bias_via_bn=False):
     """Conv2d (+fused bias/activation). Returns y, or (y, stats) when want_stats (GPU only).
 
     ``shuffle=g`` (> 1): the output channels are channel-shuffled in g groups (ShuffleNet V1;
@@ -725,7 +730,7 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=
         residual_join = None
     return _ConvFn.apply(xn, weight, bias, stride, padding, dilation, groups, ACT_IDS[act], float(slope), want_stats,
                          stats_buf, extra, join, join_role, reflect, [out] if out is not None else None, res,
-                         residual_join)
+                         residual_join, bool(bias_via_bn and bias is not None and not act))
 
 
 def _gconv_ok(x, weight, bias, stride, padding, dilation, groups, act, join=None, out=None, residual=None,
@@ -1049,6 +1054,8 @@ class _DWConvFn(torch.autograd.Function):
         ctx.bnref = (bnref if (bnref is not None and bnref.mode in (1, 2) and ld_of(x) == C and tuple(stride) == (1, 1))
                      else None)
         ctx.set_materialize_grads(False)
+        if bias_via_bn and bias is not None:
+            y._dv_bias_via_bn = True  # the consumer BN owes this bias's gradient (ops.bn.conv_bn_act)
         if want_stats:
             ctx.mark_non_differentiable(stats)
             return y, stats

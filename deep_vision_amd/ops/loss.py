@@ -30,8 +30,11 @@ class _XentFn(torch.autograd.Function):
             return grad, None, None
         # out of place: the saved buffer stays the unscaled gradient, so a second backward through
         # a retained graph scales the same values again (an in-place mul_ would have returned
-        # grad*go1*go2); the (B, classes) product is one small launch either way
-        return grad * go, None, None
+        # grad*go1*go2); the scale is read on the device by one native launch
+        go = go.detach().to(F32).reshape(1).contiguous()
+        out = torch.empty_like(grad)
+        lib().scale_by(ptr(grad), ptr(out), grad.numel(), int(grad.dtype == BF16), ptr(go), stream_handle())
+        return out, None, None
 
 
 def cross_entropy(logits, labels, label_smoothing=0.0):

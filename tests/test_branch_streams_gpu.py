@@ -1,0 +1,107 @@
+"""Stacked Hourglass branch concurrency (models/hourglass.py BRANCH_STREAMS): each level's up1
+branch on a side stream gives the same step as the single-stream run, eagerly and as a captured
+HIP graph whose replays follow the eager trajectory."""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _net():
+    from deep_vision_amd.models.hourglass import StackedHourglassNetwork
+
+    torch.manual_seed(0)
+    return StackedHourglassNetwork(num_stack=2, num_residual=1, num_heatmap=16).to(DEV)
+
+
+def _loss(ys, hm):
+    from deep_vision_amd.ops.loss import heatmap_mse
+
+    return sum(heatmap_mse(y, hm) for y in ys)
+
+
+def _grads(m):
+    return torch.cat([p.grad.detach().float().reshape(-1) for p in m.parameters() if p.grad is not None])
+
+
+def test_branch_streams_match_single_stream():
+    from deep_vision_amd import set_deterministic
+    from deep_vision_amd.models import hourglass as H
+
+    x = torch.randn(4, 3, 128, 128, device=DEV)
+    hm = torch.rand(4, 16, 32, 32, device=DEV)
+    base = _net()
+    res = []
+    saved = H.BRANCH_STREAMS
+    set_deterministic(True)
+    try:
+        for on in (False, False, True, True):
+            H.BRANCH_STREAMS = on
+            m = copy.deepcopy(base)
+            loss = _loss(m(x), hm)
+            loss.backward()
+            torch.cuda.synchronize()
+            res.append((loss.item(), _grads(m)))
+    finally:
+        H.BRANCH_STREAMS = saved
+        set_deterministic(False)
+
+    def diff(i, j):
+        return (abs(res[i][0] - res[j][0]) / abs(res[i][0]), ((res[i][1] - res[j][1]).norm() / res[i][1].norm()).item())
+
+    same = [diff(0, 1), diff(2, 3)]
+    cross = [diff(0, 2), diff(1, 3)]
+    print("run-to-run", same, "single vs branch streams", cross)
+    spread_l = max(d[0] for d in same)
+    spread_g = max(d[1] for d in same)
+    for dl, dg in cross:  # forking changes no arithmetic: the same distribution of outcomes
+        assert dl <= 3 * spread_l + 1e-6, (dl, spread_l)
+        assert dg <= 3 * spread_g + 1e-4, (dg, spread_g)
+    assert len(H._STREAMS) >= 1
+
+
+def test_branch_streams_captured_step_matches_eager():
+    from deep_vision_amd.models import hourglass as H
+    from deep_vision_amd.train.graph import CapturedStep
+
+    assert H.BRANCH_STREAMS in ("graph", True)
+    from deep_vision_amd.train.optim import FusedAdam
+
+    xs = [torch.randn(4, 3, 128, 128, device=DEV) for _ in range(6)]
+    hms = [torch.rand(4, 16, 32, 32, device=DEV) for _ in range(6)]
+    a = _net()
+    b = copy.deepcopy(a)
+    oa, ob = FusedAdam(a.parameters(), lr=1e-3), FusedAdam(b.parameters(), lr=1e-3)
+
+    def make(model, opt):
+        def step(x, hm):
+            opt.zero_grad()
+            loss = _loss(model(x), hm)
+            loss.backward()
+            opt.step()
+            return loss
+        return step
+
+    sa = make(a, oa)
+    for i in range(6):
+        sa(xs[i], hms[i])
+    warm = iter([(xs[0], hms[0]), (xs[1], hms[1])])
+    sb = make(b, ob)
+
+    def step_fn(x, hm):
+        w = next(warm, None)
+        if w is not None:
+            x.copy_(w[0]); hm.copy_(w[1])
+        return sb(x, hm)
+
+    cap = CapturedStep(step_fn, ob, (xs[0].clone(), hms[0].clone()), model=b, warmup=2)
+    for i in range(2, 6):
+        cap(xs[i], hms[i])
+    torch.cuda.synchronize()
+    assert any(k[1] == 4 for k in H._STREAMS), "capture did not fork the up1 branches"
+    pa = torch.cat([p.detach().reshape(-1) for p in a.parameters()])
+    pb = torch.cat([p.detach().reshape(-1) for p in b.parameters()])
+    assert ((pa - pb).abs().max() / pa.abs().max()).item() < 2e-3

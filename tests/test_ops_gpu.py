@@ -733,3 +733,36 @@ def test_u8_normalize_kernel(W):
     out = normalize_u8(x.to(DEV), flip.to(DEV))
     assert out.dtype == torch.bfloat16 and tuple(out.shape) == (5, 3, 17, W)
     assert torch.allclose(out.float().cpu(), ref, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("train", [True, False])
+def test_conv_bias_grad_via_bn(train):
+    """A conv bias feeding a training BatchNorm gets its gradient from the BN's backward sums
+    (bn_bwd_finalize xsum, no reduction pass over dy): it must match the fp32 reference, where it is
+    ~0 (the BN input gradient sums to zero per channel); eval statistics reduce dx explicitly."""
+    from deep_vision_amd import nn, ops as F
+
+    torch.manual_seed(5)
+    conv = nn.Conv2d(64, 128, 1).to(DEV)
+    bn = nn.BatchNorm2d(128).to(DEV)
+    if not train:
+        bn.eval()
+        bn.running_mean.uniform_(-0.5, 0.5)
+        bn.running_var.uniform_(0.5, 2.0)
+    conv_r = torch.nn.Conv2d(64, 128, 1).to(DEV)
+    bn_r = torch.nn.BatchNorm2d(128).to(DEV)
+    conv_r.load_state_dict({k: v.bfloat16().float() if k == "weight" else v for k, v in conv.state_dict().items()})
+    bn_r.load_state_dict(bn.state_dict())
+    bn_r.train(train)
+    x32 = torch.randn(4, 64, 12, 12, device=DEV).bfloat16().float()
+    y = F.conv_bn_act(_nhwc(x32), conv, bn, "relu")
+    yr = TF.relu(bn_r(conv_r(x32)))
+    g = torch.randn_like(yr).bfloat16().float()
+    y.backward(_nhwc(g))
+    yr.backward(g)
+    scale = conv_r.weight.grad.abs().max().item()
+    assert conv.bias.grad is not None
+    if train:
+        assert (conv.bias.grad - conv_r.bias.grad).abs().max().item() < 1e-2 * scale
+    else:
+        assert _rel(conv.bias.grad, conv_r.bias.grad) < 3e-2
