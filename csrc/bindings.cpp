@@ -184,6 +184,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gap_fwd", [](uptr x, uptr y, int N, int HW, int C, uptr st) { dv_gap_fwd(CP(x), P(y), N, HW, C, ST(st)); check_last("gap_fwd"); });
   m.def("gap_bwd", [](uptr dy, uptr dx, int N, int HW, int C, uptr st) { dv_gap_bwd(CP(dy), P(dx), N, HW, C, ST(st)); check_last("gap_bwd"); });
   m.def("upsample_fwd", [](uptr x, uptr y, int N, int H, int W, int C, int f, uptr st) { dv_upsample_fwd(CP(x), P(y), N, H, W, C, f, ST(st)); check_last("upsample_fwd"); });
+  m.def("upsample_add", [](uptr x, uptr r, uptr y, int N, int H, int W, int C, int f, uptr st) { dv_upsample_add(CP(x), CP(r), P(y), N, H, W, C, f, ST(st)); check_last("upsample_add"); });
   m.def("upsample_bwd", [](uptr dy, uptr dx, int N, int H, int W, int C, int f, uptr st) { dv_upsample_bwd(CP(dy), P(dx), N, H, W, C, f, ST(st)); check_last("upsample_bwd"); });
 
   m.def("act_fwd", [](uptr x, uptr y, int64_t n, int act, float slope, uptr st) { dv_act_fwd(CP(x), P(y), n, act, slope, ST(st)); check_last("act_fwd"); });

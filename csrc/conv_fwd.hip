@@ -514,8 +514,11 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
   if (p.ypart) {
     // split-K serves small grids (Hourglass 4x4-16x16 maps): 64-row blocks left 8-32 blocks walking
     // up to 16 slabs serially (37 us median); shrink the row block until ~512 blocks
+    // -- but no more row blocks than statistics shards while that is possible: one block per shard
+    // adds onto a zero, so small launches keep bitwise-reproducible BatchNorm statistics
     const int ncb = (p.N + 255) / 256;
     int fr = (int)(((int64_t)p.M * ncb + 511) / 512);
+    fr = std::max(fr, (p.M + DV_STAT_SHARDS - 1) / DV_STAT_SHARDS);
     fr = std::max(4, std::min(FR_ROWS, (fr + 3) / 4 * 4));
     const dim3 grid((unsigned)ncb, (unsigned)((p.M + fr - 1) / fr));
     splitk_finalize_kernel<<<grid, dim3(256), 0, st>>>(p.ypart, dv_g_last_ksplit, p.M, p.N, p.bias, p.act, p.slope,

@@ -576,7 +576,11 @@ int dv_conv_wgrad(const ConvWgradArgs& a, hipStream_t st) {
   // slabs are summed in a fixed order afterwards -- no atomics, reproducible bits
   // tiny accumulating launches (Hourglass 4x4 / 8x8 maps, < 4 GFLOP): the reduce pass's launch
   // costs more than the atomics it avoids, and accumulating into a zeroed buffer needs no memset
-  const bool tiny = a.accumulate && 2.0 * p.M * (double)p.N * p.K * p.G < 4e9;
+  static const bool tiny_on = [] {
+    const char* v = std::getenv("DV_WG_TINY");
+    return !(v && v[0] == '0');
+  }();
+  const bool tiny = tiny_on && a.accumulate && 2.0 * p.M * (double)p.N * p.K * p.G < 4e9;
   const bool slab = g_wg_slab == 1 || (g_wg_slab < 0 && p.splits <= SLAB_MAX_SPLITS && !tiny);
   bool det = (g_deterministic || slab) && p.splits > 1;
   float* slab_ws = det ? dv_slab_workspace((size_t)p.splits * out_elems, st) : nullptr;

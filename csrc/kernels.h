@@ -165,6 +165,7 @@ void dv_avgpool_bwd(const void* dy, void* dx, int N, int H, int W, int C, int P,
 void dv_gap_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st);
 void dv_gap_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st);
 void dv_upsample_fwd(const void* x, void* y, int N, int H, int W, int C, int f, hipStream_t st);
+void dv_upsample_add(const void* x, const void* r, void* y, int N, int H, int W, int C, int f, hipStream_t st);
 void dv_upsample_bwd(const void* dy, void* dx, int N, int H, int W, int C, int f, hipStream_t st);
 
 // ---- elementwise / layout (elementwise.hip) ----

@@ -219,6 +219,26 @@ __global__ __launch_bounds__(NT) void upsample_fwd_kernel(const u16* __restrict_
   }
 }
 
+// y = upsample_nearest(x, f) + r (Stacked Hourglass level merge, models/hourglass.py): one pass
+// instead of an upsample pass + an add pass over the upsampled tensor (16 per step)
+template <int VEC>
+__global__ __launch_bounds__(NT) void upsample_add_kernel(const u16* __restrict__ x, const u16* __restrict__ r,
+                                                            u16* __restrict__ y, int N, int H, int W, int C, int f) {
+  const int cg = C / VEC, OH = H * f, OW = W * f;
+  const int64_t total = (int64_t)N * OH * OW * cg;
+  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < total; t += (int64_t)gridDim.x * NT) {
+    const int c = (int)(t % cg) * VEC; int64_t pix = t / cg;
+    const int ow = (int)(pix % OW); pix /= OW; const int oh = (int)(pix % OH); const int n = (int)(pix / OH);
+    const int64_t o = (((int64_t)n * OH + oh) * OW + ow) * C + c;
+    float a[VEC], b[VEC];
+    V<VEC>::ld(x + (((int64_t)n * H + oh / f) * W + ow / f) * C + c, a);
+    V<VEC>::ld(r + o, b);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) a[i] += b[i];
+    V<VEC>::st(y + o, a);
+  }
+}
+
 template <int VEC>
 __global__ __launch_bounds__(NT) void upsample_bwd_kernel(const u16* __restrict__ dy, u16* __restrict__ dx, int N, int H,
                                                             int W, int C, int f) {
@@ -696,6 +716,10 @@ void dv_gap_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st) 
 void dv_upsample_fwd(const void* x, void* y, int N, int H, int W, int C, int f, hipStream_t st) {
   const int v = C % 8 == 0 ? 8 : 1;
   VDISPATCH(C, upsample_fwd_kernel, <<<grid_for((int64_t)N * H * W * f * f * C / v), NT, 0, st>>>((const u16*)x, (u16*)y, N, H, W, C, f));
+}
+void dv_upsample_add(const void* x, const void* r, void* y, int N, int H, int W, int C, int f, hipStream_t st) {
+  const int v = C % 8 == 0 ? 8 : 1;
+  VDISPATCH(C, upsample_add_kernel, <<<grid_for((int64_t)N * H * W * f * f * C / v), NT, 0, st>>>((const u16*)x, (const u16*)r, (u16*)y, N, H, W, C, f));
 }
 void dv_upsample_bwd(const void* dy, void* dx, int N, int H, int W, int C, int f, hipStream_t st) {
   const int v = C % 8 == 0 ? 8 : 1;

@@ -46,7 +46,16 @@ def available() -> bool:
         return False
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_CUR_DEV = getattr(torch._C, "_cuda_getDevice", None)
+
+
 def stream_handle(device=None) -> int:
+    """The current HIP stream of ``device`` (default: the current device) as an integer handle.
+    Called once per kernel launch: the raw-pointer query skips building a torch.cuda.Stream
+    object (a few microseconds per launch on the launch-bound models)."""
+    if device is None and _RAW_STREAM is not None:
+        return _RAW_STREAM(_CUR_DEV())
     return torch.cuda.current_stream(device).cuda_stream
 
 

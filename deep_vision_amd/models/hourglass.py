@@ -33,6 +33,7 @@ never does. Env ``DV_BRANCH_STREAMS`` = graph / 1 / 0.
 """
 from __future__ import annotations
 
+import torch
 import torch.nn as tnn
 
 from .. import nn
@@ -50,9 +51,9 @@ def _fork(x):
     if BRANCH_STREAMS is False or not F.native(x):
         return False
     if BRANCH_STREAMS == "graph":
-        import torch
+        from ..train.graph import capturing_or_warming
 
-        return torch.cuda.is_current_stream_capturing()
+        return capturing_or_warming()  # the warm-up steps fork too: they size the side streams' scratch
     return True
 
 
@@ -64,6 +65,25 @@ def _side_stream(device, depth):
     if st is None:
         st = _STREAMS[key] = torch.cuda.Stream(device=device)
     return st
+
+
+class _BranchEdge(torch.autograd.Function):
+    """Identity at a stream fork / join. Its backward runs on the branch's stream (autograd runs a
+    node's backward on its forward stream) and marks the gradient crossing the edge as used by
+    both streams: a gradient allocated on one stream and read on the other would otherwise go
+    back to its allocating stream's pool while the other stream may still read it."""
+
+    @staticmethod
+    def forward(ctx, t, other):
+        ctx.other = other
+        return t.view_as(t)
+
+    @staticmethod
+    def backward(ctx, g):
+        if g is not None:
+            g.record_stream(torch.cuda.current_stream(g.device))
+            g.record_stream(ctx.other)
+        return g, None
 
 
 def _bn(c):
@@ -107,21 +127,19 @@ class HourglassModule(tnn.Module):
 
     def forward(self, x):
         if _fork(x):
-            import torch
-
             main = torch.cuda.current_stream(x.device)
             side = _side_stream(x.device, self.order)
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                up1 = self.up1(x)
+                up1 = _BranchEdge.apply(self.up1(_BranchEdge.apply(x, main)), main)
             low = self.low3(self.low2(self.low1(F.max_pool2d(x, 2, 2))))
             main.wait_stream(side)
             x.record_stream(side)  # caching allocator: x is read on the side stream
             up1.record_stream(main)
-            return F.add(F.upsample_nearest(low, 2), up1)
+            return F.upsample_add(low, up1, 2)
         up1 = self.up1(x)
         low = self.low3(self.low2(self.low1(F.max_pool2d(x, 2, 2))))
-        return F.add(F.upsample_nearest(low, 2), up1)
+        return F.upsample_add(low, up1, 2)
 
 
 class StackedHourglassNetwork(tnn.Module):

@@ -1054,8 +1054,6 @@ class _DWConvFn(torch.autograd.Function):
         ctx.bnref = (bnref if (bnref is not None and bnref.mode in (1, 2) and ld_of(x) == C and tuple(stride) == (1, 1))
                      else None)
         ctx.set_materialize_grads(False)
-        if bias_via_bn and bias is not None:
-            y._dv_bias_via_bn = True  # the consumer BN owes this bias's gradient (ops.bn.conv_bn_act)
         if want_stats:
             ctx.mark_non_differentiable(stats)
             return y, stats

@@ -154,6 +154,44 @@ class _UpsampleFn(torch.autograd.Function):
         return dx, None
 
 
+class _UpsampleAddFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, r, f):
+        N, C, H, W = x.shape
+        y = torch.empty_like(r)
+        lib().upsample_add(ptr(x), ptr(r), ptr(y), N, H, W, C, f, stream_handle())
+        ctx.cfg = (x.shape, f)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (N, C, H, W), f = ctx.cfg
+        dy = _dense(grad_nhwc(dy))
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty((N, C, H, W), dtype=BF16, device=dy.device, memory_format=CL)
+            lib().upsample_bwd(ptr(dy), ptr(dx), N, H, W, C, f, stream_handle())
+        return dx, dy, None
+
+
+def upsample_add(x, r, scale_factor=2):
+    """upsample_nearest(x, scale_factor) + r in one native pass (the Hourglass level merge,
+    R/Hourglass/tensorflow/hourglass104.py:95-97); r's gradient is the incoming one unchanged."""
+    f = int(scale_factor)
+    if not native(x) or f != scale_factor:
+        from .act import add
+
+        return add(upsample_nearest(x, scale_factor), r)
+    x = _dense(as_nhwc(x, pad_to8=False))
+    r = _dense(as_nhwc(r, pad_to8=False))
+    N, C, H, W = x.shape
+    if tuple(r.shape) != (N, C, H * f, W * f) or r.dtype != BF16 or x.dtype != BF16:
+        from .act import add
+
+        return add(upsample_nearest(x, scale_factor), r)
+    return _UpsampleAddFn.apply(x, r, f)
+
+
 def upsample_nearest(x, scale_factor=2):
     f = int(scale_factor)
     if native(x) and f != scale_factor:

@@ -76,7 +76,7 @@ class CapturedStep:
     def _capture(self, warmup):
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
+        with torch.cuda.stream(s), capture_warmup():
             for _ in range(max(1, warmup)):  # real steps: allocator warm-up, first-step optimizer state
                 self.warmup_outputs = self.step_fn(*self.static_inputs)
         torch.cuda.current_stream().wait_stream(s)
@@ -84,7 +84,10 @@ class CapturedStep:
         self.opt.use_device_hparams(True)
         host = [(f["step"], f["first"]) if f else None for f in self.opt._flat]
         pending = {id(m): m.__dict__.get("_dv_nbt_pending", 0) for m in self._bns}
-        with torch.cuda.graph(self.graph):
+        # captured on the warm-up stream: the per-stream scratch the warm-up sized (split-K slabs,
+        # channel sums) is what the captured kernels use -- a fresh capture stream would find none
+        # and could not allocate it mid-capture
+        with torch.cuda.graph(self.graph, stream=s):
             self.outputs = self.step_fn(*self.static_inputs)
         # the capture executed nothing: undo its host-side bookkeeping
         for f, h in zip(self.opt._flat, host):
@@ -103,6 +106,27 @@ class CapturedStep:
             m._dv_nbt_pending = m.__dict__.get("_dv_nbt_pending", 0) + 1
         self.graph.replay()
         return self.outputs
+
+
+_WARMUP = [0]
+
+
+class capture_warmup:
+    """Context of the eager steps that precede a capture: code that behaves differently under
+    capture (models/hourglass.py branch streams) takes its capture-time form here too, so the
+    warm-up sizes the same per-stream scratch the captured step will use."""
+
+    def __enter__(self):
+        _WARMUP[0] += 1
+        return self
+
+    def __exit__(self, *exc):
+        _WARMUP[0] -= 1
+        return False
+
+
+def capturing_or_warming() -> bool:
+    return _WARMUP[0] > 0 or torch.cuda.is_current_stream_capturing()
 
 
 def prepare_capture_env() -> None:

@@ -364,6 +364,26 @@ def test_activations_add_upsample():
     assert torch.allclose(x.grad.float(), torch.full_like(x32, 4.0))
 
 
+def test_upsample_add_matches_reference():
+    """The fused Hourglass level merge: upsample_nearest(low) + skip, both gradients."""
+    from deep_vision_amd import ops as F
+
+    low32 = torch.randn(3, 64, 4, 4, device=DEV).bfloat16().float()
+    skip32 = torch.randn(3, 64, 8, 8, device=DEV).bfloat16().float()
+    low = _nhwc(low32).requires_grad_(True)
+    skip = _nhwc(skip32).requires_grad_(True)
+    y = F.upsample_add(low, skip, 2)
+    lr_ = low32.clone().requires_grad_(True)
+    sr = skip32.clone().requires_grad_(True)
+    yr = TF.interpolate(lr_, scale_factor=2, mode="nearest") + sr
+    assert _rel(y, yr) < 1e-2
+    dy = torch.randn_like(yr).bfloat16().float()
+    y.backward(_nhwc(dy))
+    yr.backward(dy)
+    assert _rel(low.grad, lr_.grad) < 1e-2
+    assert _rel(skip.grad, sr.grad) == 0.0
+
+
 def test_dropout_mask_consistency():
     from deep_vision_amd import ops as F
 

@@ -29,18 +29,22 @@ case "$mode" in
     timeout -k 10 400 python bench.py "$@" > gpurun_out/bench.log 2>&1
     rc=$?; tail -1 gpurun_out/bench.log | cut -c1-400 ;;
   prof)
+    # GRAPH=1: profile the HIP-graph replay step (bench.py --graph); BATCH=n overrides the batch
     m=${1:-resnet50}
+    extra=""; [ -n "$GRAPH" ] && extra="--graph"; [ -n "$BATCH" ] && extra="$extra --batch $BATCH"
+    tag=$m${GRAPH:+_graph}
     cd /tmp && export TMPDIR=/tmp && \
-    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$m" -o run --output-format csv -- \
-      python3 "$R/bench.py" --model "$m" --steps 5 --warmup 2 > "$R/gpurun_out/prof_$m.log" 2>&1
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$tag" -o run --output-format csv -- \
+      python3 "$R/bench.py" --model "$m" --steps 6 --warmup 2 $extra > "$R/gpurun_out/prof_$tag.log" 2>&1
     rc=$?; cd "$R"
-    f=$(find gpurun_out/prof_$m -name '*kernel_stats.csv' -print -quit)
-    [ -n "$f" ] && python tools/prof_summary.py "$f" 7 "$m bench.py --steps 5 --warmup 2" > gpurun_out/prof_$m.txt 2>&1
-    t=$(find gpurun_out/prof_$m -name '*kernel_trace.csv' -print -quit)
-    [ -n "$t" ] && python tools/trace_step.py "$t" > gpurun_out/trace_$m.txt 2>&1
-    [ -n "$t" ] && python tools/kernel_census.py "$t" > gpurun_out/census_$m.txt 2>&1
+    f=$(find gpurun_out/prof_$tag -name '*kernel_stats.csv' -print -quit)
+    [ -n "$f" ] && python tools/prof_summary.py "$f" 8 "$m bench.py --steps 6 --warmup 2 $extra" > gpurun_out/prof_$tag.txt 2>&1
+    t=$(find gpurun_out/prof_$tag -name '*kernel_trace.csv' -print -quit)
+    [ -n "$t" ] && python tools/step_table.py "$t" --steps 4 --title "$m bench.py $extra (rocprofv3 --kernel-trace)" > gpurun_out/step_$tag.txt 2>&1
+    [ -n "$t" ] && python tools/trace_step.py "$t" > gpurun_out/trace_$tag.txt 2>&1
+    [ -n "$t" ] && python tools/kernel_census.py "$t" > gpurun_out/census_$tag.txt 2>&1
     rm -f "$t"
-    cat gpurun_out/prof_$m.txt | cut -c1-160 | sed -n '1,45p' ;;
+    cat gpurun_out/step_$tag.txt | cut -c1-160 | sed -n '1,45p' ;;
   pmc)
     L=${1:-s2_1x1_128_512,s4_3x3_512,s1_1x1_64_256,s2_3x3_128}
     mkdir -p gpurun_out/pmc && cd /tmp && export TMPDIR=/tmp && \

@@ -16,4 +16,6 @@ for m in hourglass yolov3; do
   tail -1 gpurun_out/bg_$m.log | cut -c1-200
 done
 timeout -k 10 500 python -u tools/convergence.py --steps 300 --seeds 0 --every 50 > gpurun_out/conv_pilot.log 2>&1
-rc=$?; tail -20 gpurun_out/conv_pilot.log; exit $rc
+rc=$?; tail -20 gpurun_out/conv_pilot.log; bad $rc && exit $rc
+timeout -k 10 300 python -u tools/host_profile.py --model hourglass --steps 3 > gpurun_out/host_hg.log 2>&1 || exit $?
+head -60 gpurun_out/host_hg.log | cut -c1-160
