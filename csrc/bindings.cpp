@@ -92,9 +92,9 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("conv_wgrad", [](uptr x, uptr dy, uptr dw, int Nb, int H, int W, int Cg, int ldx, int G, int Kout, int P_, int Q,
                          int ldy, int R, int S, int sh, int sw, int ph, int pw, int dh, int dwl, int splits, int accumulate,
-                         int oirs_ig, uptr st, int reflect) {
+                         int oirs_ig, uptr st, int reflect, uptr out, int out_ig, int out_accumulate) {
     ConvWgradArgs a{CP(x), CP(dy), FP(dw), Nb, H, W, Cg, ldx, G, Kout, P_, Q, ldy, R, S, sh, sw, ph, pw, dh, dwl, splits,
-                    accumulate, oirs_ig, reflect};
+                    accumulate, oirs_ig, reflect, FP(out), out_ig, out_accumulate};
     int r = dv_conv_wgrad(a, ST(st));
     if (r < 0) throw std::runtime_error("conv_wgrad: unsupported geometry (channels must be a multiple of 8)");
     check_last("conv_wgrad");
@@ -102,7 +102,9 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("Nb"), py::arg("H"), py::arg("W"), py::arg("Cg"), py::arg("ldx"),
      py::arg("G"), py::arg("Kout"), py::arg("P"), py::arg("Q"), py::arg("ldy"), py::arg("R"), py::arg("S"), py::arg("sh"),
      py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw_"), py::arg("splits"), py::arg("accumulate"),
-     py::arg("oirs_ig"), py::arg("st"), py::arg("reflect") = 0);
+     py::arg("oirs_ig"), py::arg("st"), py::arg("reflect") = 0, py::arg("out") = 0, py::arg("out_ig") = 0,
+     py::arg("out_accumulate") = 0);
+  m.attr("WGRAD_FINAL") = DV_WGRAD_FINAL;
 
   m.def("bn_stats", [](uptr x, int64_t rows, int C, uptr acc, uptr st) { dv_bn_stats(CP(x), rows, C, FP(acc), ST(st)); check_last("bn_stats"); });
   m.def("bn_finalize", [](uptr acc, int C, double count, float eps, float mom, uptr gamma, uptr beta, uptr rm, uptr rv,
@@ -114,11 +116,13 @@ PYBIND11_MODULE(_C, m) {
     dv_bn_eval_prep(C, eps, CFP(gamma), CFP(beta), CFP(rm), CFP(rv), FP(scale), FP(shift), ST(st)); check_last("bn_eval_prep");
   });
   m.def("bn_apply", [](uptr x, uptr res, uptr out, int64_t n, int C, uptr scale, uptr shift, int act, float slope,
-                       uptr mask, uptr st, uptr rscale, uptr rshift) {
-    dv_bn_apply(CP(x), CP(res), P(out), n, C, CFP(scale), CFP(shift), act, slope, P(mask), CFP(rscale), CFP(rshift), ST(st));
+                       uptr mask, uptr st, uptr rscale, uptr rshift, int post) {
+    dv_bn_apply(CP(x), CP(res), P(out), n, C, CFP(scale), CFP(shift), act, slope, P(mask), CFP(rscale), CFP(rshift), ST(st),
+                post);
     check_last("bn_apply");
   }, py::arg("x"), py::arg("res"), py::arg("out"), py::arg("n"), py::arg("C"), py::arg("scale"), py::arg("shift"),
-     py::arg("act"), py::arg("slope"), py::arg("mask"), py::arg("st"), py::arg("rscale") = 0, py::arg("rshift") = 0);
+     py::arg("act"), py::arg("slope"), py::arg("mask"), py::arg("st"), py::arg("rscale") = 0, py::arg("rshift") = 0,
+     py::arg("post") = 0);
   m.def("bn_bwd_reduce", [](uptr dout, uptr out, uptr x, int64_t rows, int C, uptr mean, uptr invstd, uptr mscale,
                             uptr mshift, int act, float slope, uptr acc, int mask_bits, uptr st) {
     dv_bn_bwd_reduce(CP(dout), CP(out), CP(x), rows, C, CFP(mean), CFP(invstd), CFP(mscale), CFP(mshift), act, slope, FP(acc),

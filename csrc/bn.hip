@@ -226,7 +226,9 @@ struct RowTile {
 };
 
 // ---- out = act(x*scale + shift (+res)) ----
-template <int VEC, bool MB, bool RBN = false, int UNR = 2>
+// POST: out = act(x*scale + shift) + res -- a residual added after the activation (Darknet's
+// x + leaky(bn(conv(.))), models/yolov3.py), replacing a separate add pass
+template <int VEC, bool MB, bool RBN = false, int UNR = 2, bool POST = false>
 __global__ __launch_bounds__(NT) void bn_apply_kernel(const u16* __restrict__ x, const u16* __restrict__ res,
                                                         u16* __restrict__ out, int64_t rows, int C, int64_t rows_per_block,
                                                         const float* __restrict__ scale, const float* __restrict__ shift,
@@ -255,9 +257,10 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const u16* __restrict__ x,
       for (int k = 0; k < VEC; ++k) {
         float z = fmaf(v[k], sc[k], sf[k]);
         if constexpr (RBN) z = fmaf(rv[k], rs[k], z);
-        else if (res) z += rv[k];
+        else if (res && !POST) z += rv[k];
         if constexpr (MB) bits |= (z > 0.f ? 1u : 0u) << k;
         v[k] = act_fwd(z, act, slope);
+        if constexpr (POST) v[k] += rv[k];
       }
       VecIO<VEC>::store(out + o, v);
       if constexpr (MB) {  // activation mask, 1 bit per element (VEC == 8)
@@ -562,12 +565,21 @@ void dv_bn_eval_prep(int C, float eps, const float* gamma, const float* beta, co
 }
 
 void dv_bn_apply(const void* x, const void* res, void* out, int64_t n, int C, const float* scale, const float* shift,
-                 int act, float slope, void* mask, const float* rscale, const float* rshift, hipStream_t st) {
+                 int act, float slope, void* mask, const float* rscale, const float* rshift, hipStream_t st, int post) {
   const int v = vec_for(C);
   const int64_t rows = n / C;
   const int64_t rpb = apply_rows_per_block(rows, C, v);
   const int g = (int)((rows + rpb - 1) / rpb);
 #define AP_ARGS <<<g, NT, 0, st>>>((const u16*)x, (const u16*)res, (u16*)out, rows, C, rpb, scale, shift, act, slope, (uint8_t*)mask, rscale, rshift)
+  if (post && res) {  // post-activation residual: the mask comes from x in backward (no bits)
+    switch (v) {
+      case 8: bn_apply_kernel<8, false, false, 2, true> AP_ARGS; break;
+      case 4: bn_apply_kernel<4, false, false, 2, true> AP_ARGS; break;
+      case 2: bn_apply_kernel<2, false, false, 2, true> AP_ARGS; break;
+      default: bn_apply_kernel<1, false, false, 2, true> AP_ARGS; break;
+    }
+    return;
+  }
   if (g_apply_unroll == 4 && mask && v == 8) {
     if (res && rscale && rshift) bn_apply_kernel<8, true, true, 4> AP_ARGS;
     else bn_apply_kernel<8, true, false, 4> AP_ARGS;

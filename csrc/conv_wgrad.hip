@@ -478,6 +478,32 @@ float* dv_slab_workspace(size_t elems, hipStream_t st) {
   return w.ptr;
 }
 
+// The ordered slab sum of a packed [rows][RS][Ipad] weight gradient written straight into the
+// parameter's [rows][Ig][RS] (OIHW) layout: one thread per packed element sums its splits in a
+// fixed order (four loads in flight) and stores to the element's OIHW position -- the separate
+// wgrad_unprep pass (and its read + re-zero of a packed workspace) is gone. The scattered 4-B
+// stores touch only the weight tensor once; the slab reads stay coalesced.
+__global__ __launch_bounds__(256) void slab_reduce_oirs_kernel(const float* __restrict__ ws, float* __restrict__ dst,
+                                                               int rs, int ipad, int ig, int splits, int64_t slab,
+                                                               int accumulate) {
+  const int n = rs * ipad;
+  for (int64_t t = blockIdx.x * 256ll + threadIdx.x; t < slab; t += (int64_t)gridDim.x * 256) {
+    const int64_t o = t / n;
+    const int e = (int)(t - o * n), r = e / ipad, i = e - r * ipad;
+    if (i >= ig) continue;
+    float v = 0.f;
+    int sp = 0;
+    for (; sp + 4 <= splits; sp += 4) {
+      const float a0 = ws[(int64_t)sp * slab + t], a1 = ws[(int64_t)(sp + 1) * slab + t];
+      const float a2 = ws[(int64_t)(sp + 2) * slab + t], a3 = ws[(int64_t)(sp + 3) * slab + t];
+      v += a0; v += a1; v += a2; v += a3;
+    }
+    for (; sp < splits; ++sp) v += ws[(int64_t)sp * slab + t];
+    float* d = dst + (o * ig + i) * rs + r;
+    *d = accumulate ? *d + v : v;
+  }
+}
+
 void dv_slab_reduce(const float* ws, float* dst, int64_t n, int splits, int accumulate, hipStream_t st) {
   if (n % 4 == 0 && ((uintptr_t)ws & 15) == 0 && ((uintptr_t)dst & 15) == 0) {
     const int64_t n4 = n / 4;
@@ -604,6 +630,16 @@ int dv_conv_wgrad(const ConvWgradArgs& a, hipStream_t st) {
   if (plain) dispatch_wg<true>(p, bn, bw, st);
   else dispatch_wg<false>(p, bn, bw, st);
   if (det) {
+    static const bool final_on = [] {
+      const char* v = std::getenv("DV_WG_FINAL");
+      return !(v && v[0] == '0');
+    }();
+    if (final_on && a.out && p.oirs_ig == 0 && a.out_ig > 0 && a.out_ig <= p.Cg) {
+      const unsigned grid = (unsigned)std::min<int64_t>(((int64_t)out_elems + 255) / 256, 8192);
+      slab_reduce_oirs_kernel<<<grid, 256, 0, st>>>(slab_ws, a.out, a.R * a.S, p.Cg, a.out_ig, p.splits,
+                                                    (int64_t)out_elems, a.out_accumulate);
+      return p.splits | DV_WGRAD_FINAL;
+    }
     dv_slab_reduce(slab_ws, a.dw, (int64_t)out_elems, p.splits, a.accumulate, st);
   }
   return p.splits;

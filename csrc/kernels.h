@@ -92,7 +92,13 @@ struct ConvWgradArgs {
   int accumulate;  // add into dw (live gradient buffer) instead of overwriting
   int oirs_ig;     // > 0: dw is the parameter's own [G*Kout][oirs_ig][R][S] layout (padded channels dropped)
   int reflect;     // im2col with reflected out-of-image taps (see ConvFwdArgs)
+  // optional: the parameter's OIHW gradient [G*Kout][out_ig][R][S]. When the split-K partials go
+  // through ordered slabs, their reduce pass writes (or with out_accumulate adds) straight into it
+  // and dv_conv_wgrad returns splits | DV_WGRAD_FINAL; otherwise `dw` holds the packed result.
+  float* out;
+  int out_ig, out_accumulate;
 };
+constexpr int DV_WGRAD_FINAL = 1 << 30;
 
 int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st);  // 0 ok, 1 ok but BN statistics not fused, -1 unsupported
 void dv_conv_fwd_variant(int v);  // 0 = heuristic tile choice; others: benchmarking override
@@ -129,7 +135,7 @@ void dv_bn_eval_prep(int C, float eps, const float* gamma, const float* beta, co
 // out = act(x*scale + shift (+ res [* rscale + rshift])): rscale/rshift fold a second BatchNorm
 // (a residual block's projection BN) into the same pass instead of materialising its output
 void dv_bn_apply(const void* x, const void* res, void* out, int64_t n, int C, const float* scale, const float* shift,
-                 int act, float slope, void* mask, const float* rscale, const float* rshift, hipStream_t st);
+                 int act, float slope, void* mask, const float* rscale, const float* rshift, hipStream_t st, int post = 0);
 void dv_bn_bwd_reduce(const void* dout, const void* out, const void* x, int64_t rows, int C, const float* mean,
                       const float* invstd, const float* mscale, const float* mshift, int act, float slope, float* acc,
                       int mask_bits, hipStream_t st);

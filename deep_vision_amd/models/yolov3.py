@@ -22,6 +22,7 @@ import torch.nn as tnn
 
 from .. import nn
 from .. import ops as F
+from ..ops.conv import GradJoin
 
 # R/YOLO/tensorflow/yolov3.py:19-21
 ANCHORS_WH = np.array([[10, 13], [16, 30], [33, 23], [30, 61], [62, 45], [59, 119], [116, 90], [156, 198],
@@ -35,9 +36,10 @@ class DarknetConv(tnn.Module):
         self.conv = nn.Conv2d(cin, cout, k, stride=stride, padding="same_keras", bias=False)
         self.bn = nn.BatchNorm2d(cout, eps=1e-3, momentum=0.01)
 
-    def forward(self, x, residual=None):
-        return F.conv_bn_act(x, self.conv, self.bn, "leaky", 0.1) if residual is None else \
-            F.add(F.conv_bn_act(x, self.conv, self.bn, "leaky", 0.1), residual)
+    def forward(self, x, residual=None, join=None, join_role=None, residual_join=None):
+        # residual: out = leaky(bn(conv(x))) + residual, the add inside the BN apply pass
+        return F.conv_bn_act(x, self.conv, self.bn, "leaky", 0.1, residual=residual, residual_post=True, join=join,
+                             join_role=join_role, residual_join=residual_join)
 
 
 class DarknetResidual(tnn.Module):
@@ -47,8 +49,13 @@ class DarknetResidual(tnn.Module):
         self.conv_3x3 = DarknetConv(c1, c2, 3, 1)
 
     def forward(self, x):
-        # Add()([shortcut, LeakyReLU(BN(conv))]): the add follows the activation
-        return self.conv_3x3(self.conv_1x1(x), residual=x)
+        # Add()([shortcut, LeakyReLU(BN(conv))]): the add follows the activation and rides in the
+        # BN apply pass; x's two gradients (the shortcut's = the block output's gradient, and
+        # conv_1x1's input gradient) meet in conv_1x1's dgrad epilogue (ops.conv.GradJoin)
+        # instead of an autograd add
+        j = GradJoin() if F.native(x) else None
+        y = self.conv_1x1(x, join=j, join_role="consumer")
+        return self.conv_3x3(y, residual=x, residual_join=j)
 
 
 class Darknet53(tnn.Module):

@@ -76,7 +76,7 @@ class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, stats, weight, bias, running_mean, running_var, residual, training, momentum, eps, act,
                 slope, ws_fwd, ws_bwd, join=None, refbox=None, r_stats=None, r_weight=None, r_bias=None, r_rm=None,
-                r_rv=None, r_cfg=None, xjoin=None, defer_fwd=False, defer_bwd=False, prod_bias=None):
+                r_rv=None, r_cfg=None, xjoin=None, defer_fwd=False, defer_bwd=False, prod_bias=None, post_res=False):
         # xjoin (conv.GradJoin): another consumer of ``x`` stashes its gradient there (e.g. the
         # identity path of a pre-activation block); the backward apply pass adds it in place
         # r_*: a second, training-mode BatchNorm applied to ``residual`` inside the same pass
@@ -114,27 +114,30 @@ class _BNActFn(torch.autograd.Function):
         out = torch.empty_like(x)
         # activation mask in backward: recomputed from x (z = x*scale + shift) when there is no
         # residual; with a residual it is stored as bits by this pass (training, C % 8 == 0) or,
-        # failing that, read back from the saved output
-        bits = training and bool(act) and residual is not None and C % 8 == 0
+        # failing that, read back from the saved output. post_res: out = act(z) + residual (the
+        # residual after the activation): the mask is z's, from x, and d residual = d out
+        post = bool(post_res) and residual is not None and r_cfg is None
+        bits = training and bool(act) and residual is not None and C % 8 == 0 and not post
         mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=dev) if bits else None
         rsc, rsh = (rprm[0], rprm[1]) if rprm is not None else (None, None)
 
         def run_apply():
-            defer.launch_bn_apply(x, residual, out, C, scale, shift, act, slope, mask, rsc, rsh)
+            defer.launch_bn_apply(x, residual, out, C, scale, shift, act, slope, mask, rsc, rsh, post=post)
 
-        if (defer_fwd and defer.ENABLED and act in (0, 1, 2) and C % 64 == 0
+        if (defer_fwd and defer.ENABLED and not post and act in (0, 1, 2) and C % 64 == 0
                 and (residual is None or (is_nhwc(residual) and ld_of(residual) == C))):
             # the consumer 1x1 conv computes `out` while staging its A operand (ops.defer)
             out._dv_pending = defer.PendingApply.forward(out, x, residual, scale, shift, rsc, rsh, act, slope, mask,
                                                          run_apply)
         else:
             run_apply()
-        keep_out = bool(act) and residual is not None and not bits
+        keep_out = bool(act) and residual is not None and not bits and not post
         ctx.save_for_backward(x, mask if bits else (out if keep_out else None), weight, bias, prm,
                               residual if rprm is not None else None, rprm, r_weight, r_bias)
         ctx.r_ws_bwd = r_cfg[3] if r_cfg is not None else None
         ctx.bits = bits
-        ctx.cfg = (training, act, slope, residual is not None)
+        ctx.post = post
+        ctx.cfg = (training, act, slope, residual is not None and not post)
         ctx.ws_bwd = ws_bwd
         ctx.join = join
         ctx.xjoin = xjoin
@@ -142,7 +145,8 @@ class _BNActFn(torch.autograd.Function):
         ctx.has_prod_bias = prod_bias is not None
         ctx.prod_bias_param = prod_bias  # leaf parameter (not saved): its gradient may sink in place
         ctx.bnref = None
-        if refbox is not None and training and ws_bwd is not None and C % 8 == 0 and (not act or bits or residual is None):
+        if refbox is not None and training and ws_bwd is not None and C % 8 == 0 and (not act or bits or residual is None
+                                                                                       or post):
             mode = 3 if bits else (2 if act else 1)
             dual = (residual, rprm, r_cfg[3]) if (rprm is not None and DUAL_BWD) else (None, None, None)
             ctx.bnref = BNRef(x, mask if bits else None, prm, mode, act, slope, ws_bwd, *dual)
@@ -260,6 +264,8 @@ class _BNActFn(torch.autograd.Function):
         elif rprm is not None:
             dres, r_dgamma, r_dbeta = _residual_bn_backward(ctx, dout, out, r_x, rprm, r_weight, r_bias, act, slope,
                                                             fused2)
+        if ctx.post and ctx.needs_input_grad[6]:
+            dres = dout  # d(act(z) + r)/dr = 1: the incoming gradient itself, no pass
         if lazy:
             from .conv import MaskedGrad
 
@@ -275,7 +281,7 @@ class _BNActFn(torch.autograd.Function):
 
             pb_grad = _channel_sum(dx if dx.shape[1] == C else dx.contiguous(memory_format=torch.channels_last))
         return (dx, None, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None, None, None,
-                None, r_dgamma, r_dbeta, None, None, None, None, None, None, pb_grad)
+                None, r_dgamma, r_dbeta, None, None, None, None, None, None, pb_grad, None)
 
 
 def _residual_bn_coef(ctx, dout, bits, r_x, rprm, r_weight, r_bias, act, slope, fused):
@@ -485,7 +491,7 @@ def bn_momentum(bn) -> float:
 
 
 def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None, residual_join=None, residual_bn=None,
-                   input_join=None, defer_out=False, defer_bwd=False, prod_bias=None):
+                   input_join=None, defer_out=False, defer_bwd=False, prod_bias=None, residual_post=False):
     """act(BN(x) (+ residual)) with ``bn`` an nn.BatchNorm2d (parameters, buffers, mode).
     ``input_join`` (conv.GradJoin): x's gradient from another consumer, stashed there by its
     producer, is added inside this BN's backward apply pass.
@@ -508,6 +514,8 @@ def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None, residu
             residual = batch_norm_act(residual, rbn, None, 0.0, None, rstats)
             residual_bn = None
     if not native(x):
+        if residual_post and residual is not None:
+            return _torch_bn_act(x, bn, act, slope, None) + residual
         return _torch_bn_act(x, bn, act, slope, residual)
     training = bn.training or not bn.track_running_stats
     if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
@@ -536,7 +544,8 @@ def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None, residu
         rargs = (None,) * 6
     y = _BNActFn.apply(x, stats, bn.weight, bn.bias, rm, rv, residual, training, mom,
                        bn.eps, ACT_IDS[act], float(slope), ws_fwd, ws_bwd, residual_join, refbox, *rargs, input_join,
-                       bool(defer_out), bool(defer_bwd) and torch.is_grad_enabled(), prod_bias)
+                       bool(defer_out), bool(defer_bwd) and torch.is_grad_enabled(), prod_bias,
+                       bool(residual_post and residual_bn is None))
     if refbox:
         y._dv_bnref = refbox[0]  # read by the consumer conv (ops.conv._ConvFn)
     return y
@@ -561,7 +570,7 @@ def conv_bn_deferred(x, conv, bn, join=None, join_role=None):
 
 
 def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None, join=None, join_role=None, residual_join=None,
-                residual_bn=None, reflect_pad=None, shuffle=0, defer_out=False):
+                residual_bn=None, reflect_pad=None, shuffle=0, defer_out=False, residual_post=False):
     """Fused conv -> BN (batch stats from the conv epilogue) -> (+residual) -> activation.
 
     ``shuffle=g``: conv -> channel shuffle (g groups) -> BN -> act, the shuffle fused into the
@@ -586,6 +595,8 @@ def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None, join=None, join
             from .concat import channel_shuffle
 
             y = channel_shuffle(y, shuffle)
+        if residual_post and residual is not None:
+            return _torch_bn_act(y, bn, act, slope, None) + residual
         return _torch_bn_act(y, bn, act, slope, residual)
     # BN kernels need dense channels: a channel count that is not a multiple of 8 comes back as a
     # padded view, which is compacted below and gets its statistics from a separate pass
@@ -608,7 +619,7 @@ def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None, join=None, join
     bwd = (not shuffle and reflect_pad is None and y.requires_grad
            and defer.fusable_1x1(y.shape[1], ld_of(y), k[0], k[1], conv.stride, _pad2(pad), dl, conv.groups))
     return batch_norm_act(y, bn, act, slope, residual, stats, residual_join=residual_join, residual_bn=residual_bn,
-                          defer_out=defer_out, defer_bwd=bwd, prod_bias=prod_bias)
+                          defer_out=defer_out, defer_bwd=bwd, prod_bias=prod_bias, residual_post=residual_post)
 
 
 def _pad2(p):

@@ -381,11 +381,16 @@ def _wgrad(x, dy, weight, Cg_x, G, stride, padding, dilation, out=None, reflect=
         return buf
     # [G][Og][R][S][Cg] into the persistent zeroed workspace (split-K atomics, no memset), then
     # one pass to OIHW that re-zeroes the workspace as it reads it
+    # (split-K through ordered slabs: the slab reduce writes OIHW directly and the workspace is
+    # not touched -- csrc/conv_wgrad.hip slab_reduce_oirs_kernel)
     ws = _wgrad_workspace(G * Og * R * S * Cg_x, x.device)
-    lib().conv_wgrad(ptr(x), ptr(dy), ptr(ws), N, H, W, Cg_x, ld_of(x), G, Og, P, Q, ld_of(dy), R, S, sh, sw, ph, pw,
-                     dh, dw, 0, 1, 0, stream_handle(), reflect=int(reflect))
     dW = out if out is not None else torch.empty((O, Ig, R, S), dtype=F32, device=x.device)
-    lib().wgrad_unprep(ptr(ws), ptr(dW), G, Og, Ig, R, S, Cg_x, 1.0, int(out is not None), 1, stream_handle())
+    L = lib()
+    r = L.conv_wgrad(ptr(x), ptr(dy), ptr(ws), N, H, W, Cg_x, ld_of(x), G, Og, P, Q, ld_of(dy), R, S, sh, sw, ph, pw,
+                     dh, dw, 0, 1, 0, stream_handle(), reflect=int(reflect), out=ptr(dW), out_ig=Ig,
+                     out_accumulate=int(out is not None))
+    if not (r & L.WGRAD_FINAL):
+        L.wgrad_unprep(ptr(ws), ptr(dW), G, Og, Ig, R, S, Cg_x, 1.0, int(out is not None), 1, stream_handle())
     return dW
 
 

@@ -164,7 +164,7 @@ def flush():
         pend.materialize()
 
 
-def launch_bn_apply(x, residual, out, C, scale, shift, act, slope, mask, rscale=None, rshift=None):
+def launch_bn_apply(x, residual, out, C, scale, shift, act, slope, mask, rscale=None, rshift=None, post=False):
     lib().bn_apply(ptr(x), ptr(residual), ptr(out), x.numel(), C, ptr(scale), ptr(shift), act, float(slope), ptr(mask),
                    stream_handle(), rscale=ptr(rscale) if rscale is not None else 0,
-                   rshift=ptr(rshift) if rshift is not None else 0)
+                   rshift=ptr(rshift) if rshift is not None else 0, post=int(post))

@@ -786,3 +786,34 @@ def test_conv_bias_grad_via_bn(train):
         assert (conv.bias.grad - conv_r.bias.grad).abs().max().item() < 1e-2 * scale
     else:
         assert _rel(conv.bias.grad, conv_r.bias.grad) < 3e-2
+
+
+def test_darknet_residual_post_activation_add():
+    """Darknet residual block: x + leaky(bn(conv3x3(leaky(bn(conv1x1(x)))))) with the add inside
+    the BN apply pass (post-activation residual) and x's two gradients joined in conv_1x1's dgrad
+    epilogue, against the same block on the PyTorch path (fp32)."""
+    import copy
+
+    from deep_vision_amd.models.yolov3 import DarknetResidual
+    from deep_vision_amd.ops.common import set_backend
+
+    torch.manual_seed(0)
+    blk = DarknetResidual(32, 64).to(DEV)
+    ref = copy.deepcopy(blk)
+    x32 = torch.randn(4, 64, 20, 20, device=DEV).bfloat16().float()
+    x = _nhwc(x32).requires_grad_(True)
+    y = blk(x)
+    dy = torch.randn(4, 64, 20, 20, device=DEV).bfloat16().float()
+    y.backward(_nhwc(dy))
+    set_backend("torch")
+    try:
+        xr = x32.clone().requires_grad_(True)
+        yr = ref(xr)
+        yr.backward(dy)
+    finally:
+        set_backend("native")
+    assert _rel(y, yr) < 3e-2
+    # leaky-ReLU slope flips at z ~ 0 under bf16 rounding move single elements: compare globally
+    assert _cos(x.grad, xr.grad) > 0.999
+    for (n, p), (_, q) in zip(blk.named_parameters(), ref.named_parameters()):
+        assert _cos(p.grad, q.grad) > 0.998, n
