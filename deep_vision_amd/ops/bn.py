@@ -19,7 +19,7 @@ import torch
 import torch.nn.functional as TF
 
 from . import defer
-from .common import (ACT_IDS, BF16, F32, grad_nhwc, grad_sink, is_nhwc, ld_of, lib, native, ptr,
+from .common import (ACT_IDS, BF16, F32, fast_apply, grad_nhwc, grad_sink, is_nhwc, ld_of, lib, native, ptr,
                      stream_handle, workspace)
 
 STAT_SHARDS = 64
@@ -542,7 +542,7 @@ def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None, residu
                   workspace(rbn, "bn_bwd", (STAT_SHARDS, 2, C), x.device)))
     if not rargs:
         rargs = (None,) * 6
-    y = _BNActFn.apply(x, stats, bn.weight, bn.bias, rm, rv, residual, training, mom,
+    y = _BN_APPLY(x, stats, bn.weight, bn.bias, rm, rv, residual, training, mom,
                        bn.eps, ACT_IDS[act], float(slope), ws_fwd, ws_bwd, residual_join, refbox, *rargs, input_join,
                        bool(defer_out), bool(defer_bwd) and torch.is_grad_enabled(), prod_bias,
                        bool(residual_post and residual_bn is None))
@@ -627,3 +627,6 @@ def _pad2(p):
         return (p, p)
     p = tuple(p)
     return p if len(p) == 2 else ((p[0], p[2]) if p[0] == p[1] and p[2] == p[3] else (-1, -1))
+
+
+_BN_APPLY = fast_apply(_BNActFn)

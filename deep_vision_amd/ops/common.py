@@ -185,3 +185,21 @@ def workspace(owner, key, shape, device, dtype=F32):
         t = torch.zeros(shape, dtype=dtype, device=device)
         ws[k] = t
     return t
+
+
+def fast_apply(fn_cls):
+    """``fn_cls.apply`` without torch's per-call Python wrapper work: autograd.Function.apply runs
+    every argument through functorch's dead-wrapper unwrapping (a generator over the ~20-26
+    arguments of the conv / BatchNorm Functions, ~3 us per call on the launch-bound models) before
+    reaching the C++ apply. Under functorch transforms (never used by the framework) the full path
+    is taken."""
+    raw = super(torch.autograd.Function, fn_cls).apply
+    active = torch._C._are_functorch_transforms_active
+
+    def apply(*args):
+        if active():
+            return fn_cls.apply(*args)
+        return raw(*args)
+
+    return apply
+

@@ -15,7 +15,7 @@ import torch
 import torch.nn.functional as TF
 
 from . import defer, wcache
-from .common import (ACT_IDS, BF16, CL, F32, act_grad, alloc_cl, as_nhwc, empty_nhwc, grad_nhwc, grad_sink, is_nhwc,
+from .common import (ACT_IDS, BF16, CL, F32, act_grad, alloc_cl, as_nhwc, empty_nhwc, fast_apply, grad_nhwc, grad_sink, is_nhwc,
                      ld_of, lib,
                      like_layout, empty_layout, native, nhwc_numel, ptr, round8, stream_handle)
 
@@ -733,7 +733,7 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=
                                       stats_buf, join, join_role, pad_mode, out), residual)
     if res is None:
         residual_join = None
-    return _ConvFn.apply(xn, weight, bias, stride, padding, dilation, groups, ACT_IDS[act], float(slope), want_stats,
+    return _CONV_APPLY(xn, weight, bias, stride, padding, dilation, groups, ACT_IDS[act], float(slope), want_stats,
                          stats_buf, extra, join, join_role, reflect, [out] if out is not None else None, res,
                          residual_join, bool(bias_via_bn and bias is not None and not act))
 
@@ -1113,5 +1113,9 @@ def depthwise_conv2d(x, weight, bias=None, stride=1, padding=0, act=None, slope=
                      stats_buf=None, extra=(0, 0)):
     stride, padding = _pair(stride), _pair(padding)
     x = as_nhwc(x, pad_to8=False)
-    return _DWConvFn.apply(x, weight, bias, stride, padding, ACT_IDS[act], float(slope), want_stats, stats_buf,
+    return _DWCONV_APPLY(x, weight, bias, stride, padding, ACT_IDS[act], float(slope), want_stats, stats_buf,
                            extra)
+
+
+_CONV_APPLY = fast_apply(_ConvFn)
+_DWCONV_APPLY = fast_apply(_DWConvFn)
