@@ -382,7 +382,7 @@ def main():
                 f.write(json.dumps(rec) + "\n")
     if cwd is not None:
         cwd.stop()
-    if is_dist():
+    if dist.is_available() and dist.is_initialized():  # also the world-1 group of --force-dp
         dist.destroy_process_group()
 
 

@@ -13,6 +13,8 @@
 //     the plain single-pass form; afterwards the E[x^2] - mean^2 cancellation (large |mean| /
 //     std) is gone.
 // Backward uses the same shard layout for (sum dz, sum dz*xhat).
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -28,12 +30,21 @@ template <> struct VecIO<8> {
 #pragma unroll
     for (int i = 0; i < 4; ++i) { v[2 * i] = bf2f(w[i] & 0xffff); v[2 * i + 1] = bf2f(w[i] >> 16); }
   }
+  // streaming read of an apply pass's input (read once by this pass): non-temporal policy
+  DV_DEVICE static void load_nt(const u16* p, float* v) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 r = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { v[2 * i] = bf2f(w[i] & 0xffff); v[2 * i + 1] = bf2f(w[i] >> 16); }
+  }
   DV_DEVICE static void store(u16* p, const float* v) {
     uint4 r; r.x = pack2bf(v[0], v[1]); r.y = pack2bf(v[2], v[3]); r.z = pack2bf(v[4], v[5]); r.w = pack2bf(v[6], v[7]);
     *reinterpret_cast<uint4*>(p) = r;
   }
 };
 template <> struct VecIO<4> {
+  DV_DEVICE static void load_nt(const u16* p, float* v) { load(p, v); }
   DV_DEVICE static void load(const u16* p, float* v) {
     uint2 r = *reinterpret_cast<const uint2*>(p);
     v[0] = bf2f(r.x & 0xffff); v[1] = bf2f(r.x >> 16); v[2] = bf2f(r.y & 0xffff); v[3] = bf2f(r.y >> 16);
@@ -44,15 +55,31 @@ template <> struct VecIO<4> {
   }
 };
 template <> struct VecIO<2> {
+  DV_DEVICE static void load_nt(const u16* p, float* v) { load(p, v); }
   DV_DEVICE static void load(const u16* p, float* v) {
     uint32_t r = *reinterpret_cast<const uint32_t*>(p); v[0] = bf2f(r & 0xffff); v[1] = bf2f(r >> 16);
   }
   DV_DEVICE static void store(u16* p, const float* v) { *reinterpret_cast<uint32_t*>(p) = pack2bf(v[0], v[1]); }
 };
 template <> struct VecIO<1> {
+  DV_DEVICE static void load_nt(const u16* p, float* v) { load(p, v); }
   DV_DEVICE static void load(const u16* p, float* v) { v[0] = bf2f(*p); }
   DV_DEVICE static void store(u16* p, const float* v) { *p = f2bf(v[0]); }
 };
+
+// The apply passes stream tensors far larger than the 256 MB MALL at the big layers: their
+// once-read inputs go through the non-temporal policy there (512x28x28 / 1024x14x14 at batch 256:
+// 15-22 % faster, profiles/bn_apply_nt.txt) and through the default policy for tensors small
+// enough to still sit in the MALL from their producer (2048x7x7: 12 % slower with nt).
+const int64_t NT_LOAD_MIN_ELEMS = [] {
+  const char* v = std::getenv("DV_NT_MIN");  // benchmarking override (elements)
+  return v ? (int64_t)std::atoll(v) : (24ll << 20);
+}();
+template <bool NTL, int VEC>
+DV_DEVICE void ldv(const u16* p, float* v) {
+  if constexpr (NTL) VecIO<VEC>::load_nt(p, v);
+  else VecIO<VEC>::load(p, v);
+}
 
 DV_DEVICE float act_fwd(float z, int act, float slope) {
   if (act == 1) return fmaxf(z, 0.f);
@@ -228,7 +255,7 @@ struct RowTile {
 // ---- out = act(x*scale + shift (+res)) ----
 // POST: out = act(x*scale + shift) + res -- a residual added after the activation (Darknet's
 // x + leaky(bn(conv(.))), models/yolov3.py), replacing a separate add pass
-template <int VEC, bool MB, bool RBN = false, int UNR = 2, bool POST = false>
+template <int VEC, bool MB, bool RBN = false, int UNR = 2, bool POST = false, bool NTL = false>
 __global__ __launch_bounds__(NT) void bn_apply_kernel(const u16* __restrict__ x, const u16* __restrict__ res,
                                                         u16* __restrict__ out, int64_t rows, int C, int64_t rows_per_block,
                                                         const float* __restrict__ scale, const float* __restrict__ shift,
@@ -250,8 +277,8 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const u16* __restrict__ x,
     for (int64_t r = r0 + t.lane_r; r < r1; r += t.rpi) {
       const int64_t o = r * C + g * VEC;
       float v[VEC], rv[VEC];
-      VecIO<VEC>::load(x + o, v);
-      if (res) VecIO<VEC>::load(res + o, rv);
+      ldv<NTL, VEC>(x + o, v);
+      if (res) ldv<NTL, VEC>(res + o, rv);
       uint32_t bits = 0;
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
@@ -370,7 +397,7 @@ __global__ void bn_bwd_finalize_kernel(float* __restrict__ acc, int C, double co
 // same input (e.g. a pre-activation block's residual path, models/hourglass.py) summed in this pass
 // instead of a separate add; it may alias dx (each element is read before it is written by the
 // same thread), hence no __restrict__ on the two.
-template <int VEC, int MM, int UNR = 2>
+template <int VEC, int MM, int UNR = 2, bool NTL = false>
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const u16* __restrict__ dout, const u16* __restrict__ out,
                                                             const u16* __restrict__ x, u16* dx, u16* __restrict__ dres,
                                                             int64_t rows, int C, int64_t rows_per_block, const float* __restrict__ kA,
@@ -392,10 +419,10 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const u16* __restrict_
     for (int64_t r = r0 + t.lane_r; r < r1; r += t.rpi) {
       const int64_t o = r * C + g * VEC;
       float d[VEC], ov[VEC], xv[VEC], rr[VEC], av[VEC];
-      VecIO<VEC>::load(dout + o, d);
-      VecIO<VEC>::load(x + o, xv);
-      if constexpr (MM == MM_OUT) VecIO<VEC>::load(out + o, ov);
-      if (addend) VecIO<VEC>::load(addend + o, av);
+      ldv<NTL, VEC>(dout + o, d);
+      ldv<NTL, VEC>(x + o, xv);
+      if constexpr (MM == MM_OUT) ldv<NTL, VEC>(out + o, ov);
+      if (addend) ldv<NTL, VEC>(addend + o, av);
       uint32_t mb = 0;
       if constexpr (MM == MM_BITS) mb = reinterpret_cast<const uint8_t*>(out)[o >> 3];
 #pragma unroll
@@ -418,7 +445,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const u16* __restrict_
 // BN folded into the block's last pass, bn_apply_kernel RBN) share dz = act'(z) * dout: one pass
 // reads dout, the mask bits, x and x2 once and writes both input gradients (two separate apply
 // passes read dout and the bits twice). k / k2: [3][C] = kA, kB, kC of each BN.
-template <int UNR = 2>
+template <int UNR = 2, bool NTL = false>
 __global__ __launch_bounds__(NT) void bn_bwd_apply_dual_kernel(const u16* __restrict__ dout, const uint8_t* __restrict__ bits,
                                                                  const u16* __restrict__ x, const u16* __restrict__ x2,
                                                                  u16* __restrict__ dx, u16* __restrict__ dx2, int64_t rows, int C,
@@ -440,9 +467,9 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_dual_kernel(const u16* __rest
     for (int64_t r = r0 + t.lane_r; r < r1; r += t.rpi) {
       const int64_t o = r * C + g * VEC;
       float d[VEC], xv[VEC], xv2[VEC];
-      VecIO<VEC>::load(dout + o, d);
-      VecIO<VEC>::load(x + o, xv);
-      VecIO<VEC>::load(x2 + o, xv2);
+      ldv<NTL, VEC>(dout + o, d);
+      ldv<NTL, VEC>(x + o, xv);
+      ldv<NTL, VEC>(x2 + o, xv2);
       const uint32_t mb = bits[o >> 3];
 #pragma unroll
       for (int e = 0; e < VEC; ++e) {
@@ -564,8 +591,10 @@ void dv_bn_eval_prep(int C, float eps, const float* gamma, const float* beta, co
   bn_eval_prep_kernel<<<(C + 255) / 256, 256, 0, st>>>(C, eps, gamma, beta, rm, rv, scale, shift);
 }
 
-void dv_bn_apply(const void* x, const void* res, void* out, int64_t n, int C, const float* scale, const float* shift,
-                 int act, float slope, void* mask, const float* rscale, const float* rshift, hipStream_t st, int post) {
+template <bool NTL>
+static void bn_apply_dispatch(const void* x, const void* res, void* out, int64_t n, int C, const float* scale,
+                              const float* shift, int act, float slope, void* mask, const float* rscale,
+                              const float* rshift, hipStream_t st, int post) {
   const int v = vec_for(C);
   const int64_t rows = n / C;
   const int64_t rpb = apply_rows_per_block(rows, C, v);
@@ -573,34 +602,40 @@ void dv_bn_apply(const void* x, const void* res, void* out, int64_t n, int C, co
 #define AP_ARGS <<<g, NT, 0, st>>>((const u16*)x, (const u16*)res, (u16*)out, rows, C, rpb, scale, shift, act, slope, (uint8_t*)mask, rscale, rshift)
   if (post && res) {  // post-activation residual: the mask comes from x in backward (no bits)
     switch (v) {
-      case 8: bn_apply_kernel<8, false, false, 2, true> AP_ARGS; break;
-      case 4: bn_apply_kernel<4, false, false, 2, true> AP_ARGS; break;
-      case 2: bn_apply_kernel<2, false, false, 2, true> AP_ARGS; break;
-      default: bn_apply_kernel<1, false, false, 2, true> AP_ARGS; break;
+      case 8: bn_apply_kernel<8, false, false, 2, true, NTL> AP_ARGS; break;
+      case 4: bn_apply_kernel<4, false, false, 2, true, NTL> AP_ARGS; break;
+      case 2: bn_apply_kernel<2, false, false, 2, true, NTL> AP_ARGS; break;
+      default: bn_apply_kernel<1, false, false, 2, true, NTL> AP_ARGS; break;
     }
     return;
   }
   if (g_apply_unroll == 4 && mask && v == 8) {
-    if (res && rscale && rshift) bn_apply_kernel<8, true, true, 4> AP_ARGS;
-    else bn_apply_kernel<8, true, false, 4> AP_ARGS;
+    if (res && rscale && rshift) bn_apply_kernel<8, true, true, 4, false, NTL> AP_ARGS;
+    else bn_apply_kernel<8, true, false, 4, false, NTL> AP_ARGS;
     return;
   }
   if (res && rscale && rshift) {
-    if (mask && v == 8) bn_apply_kernel<8, true, true> AP_ARGS;
-    else if (v == 8) bn_apply_kernel<8, false, true> AP_ARGS;
-    else if (v == 4) bn_apply_kernel<4, false, true> AP_ARGS;
-    else if (v == 2) bn_apply_kernel<2, false, true> AP_ARGS;
-    else bn_apply_kernel<1, false, true> AP_ARGS;
+    if (mask && v == 8) bn_apply_kernel<8, true, true, 2, false, NTL> AP_ARGS;
+    else if (v == 8) bn_apply_kernel<8, false, true, 2, false, NTL> AP_ARGS;
+    else if (v == 4) bn_apply_kernel<4, false, true, 2, false, NTL> AP_ARGS;
+    else if (v == 2) bn_apply_kernel<2, false, true, 2, false, NTL> AP_ARGS;
+    else bn_apply_kernel<1, false, true, 2, false, NTL> AP_ARGS;
     return;
   }
-  if (mask && v == 8) { bn_apply_kernel<8, true> AP_ARGS; return; }
+  if (mask && v == 8) { bn_apply_kernel<8, true, false, 2, false, NTL> AP_ARGS; return; }
   switch (v) {
-    case 8: bn_apply_kernel<8, false> AP_ARGS; break;
-    case 4: bn_apply_kernel<4, false> AP_ARGS; break;
-    case 2: bn_apply_kernel<2, false> AP_ARGS; break;
-    default: bn_apply_kernel<1, false> AP_ARGS; break;
+    case 8: bn_apply_kernel<8, false, false, 2, false, NTL> AP_ARGS; break;
+    case 4: bn_apply_kernel<4, false, false, 2, false, NTL> AP_ARGS; break;
+    case 2: bn_apply_kernel<2, false, false, 2, false, NTL> AP_ARGS; break;
+    default: bn_apply_kernel<1, false, false, 2, false, NTL> AP_ARGS; break;
   }
 #undef AP_ARGS
+}
+
+void dv_bn_apply(const void* x, const void* res, void* out, int64_t n, int C, const float* scale, const float* shift,
+                 int act, float slope, void* mask, const float* rscale, const float* rshift, hipStream_t st, int post) {
+  if (n >= NT_LOAD_MIN_ELEMS) bn_apply_dispatch<true>(x, res, out, n, C, scale, shift, act, slope, mask, rscale, rshift, st, post);
+  else bn_apply_dispatch<false>(x, res, out, n, C, scale, shift, act, slope, mask, rscale, rshift, st, post);
 }
 
 template <int MM>
@@ -645,42 +680,53 @@ void dv_bn_bwd_finalize(float* acc, int C, double count, const float* gamma, con
                                                           kA, kB, kC, xsum);
 }
 
-template <int MM>
+template <int MM, bool NTL>
 static void bwd_apply_launch(int g, const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t rows,
                              int C, int64_t rpb, const float* kA, const float* kB, const float* kC, const float* mscale,
                              const float* mshift, int act, float slope, const void* addend, hipStream_t st) {
 #define BA_ARGS <<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, (u16*)dx, (u16*)dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, (const u16*)addend)
   switch (vec_for(C)) {
-    case 8: bn_bwd_apply_kernel<8, MM> BA_ARGS; break;
-    case 4: bn_bwd_apply_kernel<4, MM> BA_ARGS; break;
-    case 2: bn_bwd_apply_kernel<2, MM> BA_ARGS; break;
-    default: bn_bwd_apply_kernel<1, MM> BA_ARGS; break;
+    case 8: bn_bwd_apply_kernel<8, MM, 2, NTL> BA_ARGS; break;
+    case 4: bn_bwd_apply_kernel<4, MM, 2, NTL> BA_ARGS; break;
+    case 2: bn_bwd_apply_kernel<2, MM, 2, NTL> BA_ARGS; break;
+    default: bn_bwd_apply_kernel<1, MM, 2, NTL> BA_ARGS; break;
   }
 #undef BA_ARGS
 }
 
-void dv_bn_bwd_apply(const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t n, int C,
-                     const float* kA, const float* kB, const float* kC, const float* mscale, const float* mshift, int act,
-                     float slope, int mask_bits, const void* addend, hipStream_t st) {
+template <bool NTL>
+static void bwd_apply_dispatch(const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t n, int C,
+                               const float* kA, const float* kB, const float* kC, const float* mscale,
+                               const float* mshift, int act, float slope, int mask_bits, const void* addend,
+                               hipStream_t st) {
   const int v = vec_for(C);
   const int64_t rows = n / C;
   const int64_t rpb = apply_rows_per_block(rows, C, v);
   const int g = (int)((rows + rpb - 1) / rpb);
   if (act && mask_bits && v == 8 && g_apply_unroll == 4) {
-    bn_bwd_apply_kernel<8, MM_BITS, 4><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, (u16*)dx,
+    bn_bwd_apply_kernel<8, MM_BITS, 4, NTL><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, (u16*)dx,
                                                            (u16*)dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope,
                                                            (const u16*)addend);
     return;
   }
   if (act && mask_bits && v == 8) {
-    bn_bwd_apply_kernel<8, MM_BITS><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, (u16*)dx,
+    bn_bwd_apply_kernel<8, MM_BITS, 2, NTL><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, (u16*)dx,
                                                         (u16*)dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope,
                                                         (const u16*)addend);
     return;
   }
-  if (!act) bwd_apply_launch<MM_NONE>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, addend, st);
-  else if (out) bwd_apply_launch<MM_OUT>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, addend, st);
-  else bwd_apply_launch<MM_X>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, addend, st);
+  if (!act) bwd_apply_launch<MM_NONE, NTL>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, addend, st);
+  else if (out) bwd_apply_launch<MM_OUT, NTL>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, addend, st);
+  else bwd_apply_launch<MM_X, NTL>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, addend, st);
+}
+
+void dv_bn_bwd_apply(const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t n, int C,
+                     const float* kA, const float* kB, const float* kC, const float* mscale, const float* mshift, int act,
+                     float slope, int mask_bits, const void* addend, hipStream_t st) {
+  if (n >= NT_LOAD_MIN_ELEMS)
+    bwd_apply_dispatch<true>(dout, out, x, dx, dres, n, C, kA, kB, kC, mscale, mshift, act, slope, mask_bits, addend, st);
+  else
+    bwd_apply_dispatch<false>(dout, out, x, dx, dres, n, C, kA, kB, kC, mscale, mshift, act, slope, mask_bits, addend, st);
 }
 
 void dv_bn_bwd_apply_dual(const void* dout, const void* bits, const void* x, const void* x2, void* dx, void* dx2,
@@ -688,8 +734,12 @@ void dv_bn_bwd_apply_dual(const void* dout, const void* bits, const void* x, con
   const int64_t rows = n / C;
   const int64_t rpb = apply_rows_per_block(rows, C, 8);
   const int g = (int)((rows + rpb - 1) / rpb);
-  bn_bwd_apply_dual_kernel<><<<g, NT, 0, st>>>((const u16*)dout, (const uint8_t*)bits, (const u16*)x, (const u16*)x2,
-                                               (u16*)dx, (u16*)dx2, rows, C, rpb, k, k2, act, slope);
+  if (n >= NT_LOAD_MIN_ELEMS)
+    bn_bwd_apply_dual_kernel<2, true><<<g, NT, 0, st>>>((const u16*)dout, (const uint8_t*)bits, (const u16*)x,
+                                                         (const u16*)x2, (u16*)dx, (u16*)dx2, rows, C, rpb, k, k2, act, slope);
+  else
+    bn_bwd_apply_dual_kernel<2, false><<<g, NT, 0, st>>>((const u16*)dout, (const uint8_t*)bits, (const u16*)x,
+                                                          (const u16*)x2, (u16*)dx, (u16*)dx2, rows, C, rpb, k, k2, act, slope);
 }
 
 void dv_bn_bwd_eval(const void* dout, const void* out, void* dx, void* dres, int64_t n, int C, const float* scale,
