@@ -1,5 +1,7 @@
 // Implicit-GEMM convolution FORWARD on gfx950 MFMA: dispatch, the warp-specialised ring variant,
 // the split-K finalize pass and the host entry point. The kernel itself is in conv_fwd_core.h.
+#include <cstdlib>
+
 #include "conv_fwd_core.h"
 
 int dv_g_last_ksplit = 1;
@@ -395,6 +397,11 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
   p.bnx2 = (const u16*)a.bnx2; p.bnprm2 = a.bnprm2; p.bnacc2 = a.bnacc2;
   p.resbits = (const uint8_t*)a.resbits; p.resact = a.resact; p.resslope = a.resslope;
   p.reflect = a.reflect;
+  static const int64_t nt_min = [] {
+    const char* v = std::getenv("DV_EPI_NT_MIN");  // benchmarking override (elements of the output)
+    return v ? (int64_t)std::atoll(v) : (24ll << 20);
+  }();
+  p.ntl = (int64_t)a.P * a.Q * a.Nb * a.G * a.Kout >= nt_min;
   p.wld = a.w_ld ? a.w_ld : p.K;
   p.wkr = a.w_kr ? a.w_kr : a.S * a.Cg;
   p.wks = a.w_ks ? a.w_ks : a.Cg;

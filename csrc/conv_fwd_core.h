@@ -62,6 +62,7 @@ struct FwdParams {
   const float* bnprm2;
   float* bnacc2;
   int wld, wkr, wks;  // weight row / tap strides (kernels.h ConvFwdArgs w_ld, w_kr, w_ks)
+  int ntl;            // epilogue reads of once-used tensors (residual, BN input) with the non-temporal policy
   // A-operand transform (template AT; kernels.h ConvFwdArgs at_*)
   const u16* at_x;
   const u16* at_r;
@@ -125,6 +126,16 @@ DV_DEVICE float masked_res(float g, uint32_t mb, int e, int act, float slope) {
   return ((mb >> e) & 1u) ? g : (act == 2 ? g * slope : 0.f);
 }
 
+// 16-B load of a tensor the epilogue reads once; `nt`: non-temporal policy (tensors far beyond the
+// MALL, csrc/bn.hip NT_LOAD_MIN_ELEMS)
+DV_DEVICE uint4 ld16_once(const u16* ptr, int nt) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  if (nt) {
+    const u32x4 r = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(ptr));
+    return uint4{r.x, r.y, r.z, r.w};
+  }
+  return *reinterpret_cast<const uint4*>(ptr);
+}
 DV_DEVICE void glds16(const void* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(GLB_PTR(src), LDS_PTR(lds_wave_base), 16, 0, 0);
 }
@@ -609,13 +620,13 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
         pf_off[it] = off;
         const bool ld = off >= 0 && vec;
         if constexpr (RES) {
-          pf_res[it] = ld ? *reinterpret_cast<const uint4*>(p.res + off) : uint4{0u, 0u, 0u, 0u};
+          pf_res[it] = ld ? ld16_once(p.res + off, p.ntl) : uint4{0u, 0u, 0u, 0u};
           pf_rmb[it] = (off >= 0 && p.resbits) ? (uint32_t)p.resbits[off >> 3] : 0xffu;
         }
         if constexpr (BNR) {
-          pf_x[it] = ld ? *reinterpret_cast<const uint4*>(p.bnx + off) : uint4{0u, 0u, 0u, 0u};
+          pf_x[it] = ld ? ld16_once(p.bnx + off, p.ntl) : uint4{0u, 0u, 0u, 0u};
           pf_mb[it] = (ld && p.bnmode == 3) ? (uint32_t)p.bnbits[off >> 3] : 0u;
-          if constexpr (dual) pf_x2[it] = ld ? *reinterpret_cast<const uint4*>(p.bnx2 + off) : uint4{0u, 0u, 0u, 0u};
+          if constexpr (dual) pf_x2[it] = ld ? ld16_once(p.bnx2 + off, p.ntl) : uint4{0u, 0u, 0u, 0u};
         }
       }
     }
