@@ -428,6 +428,9 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
     fin_res = p.res; fin_stats = p.stats;  // applied by the finalize pass, not the split blocks
     p.res = nullptr; p.stats = nullptr;
   }
+  // statistics of a residual output (y = conv + bias + residual) are accumulated from the 16-B
+  // vector stores of a single-group tensor (conv_fwd_core.h RST)
+  if (p.res && p.stats && ((p.N & 7) || (p.ldy & 7) || p.G != 1)) return -1;
   if (p.reflect && (a.tgather || p.ph >= p.Hin || p.pw >= p.Win || p.ph < 0 || p.pw < 0 || p.bnmode)) return -1;
   // the mask bits are indexed by the dense element offset of y: a single-group tensor whose
   // pixel stride is its channel count, written by the identity-mapped (stride-1) epilogue

@@ -557,6 +557,21 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
       bmu2[e] = f32x2{ok0 ? p.bnprm[2 * p.N + nb + 2 * e] : 0.f, ok1 ? p.bnprm[2 * p.N + nb + 2 * e + 1] : 0.f};
     }
   }
+  // RES with statistics: the BatchNorm statistics are of the STORED output y = conv (+ bias) +
+  // residual (a pre-activation block's output feeding the next block's BN; the split-K finalize
+  // computes the same), accumulated per lane over its 8 fixed channels in the store loop (vector
+  // stores only: the host rejects the combination otherwise)
+  constexpr bool RST = RES && EPI != EPI_PLAIN;
+  f32x2 rs1[RST ? 4 : 1], rs2[RST ? 4 : 1], rkq[RST ? 4 : 1];
+  if constexpr (RST) {
+    const int nb = nw0 + (lane & 7) * 8;
+    const float* kp = p.stats ? stat_shift(p.stats, (int64_t)p.G * p.N) + grp * p.N : nullptr;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      rs1[e] = f32x2{0.f, 0.f}; rs2[e] = f32x2{0.f, 0.f};
+      rkq[e] = f32x2{(kp && nb + 2 * e < p.N) ? kp[nb + 2 * e] : 0.f, (kp && nb + 2 * e + 1 < p.N) ? kp[nb + 2 * e + 1] : 0.f};
+    }
+  }
   u16* st = reinterpret_cast<u16*>(smem + wid * EPI_WAVE_BYTES);
 #pragma unroll
   for (int h = 0; h < HM; ++h) {
@@ -571,7 +586,7 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
         kq[r] = 0.f;
         if constexpr (EPI == EPI_FULL) bv[r] = (p.bias && n < p.N) ? p.bias[grp * p.N + n] : 0.f;
         // shifted statistics: sums of (t - K), K = this BN's previous batch mean (stat_shift)
-        if constexpr (EPI != EPI_PLAIN) kq[r] = (p.stats && n < p.N) ? stat_shift(p.stats, (int64_t)p.G * p.N)[grp * p.N + n] : 0.f;
+        if constexpr (EPI != EPI_PLAIN && !RES) kq[r] = (p.stats && n < p.N) ? stat_shift(p.stats, (int64_t)p.G * p.N)[grp * p.N + n] : 0.f;
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -587,7 +602,7 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
             else if (p.act == ACT_LEAKY) t = t > 0.f ? t : t * p.slope;
           }
           v[r] = t;
-          if constexpr (EPI != EPI_PLAIN) {
+          if constexpr (EPI != EPI_PLAIN && !RES) {
             if (mv) { const float d = t - kq[r]; bsum[j][r] += d; bsq[j][r] = fmaf(d, d, bsq[j][r]); }
           }
         }
@@ -679,6 +694,14 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
           }
           const uint4 o = uint4{ov[0], ov[1], ov[2], ov[3]};
           *reinterpret_cast<uint4*>(dst) = o;
+          if constexpr (RST) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {  // of the stored bf16 values, as a separate stats pass would read them
+              const f32x2 d = bf2x(ov[e]) - rkq[e];
+              rs1[e] += d;
+              rs2[e] = __builtin_elementwise_fma(d, d, rs2[e]);
+            }
+          }
           if constexpr (BNR) {
             if constexpr (dual) bn_bwd_accum<true>(p, o, pf_x[it], pf_mb[it], bs2, bq2, bmu2, bms2, bmh2, &pf_x2[it], dq2, dmu2);
             else bn_bwd_accum(p, o, pf_x[it], pf_mb[it], bs2, bq2, bmu2, bms2, bmh2);
@@ -702,7 +725,49 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
       }
     }
   }
-  if (EPI != EPI_PLAIN && p.stats) {
+  if constexpr (RST) {
+    if (p.stats) {
+      // lanes sharing (lane & 7) hold the same 8 channels: butterfly over lane bits 3-5, then the
+      // WM waves of one channel column meet in LDS; one coalesced atomic row per block
+      float s1[8], s2[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { s1[2 * e] = rs1[e].x; s1[2 * e + 1] = rs1[e].y; s2[2 * e] = rs2[e].x; s2[2 * e + 1] = rs2[e].y; }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+#pragma unroll
+        for (int off = 8; off < 64; off <<= 1) {
+          s1[e] += __shfl_xor(s1[e], off, 64);
+          s2[e] += __shfl_xor(s2[e], off, 64);
+        }
+      }
+      float* sh = reinterpret_cast<float*>(smem + EPI_BYTES);  // [waves][64 channels][2]
+      if (lane < 8) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          sh[(wid * 64 + lane * 8 + e) * 2 + 0] = s1[e];
+          sh[(wid * 64 + lane * 8 + e) * 2 + 1] = s2[e];
+        }
+      }
+      __syncthreads();
+      if (threadIdx.x < BN_) {
+        const int nl = threadIdx.x, n = n0 + nl;
+        if (n < p.N) {
+          float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+          for (int wm = 0; wm < WM; ++wm) {
+            const int w = wm * WN + nl / 64;
+            t1 += sh[(w * 64 + (nl & 63)) * 2];
+            t2 += sh[(w * 64 + (nl & 63)) * 2 + 1];
+          }
+          const int64_t ncols = (int64_t)p.G * p.N;
+          float* a = p.stats + (int64_t)(tm % DV_STAT_SHARDS) * 2 * ncols;
+          atomicAdd(a + grp * p.N + n, t1);
+          atomicAdd(a + ncols + grp * p.N + n, t2);
+        }
+      }
+    }
+  }
+  if (!RES && EPI != EPI_PLAIN && p.stats) {
     float* sh = reinterpret_cast<float*>(smem + EPI_BYTES);  // [WM][BN_][2]
 #pragma unroll
     for (int j = 0; j < 4; ++j)

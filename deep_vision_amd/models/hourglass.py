@@ -38,6 +38,8 @@ import torch.nn as tnn
 
 from .. import nn
 from .. import ops as F
+from ..ops.bn import STAT_ROWS, STAT_SHARDS
+from ..ops.common import workspace
 from ..ops.conv import GradJoin
 
 
@@ -45,6 +47,7 @@ import os
 
 BRANCH_STREAMS = {"1": True, "0": False}.get(os.environ.get("DV_BRANCH_STREAMS", "graph"), "graph")
 _STREAMS = {}
+HANDOFF_STATS = True  # a block's conv3 epilogue accumulates the next block's pre-activation BN statistics
 
 
 def _fork(x):
@@ -101,16 +104,59 @@ class BottleneckBlock(tnn.Module):
         self.bn3 = _bn(filters // 2)
         self.conv3 = nn.Conv2d(filters // 2, filters, 1)
 
-    def forward(self, x):
+    def forward(self, x, next_bn=None):
         # identity blocks: x's two gradients (the residual path's dy and BN1's dx) meet in BN1's
         # backward apply pass (GradJoin) instead of an autograd add -- 73 add passes per step
         j = GradJoin() if self.downsample is None and F.native(x) else None
         identity = self.downsample(x) if self.downsample is not None else x
-        y = F.batch_norm_act(x, self.bn1, "relu", input_join=j)
+        y = F.batch_norm_act(x, self.bn1, "relu", input_join=j, stats=_take_block_stats(self.bn1, x))
         y = F.conv_bn_act(y, self.conv1, self.bn2, "relu")
         y = F.conv_bn_act(y, self.conv2, self.bn3, "relu")
-        # the residual add rides in conv3's store epilogue (ops.conv2d residual=)
+        # the residual add rides in conv3's store epilogue (ops.conv2d residual=); when the next
+        # block's pre-activation BN is known, the same epilogue accumulates that BN's batch
+        # statistics of the block output (no separate statistics pass over it)
+        if HANDOFF_STATS and next_bn is not None and next_bn.training and F.native(y):
+            sbuf = workspace(next_bn, "bn_fwd", (STAT_ROWS, self.conv3.out_channels), y.device)
+            out, st = F.conv2d(y, self.conv3.weight, self.conv3.bias, residual=identity, residual_join=j,
+                               want_stats=True, stats_buf=sbuf)
+            if st is not None:
+                next_bn.__dict__["_dv_block_stats"] = (out.data_ptr(), out._version, tuple(out.shape), st)
+            return out
         return F.conv2d(y, self.conv3.weight, self.conv3.bias, residual=identity, residual_join=j)
+
+
+def _take_block_stats(bn, x):
+    """The statistics a producing block's conv3 epilogue accumulated for ``bn`` -- if they are of
+    exactly ``x``; otherwise their shards are cleared (the workspace must be clean for the
+    statistics pass the BN then runs itself)."""
+    pre = bn.__dict__.pop("_dv_block_stats", None)
+    if pre is None:
+        return None
+    if pre[:3] == (x.data_ptr(), x._version, tuple(x.shape)):
+        return pre[3]
+    pre[3][: 2 * STAT_SHARDS].zero_()
+    return None
+
+
+def _entry_bn(m):
+    """The pre-activation BN that first reads the input of ``m`` (a block, a block sequence or
+    an hourglass level, whose input feeds its up1 branch), or None."""
+    if isinstance(m, BottleneckBlock):
+        return m.bn1
+    if isinstance(m, tnn.Sequential) and len(m) and isinstance(m[0], BottleneckBlock):
+        return m[0].bn1
+    if isinstance(m, HourglassModule):
+        return _entry_bn(m.up1)
+    return None
+
+
+def _run_blocks(blocks, x, next_bn=None):
+    """A block sequence, each block handing the next one's BN statistics over (see
+    BottleneckBlock.forward); the last block hands over to ``next_bn``."""
+    n = len(blocks)
+    for i, b in enumerate(blocks):
+        x = b(x, next_bn=blocks[i + 1].bn1 if i + 1 < n else next_bn)
+    return x
 
 
 class HourglassModule(tnn.Module):
@@ -125,21 +171,25 @@ class HourglassModule(tnn.Module):
             self.low2 = tnn.Sequential(*[BottleneckBlock(filters, filters) for _ in range(num_residual)])
         self.low3 = tnn.Sequential(*[BottleneckBlock(filters, filters) for _ in range(num_residual)])
 
+    def _low(self, x):
+        low = _run_blocks(self.low1, F.max_pool2d(x, 2, 2), next_bn=_entry_bn(self.low2))
+        low = self.low2(low) if isinstance(self.low2, HourglassModule) else _run_blocks(self.low2, low)
+        return _run_blocks(self.low3, low)
+
     def forward(self, x):
         if _fork(x):
             main = torch.cuda.current_stream(x.device)
             side = _side_stream(x.device, self.order)
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                up1 = _BranchEdge.apply(self.up1(_BranchEdge.apply(x, main)), main)
-            low = self.low3(self.low2(self.low1(F.max_pool2d(x, 2, 2))))
+                up1 = _BranchEdge.apply(_run_blocks(self.up1, _BranchEdge.apply(x, main)), main)
+            low = self._low(x)
             main.wait_stream(side)
             x.record_stream(side)  # caching allocator: x is read on the side stream
             up1.record_stream(main)
             return F.upsample_add(low, up1, 2)
-        up1 = self.up1(x)
-        low = self.low3(self.low2(self.low1(F.max_pool2d(x, 2, 2))))
-        return F.upsample_add(low, up1, 2)
+        up1 = _run_blocks(self.up1, x)
+        return F.upsample_add(self._low(x), up1, 2)
 
 
 class StackedHourglassNetwork(tnn.Module):
@@ -162,12 +212,12 @@ class StackedHourglassNetwork(tnn.Module):
 
     def forward(self, x):
         x = F.conv_bn_act(x, self.stem, self.stem_bn, "relu")
-        x = self.pre(x)
+        x = _run_blocks(self.pre, x)
         x = F.max_pool2d(x, 2, 2)
-        x = self.pre2(x)
+        x = _run_blocks(self.pre2, x, next_bn=_entry_bn(self.hourglass[0]))
         ys = []
         for i in range(self.num_stack):
-            x = self.residual[i](self.hourglass[i](x))
+            x = _run_blocks(self.residual[i], self.hourglass[i](x))
             lin = self.linear[i]
             x = F.conv_bn_act(x, lin["conv"], lin["bn"], "relu")
             y = self.heatmap[i](x)

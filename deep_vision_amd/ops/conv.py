@@ -658,12 +658,15 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=
                    join_role, pad_mode, out, residual, residual_join)
         y = channel_shuffle(y, shuffle)
         return (y, None) if want_stats else y
-    if residual is not None and (act or want_stats or out is not None or not native(x)):
-        y = conv2d(x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats, stats_buf, join,
+    # want_stats with a residual: statistics of the final y = conv + bias + residual (the conv
+    # epilogue accumulates them from its stores; a pre-activation block output feeding a BN)
+    res_stats_ok = (want_stats and native(x) and not act and out is None and groups == 1 and pad_mode == "zeros"
+                    and weight.shape[0] % 8 == 0)
+    if residual is not None and (act or (want_stats and not res_stats_ok) or out is not None or not native(x)):
+        y = conv2d(x, weight, bias, stride, padding, dilation, groups, act, slope, False, None, join,
                    join_role, pad_mode, out)
-        if want_stats:
-            raise NotImplementedError("conv2d residual= with want_stats")
-        return y + residual if not native(x) else _add_native(y, residual)
+        y = y + residual if not native(x) else _add_native(y, residual)
+        return (y, None) if want_stats else y
     if isinstance(padding, str):
         raise NotImplementedError("string padding: use nn.Conv2d(padding='same_keras')")
     stride, dilation = _pair(stride), _pair(dilation)
@@ -722,15 +725,15 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=
         join = None
     res = None
     if residual is not None:
-        if dw or padded_groups or geo is not None:
-            return _add_native(conv2d(x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats,
-                                      stats_buf, join, join_role, pad_mode, out), residual)
-        res = as_nhwc(residual, pad_to8=True)
-        if ld_of(res) != round8(weight.shape[0]) or res.data_ptr() % 16:
-            res = res.contiguous(memory_format=torch.channels_last) if round8(weight.shape[0]) == weight.shape[0] else None
-        if res is None:
-            return _add_native(conv2d(x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats,
-                                      stats_buf, join, join_role, pad_mode, out), residual)
+        if not (dw or padded_groups or geo is not None):
+            res = as_nhwc(residual, pad_to8=True)
+            if ld_of(res) != round8(weight.shape[0]) or res.data_ptr() % 16:
+                res = (res.contiguous(memory_format=torch.channels_last) if round8(weight.shape[0]) == weight.shape[0]
+                       else None)
+        if res is None:  # the add as its own pass (no statistics from it)
+            y = _add_native(conv2d(x, weight, bias, stride, padding, dilation, groups, act, slope, False, None, join,
+                                   join_role, pad_mode, out), residual)
+            return (y, None) if want_stats else y
     if res is None:
         residual_join = None
     return _CONV_APPLY(xn, weight, bias, stride, padding, dilation, groups, ACT_IDS[act], float(slope), want_stats,

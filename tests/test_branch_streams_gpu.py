@@ -117,3 +117,35 @@ def test_branch_streams_captured_step_matches_eager():
     for k, v in enumerate(lc, start=1):
         spread = abs(e1[k] - e2[k])
         assert abs(v - e1[k]) <= 3 * spread + 5e-3 * abs(e1[k]), (k, e1, e2, lc)
+
+
+def test_block_statistics_handoff_matches_separate_pass():
+    """BottleneckBlock conv3 epilogues accumulating the next block's pre-activation BN statistics
+    (post-residual, csrc/conv_fwd_core.h RST) give the forward / backward of the separate
+    statistics pass: two chained blocks (shallow enough that rounding differences stay
+    rounding-sized), batch statistics, running statistics and gradients compared."""
+    from deep_vision_amd.models import hourglass as H
+
+    torch.manual_seed(0)
+    blocks = torch.nn.Sequential(H.BottleneckBlock(128, 128), H.BottleneckBlock(128, 128)).to(DEV)
+    x32 = torch.randn(8, 128, 24, 24, device=DEV) * 2 + 0.5
+    res = {}
+    try:
+        for on in (False, True):
+            H.HANDOFF_STATS = on
+            m = copy.deepcopy(blocks)
+            x = x32.to(torch.bfloat16).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+            y = H._run_blocks(m, x)
+            g = torch.randn(y.shape, device=DEV, generator=torch.Generator(device=DEV).manual_seed(1))
+            y.backward(g.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+            torch.cuda.synchronize()
+            res[on] = (y.detach().float(), x.grad.float(), _grads(m), m[1].bn1.running_mean.clone(),
+                       m[1].bn1.running_var.clone())
+    finally:
+        H.HANDOFF_STATS = True
+    (y0, dx0, g0, rm0, rv0), (y1, dx1, g1, rm1, rv1) = res[False], res[True]
+    assert torch.allclose(rm0, rm1, rtol=1e-3, atol=1e-4) and torch.allclose(rv0, rv1, rtol=1e-3, atol=1e-4)
+    assert ((y0 - y1).norm() / y0.norm()).item() < 1e-2
+    cos = lambda a, b: torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()
+    assert cos(dx0, dx1) > 0.999 and cos(g0, g1) > 0.999
+    assert not any("_dv_block_stats" in b.__dict__ for b in blocks.modules())

@@ -1,4 +1,4 @@
 #!/bin/bash
 mkdir -p gpurun_out
-timeout -k 10 400 python -u tools/dw_bench.py --variants 0,1,2,3,4,5 > gpurun_out/dw_var.log 2>&1 || exit $?
-grep -v amdgpu gpurun_out/dw_var.log | grep -E "H  14|H   7|H  28" | head -80
+timeout -k 10 300 python -u -m pytest -q -s --timeout 200 --timeout-method thread tests/test_branch_streams_gpu.py > gpurun_out/t_b.log 2>&1
+rc=$?; tail -2 gpurun_out/t_b.log; grep -E "^FAILED|^E  " gpurun_out/t_b.log | head -20; exit $rc
