@@ -489,9 +489,10 @@ def _count_batch(bn):
         _flush_batch_count(bn)
         bn.num_batches_tracked.add_(1)
         return
-    if "_dv_nbt_hook" not in bn.__dict__:
-        bn._dv_nbt_hook = bn.register_state_dict_pre_hook(lambda m, *a, **k: _flush_batch_count(m))
-    bn._dv_nbt_pending = bn.__dict__.get("_dv_nbt_pending", 0) + 1
+    d = bn.__dict__  # plain instance attributes: no nn.Module.__setattr__ on the per-call path
+    if "_dv_nbt_hook" not in d:
+        d["_dv_nbt_hook"] = bn.register_state_dict_pre_hook(lambda m, *a, **k: _flush_batch_count(m))
+    d["_dv_nbt_pending"] = d.get("_dv_nbt_pending", 0) + 1
 
 
 def bn_momentum(bn) -> float:

@@ -52,9 +52,11 @@ def round8(c: int) -> int:
 
 def ld_of(x: torch.Tensor) -> int:
     """Pixel (channel) stride of a channels_last 4-D tensor / row stride of a 2-D tensor."""
-    if x.dim() == 4:
-        return x.stride(3) if x.size(3) > 1 else (x.stride(2) if x.size(2) > 1 else x.stride(0) // max(1, x.size(2) * x.size(3)))
-    return x.stride(0)
+    st = x.stride()
+    if len(st) == 4:
+        sz = x.shape
+        return st[3] if sz[3] > 1 else (st[2] if sz[2] > 1 else st[0] // max(1, sz[2] * sz[3]))
+    return st[0]
 
 
 def is_nhwc(x: torch.Tensor) -> bool:
@@ -62,12 +64,13 @@ def is_nhwc(x: torch.Tensor) -> bool:
     if x.dtype != BF16 or x.dim() != 4:
         return False
     N, C, H, W = x.shape
-    if C > 1 and x.stride(1) != 1:
+    s0, s1, s2, s3 = x.stride()
+    if C > 1 and s1 != 1:
         return False
-    ld = ld_of(x)
+    ld = s3 if W > 1 else (s2 if H > 1 else s0 // max(1, H * W))  # ld_of
     if ld < C or ld % 8 != 0 and ld != C:
         return False
-    return (W == 1 or x.stride(3) == ld) and (H == 1 or x.stride(2) == W * ld) and (N == 1 or x.stride(0) == H * W * ld)
+    return (W == 1 or s3 == ld) and (H == 1 or s2 == W * ld) and (N == 1 or s0 == H * W * ld)
 
 
 def empty_nhwc(N: int, C: int, H: int, W: int, device, zero: bool = False) -> torch.Tensor:
@@ -178,8 +181,12 @@ def grad_sink(param):
 
 def workspace(owner, key, shape, device, dtype=F32):
     """Persistent zero-initialised buffer owned by a module (self-cleaning accumulators)."""
-    ws = owner.__dict__.setdefault("_dv_ws", {})
-    k = (key, tuple(shape), str(device), dtype)
+    ws = owner.__dict__.get("_dv_ws")
+    if ws is None:
+        ws = owner.__dict__["_dv_ws"] = {}
+    if type(device) is not torch.device:
+        device = torch.device(device)
+    k = (key, shape if type(shape) is tuple else tuple(shape), device, dtype)
     t = ws.get(k)
     if t is None:
         t = torch.zeros(shape, dtype=dtype, device=device)

@@ -55,8 +55,10 @@ def test_fused_finalize_matches_separate_pass(case):
                 n0 = B.COUNTERS["fwd_finalize_fused"]
                 outs[v] = F.conv_bn_act(x, cm, bm, "relu")
                 torch.cuda.synchronize()
+                live = {t.data_ptr() for t in bm.__dict__.get("_dv_ws", {}).values()}
                 assert (B.COUNTERS["fwd_finalize_fused"] - n0) == (1 if v == "fused" and fused else 0), (v, case)
-                ws = workspace(bm, "bn_fwd", (B.STAT_ROWS, O), DEV)
+                ws = workspace(bm, "bn_fwd", (B.STAT_ROWS, O), x.device)
+                assert ws.data_ptr() in live, "not the BN's statistics workspace"
                 assert not ws[: 2 * B.STAT_SHARDS].any(), "shards not re-zeroed"
                 assert not ws[2 * B.STAT_SHARDS + 1].any(), "tickets not reset"
             a, b = outs["sep"].float(), outs["fused"].float()
@@ -65,8 +67,10 @@ def test_fused_finalize_matches_separate_pass(case):
             sb, fb = mods["sep"][1], mods["fused"][1]
             torch.testing.assert_close(fb.running_mean, sb.running_mean, rtol=1e-5, atol=1e-6)
             torch.testing.assert_close(fb.running_var, sb.running_var, rtol=1e-5, atol=1e-6)
-            ks = workspace(sb, "bn_fwd", (B.STAT_ROWS, O), DEV)[2 * B.STAT_SHARDS]
-            kf = workspace(fb, "bn_fwd", (B.STAT_ROWS, O), DEV)[2 * B.STAT_SHARDS]
+            ks = workspace(sb, "bn_fwd", (B.STAT_ROWS, O), x.device)[2 * B.STAT_SHARDS]
+            kf = workspace(fb, "bn_fwd", (B.STAT_ROWS, O), x.device)[2 * B.STAT_SHARDS]
+            if step:
+                assert ks.abs().sum() > 0  # the shift row holds the previous batch's mean
             torch.testing.assert_close(kf, ks, rtol=1e-5, atol=1e-6)  # the next batch's shift
     finally:
         B.FUSE_FINALIZE = saved

@@ -49,7 +49,9 @@ def test_depthwise_epilogue_and_stats(C, s, bias, act):
     # statistics of the fp32 outputs (before bf16 rounding), summed over the shards; a fresh
     # buffer's shift row (csrc/kernels.h DV_STAT_ROWS) is zero, so these are the plain sums
     yq = y.float()
-    assert stats.shape[0] == 129 and not stats[128].any()
+    from deep_vision_amd.ops.bn import STAT_ROWS
+
+    assert stats.shape[0] == STAT_ROWS and not stats[128:].any()  # shift row and ticket row
     tot = stats[:128].reshape(64, 2, -1).sum(0)
     assert _rel(tot[0, :C], yq.sum((0, 2, 3))) < 5e-3
     assert _rel(tot[1, :C], (yq * yq).sum((0, 2, 3))) < 5e-3
