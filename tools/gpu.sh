@@ -7,6 +7,12 @@
 #                                (PMC_ARGS=--wgrad for the weight-gradient kernels; PAT filters kernel names)
 #   tools/gpu.sh models          bench every BASELINE.json GPU config (native and torch/MIOpen reference)
 #   tools/gpu.sh tests [-k EXPR] GPU tests only
+#   tools/gpu.sh records         eager + graph bench records of the BASELINE GPU configs
+#   tools/gpu.sh evidence        kernel tables of the four BASELINE models + conv-vs-MIOpen table
+#   tools/gpu.sh host            Python host profiles of the eager launch-bound models
+#   tools/gpu.sh convergence     ResNet-50 1,000-step native vs torch-bf16 curves, 2 seeds
+#   tools/gpu.sh overlap         DP bucket overlap test + force-DP kernel timeline
+#   AB=VAR tools/gpu.sh ab       bench + kernel-trace A/B of an env toggle (DV_DEFER, DV_FUSE_FINALIZE)
 # Every GPU step has its own time limit and the steps are chained with &&: after a fault,
 # abort or timeout nothing else runs on the GPU in that call.
 set -o pipefail
@@ -82,6 +88,68 @@ case "$mode" in
     timeout -k 10 600 python tools/lc_sweep.py --models ${MODELS:-resnet50} --grid ${GRID:-0.05:1.0,0.02:1.0} \
       --out gpurun_out/lc_sweep.txt > gpurun_out/lc_sweep.log 2>&1
     rc=$?; cat gpurun_out/lc_sweep.log | cut -c1-200 ;;
+  records)
+    # native bench records (eager + graph) of the BASELINE GPU configs -> gpurun_out/rec/*.log
+    mkdir -p gpurun_out/rec; rc=0
+    timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/rec/resnet50_eager.log 2>&1 && \
+    timeout -k 10 300 python bench.py --steps 20 --warmup 5 --graph > gpurun_out/rec/resnet50_graph.log 2>&1 || rc=$?
+    for m in mobilenet1 hourglass yolov3; do
+      [ $rc -ne 0 ] && break
+      s=20; [ $m != mobilenet1 ] && s=10
+      timeout -k 10 300 python bench.py --model $m --steps $s --warmup 3 > gpurun_out/rec/${m}_eager.log 2>&1 && \
+      timeout -k 10 300 python bench.py --model $m --steps $s --warmup 3 --graph > gpurun_out/rec/${m}_graph.log 2>&1 || rc=$?
+    done
+    for f in gpurun_out/rec/*.log; do echo "$f $(grep '^{' $f | tail -1 | cut -c1-150)"; done ;;
+  evidence)
+    # steady-state kernel tables (ResNet-50 eager, MobileNet / Hourglass / YOLOv3 graph) and the
+    # per-layer conv-vs-MIOpen table
+    bash tools/gpu.sh prof resnet50 > gpurun_out/j_prof_rn.log 2>&1 && \
+    GRAPH=1 bash tools/gpu.sh prof mobilenet1 > gpurun_out/j_prof_mb.log 2>&1 && \
+    GRAPH=1 bash tools/gpu.sh prof hourglass > gpurun_out/j_prof_hg.log 2>&1 && \
+    GRAPH=1 bash tools/gpu.sh prof yolov3 > gpurun_out/j_prof_yl.log 2>&1 && \
+    timeout -k 10 600 python -u tools/conv_vs_miopen.py --iters 10 --out gpurun_out/conv_vs_miopen.txt > gpurun_out/conv_vs_miopen.log 2>&1
+    rc=$?; for f in gpurun_out/step_*.txt; do head -3 $f; done ;;
+  host)
+    # host-side (Python) profiles of the eager launch-bound models
+    timeout -k 10 300 python tools/host_profile.py --model hourglass --steps 5 --top 45 > gpurun_out/host_hourglass.txt 2>&1 && \
+    timeout -k 10 300 python tools/host_profile.py --model yolov3 --steps 5 --top 45 > gpurun_out/host_yolov3.txt 2>&1
+    rc=$?; head -14 gpurun_out/host_hourglass.txt | cut -c1-150 ;;
+  convergence)
+    # ResNet-50 1,000 steps x 2 seeds, native vs torch autocast-bf16 (tools/convergence.py)
+    timeout -k 10 1100 python -u tools/convergence.py --steps 1000 --seeds 0 1 --every 100 \
+      --out gpurun_out/convergence_resnet50.json > gpurun_out/convergence.log 2>&1
+    rc=$?; grep -v amdgpu.ids gpurun_out/convergence.log | tail -50 ;;
+  overlap)
+    # bucket all-reduce overlap evidence (world-1 RCCL, DataParallel forced on): the issue-order GPU
+    # test, then a kernel trace of the force-DP ResNet-50 step summarised by tools/comm_timeline.py
+    timeout -k 10 400 $PYT -s tests/test_ddp_gpu.py -k overlap > gpurun_out/overlap_test.log 2>&1 && \
+    cd /tmp && export TMPDIR=/tmp && \
+    timeout -k 10 400 rocprofv3 --kernel-trace -d "$R/gpurun_out/prof_dp" -o run --output-format csv -- \
+      python3 "$R/bench.py" --force-dp --bucket-mb 8 --steps 3 --warmup 2 > "$R/gpurun_out/prof_dp.log" 2>&1
+    rc=$?; cd "$R"
+    t=$(find gpurun_out/prof_dp -name '*kernel_trace.csv' -print -quit 2>/dev/null)
+    [ -n "$t" ] && python tools/comm_timeline.py "$t" > gpurun_out/comm_timeline.txt 2>&1; rm -f "$t"
+    grep -E "PASS|FAIL|backward .* ms" gpurun_out/overlap_test.log | head; head -40 gpurun_out/comm_timeline.txt 2>/dev/null ;;
+  ab)
+    # A/B of an environment toggle on the ResNet-50 bench + kernel traces of both arms:
+    #   AB="DV_DEFER" (BN apply deferred into the consumer conv, tests/test_defer_gpu.py first)
+    #   AB="DV_FUSE_FINALIZE" (BN finalize in the producer conv, tests/test_bn_finalize_fused_gpu.py first)
+    v=${AB:-DV_FUSE_FINALIZE}; t=tests/test_bn_finalize_fused_gpu.py; [ "$v" = DV_DEFER ] && t=tests/test_defer_gpu.py
+    timeout -k 10 600 $PYT $t > gpurun_out/ab_tests.log 2>&1 && \
+    env $v=0 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/ab_off.log 2>&1 && \
+    env $v=1 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/ab_on.log 2>&1 && \
+    cd /tmp && export TMPDIR=/tmp && \
+    env $v=0 timeout -k 10 300 rocprofv3 --kernel-trace -d "$R/gpurun_out/ab_prof_off" -o run --output-format csv -- \
+      python3 "$R/bench.py" --steps 6 --warmup 2 > "$R/gpurun_out/ab_prof_off.log" 2>&1 && \
+    env $v=1 timeout -k 10 300 rocprofv3 --kernel-trace -d "$R/gpurun_out/ab_prof_on" -o run --output-format csv -- \
+      python3 "$R/bench.py" --steps 6 --warmup 2 > "$R/gpurun_out/ab_prof_on.log" 2>&1
+    rc=$?; cd "$R"
+    for a in off on; do
+      t=$(find gpurun_out/ab_prof_$a -name '*kernel_trace.csv' -print -quit 2>/dev/null)
+      [ -n "$t" ] && python tools/step_table.py "$t" --steps 4 --title "resnet50 $v=$a" > gpurun_out/ab_step_$a.txt 2>&1
+      rm -f "$t"
+      echo "$v=$a: $(grep '^{' gpurun_out/ab_$a.log | tail -1 | cut -c1-120)"; sed -n 3,12p gpurun_out/ab_step_$a.txt 2>/dev/null
+    done ;;
   *) echo "unknown mode $mode"; exit 2 ;;
 esac
 echo "rc=$rc"
