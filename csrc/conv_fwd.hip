@@ -452,21 +452,6 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
     if (!ok) { p.bnmode = 0; bn_status = 1; }
   }
   if (!p.bnmode) p.bnx2 = nullptr;
-  // fused BatchNorm finalize: one pass of the main kernel writes every element's statistics (no
-  // split-K slabs, no residual / post-residual statistics, no dgrad scatter, no warp-specialised
-  // ring variant)
-  p.fin_prm = nullptr;
-  if (a.fin_prm && p.stats && !p.ypart && !p.res && p.identity_map && a.tgather != 1 && !p.zfill && !p.bnmode &&
-      !(dv_g_fwd_variant >= 20 && dv_g_fwd_variant <= 23) && (a.fin_rm == nullptr) == (a.fin_rv == nullptr)) {
-    p.fin_prm = a.fin_prm; p.fin_gamma = a.fin_gamma; p.fin_beta = a.fin_beta;
-    p.fin_rm = a.fin_rm; p.fin_rv = a.fin_rv; p.fin_eps = a.fin_eps; p.fin_mom = a.fin_mom;
-    static const int fin_loads = [] {
-      const char* v = std::getenv("DV_FIN_LOADS");
-      return v ? std::atoi(v) : 0;
-    }();
-    p.fin_loads = fin_loads;
-    bn_status |= DV_FWD_FINALIZED;
-  }
   p.div_pq = make_fastdiv((uint32_t)(a.P * a.Q));
   p.div_q = make_fastdiv((uint32_t)a.Q);
   if (a.tgather == 2) {

@@ -71,14 +71,6 @@ struct FwdParams {
   u16* at_side;
   const float* at_c[5];
   int at_act; float at_slope;
-  // fused BatchNorm finalize of `stats` (kernels.h ConvFwdArgs fin_*; fin_tail below)
-  float* fin_prm;
-  const float* fin_gamma;
-  const float* fin_beta;
-  float* fin_rm;
-  float* fin_rv;
-  float fin_eps, fin_mom;
-  int fin_loads;
 };
 
 }  // namespace dvconv
@@ -210,92 +202,6 @@ template <int N>
 DV_DEVICE void wait_vm() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   __builtin_amdgcn_s_waitcnt((N & 0xF) | (0x7 << 4) | (0xF << 8) | ((N >> 4) << 14));
-}
-
-// Fused BatchNorm finalize (kernels.h ConvFwdArgs fin_*). Every block of an output-column tile
-// takes a ticket once its statistics atomics have been performed (vmcnt drained); the block that
-// draws the last ticket folds the 64 shards of the tile's channels -- in fixed shard order, so the
-// result does not depend on which block came last -- re-zeroes them and writes what
-// csrc/bn.hip bn_finalize_kernel would: scale / shift / mean / invstd, the next shift K and the
-// running statistics. The shards are read with atomic exchanges: performed where the other
-// blocks' atomics were, no cache can hand back a stale copy, and the read re-zeroes in one
-// operation (fin_loads, env DV_FIN_LOADS=1: agent-scope atomic loads + stores instead, the sc1
-// vector forms).
-// Saves one dependent launch per conv -> BatchNorm (53 per ResNet-50 forward).
-template <int NT, int BN_>
-DV_DEVICE void fin_tail(const FwdParams& p, int grp, int tn, int n0, int tiles_m, int tiles_n, char* lds) {
-  static_assert(NT % BN_ == 0 && DV_STAT_SHARDS % (NT / BN_) == 0, "shard split");
-  constexpr int PARTS = NT / BN_, PER = DV_STAT_SHARDS / PARTS;
-  const int64_t ncols = (int64_t)p.G * p.N;
-  float* krow = stat_shift(p.stats, ncols);
-  int* ticket = reinterpret_cast<int*>(krow + ncols) + grp * tiles_n + tn;
-  int* flag = reinterpret_cast<int*>(lds);
-  if (threadIdx.x < BN_) wait_vm<0>();  // the statistics atomics of this wave have been performed
-  __syncthreads();
-  if (threadIdx.x == 0) flag[0] = atomicAdd(ticket, 1) == tiles_m - 1;
-  __syncthreads();
-  if (!flag[0]) return;
-  const int cl = threadIdx.x % BN_, part = threadIdx.x / BN_;
-  const int n = n0 + cl;
-  const bool ok = n < p.N;
-  const int64_t c = (int64_t)grp * p.N + n;
-  float k = 0.f, g = 1.f, b = 0.f, rm0 = 0.f, rv0 = 0.f;
-  if (ok && part == 0) {  // per-channel operands fetched alongside the shard reads
-    k = krow[c];
-    if (p.fin_gamma) g = p.fin_gamma[c];
-    if (p.fin_beta) b = p.fin_beta[c];
-    if (p.fin_rm) { rm0 = p.fin_rm[c]; rv0 = p.fin_rv[c]; }
-  }
-  double s = 0.0, q = 0.0;
-  if (ok) {
-    float va[PER], vb[PER];
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      float* sp = p.stats + (int64_t)(part * PER + i) * 2 * ncols + c;
-      if (p.fin_loads) {
-        va[i] = __hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        vb[i] = __hip_atomic_load(sp + ncols, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        va[i] = atomicExch(sp, 0.f);
-        vb[i] = atomicExch(sp + ncols, 0.f);
-      }
-    }
-    if (p.fin_loads) {
-#pragma unroll
-      for (int i = 0; i < PER; ++i) {
-        float* sp = p.stats + (int64_t)(part * PER + i) * 2 * ncols + c;
-        __hip_atomic_store(sp, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(sp + ncols, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < PER; ++i) { s += va[i]; q += vb[i]; }
-  }
-  double* red = reinterpret_cast<double*>(lds + 16);  // [2][PARTS][BN_]
-  red[part * BN_ + cl] = s;
-  red[(PARTS + part) * BN_ + cl] = q;
-  __syncthreads();
-  if (threadIdx.x == 0) atomicExch(ticket, 0);  // every ticket of the tile has been drawn
-  if (part != 0 || !ok) return;
-  s = 0.0; q = 0.0;
-#pragma unroll
-  for (int j = 0; j < PARTS; ++j) { s += red[j * BN_ + cl]; q += red[(PARTS + j) * BN_ + cl]; }
-  const double count = (double)p.M;
-  const double dm = s / count;
-  const double mean = (double)k + dm;
-  double var = q / count - dm * dm;
-  if (var < 0) var = 0;
-  krow[c] = isfinite(mean) ? (float)mean : 0.f;  // see bn_finalize_kernel: a non-finite batch resets K
-  const float invstd = (float)(1.0 / sqrt(var + (double)p.fin_eps));
-  p.fin_prm[c] = g * invstd;
-  p.fin_prm[ncols + c] = b - (float)mean * g * invstd;
-  p.fin_prm[2 * ncols + c] = (float)mean;
-  p.fin_prm[3 * ncols + c] = invstd;
-  if (p.fin_rm && isfinite(mean) && isfinite(var)) {
-    const double unb = count > 1 ? var * count / (count - 1) : var;
-    p.fin_rm[c] = (1.f - p.fin_mom) * rm0 + p.fin_mom * (float)mean;
-    p.fin_rv[c] = (1.f - p.fin_mom) * rv0 + p.fin_mom * (float)unb;
-  }
 }
 
 // EPI (compile-time epilogue): EPI_PLAIN = store only (dgrad, ConvTranspose), EPI_STATS = + BN
@@ -888,7 +794,6 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
         atomicAdd(a + ncols + grp * p.N + n, s2);
       }
     }
-    if (p.fin_prm) fin_tail<64 * NW, BN_>(p, grp, tn, n0, tiles_m, tiles_n, smem);
   }
   if constexpr (BNR) {
     // lanes sharing (lane & 7) hold partials of the same 8 channels: butterfly over lane bits 3-5,

@@ -8,10 +8,8 @@
 // Forward BatchNorm statistics accumulator of C channels: [DV_STAT_SHARDS][2][C] shard partial
 // sums of (x - K) and (x - K)^2, then one row [C] holding the per-channel shift K (the previous
 // batch mean of that BN; csrc/bn.hip bn_finalize_kernel). Shifting keeps the single-pass
-// variance free of E[x^2] - mean^2 cancellation when |mean| >> std. A last row of C ints holds
-// the per-column-tile tickets of a producer conv that finalizes the statistics itself
-// (ConvFwdArgs fin_*; zero between launches).
-#define DV_STAT_ROWS (2 * DV_STAT_SHARDS + 2)
+// variance free of E[x^2] - mean^2 cancellation when |mean| >> std.
+#define DV_STAT_ROWS (2 * DV_STAT_SHARDS + 1)
 static_assert(DV_STAT_SHARDS == 64, "common.h stat_shift() hard-codes the shard count");
 
 struct ConvFwdArgs {
@@ -81,19 +79,7 @@ struct ConvFwdArgs {
   void* at_bits_out = nullptr;      // at 1: mask bits of z (1 bit per element) or nullptr
   void* at_side = nullptr;          // materialised a (dense, ld = ldx) or nullptr
   const float* at_c[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // per-channel [K] coefficients
-  // optional fused BatchNorm finalize of `stats` (training-mode BN fed by this conv): the last
-  // block of every output-column tile folds the shards of its channels and writes what
-  // bn_finalize_kernel would ([4][C] scale, shift, mean, invstd; the next shift row; running
-  // statistics). Needs the ticket row of the statistics buffer (DV_STAT_ROWS). dv_conv_fwd
-  // returns with DV_FWD_FINALIZED set when it ran (single-pass launches of the main kernel).
-  float* fin_prm = nullptr;
-  const float* fin_gamma = nullptr;
-  const float* fin_beta = nullptr;
-  float* fin_rm = nullptr;
-  float* fin_rv = nullptr;
-  float fin_eps = 1e-5f, fin_mom = 0.1f;
 };
-constexpr int DV_FWD_FINALIZED = 2;
 
 struct ConvWgradArgs {
   const void* x;   // bf16 NHWC forward input (im2col source)

@@ -15,29 +15,20 @@ models (eps 1e-3, momentum 0.99 -> PyTorch momentum 0.01; Hourglass 0.9 -> 0.1).
 """
 from __future__ import annotations
 
-import os
-
 import torch
 import torch.nn.functional as TF
 
 from . import defer
-from .common import (ACT_IDS, BF16, F32, BNFinalize, fast_apply, grad_nhwc, grad_sink, is_nhwc, ld_of, lib, native,
-                     ptr, stream_handle, workspace)
+from .common import (ACT_IDS, BF16, F32, fast_apply, grad_nhwc, grad_sink, is_nhwc, ld_of, lib, native, ptr,
+                     stream_handle, workspace)
 
 STAT_SHARDS = 64
-STAT_ROWS = 2 * STAT_SHARDS + 2  # forward statistics: shard sums, shift row, ticket row (csrc/kernels.h)
+STAT_ROWS = 2 * STAT_SHARDS + 1  # forward statistics: shard sums + the shift row (csrc/kernels.h)
 FUSE_BWD_STATS = True  # fold the backward reduction into the consumer conv's dgrad epilogue
 LAZY_SHORTCUT = True   # identity-shortcut gradient masked inside the consumer's dgrad epilogue
 FOLD_RESIDUAL_BN = True  # projection-shortcut BN applied inside the block's last BN pass
 DUAL_BWD = True  # ...and its backward: reduction in the consumer dgrad's epilogue, one dual apply pass
-# the producer conv's last block per channel tile finalizes the statistics (csrc/conv_fwd_core.h
-# fin_tail). Off by default: measured slower (ResNet-50 12,835 -> 12,605 img/s on one box; conv
-# kernels +0.48 ms/step against -0.23 ms of finalize launches, profiles/bn_finalize_fused_experiment.txt):
-# the fold sits on the kernel's critical path exactly where the separate launch did, and every
-# block waits for its own atomics before taking a ticket. DV_FUSE_FINALIZE=1 enables it.
-FUSE_FINALIZE = os.environ.get("DV_FUSE_FINALIZE", "0") == "1"
-COUNTERS = {"bwd_reduce_fused": 0, "bwd_reduce_pass": 0, "shortcut_lazy": 0, "dual_apply": 0, "dual_fused": 0,
-            "fwd_finalize_fused": 0}
+COUNTERS = {"bwd_reduce_fused": 0, "bwd_reduce_pass": 0, "shortcut_lazy": 0, "dual_apply": 0, "dual_fused": 0}
 
 
 class BNRef:
@@ -97,20 +88,18 @@ class _BNActFn(torch.autograd.Function):
         dev = x.device
         st = stream_handle()
         L = lib()
-        fin = stats if isinstance(stats, BNFinalize) else None
-        # scale, shift, mean, invstd (already written by the producer conv when it finalized)
-        prm = fin.prm if fin is not None else torch.empty((4, C), dtype=F32, device=dev)
+        prm = torch.empty((4, C), dtype=F32, device=dev)  # scale, shift, mean, invstd
         scale, shift, mean, invstd = prm[0], prm[1], prm[2], prm[3]
         rows = N * H * W
         g = weight.detach() if weight is not None else None
         b = bias.detach() if bias is not None else None
-        if training and fin is None:
+        if training:
             if stats is None:
                 stats = ws_fwd
                 L.bn_stats(ptr(x), rows, C, ptr(stats), st)
             L.bn_finalize(ptr(stats), C, float(rows), float(eps), float(momentum), ptr(g), ptr(b), ptr(running_mean),
                           ptr(running_var), ptr(mean), ptr(invstd), ptr(scale), ptr(shift), st)
-        elif not training:
+        else:
             L.bn_eval_prep(C, float(eps), ptr(g), ptr(b), ptr(running_mean), ptr(running_var), ptr(scale), ptr(shift), st)
             if weight is not None and weight.requires_grad:  # dgamma needs xhat of the running stats
                 mean.copy_(running_mean)
@@ -619,18 +608,9 @@ def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None, join=None, join
     if reflect_pad is not None:  # ReflectionPad2d in front of a pad-0 conv: fused into the gather
         pad, mode = reflect_pad, "reflect"
     bvb = conv.bias is not None and bn.training and not shuffle  # bias gradient from the BN (bn_bwd_finalize xsum)
-    fin = None
-    if (want and FUSE_FINALIZE and bn.training and bn.track_running_stats and bn.momentum is not None
-            and not shuffle):
-        fin = BNFinalize(sbuf, torch.empty((4, conv.out_channels), dtype=F32, device=x.device), bn.weight, bn.bias,
-                         bn.running_mean, bn.running_var, bn.eps, bn.momentum)
     r = conv2d(x, conv.weight, conv.bias, conv.stride, pad, conv.dilation, conv.groups, want_stats=want,
-               stats_buf=sbuf, join=join, join_role=join_role, pad_mode=mode, shuffle=shuffle, bias_via_bn=bvb,
-               bn_fin=fin)
+               stats_buf=sbuf, join=join, join_role=join_role, pad_mode=mode, shuffle=shuffle, bias_via_bn=bvb)
     y, stats = r if want else (r, None)
-    if fin is not None and fin.done:
-        COUNTERS["fwd_finalize_fused"] += 1
-        stats = fin  # mean / invstd / scale / shift and the running statistics are already written
     prod_bias = conv.bias if (bvb and getattr(y, "_dv_bias_via_bn", False)) else None
     if y.shape[1] % 8 != 0:  # padded view: BN kernels require dense channels
         y = y.contiguous(memory_format=torch.channels_last)

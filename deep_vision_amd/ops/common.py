@@ -194,28 +194,6 @@ def workspace(owner, key, shape, device, dtype=F32):
     return t
 
 
-class BNFinalize:
-    """Request that a conv producing a training-mode BatchNorm's statistics also finalizes them
-    (csrc/conv_fwd_core.h fin_tail): ``buf`` the BN's statistics workspace, ``prm`` the [4][C]
-    scale / shift / mean / invstd it fills, plus the BN's affine parameters, running buffers,
-    eps and momentum. ``done`` is set when the conv launch did it; ops.bn then skips its finalize."""
-
-    __slots__ = ("buf", "prm", "gamma", "beta", "rm", "rv", "eps", "momentum", "done")
-
-    def __init__(self, buf, prm, gamma, beta, rm, rv, eps, momentum):
-        self.buf, self.prm, self.gamma, self.beta, self.rm, self.rv = buf, prm, gamma, beta, rm, rv
-        self.eps, self.momentum = float(eps), float(momentum)
-        self.done = False
-
-    def kernel_args(self):
-        return dict(fin_prm=self.prm.data_ptr(), fin_gamma=ptr_or0(self.gamma), fin_beta=ptr_or0(self.beta),
-                    fin_rm=ptr_or0(self.rm), fin_rv=ptr_or0(self.rv), fin_eps=self.eps, fin_mom=self.momentum)
-
-
-def ptr_or0(t):
-    return t.detach().data_ptr() if t is not None else 0
-
-
 def fast_apply(fn_cls):
     """``fn_cls.apply`` without torch's per-call Python wrapper work: autograd.Function.apply runs
     every argument through functorch's dead-wrapper unwrapping (a generator over the ~20-26

@@ -15,12 +15,12 @@ import torch
 import torch.nn.functional as TF
 
 from . import defer, wcache
-from .common import (ACT_IDS, BF16, BNFinalize, CL, F32, act_grad, alloc_cl, as_nhwc, empty_nhwc, fast_apply,
-                     grad_nhwc, grad_sink, is_nhwc, ld_of, lib,
+from .common import (ACT_IDS, BF16, CL, F32, act_grad, alloc_cl, as_nhwc, empty_nhwc, fast_apply, grad_nhwc, grad_sink, is_nhwc,
+                     ld_of, lib,
                      like_layout, empty_layout, native, nhwc_numel, ptr, round8, stream_handle)
 
 STAT_SHARDS = 64
-STAT_ROWS = 2 * STAT_SHARDS + 2  # forward statistics: shard sums, shift row, ticket row (csrc/kernels.h)
+STAT_ROWS = 2 * STAT_SHARDS + 1  # forward statistics: shard sums + the shift row (csrc/kernels.h)
 
 
 def _pair(v):
@@ -129,14 +129,12 @@ def conv_ksplit(M, O, K, G=1):
 
 def conv_fwd_raw(x, wk, y, bias, stats, N, H, W, Cg, ldx, G, Kout, P, Q, R, S, stride, padding, dilation,
                  act=0, slope=0.0, tgather=0, omap=None, ldy=None, res=None, bnref=None, resmask=None, reflect=False,
-                 ksplit=1, zfill=0, at=None, wlayout=None, fin=None):
+                 ksplit=1, zfill=0, at=None, wlayout=None):
     """Launch the implicit-GEMM kernel. ``bnref`` (ops.bn.BNRef): also reduce that BatchNorm's
     backward statistics over ``y`` in the epilogue; returns True when that was done.
     ``resmask`` (bits, act, slope): ``res`` is a raw gradient masked by act'() before the add.
     ``at`` (ops.defer.PendingApply): the A operand is that deferred BN apply, computed while
-    staging and materialised by the kernel as a side output (csrc/conv_fwd.hip AT_*).
-    ``fin`` (ops.common.BNFinalize): finalize the statistics in the same launch when the kernel
-    path allows it (sets ``fin.done``)."""
+    staging and materialised by the kernel as a side output (csrc/conv_fwd.hip AT_*)."""
     sh, sw = stride
     ph, pw = padding
     dh, dw = dilation
@@ -162,16 +160,12 @@ def conv_fwd_raw(x, wk, y, bias, stats, N, H, W, Cg, ldx, G, Kout, P, Q, R, S, s
         bn.update(at.kernel_args())
     if wlayout is not None:  # (row stride, tap-row stride, tap stride) of a tap subset read in place
         bn.update(w_ld=int(wlayout[0]), w_kr=int(wlayout[1]), w_ks=int(wlayout[2]))
-    if fin is not None and stats is not None and ksplit == 1 and res is None:
-        bn.update(fin.kernel_args())
     r = lib().conv_fwd(ptr(x), ptr(wk), ptr(y), ptr(bias), ptr(stats), N, H, W, Cg, ldx, G, Kout, P, Q, R, S, sh, sw,
                        ph, pw, dh, dw, tgather, OH, OW, osh, osw, oph, opw, ldy if ldy is not None else ld_of(y), act,
                        float(slope), ptr(res), stream_handle(), **bn)
     if at is not None:
         at.fused()
-    if fin is not None:
-        fin.done = bool(r & lib().FWD_FINALIZED) and "fin_prm" in bn
-    return bnref is not None and (r & 1) == 0
+    return bnref is not None and r == 0
 
 
 def _gather_channels(t: torch.Tensor, per_group: int, G: int) -> int:
@@ -440,16 +434,13 @@ class _ConvFn(torch.autograd.Function):
         else:
             y = empty_nhwc(N, O, P, Q, x.device)
         stats = None
-        fin = None
-        if isinstance(stats_buf, BNFinalize):  # the consumer BN's finalize rides on this launch
-            fin, stats_buf = stats_buf, stats_buf.buf
         if want_stats:
             stats = stats_buf if stats_buf is not None else torch.zeros((STAT_ROWS, O), dtype=F32, device=x.device)
         b = bias.detach().float().contiguous() if bias is not None else None
         # residual: y = conv + b + residual in the store epilogue (same NHWC layout as y)
         ks = 1 if reflect else conv_ksplit(N * P * Q, Og, R * S * Cg_x, G)
         conv_fwd_raw(x, wk, y, b, stats, N, H, W, Cg_x, ldx, G, Og, P, Q, R, S, stride, padding, dilation,
-                     act=act, slope=slope, reflect=reflect, res=residual, ksplit=ks, at=at, fin=fin)
+                     act=act, slope=slope, reflect=reflect, res=residual, ksplit=ks, at=at)
         ctx.has_residual = residual is not None
         ctx.rjoin = residual_join  # the residual's gradient (= dy) is stashed there for its other consumer
         ctx.save_for_backward(x, weight, y if act else None)
@@ -639,11 +630,8 @@ class _StemConvFn(torch.autograd.Function):
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=None, slope=0.0,
            want_stats=False, stats_buf=None, join=None, join_role=None, pad_mode="zeros", out=None, residual=None,
-           residual_join=None, shuffle=0, bias_via_bn=False, bn_fin=None):
+           residual_join=None, shuffle=0, bias_via_bn=False):
     """Conv2d (+fused bias/activation). Returns y, or (y, stats) when want_stats (GPU only).
-
-    ``bn_fin`` (ops.common.BNFinalize, with ``stats_buf`` its ``buf``): the dense kernel path also
-    finalizes the BatchNorm statistics (``bn_fin.done`` tells whether it did).
 
     ``shuffle=g`` (> 1): the output channels are channel-shuffled in g groups (ShuffleNet V1;
     fused into the grouped 1x1 kernel's store on the native path, csrc/gconv.hip).
@@ -748,8 +736,6 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=
             return (y, None) if want_stats else y
     if res is None:
         residual_join = None
-    if bn_fin is not None and want_stats and res is None and stats_buf is bn_fin.buf:
-        stats_buf = bn_fin
     return _CONV_APPLY(xn, weight, bias, stride, padding, dilation, groups, ACT_IDS[act], float(slope), want_stats,
                          stats_buf, extra, join, join_role, reflect, [out] if out is not None else None, res,
                          residual_join, bool(bias_via_bn and bias is not None and not act))
