@@ -12,7 +12,8 @@
 #   tools/gpu.sh host            Python host profiles of the eager launch-bound models
 #   tools/gpu.sh convergence     ResNet-50 1,000-step native vs torch-bf16 curves, 2 seeds
 #   tools/gpu.sh overlap         DP bucket overlap test + force-DP kernel timeline
-#   AB=VAR tools/gpu.sh ab       bench + kernel-trace A/B of an env toggle (DV_DEFER, DV_FUSE_FINALIZE)
+#   AB=VAR tools/gpu.sh ab       bench + kernel-trace A/B of an env toggle (DV_DEFER)
+#   tools/gpu.sh abtree          same-box bench A/B of ./ab_old (tools/ab_tree.sh <commit>) vs the tree
 # Every GPU step has its own time limit and the steps are chained with &&: after a fault,
 # abort or timeout nothing else runs on the GPU in that call.
 set -o pipefail
@@ -133,8 +134,7 @@ case "$mode" in
   ab)
     # A/B of an environment toggle on the ResNet-50 bench + kernel traces of both arms:
     #   AB="DV_DEFER" (BN apply deferred into the consumer conv, tests/test_defer_gpu.py first)
-    #   AB="DV_FUSE_FINALIZE" (BN finalize in the producer conv, tests/test_bn_finalize_fused_gpu.py first)
-    v=${AB:-DV_FUSE_FINALIZE}; t=tests/test_bn_finalize_fused_gpu.py; [ "$v" = DV_DEFER ] && t=tests/test_defer_gpu.py
+    v=${AB:-DV_DEFER}; t=tests/test_defer_gpu.py
     timeout -k 10 600 $PYT $t > gpurun_out/ab_tests.log 2>&1 && \
     env $v=0 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/ab_off.log 2>&1 && \
     env $v=1 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/ab_on.log 2>&1 && \
@@ -150,6 +150,19 @@ case "$mode" in
       rm -f "$t"
       echo "$v=$a: $(grep '^{' gpurun_out/ab_$a.log | tail -1 | cut -c1-120)"; sed -n 3,12p gpurun_out/ab_step_$a.txt 2>/dev/null
     done ;;
+  abtree)
+    # same-box A/B of the tree in ./ab_old (tools/ab_tree.sh <commit>) against the working tree:
+    # ResNet-50 eager, alternating old / new twice, then MobileNet --graph once each
+    [ -d ab_old ] || { echo "no ab_old/ (run tools/ab_tree.sh <commit> first)"; exit 2; }
+    mkdir -p gpurun_out/abx; rc=0
+    for i in 1 2; do
+      (cd ab_old && timeout -k 10 300 python bench.py --steps 20 --warmup 5) > gpurun_out/abx/old_$i.log 2>&1 && \
+      timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/abx/new_$i.log 2>&1 || { rc=$?; break; }
+    done
+    [ $rc -eq 0 ] && { (cd ab_old && timeout -k 10 300 python bench.py --model mobilenet1 --graph --steps 20 --warmup 3) \
+      > gpurun_out/abx/old_mb.log 2>&1 && timeout -k 10 300 python bench.py --model mobilenet1 --graph --steps 20 \
+      --warmup 3 > gpurun_out/abx/new_mb.log 2>&1 || rc=$?; }
+    for f in gpurun_out/abx/*.log; do echo "$f $(grep '^{' $f | tail -1 | cut -c1-110)"; done ;;
   *) echo "unknown mode $mode"; exit 2 ;;
 esac
 echo "rc=$rc"
