@@ -406,10 +406,6 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
   p.wkr = a.w_kr ? a.w_kr : a.S * a.Cg;
   p.wks = a.w_ks ? a.w_ks : a.Cg;
   p.ksplit = 1; p.kt_per = 1 << 30; p.ypart = nullptr;
-  p.at_x = (const u16*)a.at_x; p.at_r = (const u16*)a.at_r; p.at_bits_in = (const uint8_t*)a.at_bits_in;
-  p.at_bits_out = (uint8_t*)a.at_bits_out; p.at_side = (u16*)a.at_side;
-  for (int j = 0; j < 5; ++j) p.at_c[j] = a.at_c[j];
-  p.at_act = a.at_act; p.at_slope = a.at_slope;
   // zero-filling scatter: plain epilogue, no residual, a strided map with no offset whose
   // siblings tile the output grid (OH <= P*osh, OW <= Q*osw), vector stores
   p.zfill = a.zfill;
@@ -485,22 +481,6 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
     return bn_status;
   }
   if (p.Cg % 8 != 0 || p.ldx % 8 != 0) return -1;
-  if (a.at) {
-    // A-transform: every A row is one dense source row (1x1, stride 1, no padding, one group, the
-    // fast loader's whole K-tiles), no split-K; the coefficient vectors must all be present
-    const bool geo = a.R == 1 && a.S == 1 && a.sh == 1 && a.sw == 1 && a.ph == 0 && a.pw == 0 && a.H == a.P &&
-                     a.W == a.Q && a.G == 1 && !a.tgather && !a.reflect && !p.ypart && !p.zfill && p.Cg % 64 == 0 &&
-                     a.at_x && (a.at < AT_JOIN || a.at_r) && (a.at != AT_BWDB || a.at_bits_in);
-    int nco = a.at == AT_BN ? 2 : a.at == AT_JOIN ? 4 : a.at == AT_BWDB ? 3 : a.at == AT_BWDX ? 5 : -1;
-    bool cok = nco > 0;
-    for (int j = 0; j < nco && cok; ++j) cok = a.at_c[j] != nullptr && ((uintptr_t)a.at_c[j] & 15) == 0;
-    // the 128x128 / 256x64 tiles' stages (<= 64 KB) plus the coefficients must fit one block's LDS
-    // the widest A-transform stage set: 3 x 256x64x32 stages with dout + bits (about 122 KB)
-    if (!geo || !cok || (size_t)3 * 41984 + (size_t)nco * p.K * 4 > LDS_MAX) return -1;
-    p.x = p.at_x;  // the LDS-DMA loader stages the raw BN input; the transform runs per fragment
-    dv_conv_fwd_at(p, a.at, st);
-    return bn_status;
-  }
   // warp-specialised ring (benchmark variants 20: 128x128, 21: 256x64, 22: 256x128, 23: 128x256)
   if (dv_g_fwd_variant >= 20 && dv_g_fwd_variant <= 23 && !a.tgather && p.Cg % 64 == 0 && p.R <= 16 && p.S <= 16 &&
       !p.reflect && p.G == 1 && p.identity_map && !p.bias && !p.act && !p.res && !p.bnmode && !p.ypart && !p.zfill &&

@@ -1,7 +1,6 @@
 #pragma once
-// Shared core of the implicit-GEMM convolution (csrc/conv_fwd.hip, csrc/conv_fwd_at.hip): the
-// parameter block, the main kernel template and its launchers. Split across two translation
-// units only so the register-staged A-transform instantiations compile in parallel.
+// Shared core of the implicit-GEMM convolution (csrc/conv_fwd.hip): the parameter block, the
+// main kernel template and its launchers.
 // Implicit-GEMM convolution FORWARD on gfx950 MFMA (bf16 in, fp32 accumulate).
 // Also serves conv dgrad, ConvTranspose forward and Linear forward/dgrad (SURVEY §2.7 K1-K4,
 // K9, K13).
@@ -63,14 +62,6 @@ struct FwdParams {
   float* bnacc2;
   int wld, wkr, wks;  // weight row / tap strides (kernels.h ConvFwdArgs w_ld, w_kr, w_ks)
   int ntl;            // epilogue reads of once-used tensors (residual, BN input) with the non-temporal policy
-  // A-operand transform (template AT; kernels.h ConvFwdArgs at_*)
-  const u16* at_x;
-  const u16* at_r;
-  const uint8_t* at_bits_in;
-  uint8_t* at_bits_out;
-  u16* at_side;
-  const float* at_c[5];
-  int at_act; float at_slope;
 };
 
 }  // namespace dvconv
@@ -99,21 +90,6 @@ constexpr int stat_bytes() { return n_waves<BM_, BN_, WMT>() * 64 * 3 * 4; }
 enum { KM_FAST = 0, KM_GENERIC = 1, KM_TGATHER = 2 };
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_LEAKY = 2 };
 
-
-// A-operand transforms (compile time). The A tile is staged through registers: global loads of
-// the source rows, the per-element BatchNorm form, ds_write into the same swizzled LDS image the
-// LDS-DMA path would have produced. Only 1x1 / stride-1 / unpadded single-group convs and dgrads:
-// A row m is source row m (dense, ld = ldx).
-//   AT_BN   a = act(x*c0 + c1)                        (BN -> act feeding the conv)
-//   AT_JOIN a = act(x*c0 + (c1 + c3) + r*c2)           (residual join, r the identity (c2 = 1, c3 = 0)
-//                                                       or a second BN's input; + mask bits)
-//   AT_BWDB a = c0*dz + c1*x + c2, dz = bit ? r : slope*r / 0  (BN backward, stored mask bits)
-//   AT_BWDX a = c0*dz + c1*x + c2, dz = act'(x*c3 + c4) * r    (BN backward, mask recomputed)
-enum { AT_NONE = 0, AT_BN = 1, AT_JOIN = 2, AT_BWDB = 3, AT_BWDX = 4 };
-template <int AT>
-constexpr int at_ncoef() { return AT == AT_BN ? 2 : AT == AT_JOIN ? 4 : AT == AT_BWDB ? 3 : AT == AT_BWDX ? 5 : 0; }
-template <int AT>
-constexpr bool at_has_r() { return AT >= AT_JOIN; }
 
 // ReflectionPad2d index map (pad < n): -1 -> 1, n -> n - 2
 DV_DEVICE int reflect_idx(int i, int n) {
@@ -153,12 +129,6 @@ DV_DEVICE bf16x8 read_kc(const char* img, int row, int chunk) {
 
 template <int BM_, int BN_, int BK_>
 constexpr int stage_bytes() { return (BM_ + BN_) * BK_ * 2; }
-// an A-transform stage also holds the raw second source (residual / dout, same image layout as
-// the A operand) and, for AT_BWDB, the tile's mask bits ([BM_][BK_/8] bytes, row-major)
-template <int BM_, int BN_, int BK_, int AT>
-constexpr int at_stage_bytes() {
-  return stage_bytes<BM_, BN_, BK_>() + (AT >= AT_JOIN ? BM_ * BK_ * 2 : 0) + (AT == AT_BWDB ? BM_ * BK_ / 8 : 0);
-}
 
 // BatchNorm-backward reduction terms of 8 stored gradient values `o` (bf16, exactly what the
 // unfused bn_bwd_reduce pass would read back) at element offset `off` of the BN input / mask:
@@ -214,7 +184,7 @@ enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_FULL = 2 };
 // from one block, whose deep LDS ring then holds one CU); __launch_bounds__' second argument is
 // waves per SIMD, so both forms get up to 256 VGPRs.
 template <int BM_, int BN_, int BK_, int KMODE, bool RES, int STAGES, int BNR = 0, int EPI = EPI_FULL,
-          int WMT = 64, int AT = AT_NONE>
+          int WMT = 64>
 __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_kernel(FwdParams p) {
   constexpr int WN = BN_ / 64, WM = BM_ / WMT;
   constexpr int NW = WN * WM;
@@ -229,15 +199,8 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
   constexpr int NI = BN_ / RPI / NW;   // N-operand DMA instructions per wave per K-tile
   static_assert(MI * RPI * NW == BM_ && NI * RPI * NW == BN_, "loader rows must split evenly over the waves");
   constexpr int KK = BK_ / 32;         // 32-deep MFMA steps per K-tile
-  constexpr int STAGE = at_stage_bytes<BM_, BN_, BK_, AT>();
-  constexpr int NCO = at_ncoef<AT>();
-  // AT: second-source DMAs (MI per wave) and the tile's mask bits as 4-byte-per-lane DMAs (the
-  // sub-dword LDS-DMA forms do not pack lanes at their own width): NBW waves issue one each --
-  // all of them on the 256x64 tile, whose 3-deep ring counts them per wave (IPT)
-  constexpr int NBW = AT == AT_BWDB ? BM_ * BK_ / 8 / 256 : 0;
-  static_assert(AT != AT_BWDB || (NBW >= 1 && NBW <= NW && (STAGES == 2 || NBW == NW)), "mask-bit DMA split");
-  static_assert(AT == AT_NONE || (BK_ == 32 && KMODE == KM_FAST), "A-transform: BK 32 on the fast loader");
-  constexpr int IPT = MI + NI + (AT >= AT_JOIN ? MI : 0) + (AT == AT_BWDB ? 1 : 0);  // DMAs per wave per tile
+  constexpr int STAGE = stage_bytes<BM_, BN_, BK_>();
+  constexpr int IPT = MI + NI;         // DMA instructions per wave per K-tile
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -321,24 +284,6 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
         const bool ok = (tapmask[j] >> sh_r) & (tapmask[j] >> sh_s) & 1u;
         glds16(ok ? (const void*)(xrow[j] + koff) : (const void*)zero, img_m + (wid * MI + j) * 1024);
       }
-      if constexpr (AT >= AT_JOIN) {  // raw residual / dout rows into the second image, same layout
-        char* img_r = img_m + BM_ * BK_ * 2;
-#pragma unroll
-        for (int j = 0; j < MI; ++j) {
-          const bool ok = (tapmask[j] >> sh_r) & (tapmask[j] >> sh_s) & 1u;
-          glds16(ok ? (const void*)(p.at_r + (xrow[j] - p.x) + koff) : (const void*)zero, img_r + (wid * MI + j) * 1024);
-        }
-      }
-      if constexpr (AT == AT_BWDB) {  // mask bits of the tile: [BM_][BK_/8] bytes, 4 per lane
-        if (wid < NBW) {
-          char* img_b = img_m + 2 * BM_ * BK_ * 2;
-          const int off = (wid * 64 + lane) * 4, row = off / (BK_ / 8), byte = off % (BK_ / 8);
-          const int m = m0 + row;
-          const void* src =
-              m < p.M ? (const void*)(p.at_bits_in + (((int64_t)m * p.ldx + t_c) >> 3) + byte) : (const void*)zero;
-          __builtin_amdgcn_global_load_lds(GLB_PTR(src), LDS_PTR(img_b + wid * 256), 4, 0, 0);
-        }
-      }
     } else {
 #pragma unroll
       for (int j = 0; j < MI; ++j) {
@@ -377,59 +322,6 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
 #pragma unroll
     for (int b = 0; b < FM; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  float* coef = reinterpret_cast<float*>(smem + STAGES * STAGE);  // AT: [NCO][K] per-channel coefficients
-  // AT side output: the waves of output-column tile 0 (wave_n 0) store each transformed A element once
-  const bool a_side = AT != AT_NONE && tn == 0 && split == 0 && grp == 0 && wave_n == 0;
-  // A-transform of one fragment (8 consecutive channels of one pixel row) in registers, right before
-  // its MFMAs: the BN / join / BN-backward expression of kernels.h ConvFwdArgs at_*
-  auto at_fragment = [&](bf16x8& f, const char* img_m, int row, int chunk, int kt, const f32x2 (*cf)[4]) {
-    const uint4 xv = __builtin_bit_cast(uint4, f);
-    uint4 rv = uint4{0u, 0u, 0u, 0u};
-    uint32_t mbits = 0;
-    if constexpr (AT >= AT_JOIN)
-      rv = *reinterpret_cast<const uint4*>(img_m + BM_ * BK_ * 2 + row * (BK_ * 2) + ((chunk ^ kc_swz<BK_>(row)) << 4));
-    if constexpr (AT == AT_BWDB) mbits = *reinterpret_cast<const uint8_t*>(img_m + 2 * BM_ * BK_ * 2 + row * (BK_ / 8) + chunk);
-    const uint32_t xw[4] = {xv.x, xv.y, xv.z, xv.w}, rw[4] = {rv.x, rv.y, rv.z, rv.w};
-    uint32_t ow[4], mb = 0;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const f32x2 x = bf2x(xw[e]);
-      f32x2 v;
-      if constexpr (AT == AT_BN || AT == AT_JOIN) {
-        f32x2 z = __builtin_elementwise_fma(x, cf[0][e], cf[1][e]);
-        if constexpr (AT == AT_JOIN) z = __builtin_elementwise_fma(bf2x(rw[e]), cf[2][e], z);
-        mb |= (z.x > 0.f ? 1u : 0u) << (2 * e);
-        mb |= (z.y > 0.f ? 1u : 0u) << (2 * e + 1);
-        if (p.at_act == ACT_RELU) { v.x = fmaxf(z.x, 0.f); v.y = fmaxf(z.y, 0.f); }
-        else if (p.at_act == ACT_LEAKY) { v.x = z.x > 0.f ? z.x : z.x * p.at_slope; v.y = z.y > 0.f ? z.y : z.y * p.at_slope; }
-        else v = z;
-      } else {
-        const f32x2 d = bf2x(rw[e]);
-        const f32x2 neg = p.at_act == ACT_LEAKY ? d * p.at_slope : f32x2{0.f, 0.f};
-        f32x2 dz = d;
-        if constexpr (AT == AT_BWDB) {
-          dz.x = ((mbits >> (2 * e)) & 1u) ? d.x : neg.x;
-          dz.y = ((mbits >> (2 * e + 1)) & 1u) ? d.y : neg.y;
-        } else if (p.at_act) {
-          const f32x2 z = __builtin_elementwise_fma(x, cf[3][e], cf[4][e]);
-          dz.x = z.x > 0.f ? d.x : neg.x;
-          dz.y = z.y > 0.f ? d.y : neg.y;
-        }
-        v = __builtin_elementwise_fma(cf[0][e], dz, __builtin_elementwise_fma(cf[1][e], x, cf[2][e]));
-      }
-      ow[e] = pack2bf(v.x, v.y);
-    }
-    const uint4 o = uint4{ow[0], ow[1], ow[2], ow[3]};
-    f = __builtin_bit_cast(bf16x8, o);
-    const int m = m0 + row;
-    if (a_side && m < p.M) {
-      const int64_t off = (int64_t)m * p.ldx + kt * BK_ + chunk * 8;
-      *reinterpret_cast<uint4*>(p.at_side + off) = o;
-      if constexpr (AT == AT_BN || AT == AT_JOIN) {
-        if (p.at_bits_out) p.at_bits_out[off >> 3] = (uint8_t)mb;
-      }
-    }
-  };
   auto compute = [&](int buf, int kt) {
     const char* img_n = smem + buf * STAGE;
     const char* img_m = img_n + BN_ * BK_ * 2;
@@ -442,24 +334,6 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
 #pragma unroll
       for (int i = 0; i < FM; ++i)
         fb[i] = read_kc<BK_>(img_m, wave_m * WMT + i * 16 + (lane & 15), kk * 4 + (lane >> 4));
-      if constexpr (AT != AT_NONE) {
-        const int chunk = kk * 4 + (lane >> 4);
-        const int kc = kt * BK_ + chunk * 8;
-        f32x2 cf[NCO > 0 ? NCO : 1][4];
-#pragma unroll
-        for (int j = 0; j < NCO; ++j) {
-          const f32x4 lo = *reinterpret_cast<const f32x4*>(coef + j * p.K + kc);
-          const f32x4 hi = *reinterpret_cast<const f32x4*>(coef + j * p.K + kc + 4);
-          cf[j][0] = f32x2{lo[0], lo[1]}; cf[j][1] = f32x2{lo[2], lo[3]};
-          cf[j][2] = f32x2{hi[0], hi[1]}; cf[j][3] = f32x2{hi[2], hi[3]};
-        }
-        if constexpr (AT == AT_JOIN) {  // one shift per channel: c1 + c3 (bn_apply_kernel RBN order)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) cf[1][e] += cf[3][e];
-        }
-#pragma unroll
-        for (int i = 0; i < FM; ++i) at_fragment(fb[i], img_m, wave_m * WMT + i * 16 + (lane & 15), chunk, kt, cf);
-      }
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -467,14 +341,6 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
           acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[j], fb[i], acc[j][i], 0, 0, 0);
     }
   };
-  if constexpr (AT != AT_NONE) {
-    // coefficient vectors -> LDS once per block (behind the operand stages); the first barrier of
-    // the K loop orders them before any read
-#pragma unroll
-    for (int j = 0; j < NCO; ++j)
-      for (int k = threadIdx.x * 4; k < p.K; k += 64 * NW * 4)
-        *reinterpret_cast<f32x4*>(coef + j * p.K + k) = *reinterpret_cast<const f32x4*>(p.at_c[j] + k);
-  }
   if constexpr (STAGES == 2) {
     // double buffer, one barrier per K-tile: the DMA of tile t+1 overlaps the MFMAs of tile t
     stage(kt0, 0);
@@ -863,23 +729,16 @@ constexpr int lds_bytes(int stages) {
   return stages * stage_bytes<BM_, BN_, BK_>() > epi ? stages * stage_bytes<BM_, BN_, BK_>() : epi;
 }
 
-// dynamic LDS of an A-transform launch: the (wider) operand stages, then the [NCO][K] coefficients
-template <int BM_, int BN_, int BK_, int WMT, int AT>
-size_t at_lds_bytes(int K, int stages) {
-  const size_t a = (size_t)stages * at_stage_bytes<BM_, BN_, BK_, AT>() + (size_t)at_ncoef<AT>() * K * 4;
-  const size_t b = lds_bytes<BM_, BN_, BK_, WMT>(stages);
-  return a > b ? a : b;
-}
 constexpr size_t LDS_MAX = 160 * 1024;
 
 template <int BM_, int BN_, int BK_, int KMODE, bool RES, int STAGES, int BNR = 0, int EPI = EPI_FULL,
-          int WMT = 64, int AT = AT_NONE>
+          int WMT = 64>
 void launch_fwd(const FwdParams& p, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES, BNR, EPI, WMT, AT>,
+    hipFuncSetAttribute((const void*)conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES, BNR, EPI, WMT>,
                         hipFuncAttributeMaxDynamicSharedMemorySize,
-                        AT != AT_NONE ? (int)LDS_MAX : lds_bytes<BM_, BN_, BK_, WMT>(STAGES));
+                        lds_bytes<BM_, BN_, BK_, WMT>(STAGES));
     attr = true;
   }
   FwdParams q = p;
@@ -888,10 +747,9 @@ void launch_fwd(const FwdParams& p, hipStream_t st) {
   q.kt_per = (nt_all + q.ksplit - 1) / q.ksplit;
   q.ksplit = (nt_all + q.kt_per - 1) / q.kt_per;  // no empty splits
   const int nt = q.kt_per;
-  const size_t lds = AT != AT_NONE ? at_lds_bytes<BM_, BN_, BK_, WMT, AT>(p.K, STAGES)
-                                   : lds_bytes<BM_, BN_, BK_, WMT>(nt < STAGES ? nt : STAGES);
+  const size_t lds = lds_bytes<BM_, BN_, BK_, WMT>(nt < STAGES ? nt : STAGES);
   const int blocks = ((p.M + BM_ - 1) / BM_) * ((p.N + BN_ - 1) / BN_) * p.G * q.ksplit;
-  conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES, BNR, EPI, WMT, AT>
+  conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES, BNR, EPI, WMT>
       <<<dim3(blocks), dim3(64 * n_waves<BM_, BN_, WMT>()), lds, st>>>(q);
   if (p.ypart) dv_g_last_ksplit = q.ksplit;
 }
@@ -914,47 +772,5 @@ bool big_tile_ok(const FwdParams& p) {
   return tiles >= 192 || dv_g_fwd_variant == 100;  // 100: tests force it at small shapes
 }
 
-// A-transform launches (csrc kernels.h ConvFwdArgs at_*): the transform runs on each A fragment
-// right before its MFMAs, so the tiles whose A fragments are read by one wave column (256x64,
-// N <= 64) or two (128x128) keep it cheap; BK 32, the heuristic's LDS-DMA pipeline (the 3-deep
-// ring on the short-K 64-channel layers)
-template <int AT, bool RES, int BNR, int EPI>
-void launch_at(const FwdParams& p, hipStream_t st) {
-  if (p.N <= 64) {
-    if (p.K <= 256) launch_fwd<256, 64, 32, KM_FAST, RES, 3, BNR, EPI, 64, AT>(p, st);
-    else launch_fwd<256, 64, 32, KM_FAST, RES, 2, BNR, EPI, 64, AT>(p, st);
-  } else {
-    launch_fwd<128, 128, 32, KM_FAST, RES, 2, BNR, EPI, 64, AT>(p, st);
-  }
-}
-
-template <int AT, bool RES, int BNR>
-void dispatch_at_epi(const FwdParams& p, hipStream_t st) {
-  if constexpr (AT == AT_BWDB || AT == AT_BWDX || BNR) {
-    launch_at<AT, RES, BNR, EPI_PLAIN>(p, st);  // dgrads: plain store (+ fused BN-backward sums)
-  } else {
-    const bool full = p.bias || p.act;
-    if (full) launch_at<AT, RES, 0, EPI_FULL>(p, st);
-    else if (p.stats) launch_at<AT, RES, 0, EPI_STATS>(p, st);
-    else launch_at<AT, RES, 0, EPI_PLAIN>(p, st);
-  }
-}
-
-template <int AT>
-void dispatch_at(const FwdParams& p, hipStream_t st) {
-  const int bnr = p.bnmode ? (p.bnx2 ? 2 : 1) : 0;
-  if (p.res) {
-    if (bnr == 2) dispatch_at_epi<AT, true, 2>(p, st);
-    else if (bnr == 1) dispatch_at_epi<AT, true, 1>(p, st);
-    else dispatch_at_epi<AT, true, 0>(p, st);
-  } else {
-    if (bnr == 2) dispatch_at_epi<AT, false, 2>(p, st);
-    else if (bnr == 1) dispatch_at_epi<AT, false, 1>(p, st);
-    else dispatch_at_epi<AT, false, 0>(p, st);
-  }
-}
-
 }  // namespace
 
-// A-transform launch (conv_fwd_at.hip): the dispatch over AT / residual / BN-backward epilogue
-void dv_conv_fwd_at(const dvconv::FwdParams& p, int at, hipStream_t st);

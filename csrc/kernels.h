@@ -57,28 +57,10 @@ struct ConvFwdArgs {
   const void* bnx2 = nullptr;
   const float* bnprm2 = nullptr;
   float* bnacc2 = nullptr;
-  // A-operand transform (a deferred BatchNorm apply folded into its consumer's operand load; 1x1,
-  // stride-1, unpadded, single-group convs and dgrads only: every A row is one dense source row).
-  // The block stages A through registers instead of LDS-DMA: it loads the source rows, applies
-  //   at = 1 (forward):  a = act(x*c0 + c1 [+ r | + r*c2 + c3])   (bn_apply_kernel, residual join)
-  //   at = 2 (backward): a = c0*dz + c1*x + c2, dz = act'(.) * r   (bn_bwd_apply_kernel)
-  // and writes `a` into the LDS image. Blocks of output-column tile 0 also store `a` (and the
-  // forward activation mask bits) to at_side / at_bits_out: the materialised BN output /
-  // gradient the rest of the graph reads, written once instead of by a separate apply pass.
   // weight operand layout (fast loader only): elements between output-channel rows (0 = R*S*Cg)
   // and between consecutive taps of a row / column (0 = S*Cg / Cg). A tap subset of a larger
   // filter reads the full cached weight in place: w points at its first tap (sub-pixel dgrad)
   int w_ld = 0, w_kr = 0, w_ks = 0;
-  int at = 0;
-  int at_flags = 0;           // at 1: bit0 residual r, bit1 residual BN (c2, c3); at 2: mask mode 1/2/3
-  int at_act = 0;
-  float at_slope = 0.f;
-  const void* at_x = nullptr;       // BN input (same dense layout as the gathered x, ld = ldx)
-  const void* at_r = nullptr;       // residual (at 1) / incoming gradient dout (at 2)
-  const void* at_bits_in = nullptr; // at 2, mask mode 3: the forward's mask bits of dout's BN
-  void* at_bits_out = nullptr;      // at 1: mask bits of z (1 bit per element) or nullptr
-  void* at_side = nullptr;          // materialised a (dense, ld = ldx) or nullptr
-  const float* at_c[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // per-channel [K] coefficients
 };
 
 struct ConvWgradArgs {

@@ -73,16 +73,10 @@ class BottleneckBlock(tnn.Module):
             self.projection = nn.Sequential(
                 nn.Conv2d(in_channels, out2, 1, stride=stride, bias=False), nn.BatchNorm2d(out2))
 
-    # set by the stage builder on every block but the last: the block output feeds the next
-    # block's conv1 (1x1, stride 1), which applies this block's BN3 + add + ReLU join while
-    # loading its operand and materialises the output as a side store (ops.defer)
-    defer_out = False
-
     def forward(self, x):
         j = GradJoin() if F.native(x) else None
         out = F.conv_bn_act(x, self.conv1, self.bn1, "relu", join=j, join_role="consumer")
-        # bn2 -> ReLU is applied by conv3 (1x1) while it stages its A operand
-        out = F.conv_bn_act(out, self.conv2, self.bn2, "relu", defer_out=True)
+        out = F.conv_bn_act(out, self.conv2, self.bn2, "relu")
         # projection created after the main path: its backward runs first and stashes its dx;
         # its BatchNorm is applied inside bn3's BN+add+ReLU pass (ops.bn.conv_bn_deferred)
         rbn = None
@@ -91,8 +85,7 @@ class BottleneckBlock(tnn.Module):
             rj = None
         else:
             identity, rj = x, j
-        return F.conv_bn_act(out, self.conv3, self.bn3, "relu", residual=identity, residual_join=rj, residual_bn=rbn,
-                             defer_out=self.defer_out)
+        return F.conv_bn_act(out, self.conv3, self.bn3, "relu", residual=identity, residual_join=rj, residual_bn=rbn)
 
 
 class _ResNetBase(tnn.Module):
@@ -155,8 +148,6 @@ class _Bottleneck(_ResNetBase):
     def _make_blocks(n, cin, out1, out2, stride):
         blocks = [BottleneckBlock(cin, out1, out2, stride=stride, downsample=True)]
         blocks += [BottleneckBlock(out2, out1, out2) for _ in range(1, n)]
-        for b in blocks[:-1]:  # the next block's conv1 folds this block's output join (ops.defer)
-            b.defer_out = True
         return nn.Sequential(*blocks)
 
 

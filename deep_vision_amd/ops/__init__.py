@@ -8,6 +8,5 @@ from .bn import batch_norm_act, batch_norm_act_maxpool, conv_bn_act, conv_bn_act
 from .common import as_nhwc, backend, native, set_backend  # noqa: F401
 from .concat import channel_shuffle, concat, concat_slices, slice_cat  # noqa: F401
 from .conv import conv2d, conv_transpose2d, linear  # noqa: F401
-from .defer import resolve  # noqa: F401
 from .loss import cross_entropy  # noqa: F401
 from .pool import adaptive_avg_pool2d, avg_pool2d, max_pool2d, upsample_add, upsample_nearest  # noqa: F401

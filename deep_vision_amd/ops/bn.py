@@ -18,7 +18,6 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as TF
 
-from . import defer
 from .common import (ACT_IDS, BF16, F32, fast_apply, grad_nhwc, grad_sink, is_nhwc, ld_of, lib, native, ptr,
                      stream_handle, workspace)
 
@@ -76,7 +75,7 @@ class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, stats, weight, bias, running_mean, running_var, residual, training, momentum, eps, act,
                 slope, ws_fwd, ws_bwd, join=None, refbox=None, r_stats=None, r_weight=None, r_bias=None, r_rm=None,
-                r_rv=None, r_cfg=None, xjoin=None, defer_fwd=False, defer_bwd=False, prod_bias=None, post_res=False):
+                r_rv=None, r_cfg=None, xjoin=None, prod_bias=None, post_res=False):
         # xjoin (conv.GradJoin): another consumer of ``x`` stashes its gradient there (e.g. the
         # identity path of a pre-activation block); the backward apply pass adds it in place
         # r_*: a second, training-mode BatchNorm applied to ``residual`` inside the same pass
@@ -121,16 +120,9 @@ class _BNActFn(torch.autograd.Function):
         mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=dev) if bits else None
         rsc, rsh = (rprm[0], rprm[1]) if rprm is not None else (None, None)
 
-        def run_apply():
-            defer.launch_bn_apply(x, residual, out, C, scale, shift, act, slope, mask, rsc, rsh, post=post)
-
-        if (defer_fwd and defer.ENABLED and not post and act in (0, 1, 2) and C % 64 == 0
-                and (residual is None or (is_nhwc(residual) and ld_of(residual) == C))):
-            # the consumer 1x1 conv computes `out` while staging its A operand (ops.defer)
-            out._dv_pending = defer.PendingApply.forward(out, x, residual, scale, shift, rsc, rsh, act, slope, mask,
-                                                         run_apply)
-        else:
-            run_apply()
+        L.bn_apply(ptr(x), ptr(residual), ptr(out), x.numel(), C, ptr(scale), ptr(shift), act, float(slope), ptr(mask),
+                   st, rscale=ptr(rsc) if rsc is not None else 0, rshift=ptr(rsh) if rsh is not None else 0,
+                   post=int(post))
         keep_out = bool(act) and residual is not None and not bits and not post
         ctx.save_for_backward(x, mask if bits else (out if keep_out else None), weight, bias, prm,
                               residual if rprm is not None else None, rprm, r_weight, r_bias)
@@ -141,7 +133,6 @@ class _BNActFn(torch.autograd.Function):
         ctx.ws_bwd = ws_bwd
         ctx.join = join
         ctx.xjoin = xjoin
-        ctx.defer_bwd = bool(defer_bwd) and training
         ctx.has_prod_bias = prod_bias is not None
         ctx.prod_bias_param = prod_bias  # leaf parameter (not saved): its gradient may sink in place
         ctx.bnref = None
@@ -201,7 +192,7 @@ class _BNActFn(torch.autograd.Function):
             coef = torch.empty((3, C), dtype=F32, device=dev)
             # the producing conv's bias gradient = sum of this BN's input gradient, from the same sums
             # in the finalize (training statistics, no other gradient folded into dx)
-            if ctx.has_prod_bias and ctx.needs_input_grad[25]:
+            if ctx.has_prod_bias and ctx.needs_input_grad[23]:
                 if training and xg is None:
                     pb_sink = grad_sink(ctx.prod_bias_param)
                     if pb_sink is None:
@@ -213,35 +204,7 @@ class _BNActFn(torch.autograd.Function):
         # residual join with the projection BN folded in: both input gradients from one pass
         dual = (DUAL_BWD and training and rprm is not None and ctx.bits and not fold_x and ctx.needs_input_grad[6]
                 and dout.is_contiguous(memory_format=torch.channels_last))
-        # dx deferred into the producing 1x1 conv's dgrad A operand (ops.defer): no apply pass for
-        # it here; the mask must come from the stored bits or from x (not from a saved output)
-        bwd_defer = (ctx.defer_bwd and defer.ENABLED and training and xg is None and dres is None and C % 64 == 0
-                     and (ctx.bits or not has_res) and act in (0, 1, 2) and ld_of(dout) == C
-                     and dout.is_contiguous(memory_format=torch.channels_last) and ctx.needs_input_grad[0])
-        if bwd_defer:
-            bits_t = out if ctx.bits else None
-            mb = int(ctx.bits)
-            dres_p = 0
-
-            def run_bwd():
-                L.bn_bwd_apply(ptr(dout), ptr(out), ptr(x), ptr(dx), dres_p, x.numel(), C, ptr(coef[0]), ptr(coef[1]),
-                               ptr(coef[2]), ptr(scale), ptr(shift), act, float(slope), mb, stream_handle())
-
-            defer.register_grad(dx, defer.PendingApply.backward(dx, dout, x, bits_t, coef[0], coef[1], coef[2], scale,
-                                                                shift, act, slope, run_bwd))
-        if bwd_defer and dual:
-            # the projection BN's input gradient alone: one single apply pass over (dout, bits, r_x)
-            COUNTERS["dual_apply"] += 1
-            COUNTERS["dual_fused"] += int(fused2)
-            coef_r, r_dgamma, r_dbeta = _residual_bn_coef(ctx, dout, out, r_x, rprm, r_weight, r_bias, act, slope, fused2)
-            dres = torch.empty_like(r_x)
-            L.bn_bwd_apply(ptr(dout), ptr(out), ptr(r_x), ptr(dres), 0, r_x.numel(), C, ptr(coef_r[0]), ptr(coef_r[1]),
-                           ptr(coef_r[2]), 0, 0, act, float(slope), 1, st)
-            dual = False
-            rprm_done = True
-        else:
-            rprm_done = False
-        if training and not dual and not bwd_defer:
+        if training and not dual:
             L.bn_bwd_apply(ptr(dout), ptr(out), ptr(x), ptr(dx), ptr(dres), x.numel(), C, ptr(coef[0]), ptr(coef[1]),
                            ptr(coef[2]), ptr(scale), ptr(shift), act, float(slope), int(ctx.bits), st,
                            addend=ptr(xg) if fold_x else 0)
@@ -250,11 +213,8 @@ class _BNActFn(torch.autograd.Function):
                 out = torch.empty_like(x)
                 L.bn_apply(ptr(x), 0, ptr(out), x.numel(), C, ptr(scale), ptr(shift), act, float(slope), 0, st)
             L.bn_bwd_eval(ptr(dout), ptr(out), ptr(dx), ptr(dres), x.numel(), C, ptr(scale), act, float(slope), st)
-        if not rprm_done:
-            r_dgamma = r_dbeta = None
-        if rprm_done:
-            pass
-        elif dual:
+        r_dgamma = r_dbeta = None
+        if dual:
             COUNTERS["dual_apply"] += 1
             COUNTERS["dual_fused"] += int(fused2)
             coef_r, r_dgamma, r_dbeta = _residual_bn_coef(ctx, dout, out, r_x, rprm, r_weight, r_bias, act, slope, fused2)
@@ -275,13 +235,13 @@ class _BNActFn(torch.autograd.Function):
             dres = ctx.join.produce(dres)  # folded into the shortcut consumer's dgrad epilogue
         if xg is not None and not fold_x:
             dx = dx + xg
-        if ctx.has_prod_bias and ctx.needs_input_grad[25] and pb_sink is None and pb_grad is None:
+        if ctx.has_prod_bias and ctx.needs_input_grad[23] and pb_sink is None and pb_grad is None:
             # eval statistics / a folded second gradient: reduce the final dx explicitly
             from .conv import _channel_sum
 
             pb_grad = _channel_sum(dx if dx.shape[1] == C else dx.contiguous(memory_format=torch.channels_last))
         return (dx, None, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None, None, None,
-                None, r_dgamma, r_dbeta, None, None, None, None, None, None, pb_grad, None)
+                None, r_dgamma, r_dbeta, None, None, None, None, pb_grad, None)
 
 
 def _residual_bn_coef(ctx, dout, bits, r_x, rprm, r_weight, r_bias, act, slope, fused):
@@ -492,19 +452,13 @@ def bn_momentum(bn) -> float:
 
 
 def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None, residual_join=None, residual_bn=None,
-                   input_join=None, defer_out=False, defer_bwd=False, prod_bias=None, residual_post=False):
+                   input_join=None, prod_bias=None, residual_post=False):
     """act(BN(x) (+ residual)) with ``bn`` an nn.BatchNorm2d (parameters, buffers, mode).
     ``input_join`` (conv.GradJoin): x's gradient from another consumer, stashed there by its
     producer, is added inside this BN's backward apply pass.
     ``residual_bn=(bn_r, stats_r)``: ``residual`` is a raw conv output still to be normalised by
     ``bn_r`` (training mode, batch statistics ``stats_r`` from its conv epilogue); the two BNs,
-    the add and the activation run as one pass (see conv_bn_deferred).
-    ``defer_out``: the caller's next op is a 1x1 conv that applies this BN while loading its
-    operand (ops.defer; the output comes back unwritten with a pending apply). ``defer_bwd``: x
-    is the output of a 1x1 conv made in the same fused op, whose dgrad can apply this BN's
-    backward the same way."""
-    defer.resolve(x)
-    defer.resolve(residual)
+    the add and the activation run as one pass (see conv_bn_deferred)."""
     if residual_bn is not None:
         rbn, rstats = residual_bn
         C = x.shape[1]
@@ -545,8 +499,7 @@ def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None, residu
         rargs = (None,) * 6
     y = _BN_APPLY(x, stats, bn.weight, bn.bias, rm, rv, residual, training, mom,
                        bn.eps, ACT_IDS[act], float(slope), ws_fwd, ws_bwd, residual_join, refbox, *rargs, input_join,
-                       bool(defer_out), bool(defer_bwd) and torch.is_grad_enabled(), prod_bias,
-                       bool(residual_post and residual_bn is None))
+                       prod_bias, bool(residual_post and residual_bn is None))
     if refbox:
         y._dv_bnref = refbox[0]  # read by the consumer conv (ops.conv._ConvFn)
     return y
@@ -571,7 +524,7 @@ def conv_bn_deferred(x, conv, bn, join=None, join_role=None):
 
 
 def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None, join=None, join_role=None, residual_join=None,
-                residual_bn=None, reflect_pad=None, shuffle=0, defer_out=False, residual_post=False):
+                residual_bn=None, reflect_pad=None, shuffle=0, residual_post=False):
     """Fused conv -> BN (batch stats from the conv epilogue) -> (+residual) -> activation.
 
     ``shuffle=g``: conv -> channel shuffle (g groups) -> BN -> act, the shuffle fused into the
@@ -579,10 +532,7 @@ def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None, join=None, join
 
     ``join`` / ``join_role`` ('consumer' | 'producer') and ``residual_join``: a conv.GradJoin
     shared by the two consumers of a block input (see models/resnet.py) so the gradient sum
-    is folded into the consumer conv's dgrad epilogue.
-
-    ``defer_out``: the BN output feeds a 1x1 conv next (ops.defer, forward). The BN backward is
-    deferred into this conv's dgrad automatically when the conv is a fusable 1x1."""
+    is folded into the consumer conv's dgrad epilogue."""
     from .conv import conv2d
 
     if not native(x):
@@ -615,19 +565,8 @@ def conv_bn_act(x, conv, bn, act=None, slope=0.0, residual=None, join=None, join
     if y.shape[1] % 8 != 0:  # padded view: BN kernels require dense channels
         y = y.contiguous(memory_format=torch.channels_last)
         stats = None
-    k = conv.kernel_size if isinstance(conv.kernel_size, tuple) else (conv.kernel_size,) * 2
-    dl = conv.dilation if isinstance(conv.dilation, tuple) else (conv.dilation,) * 2
-    bwd = (not shuffle and reflect_pad is None and y.requires_grad
-           and defer.fusable_1x1(y.shape[1], ld_of(y), k[0], k[1], conv.stride, _pad2(pad), dl, conv.groups))
     return batch_norm_act(y, bn, act, slope, residual, stats, residual_join=residual_join, residual_bn=residual_bn,
-                          defer_out=defer_out, defer_bwd=bwd, prod_bias=prod_bias, residual_post=residual_post)
-
-
-def _pad2(p):
-    if isinstance(p, int):
-        return (p, p)
-    p = tuple(p)
-    return p if len(p) == 2 else ((p[0], p[2]) if p[0] == p[1] and p[2] == p[3] else (-1, -1))
+                          prod_bias=prod_bias, residual_post=residual_post)
 
 
 _BN_APPLY = fast_apply(_BNActFn)

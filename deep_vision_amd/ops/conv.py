@@ -14,7 +14,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as TF
 
-from . import defer, wcache
+from . import wcache
 from .common import (ACT_IDS, BF16, CL, F32, act_grad, alloc_cl, as_nhwc, empty_nhwc, fast_apply, grad_nhwc, grad_sink, is_nhwc,
                      ld_of, lib,
                      like_layout, empty_layout, native, nhwc_numel, ptr, round8, stream_handle)
@@ -129,12 +129,10 @@ def conv_ksplit(M, O, K, G=1):
 
 def conv_fwd_raw(x, wk, y, bias, stats, N, H, W, Cg, ldx, G, Kout, P, Q, R, S, stride, padding, dilation,
                  act=0, slope=0.0, tgather=0, omap=None, ldy=None, res=None, bnref=None, resmask=None, reflect=False,
-                 ksplit=1, zfill=0, at=None, wlayout=None):
+                 ksplit=1, zfill=0, wlayout=None):
     """Launch the implicit-GEMM kernel. ``bnref`` (ops.bn.BNRef): also reduce that BatchNorm's
     backward statistics over ``y`` in the epilogue; returns True when that was done.
-    ``resmask`` (bits, act, slope): ``res`` is a raw gradient masked by act'() before the add.
-    ``at`` (ops.defer.PendingApply): the A operand is that deferred BN apply, computed while
-    staging and materialised by the kernel as a side output (csrc/conv_fwd.hip AT_*)."""
+    ``resmask`` (bits, act, slope): ``res`` is a raw gradient masked by act'() before the add."""
     sh, sw = stride
     ph, pw = padding
     dh, dw = dilation
@@ -156,15 +154,11 @@ def conv_fwd_raw(x, wk, y, bias, stats, N, H, W, Cg, ldx, G, Kout, P, Q, R, S, s
     if ksplit > 1:  # fp32 slabs [ksplit][M][Kout], summed + bias + act by the finalize pass
         part = torch.empty((ksplit, N * P * Q, Kout), dtype=F32, device=y.device)
         bn.update(ksplit=int(ksplit), ypart=ptr(part))
-    if at is not None:
-        bn.update(at.kernel_args())
     if wlayout is not None:  # (row stride, tap-row stride, tap stride) of a tap subset read in place
         bn.update(w_ld=int(wlayout[0]), w_kr=int(wlayout[1]), w_ks=int(wlayout[2]))
     r = lib().conv_fwd(ptr(x), ptr(wk), ptr(y), ptr(bias), ptr(stats), N, H, W, Cg, ldx, G, Kout, P, Q, R, S, sh, sw,
                        ph, pw, dh, dw, tgather, OH, OW, osh, osw, oph, opw, ldy if ldy is not None else ld_of(y), act,
                        float(slope), ptr(res), stream_handle(), **bn)
-    if at is not None:
-        at.fused()
     return bnref is not None and r == 0
 
 
@@ -186,7 +180,7 @@ def _accumulable(t, shape):
             and t.is_contiguous(memory_format=CL))
 
 
-def _dgrad(dy, weight, x_shape, Cg_x, G, stride, padding, dilation, device, accum=None, bnref=None, at=None):
+def _dgrad(dy, weight, x_shape, Cg_x, G, stride, padding, dilation, device, accum=None, bnref=None):
     """dX (N, G*Cg_x, H, W) from dY; Cg_x may include zero-padding channels.
 
     ``accum``: a dense gradient of the same input from another consumer (residual shortcut /
@@ -220,14 +214,10 @@ def _dgrad(dy, weight, x_shape, Cg_x, G, stride, padding, dilation, device, accu
         # (no separate fill pass) when the output is one dense group
         zfill = int(scatter and Cg_x == Ig and G == 1 and Ig % 8 == 0 and H <= P * sh and W <= Q * sw)
         dX, res = alloc_cl((N, G * Cg_x, H, W), zero=((scatter and not zfill) or Cg_x != Ig), device=device), None
-    # a deferred BN-backward apply producing dy rides on the A operand of the 1x1 forms only
-    if at is not None and not ((sh, sw) == (1, 1) or (scatter and not zfill)) or at is not None and R * S != 1:
-        at.materialize()
-        at = None
     if (sh, sw) == (1, 1):
         fuse = bnref if (bnref is not None and G == 1 and Cg_x == Ig and (res is not None or accum is None)) else None
         if conv_fwd_raw(dy, wd, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, H, W, R, S, (1, 1), (-ph, -pw),
-                        (-dh, -dw), ldy=G * Cg_x, res=res, bnref=fuse, resmask=resmask, at=at):
+                        (-dh, -dw), ldy=G * Cg_x, res=res, bnref=fuse, resmask=resmask):
             fuse.mark_fused(dX)
     elif scatter:
         # the BatchNorm-backward sums ride on the scatter too (the unwritten pixels' zero gradient
@@ -235,7 +225,7 @@ def _dgrad(dy, weight, x_shape, Cg_x, G, stride, padding, dilation, device, accu
         fuse = (bnref if (bnref is not None and G == 1 and Cg_x == Ig and not zfill and (res is not None or accum is None))
                 else None)
         if conv_fwd_raw(dy, wd, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, P, Q, 1, 1, (1, 1), (0, 0), (1, 1),
-                        omap=(H, W, sh, sw, 0, 0), ldy=G * Cg_x, res=res, zfill=zfill, bnref=fuse, at=at):
+                        omap=(H, W, sh, sw, 0, 0), ldy=G * Cg_x, res=res, zfill=zfill, bnref=fuse):
             fuse.mark_fused(dX)
     elif SUBPIXEL_DGRAD and tuple(dilation) == (1, 1) and Cg_dy % 64 == 0 and R <= 16 and S <= 16:
         _subpixel_dgrad(dy, wd, dX, res, bnref, N, H, W, P, Q, Cg_dy, ldy_in, G, Ig, Cg_x, R, S, stride, padding)
@@ -419,13 +409,6 @@ class _ConvFn(torch.autograd.Function):
         ldx = ld_of(x)
         Cg_x = _gather_channels(x, Cx // G, G)  # padded channels (G == 1) are zeros
         P, Q = out_size(H + extra[0], W + extra[1], R, S, stride, padding, dilation)
-        at = defer.pending(x)  # x's BatchNorm apply folded into this conv's A-operand load
-        if at is not None and not (defer.fusable_1x1(Cx, ldx, R, S, stride, padding, dilation, G)
-                                   and tuple(stride) == (1, 1) and tuple(extra) == (0, 0) and not reflect
-                                   and not out_box and residual is None and (P, Q) == (H, W)
-                                   and conv_ksplit(N * P * Q, Og, R * S * Cg_x, G) == 1):
-            at.materialize()
-            at = None
         wk = _prep_weight(weight, G, Cg_x, mode=0)
         if out_box:  # write-into-slice: the epilogue stores into a channel slice of a concat buffer
             y = out_box[0]
@@ -440,7 +423,7 @@ class _ConvFn(torch.autograd.Function):
         # residual: y = conv + b + residual in the store epilogue (same NHWC layout as y)
         ks = 1 if reflect else conv_ksplit(N * P * Q, Og, R * S * Cg_x, G)
         conv_fwd_raw(x, wk, y, b, stats, N, H, W, Cg_x, ldx, G, Og, P, Q, R, S, stride, padding, dilation,
-                     act=act, slope=slope, reflect=reflect, res=residual, ksplit=ks, at=at)
+                     act=act, slope=slope, reflect=reflect, res=residual, ksplit=ks)
         ctx.has_residual = residual is not None
         ctx.rjoin = residual_join  # the residual's gradient (= dy) is stashed there for its other consumer
         ctx.save_for_backward(x, weight, y if act else None)
@@ -472,12 +455,6 @@ class _ConvFn(torch.autograd.Function):
                     g = g.materialize()
                 return (g, None, None) + (None,) * 16
             return (None,) * 19
-        at = defer.take_grad(dy)  # dy = a deferred BN-backward apply (ops.defer): fold or run it first
-        if at is not None and (act or ctx.reflect or not ctx.needs_input_grad[0] or G != 1
-                               or not defer.fusable_1x1(dy.shape[1], ld_of(dy), *weight.shape[2:], stride, padding,
-                                                        dilation, G)):
-            at.materialize()
-            at = None
         dy = grad_nhwc(dy)
         if act:  # y and dy may be channel-slice views of concat buffers: strided rows kernel
             dy = act_grad(dy, y, act, slope)
@@ -489,7 +466,7 @@ class _ConvFn(torch.autograd.Function):
                 dx = _reflect_dgrad(dy, weight, x, Cg_x, G, stride, padding, dilation)
             else:
                 dx = _dgrad(dy, weight, x.shape, Cg_x, G, stride, padding, dilation, x.device, accum=accum,
-                            bnref=ctx.bnref, at=at)
+                            bnref=ctx.bnref)
             if dx.shape[1] != x.shape[1]:
                 dx = dx[:, : x.shape[1]]
             if join is not None and role == "producer":
@@ -643,9 +620,6 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=
     concat, ops.concat.slice_cat); native path only.
     ``residual``: y = conv(x) + bias + residual, the add fused into the store epilogue (no
     activation / statistics; Hourglass bottleneck output, R/Hourglass/tensorflow/hourglass104.py:62-67)."""
-    if defer.pending(x) is not None and not (native(x) and not (shuffle and shuffle > 1) and residual is None
-                                             and groups == 1 and pad_mode == "zeros" and out is None):
-        defer.resolve(x)  # only the dense _ConvFn path folds a pending BN apply (ops.defer)
     if shuffle and shuffle > 1:
         if native(x) and _gconv_ok(x, weight, bias, stride, padding, dilation, groups, act, join=join, out=out,
                                    residual=residual, pad_mode=pad_mode):
