@@ -14,6 +14,9 @@
 //     std) is gone.
 // Backward uses the same shard layout for (sum dz, sum dz*xhat).
 #include <cstdlib>
+#include <stdexcept>
+#include <unordered_map>
+#include <vector>
 
 #include "common.h"
 #include "kernels.h"
@@ -116,7 +119,7 @@ struct SlabTile {
 // shard atomics with consecutive lanes on consecutive channels (256-B coalesced atomic rows;
 // lane-strided atomics run ~8x slower, MI355X_MICROARCH.md "Global float atomics")
 template <int VEC>
-DV_DEVICE void slab_commit(const SlabTile& t, float* s, float* q, float* __restrict__ acc, int C) {
+DV_DEVICE void slab_commit(const SlabTile& t, float* s, float* q, float* __restrict__ acc, int C, float* det) {
   __shared__ float sh[2][NT * VEC];
   const int tid = threadIdx.x;
 #pragma unroll
@@ -124,7 +127,7 @@ DV_DEVICE void slab_commit(const SlabTile& t, float* s, float* q, float* __restr
   __syncthreads();
   const int sw = t.tpr * VEC;  // slab width (channels); sh is [row lane][slab channel]
   const int c0 = blockIdx.y * sw;
-  float* a = acc + (int64_t)(blockIdx.x % SHARDS) * 2 * C;
+  float* a = stat_row(acc, det, blockIdx.x, C);
   for (int ch = tid; ch < sw; ch += NT) {
     if (c0 + ch < C) {
       float ss = 0.f, qq = 0.f;
@@ -137,7 +140,7 @@ DV_DEVICE void slab_commit(const SlabTile& t, float* s, float* q, float* __restr
 
 template <int VEC>
 __global__ __launch_bounds__(NT) void bn_stats_kernel(const u16* __restrict__ x, int64_t rows, int C,
-                                                        float* __restrict__ acc) {
+                                                        float* __restrict__ acc, float* __restrict__ det) {
   SlabTile t(C, VEC, rows);
   float s[VEC], q[VEC], kq[VEC];
 #pragma unroll
@@ -153,7 +156,7 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(const u16* __restrict__ x,
       for (int i = 0; i < VEC; ++i) { const float d = v[i] - kq[i]; s[i] += d; q[i] = fmaf(d, d, q[i]); }
     }
   }
-  slab_commit<VEC>(t, s, q, acc, C);
+  slab_commit<VEC>(t, s, q, acc, C, det);
 }
 
 // Fold the SHARDS partial (a, b) pairs of channel blockIdx.x*64 + (tid & 63) and re-zero them
@@ -319,7 +322,8 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(const u16* __restrict
                                                              const u16* __restrict__ x, int64_t rows, int C,
                                                              const float* __restrict__ mean, const float* __restrict__ invstd,
                                                              const float* __restrict__ mscale, const float* __restrict__ mshift,
-                                                             int act, float slope, float* __restrict__ acc) {
+                                                             int act, float slope, float* __restrict__ acc,
+                                                             float* __restrict__ det) {
   SlabTile t(C, VEC, rows);
   const int g = t.g;
   float s[VEC], q[VEC], mu[VEC], is[VEC], ms[VEC], mh[VEC];
@@ -350,7 +354,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(const u16* __restrict
       }
     }
   }
-  slab_commit<VEC>(t, s, q, acc, C);
+  slab_commit<VEC>(t, s, q, acc, C, det);
 }
 
 // fold backward shards (and re-zero them): dbeta = sum dz, dgamma = sum dz*xhat (written, or
@@ -539,6 +543,90 @@ inline int64_t apply_rows_per_block(int64_t rows, int C, int v) {
 }
 }  // namespace
 
+// ---- deterministic mode (kernels.h DetStats) ----
+// Per-stream, zero-kept fp32 scratch for the per-block statistics rows of one producer launch.
+// Grow-only like dv_slab_workspace: a captured graph keeps the pointer it recorded, so a buffer
+// is never freed once handed out; it cannot grow while the stream is being captured.
+namespace {
+struct DetWs {
+  float* ptr = nullptr;
+  size_t elems = 0;
+};
+std::unordered_map<hipStream_t, DetWs> g_det_ws;
+std::vector<float*> g_det_retired;
+
+// slab rows [blocks][width] -> the 64 shard rows of acc (row stride `stride`): shard g gets the
+// in-order sum of rows [g*rows/64, (g+1)*rows/64) (4 partial chains over r mod 4, combined in
+// fixed order), then those slab rows are zeroed again. One atomic per (shard, column): at most
+// two producers on concurrent streams meet in a shard, 0 + a + b == 0 + b + a.
+__global__ __launch_bounds__(256) void det_fold_kernel(float* __restrict__ slab, int64_t rows, int64_t width,
+                                                      float* __restrict__ acc, int64_t stride) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= width) return;
+  const int g = blockIdx.y;
+  const int64_t r0 = rows * g / SHARDS, r1 = rows * (g + 1) / SHARDS;
+  float p0 = 0.f, p1 = 0.f, p2 = 0.f, p3 = 0.f;
+  int64_t r = r0;
+  for (; r + 3 < r1; r += 4) {
+    float* a = slab + r * width + j;
+    p0 += a[0]; p1 += a[width]; p2 += a[2 * width]; p3 += a[3 * width];
+    a[0] = 0.f; a[width] = 0.f; a[2 * width] = 0.f; a[3 * width] = 0.f;
+  }
+  for (; r < r1; ++r) { float* a = slab + r * width + j; p0 += a[0]; a[0] = 0.f; }
+  const float t = (p0 + p1) + (p2 + p3);
+  if (r1 > r0) atomicAdd(acc + (int64_t)g * stride + j, t);
+}
+}  // namespace
+
+float* dv_det_workspace(size_t elems, hipStream_t st) {
+  DetWs& w = g_det_ws[st];
+  if (elems > w.elems) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+      throw std::runtime_error("deterministic mode: statistics scratch must grow during a stream capture "
+                               "(run an eager warm-up step with the same shapes first)");
+    const size_t want = elems + elems / 2;
+    float* fresh = nullptr;
+    if (hipMalloc(&fresh, want * sizeof(float)) != hipSuccess)
+      throw std::runtime_error("deterministic mode: out of memory for the statistics scratch");
+    if (hipMemsetAsync(fresh, 0, want * sizeof(float), st) != hipSuccess)
+      throw std::runtime_error("deterministic mode: scratch memset failed");
+    if (w.ptr) g_det_retired.push_back(w.ptr);
+    w.ptr = fresh;
+    w.elems = want;
+  }
+  return w.ptr;
+}
+
+// dst[j] += sum over the slab rows of column j: one block per column, a fixed thread <- row
+// assignment and a fixed tree (reproducible bits); the slab is zeroed again
+__global__ __launch_bounds__(256) void det_sum_kernel(float* __restrict__ slab, int64_t rows, int64_t width,
+                                                     float* __restrict__ dst) {
+  __shared__ float sh[256];
+  const int64_t j = blockIdx.x;
+  float v = 0.f;
+  for (int64_t r = threadIdx.x; r < rows; r += 256) {
+    v += slab[r * width + j];
+    slab[r * width + j] = 0.f;
+  }
+  sh[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) dst[j] += sh[0];
+}
+
+void dv_det_sum(float* slab, int64_t rows, int64_t width, float* dst, hipStream_t st) {
+  det_sum_kernel<<<(unsigned)width, 256, 0, st>>>(slab, rows, width, dst);
+}
+
+void dv_det_fold(float* slab, int64_t rows, int64_t width, float* acc, int64_t stride, hipStream_t st) {
+  const dim3 grid((unsigned)((width + 255) / 256), SHARDS);
+  det_fold_kernel<<<grid, 256, 0, st>>>(slab, rows, width, acc, stride);
+}
+
 #define DISPATCH_VEC(C, KERNEL, ...)                                              \
   switch (vec_for(C)) {                                                          \
     case 8: KERNEL<8> __VA_ARGS__; break;                                          \
@@ -559,7 +647,9 @@ void dv_bn_apply_tuning(int blocks, int unroll) {
 
 void dv_bn_stats(const void* x, int64_t rows, int C, float* acc, hipStream_t st) {
   const dim3 g = reduce_grid(rows, C);
-  DISPATCH_VEC(C, bn_stats_kernel, <<<g, NT, 0, st>>>((const u16*)x, rows, C, acc))
+  DetStats d(g.x, C, st);
+  DISPATCH_VEC(C, bn_stats_kernel, <<<g, NT, 0, st>>>((const u16*)x, rows, C, acc, d.slab))
+  d.fold(acc);
 }
 
 // Per-channel sum of an NHWC tensor (conv / Linear bias gradient): the statistics reduction into
@@ -641,12 +731,12 @@ void dv_bn_apply(const void* x, const void* res, void* out, int64_t n, int C, co
 template <int MM>
 static void bwd_reduce_launch(dim3 g, const void* dout, const void* out, const void* x, int64_t rows, int C, const float* mean,
                               const float* invstd, const float* mscale, const float* mshift, int act, float slope, float* acc,
-                              hipStream_t st) {
+                              float* det, hipStream_t st) {
   switch (vec_for(C)) {
-    case 8: bn_bwd_reduce_kernel<8, MM><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, rows, C, mean, invstd, mscale, mshift, act, slope, acc); break;
-    case 4: bn_bwd_reduce_kernel<4, MM><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, rows, C, mean, invstd, mscale, mshift, act, slope, acc); break;
-    case 2: bn_bwd_reduce_kernel<2, MM><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, rows, C, mean, invstd, mscale, mshift, act, slope, acc); break;
-    default: bn_bwd_reduce_kernel<1, MM><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, rows, C, mean, invstd, mscale, mshift, act, slope, acc); break;
+    case 8: bn_bwd_reduce_kernel<8, MM><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, rows, C, mean, invstd, mscale, mshift, act, slope, acc, det); break;
+    case 4: bn_bwd_reduce_kernel<4, MM><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, rows, C, mean, invstd, mscale, mshift, act, slope, acc, det); break;
+    case 2: bn_bwd_reduce_kernel<2, MM><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, rows, C, mean, invstd, mscale, mshift, act, slope, acc, det); break;
+    default: bn_bwd_reduce_kernel<1, MM><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, rows, C, mean, invstd, mscale, mshift, act, slope, acc, det); break;
   }
 }
 
@@ -654,23 +744,26 @@ void dv_bn_bwd_reduce(const void* dout, const void* out, const void* x, int64_t 
                       const float* invstd, const float* mscale, const float* mshift, int act, float slope, float* acc,
                       int mask_bits, hipStream_t st) {
   const dim3 g = reduce_grid(rows, C);
+  DetStats d(g.x, C, st);
+  float* det = d.slab;
   if (act && mask_bits && vec_for(C) == 8) {
     if (g_reduce_unroll == 4)
       bn_bwd_reduce_kernel<8, MM_BITS, 4><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, rows, C, mean,
-                                                              invstd, mscale, mshift, act, slope, acc);
+                                                              invstd, mscale, mshift, act, slope, acc, det);
     else
       bn_bwd_reduce_kernel<8, MM_BITS><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, rows, C, mean,
-                                                           invstd, mscale, mshift, act, slope, acc);
-    return;
-  }
-  if (act && !out && vec_for(C) == 8 && g_reduce_unroll == 4) {
+                                                           invstd, mscale, mshift, act, slope, acc, det);
+  } else if (act && !out && vec_for(C) == 8 && g_reduce_unroll == 4) {
     bn_bwd_reduce_kernel<8, MM_X, 4><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, rows, C, mean,
-                                                         invstd, mscale, mshift, act, slope, acc);
-    return;
+                                                         invstd, mscale, mshift, act, slope, acc, det);
+  } else if (!act) {
+    bwd_reduce_launch<MM_NONE>(g, dout, out, x, rows, C, mean, invstd, mscale, mshift, act, slope, acc, det, st);
+  } else if (out) {
+    bwd_reduce_launch<MM_OUT>(g, dout, out, x, rows, C, mean, invstd, mscale, mshift, act, slope, acc, det, st);
+  } else {
+    bwd_reduce_launch<MM_X>(g, dout, out, x, rows, C, mean, invstd, mscale, mshift, act, slope, acc, det, st);
   }
-  if (!act) bwd_reduce_launch<MM_NONE>(g, dout, out, x, rows, C, mean, invstd, mscale, mshift, act, slope, acc, st);
-  else if (out) bwd_reduce_launch<MM_OUT>(g, dout, out, x, rows, C, mean, invstd, mscale, mshift, act, slope, acc, st);
-  else bwd_reduce_launch<MM_X>(g, dout, out, x, rows, C, mean, invstd, mscale, mshift, act, slope, acc, st);
+  d.fold(acc);
 }
 
 void dv_bn_bwd_finalize(float* acc, int C, double count, const float* gamma, const float* mean, const float* invstd,

@@ -104,3 +104,9 @@ static __device__ __attribute__((aligned(16))) char dv_zero_page[256];
 // Per-channel shift row of a forward BatchNorm statistics accumulator of `ncols` channels
 // (layout: kernels.h DV_STAT_ROWS; 64 = DV_STAT_SHARDS, asserted there).
 DV_DEVICE float* stat_shift(float* acc, int64_t ncols) { return acc + (int64_t)2 * 64 * ncols; }
+// The [2][ncols] partial-sum row a block with reduction index `blk` adds into: shard blk % 64 of
+// the accumulator, or -- deterministic mode (kernels.h DetStats) -- its own row of the launch's
+// zeroed slab (one contribution per element, folded in a fixed order afterwards).
+DV_DEVICE float* stat_row(float* acc, float* det, int64_t blk, int64_t ncols) {
+  return det ? det + blk * 2 * ncols : acc + (blk % 64) * 2 * ncols;
+}

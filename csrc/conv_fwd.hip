@@ -327,7 +327,7 @@ constexpr int FR_ROWS = 64;  // rows per block on large grids; small ones shrink
 __global__ __launch_bounds__(256) void splitk_finalize_kernel(const float* __restrict__ ypart, int ksplit, int M, int N,
                                                               const float* __restrict__ bias, int act, float slope,
                                                               const u16* __restrict__ res, float* __restrict__ stats,
-                                                              u16* __restrict__ y, int ldy, int fr) {
+                                                              u16* __restrict__ y, int ldy, int fr, float* __restrict__ det) {
   __shared__ float red[2][4][256];
   const int lc = threadIdx.x & 63, lr = threadIdx.x >> 6;
   const int n = blockIdx.x * 256 + lc * 4;
@@ -371,7 +371,7 @@ __global__ __launch_bounds__(256) void splitk_finalize_kernel(const float* __res
     float t1 = 0.f, t2 = 0.f;
 #pragma unroll
     for (int q = 0; q < 4; ++q) { t1 += red[0][q][threadIdx.x]; t2 += red[1][q][threadIdx.x]; }
-    float* sh = stats + (int64_t)(blockIdx.y % DV_STAT_SHARDS) * 2 * N;
+    float* sh = stat_row(stats, det, blockIdx.y, N);
     atomicAdd(sh + c, t1);
     atomicAdd(sh + N + c, t2);
   }
@@ -450,6 +450,18 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
   if (!p.bnmode) p.bnx2 = nullptr;
   p.div_pq = make_fastdiv((uint32_t)(a.P * a.Q));
   p.div_q = make_fastdiv((uint32_t)a.Q);
+  // deterministic statistics (kernels.h DetStats): one slab row per 128-row tile (every tile
+  // shape has >= 128 rows), regions: forward statistics, BN-backward sums, the dual BN's sums
+  const bool want_s = p.stats != nullptr, want_b = p.bnmode != 0;
+  const DetStats det((want_s || want_b) ? (p.M + 127) / 128 : 0, (int64_t)p.G * p.N, st, 3);
+  p.sdet = want_s ? det.region(0) : nullptr;
+  p.bdet = want_b ? det.region(1) : nullptr;
+  p.bdet2 = (want_b && p.bnx2) ? det.region(2) : nullptr;
+  auto det_fold = [&]() {
+    if (p.sdet) det.fold(p.stats, 0);
+    if (p.bdet) det.fold(p.bnacc, 1);
+    if (p.bdet2) det.fold(p.bnacc2, 2);
+  };
   if (a.tgather == 2) {
     p.bnmode = 0;
     // Tap-packed input (stem convs with <= 4 input channels, ops/conv.py _StemConvFn): a padded
@@ -478,11 +490,12 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
         else launch_fwd<128, 128, 32, KM_FAST, false, 2, false, EPI_PLAIN>(p, st);
       }
     }
+    det_fold();
     return bn_status;
   }
   if (p.Cg % 8 != 0 || p.ldx % 8 != 0) return -1;
   // warp-specialised ring (benchmark variants 20: 128x128, 21: 256x64, 22: 256x128, 23: 128x256)
-  if (dv_g_fwd_variant >= 20 && dv_g_fwd_variant <= 23 && !a.tgather && p.Cg % 64 == 0 && p.R <= 16 && p.S <= 16 &&
+  if (dv_g_fwd_variant >= 20 && dv_g_fwd_variant <= 23 && !det.slab && !a.tgather && p.Cg % 64 == 0 && p.R <= 16 && p.S <= 16 &&
       !p.reflect && p.G == 1 && p.identity_map && !p.bias && !p.act && !p.res && !p.bnmode && !p.ypart && !p.zfill &&
       (p.N % 8) == 0 && (p.ldy % 8) == 0) {
     const bool sts = p.stats != nullptr;
@@ -501,6 +514,7 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
   if (a.tgather) dispatch_tile<KM_TGATHER>(p, st);
   else if (p.Cg % 64 == 0 && p.R <= 16 && p.S <= 16 && !p.reflect) dispatch_tile<KM_FAST>(p, st);
   else dispatch_tile<KM_GENERIC>(p, st);
+  det_fold();
   if (p.ypart) {
     // split-K serves small grids (Hourglass 4x4-16x16 maps): 64-row blocks left 8-32 blocks walking
     // up to 16 slabs serially (37 us median); shrink the row block until ~512 blocks
@@ -511,8 +525,10 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
     fr = std::max(fr, (p.M + DV_STAT_SHARDS - 1) / DV_STAT_SHARDS);
     fr = std::max(4, std::min(FR_ROWS, (fr + 3) / 4 * 4));
     const dim3 grid((unsigned)ncb, (unsigned)((p.M + fr - 1) / fr));
+    const DetStats fdet(fin_stats ? grid.y : 0, p.N, st);
     splitk_finalize_kernel<<<grid, dim3(256), 0, st>>>(p.ypart, dv_g_last_ksplit, p.M, p.N, p.bias, p.act, p.slope,
-                                                       fin_res, fin_stats, p.y, p.ldy, fr);
+                                                       fin_res, fin_stats, p.y, p.ldy, fr, fdet.slab);
+    fdet.fold(fin_stats);
   }
   return bn_status;
 }

@@ -62,6 +62,10 @@ struct FwdParams {
   float* bnacc2;
   int wld, wkr, wks;  // weight row / tap strides (kernels.h ConvFwdArgs w_ld, w_kr, w_ks)
   int ntl;            // epilogue reads of once-used tensors (residual, BN input) with the non-temporal policy
+  // deterministic mode (kernels.h DetStats): per-row-tile slabs of stats / bnacc / bnacc2, or nullptr
+  float* sdet;
+  float* bdet;
+  float* bdet2;
 };
 
 }  // namespace dvconv
@@ -626,7 +630,7 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
             t2 += sh[(w * 64 + (nl & 63)) * 2 + 1];
           }
           const int64_t ncols = (int64_t)p.G * p.N;
-          float* a = p.stats + (int64_t)(tm % DV_STAT_SHARDS) * 2 * ncols;
+          float* a = stat_row(p.stats, p.sdet, tm, ncols);
           atomicAdd(a + grp * p.N + n, t1);
           atomicAdd(a + ncols + grp * p.N + n, t2);
         }
@@ -655,7 +659,7 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
 #pragma unroll
         for (int w = 0; w < WM; ++w) { s1 += sh[(w * BN_ + threadIdx.x) * 2]; s2 += sh[(w * BN_ + threadIdx.x) * 2 + 1]; }
         const int64_t ncols = (int64_t)p.G * p.N;
-        float* a = p.stats + (int64_t)(tm % DV_STAT_SHARDS) * 2 * ncols;
+        float* a = stat_row(p.stats, p.sdet, tm, ncols);
         atomicAdd(a + grp * p.N + n, s1);
         atomicAdd(a + ncols + grp * p.N + n, s2);
       }
@@ -708,12 +712,11 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
           s2 += sh[(w * 64 + (nl & 63)) * 3 + 1];
           s3 += sh[(w * 64 + (nl & 63)) * 3 + 2];
         }
-        const int64_t shard = (int64_t)(tm % DV_STAT_SHARDS) * 2 * p.N;
-        float* a = p.bnacc + shard;
+        float* a = stat_row(p.bnacc, p.bdet, tm, p.N);
         atomicAdd(a + n, s1);
         atomicAdd(a + p.N + n, s2);
         if constexpr (dual) {  // the same dz: the second BN's sum dz is s1
-          float* a2 = p.bnacc2 + shard;
+          float* a2 = stat_row(p.bnacc2, p.bdet2, tm, p.N);
           atomicAdd(a2 + n, s1);
           atomicAdd(a2 + p.N + n, s3);
         }

@@ -67,6 +67,7 @@ struct DwBnr {
   float* acc;         // [SHARDS][2][C]
   int mode, act;      // mode 1: no activation, 2: mask recomputed from x
   float slope;
+  float* det = nullptr;  // deterministic mode: per-block slab rows (kernels.h DetStats)
 };
 struct DwBnrLane {  // this thread's 8 channels
   f32x2 ms[4], mh[4], mu[4], s[4], q[4];
@@ -111,7 +112,7 @@ DV_DEVICE void bnr_commit(const DwBnr& b, const DwBnrLane& l, int C, int tpr, in
   }
   __syncthreads();
   const int sw = tpr * 8;
-  float* a = b.acc + (int64_t)(blockIdx.x % DV_STAT_SHARDS) * 2 * C;
+  float* a = stat_row(b.acc, b.det, blockIdx.x, C);
   const int cbase = (int)blockIdx.y * SLAB * 8;
   for (int ch = threadIdx.x; ch < sw; ch += NT) {
     float s1v = 0.f, s2v = 0.f;
@@ -142,7 +143,7 @@ template <int KS, int SW, int QT, bool FLIP, int OCC = 1, bool BNR = false>
 __global__ __launch_bounds__(NT, OCC) void dw_fwd_kernel(const u16* __restrict__ x, const float* __restrict__ w,
                                                       const float* __restrict__ bias, u16* __restrict__ y, DwGeo g,
                                                       int act, float slope, float* __restrict__ stats,
-                                                      int strips_per_block, DwBnr bnr) {
+                                                      int strips_per_block, DwBnr bnr, float* __restrict__ sdet) {
   __shared__ float sh[2][NT * 8];
   DwTile t(g.C);
   DwBnrLane bl;
@@ -243,7 +244,7 @@ __global__ __launch_bounds__(NT, OCC) void dw_fwd_kernel(const u16* __restrict__
     }
     __syncthreads();
     const int sw = t.tpr * 8;  // slab width in channels; sh is [strip lane][slab channel]
-    float* a = stats + (int64_t)(blockIdx.x % DV_STAT_SHARDS) * 2 * g.C;
+    float* a = stat_row(stats, sdet, blockIdx.x, g.C);
     const int cbase = (int)blockIdx.y * SLAB * 8;
     for (int ch = threadIdx.x; ch < sw; ch += NT) {
       float s1v = 0.f, s2v = 0.f;
@@ -653,12 +654,18 @@ void fwd_launch(const void* x, const float* w, const float* bias, void* y, const
   const int64_t spb = per_block(nstrips, rpi, slabs, target);
   const dim3 grid((unsigned)((nstrips + spb - 1) / spb), (unsigned)slabs);
   const DwGeo gs = with_strips(g, (g.Q + QT - 1) / QT, g.P);
-  if (bnr)
+  const DetStats det((bnr || stats) ? grid.x : 0, g.C, st);
+  if (bnr) {
+    DwBnr b = *bnr;
+    b.det = det.slab;
     dw_fwd_kernel<KS, SW, QT, FLIP, OCC, true><<<grid, NT, 0, st>>>((const u16*)x, w, bias, (u16*)y, gs, act, slope,
-                                                                     stats, (int)spb, *bnr);
-  else
+                                                                     stats, (int)spb, b, nullptr);
+    det.fold(bnr->acc);
+  } else {
     dw_fwd_kernel<KS, SW, QT, FLIP, OCC><<<grid, NT, 0, st>>>((const u16*)x, w, bias, (u16*)y, gs, act, slope, stats,
-                                                             (int)spb, DwBnr{});
+                                                             (int)spb, DwBnr{}, det.slab);
+    det.fold(stats);
+  }
 }
 template <int KS, int SW, bool FLIP>
 void fwd_variants(const void* x, const float* w, const float* bias, void* y, const DwGeo& g, int act, float slope,
@@ -676,7 +683,7 @@ void fwd_variants(const void* x, const float* w, const float* bias, void* y, con
   }
   // the whole-plane forward measured no faster on 14x14 and slower on 7x7 outputs than the strip
   // kernel (profiles/dw_bench_r3.txt): benchmark variant 51 only
-  if (g_dw_variant == 51 && plane_fwd<KS, SW, FLIP>(x, w, bias, y, g, act, slope, stats, st)) return;
+  if (g_dw_variant == 51 && !dv_deterministic() && plane_fwd<KS, SW, FLIP>(x, w, bias, y, g, act, slope, stats, st)) return;
   fwd_launch<KS, SW, FLIP, 4, 1>(x, w, bias, y, g, act, slope, stats, 4096, st);
 }
 template <int KS, int SW, int QT, int OCC>
@@ -717,9 +724,13 @@ void dgrad2_launch(const void* dy, const float* w, void* dx, const DwGeo& g, int
   const int64_t spb = per_block(nstrips, rpi, slabs, target);
   const dim3 grid((unsigned)((nstrips + spb - 1) / spb), (unsigned)slabs);
   const DwGeo gs = with_strips(g, (g.W + QT - 1) / QT, g.H);
-  if (bnr)
-    dw_dgrad2_kernel<KS, QT, OCC, true><<<grid, NT, 0, st>>>((const u16*)dy, w, (u16*)dx, gs, (int)spb, *bnr);
-  else
+  if (bnr) {
+    const DetStats det(grid.x, g.C, st);
+    DwBnr b = *bnr;
+    b.det = det.slab;
+    dw_dgrad2_kernel<KS, QT, OCC, true><<<grid, NT, 0, st>>>((const u16*)dy, w, (u16*)dx, gs, (int)spb, b);
+    det.fold(bnr->acc);
+  } else
     dw_dgrad2_kernel<KS, QT, OCC><<<grid, NT, 0, st>>>((const u16*)dy, w, (u16*)dx, gs, (int)spb, DwBnr{});
 }
 template <int KS>

@@ -44,12 +44,17 @@ struct GcParams {
   int M, G, Cg, Og, Kp;
   float* stats;  // shifted BN statistics of y by stored channel position, or nullptr
   FastDiv div_upr, div_kc;  // chunks per row (G*Kp/8), chunks per group (Kp/8)
+  // deterministic mode (kernels.h DetStats): per-block slab rows; the 4 waves then keep separate
+  // LDS statistics rows summed in wave order (LDS float atomics from several waves have no order)
+  float* sdet;
 };
 
-inline __host__ __device__ size_t gc_lds_bytes(int BM, int G, int Kp, int Cout, bool stats) {
+// LDS statistics rows: one shared row, or one per wave in deterministic mode
+inline __host__ __device__ int gc_stat_rows(bool det) { return det ? NT / 64 : 1; }
+inline __host__ __device__ size_t gc_lds_bytes(int BM, int G, int Kp, int Cout, bool stats, bool det = false) {
   // [BM][G*Kp + 8] logical input image | [BM][r8(Cout) + 8] output tile | [Cout] table | stats
-  return (size_t)BM * ((G * Kp + 8) + (r8(Cout) + 8)) * 2 + (size_t)Cout * 2 + (stats ? (size_t)2 * Cout * 4 : 0) + 16 +
-         (size_t)G * Kp * 2;  // + the input position table
+  return (size_t)BM * ((G * Kp + 8) + (r8(Cout) + 8)) * 2 + (size_t)Cout * 2 +
+         (stats ? (size_t)2 * Cout * 4 * gc_stat_rows(det) : 0) + 16 + (size_t)G * Kp * 2;  // + the input position table
 }
 
 template <int BM, int MODE>
@@ -60,8 +65,10 @@ __global__ __launch_bounds__(NT) void gconv_kernel(GcParams p) {
   u16* ys = pk + BM * PP;
   int16_t* tout = reinterpret_cast<int16_t*>(ys + BM * YP);
   float* st = reinterpret_cast<float*>(smem + (((size_t)BM * (PP + YP) * 2 + (size_t)p.Cout * 2 + 15) & ~(size_t)15));
-  int16_t* tin = reinterpret_cast<int16_t*>(st + (p.stats ? 2 * p.Cout : 0));  // [G*Kp] (GATHER)
+  const int srows = gc_stat_rows(p.sdet != nullptr);
+  int16_t* tin = reinterpret_cast<int16_t*>(st + (p.stats ? 2 * p.Cout * srows : 0));  // [G*Kp] (GATHER)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  float* stw = st + (srows > 1 ? wid * 2 * p.Cout : 0);  // this wave's LDS statistics row
   const int m0 = blockIdx.x * BM;
 
   for (int c = tid; c < p.Cout; c += NT) tout[c] = p.tout ? p.tout[c] : (int16_t)c;
@@ -73,7 +80,7 @@ __global__ __launch_bounds__(NT) void gconv_kernel(GcParams p) {
     __syncthreads();
   }
   if (p.stats)
-    for (int i = tid; i < 2 * p.Cout; i += NT) st[i] = 0.f;
+    for (int i = tid; i < 2 * p.Cout * srows; i += NT) st[i] = 0.f;
   // 1. logical zero-padded input image, one 8-channel piece per step. The loads of 8 pieces are
   // issued before any LDS write and never sit behind a branch (hipcc waits for a load right at
   // a branch around it): padding / out-of-range pieces read the zero page instead.
@@ -179,8 +186,8 @@ __global__ __launch_bounds__(NT) void gconv_kernel(GcParams p) {
           const float d = (jv && mv) ? v - shift[pos] : 0.f;
           const float s1 = row16_sum(d), s2 = row16_sum(d * d);
           if ((lane & 15) == 0 && jv) {
-            atomicAdd(st + pos, s1);
-            atomicAdd(st + p.Cout + pos, s2);
+            atomicAdd(stw + pos, s1);
+            atomicAdd(stw + p.Cout + pos, s2);
           }
         }
       }
@@ -188,10 +195,12 @@ __global__ __launch_bounds__(NT) void gconv_kernel(GcParams p) {
   }
   __syncthreads();
   if (p.stats) {
-    float* a = p.stats + (int64_t)(blockIdx.x % DV_STAT_SHARDS) * 2 * p.Cout;
+    float* a = stat_row(p.stats, p.sdet, blockIdx.x, p.Cout);
     for (int c = tid; c < p.Cout; c += NT) {
-      atomicAdd(a + c, st[c]);
-      atomicAdd(a + p.Cout + c, st[p.Cout + c]);
+      float s1 = st[c], s2 = st[p.Cout + c];
+      for (int w = 1; w < srows; ++w) { s1 += st[w * 2 * p.Cout + c]; s2 += st[w * 2 * p.Cout + p.Cout + c]; }
+      atomicAdd(a + c, s1);
+      atomicAdd(a + p.Cout + c, s2);
     }
   }
   // 4. output rows: 16-B / 8-B / 2-B pieces by alignment
@@ -226,6 +235,7 @@ struct GwParams {
   int nkf, nfrag;    // fragments: ceil(Og/16) x ceil(Cg/16), row-major over (jf, kf)
   int fchunks;       // blockIdx.y = g * fchunks + fragment chunk (4 * FPW fragments)
   int tiles_per_block;
+  float* slab;       // deterministic mode: block-row x's partial dW at slab + x * G*Og*Cg (plain stores)
 };
 
 // 16-byte-chunk XOR key of pixel row k (conv_wgrad.hip mn_swz): 8 keys for rows >= 256 B,
@@ -355,7 +365,11 @@ __global__ __launch_bounds__(NT) void gconv_wgrad_kernel(GwParams p) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int j = jf * 16 + (lane >> 4) * 4 + r;
-      if (j < p.Og && k < p.Cg) atomicAdd(p.dw + (int64_t)(g * p.Og + j) * p.Cg + k, acc[f][r]);
+      if (j < p.Og && k < p.Cg) {
+        const int64_t o = (int64_t)(g * p.Og + j) * p.Cg + k;
+        if (p.slab) p.slab[(int64_t)blockIdx.x * p.G * p.Og * p.Cg + o] = acc[f][r];
+        else atomicAdd(p.dw + o, acc[f][r]);
+      }
     }
   }
 }
@@ -367,13 +381,15 @@ int dv_gconv(const void* x, int ldx, int Cin, const int16_t* tin, const void* w,
   if (Cin != G * Cg || Cout != G * Og || Kp % 32 || Kp < Cg || ldx % 8 || ldy % 4 || (uintptr_t)x % 16 ||
       (uintptr_t)w % 16 || Orows < Og || Cout > 32767 || Cin > 32767)
     return -1;
+  const bool detm = dv_deterministic() && stats;
   int BM = 64;  // two blocks per CU where the tiles allow
-  while (BM > 16 && gc_lds_bytes(BM, G, Kp, Cout, stats) > 80 * 1024) BM /= 2;
-  const size_t lds = gc_lds_bytes(BM, G, Kp, Cout, stats);
+  while (BM > 16 && gc_lds_bytes(BM, G, Kp, Cout, stats, detm) > 80 * 1024) BM /= 2;
+  const size_t lds = gc_lds_bytes(BM, G, Kp, Cout, stats, detm);
   if (lds > 160 * 1024) return -1;
-  GcParams p{(const u16*)x, ldx, Cin, tin, (const u16*)w, Orows, (u16*)y, ldy, Cout, tout, M, G, Cg, Og, Kp, stats,
-             make_fastdiv((uint32_t)(G * Kp / 8)), make_fastdiv((uint32_t)(Kp / 8))};
   const unsigned grid = (unsigned)((M + BM - 1) / BM);
+  const DetStats det(detm ? grid : 0, Cout, st);
+  GcParams p{(const u16*)x, ldx, Cin, tin, (const u16*)w, Orows, (u16*)y, ldy, Cout, tout, M, G, Cg, Og, Kp, stats,
+             make_fastdiv((uint32_t)(G * Kp / 8)), make_fastdiv((uint32_t)(Kp / 8)), det.slab};
   const int mode = tin ? GW_GATHER : (Cg % 8 == 0) ? GW_V16 : (Cg % 2 == 0) ? GW_PAIR : GW_GATHER;
   static bool attr[9] = {};
 #define GC_LAUNCH(B, MD, I)                                                                                         \
@@ -393,6 +409,7 @@ int dv_gconv(const void* x, int ldx, int Cin, const int16_t* tin, const void* w,
   else { GC_BM(GW_GATHER, 6) }
 #undef GC_BM
 #undef GC_LAUNCH
+  det.fold(stats);
   return 0;
 }
 
@@ -429,9 +446,13 @@ int dv_gconv_wgrad(const void* x, int ldx, const int16_t* tin, const void* dy, i
   p.tiles_per_block = (ntiles + rchunks - 1) / rchunks;
   const int gx = (ntiles + p.tiles_per_block - 1) / p.tiles_per_block;
   const dim3 grid((unsigned)gx, (unsigned)cols);
+  const int64_t nout = (int64_t)G * Og * Cg;
+  p.slab = dv_deterministic() ? dv_slab_workspace((size_t)gx * nout, st) : nullptr;
+  if (dv_deterministic() && !p.slab) return -1;
 #define GW_CASE(A, B, P)                                                                                          \
   if (my == A && mx == B) {                                                                                       \
     gconv_wgrad_kernel<A, B, P><<<grid, NT, lds, st>>>(p);                                                        \
+    if (p.slab) dv_slab_reduce(p.slab, dw, nout, gx, 1, st);                                                      \
     return 0;                                                                                                     \
   }
   GW_CASE(GW_V16, GW_V16, 8) GW_CASE(GW_V16, GW_PAIR, 8) GW_CASE(GW_PAIR, GW_V16, 8) GW_CASE(GW_PAIR, GW_PAIR, 8)

@@ -102,6 +102,28 @@ int dv_deterministic();
 // shared fp32 slab workspace (grown on demand) and the fixed-order slab sum
 // dst[i] (+)= sum_{s < splits} ws[s * n + i] used by every deterministic weight gradient
 float* dv_slab_workspace(size_t elems, hipStream_t st);
+// Deterministic BatchNorm statistics: a statistics-producing launch with `rows` reduction blocks
+// writes each block's [2][ncols] partial row into its own row of a zeroed per-stream slab
+// (common.h stat_row) instead of atomics into shard blk % 64; fold() then adds the slab rows, in
+// a fixed order, into the accumulator's 64 shards (and re-zeroes the slab). Off (slab == nullptr,
+// fold() a no-op) unless dv_deterministic().
+float* dv_det_workspace(size_t elems, hipStream_t st);
+void dv_det_fold(float* slab, int64_t rows, int64_t width, float* acc, int64_t stride, hipStream_t st);
+// scalar-ish sums (loss totals): dst[j] += sum_r slab[r][j] in a fixed order, slab re-zeroed
+void dv_det_sum(float* slab, int64_t rows, int64_t width, float* dst, hipStream_t st);
+struct DetStats {
+  float* slab = nullptr;
+  int64_t rows = 0, width = 0;
+  hipStream_t st = nullptr;
+  DetStats(int64_t rows_, int64_t ncols, hipStream_t st_, int regions = 1) : rows(rows_), width(2 * ncols), st(st_) {
+    if (dv_deterministic() && rows > 0) slab = dv_det_workspace((size_t)(rows * width * regions), st);
+  }
+  float* region(int i) const { return slab ? slab + (int64_t)i * rows * width : nullptr; }
+  // shards of acc are [64][2][ncols]: row stride = width
+  void fold(float* acc, int i = 0) const {
+    if (slab && acc) dv_det_fold(region(i), rows, width, acc, width, st);
+  }
+};
 void dv_slab_reduce(const float* ws, float* dst, int64_t n, int splits, int accumulate, hipStream_t st);
 int dv_conv_stats_tiles(int Nb, int P, int Q);
 

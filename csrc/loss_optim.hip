@@ -125,12 +125,13 @@ __global__ __launch_bounds__(NT) void rmsprop_kernel(float* __restrict__ p, cons
 }
 
 // sum of squares (grad-norm / non-finite detection): block partials -> atomic
-__global__ __launch_bounds__(NT) void sumsq_kernel(const float* __restrict__ x, int64_t n, float* __restrict__ out) {
+__global__ __launch_bounds__(NT) void sumsq_kernel(const float* __restrict__ x, int64_t n, float* __restrict__ out,
+                                                   float* __restrict__ det) {
   __shared__ float sh[NT / 64];
   float s = 0.f;
   for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) { const float v = x[i]; s += v * v; }
   s = block_sum<NT>(s, sh);
-  if (threadIdx.x == 0) atomicAdd(out, s);
+  if (threadIdx.x == 0) atomicAdd(det ? det + blockIdx.x : out, s);  // det: this block's slab row
 }
 
 // Device-side non-finite guard (graph-captured steps: no host sync). guard = [flag, skipped total,
@@ -227,5 +228,8 @@ void dv_nonfinite_check(const float* g, int64_t n, float* guard, hipStream_t st)
 }
 void dv_nonfinite_tally(float* guard, hipStream_t st) { nonfinite_tally_kernel<<<1, 1, 0, st>>>(guard); }
 void dv_sumsq(const float* x, int64_t n, float* out, hipStream_t st) {
-  sumsq_kernel<<<std::min(grid_for(n), 1024), NT, 0, st>>>(x, n, out);
+  const int grid = std::min(grid_for(n), 1024);
+  float* det = dv_deterministic() ? dv_det_workspace((size_t)grid, st) : nullptr;
+  sumsq_kernel<<<grid, NT, 0, st>>>(x, n, out, det);
+  if (det) dv_det_sum(det, grid, 1, out, st);
 }

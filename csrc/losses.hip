@@ -67,7 +67,7 @@ __global__ __launch_bounds__(NT) void pw_loss_kernel(int kind, const TP* __restr
                                                      float tval, const float* __restrict__ wt, int64_t rows, int C,
                                                      int ldp, int ldt, float a, float b, float* __restrict__ sums,
                                                      TP* __restrict__ grad, const float* __restrict__ gscale,
-                                                     float hscale) {
+                                                     float hscale, float* __restrict__ det) {
   __shared__ float sh[NT / 64];
   const int ldg = ldp;
   const int64_t total = rows * ldg;
@@ -95,8 +95,9 @@ __global__ __launch_bounds__(NT) void pw_loss_kernel(int kind, const TP* __restr
     ls = block_sum<NT>(ls, sh);
     if (kind == K_FOCAL) ps = block_sum<NT>(ps, sh);
     if (threadIdx.x == 0) {
-      atomicAdd(sums, ls);
-      if (kind == K_FOCAL) atomicAdd(sums + 1, ps);
+      float* d = det ? det + blockIdx.x * 2 : sums;  // deterministic mode: this block's own slab row
+      atomicAdd(d, ls);
+      if (kind == K_FOCAL) atomicAdd(d + 1, ps);
     }
   }
 }
@@ -106,8 +107,10 @@ void launch(int kind, const void* pred, const void* tgt, float tval, const float
             int ldt, float a, float b, float* sums, void* grad, const float* gscale, float hscale, hipStream_t st) {
   const int64_t total = rows * ldp;
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((total + NT - 1) / NT, 2048));
+  float* det = (sums && dv_deterministic()) ? dv_det_workspace((size_t)blocks * 2, st) : nullptr;
   pw_loss_kernel<TP, TT><<<blocks, NT, 0, st>>>(kind, (const TP*)pred, (const TT*)tgt, tval, wt, rows, C, ldp, ldt, a,
-                                                b, sums, (TP*)grad, gscale, hscale);
+                                                b, sums, (TP*)grad, gscale, hscale, det);
+  if (det) dv_det_sum(det, blocks, kind == K_FOCAL ? 2 : 1, sums, st);
 }
 }  // namespace
 

@@ -421,7 +421,7 @@ __global__ __launch_bounds__(NT) void bn_act_maxpool_bwd_kernel(const u16* __res
                                                                 FastDiv div_cg, FastDiv div_w, FastDiv div_h, int64_t total,
                                                                 const float* __restrict__ prm,
                                                                 const float* __restrict__ coef, int act, float slope,
-                                                                float* __restrict__ acc) {
+                                                                float* __restrict__ acc, float* __restrict__ det) {
   using Wn = PoolWin<KH, KW, SH, SW>;
   const int kh = Wn::kh(g), kw = Wn::kw(g), sh = Wn::sh(g), sw = Wn::sw(g);
   const int cg = g.C / 8;
@@ -491,7 +491,7 @@ __global__ __launch_bounds__(NT) void bn_act_maxpool_bwd_kernel(const u16* __res
   for (int i = 0; i < 8; ++i) { sh_[0][threadIdx.x * 8 + i] = s1[i]; sh_[1][threadIdx.x * 8 + i] = s2[i]; }
   __syncthreads();
   const int lanes = NT / cg;
-  float* a = acc + (int64_t)(blockIdx.x % DV_STAT_SHARDS) * 2 * g.C;
+  float* a = stat_row(acc, det, blockIdx.x, g.C);
   for (int ch = threadIdx.x; ch < g.C; ch += NT) {
     const int gi = ch / 8, e = ch % 8;
     float t1 = 0.f, t2 = 0.f;
@@ -522,7 +522,7 @@ __global__ __launch_bounds__(NT) void bn_act_maxpool_bwd_s2_kernel(const u16* __
                                                                    PoolGeo g, FastDiv div_cg, FastDiv div_q, FastDiv div_p,
                                                                    int64_t total, const float* __restrict__ prm,
                                                                    const float* __restrict__ coef, float slope,
-                                                                   float* __restrict__ acc) {
+                                                                   float* __restrict__ acc, float* __restrict__ det) {
   const int cg = g.C / 8;
   const uint32_t t0 = blockIdx.x * NT + threadIdx.x;
   const int lc = (int)(t0 - fdiv(t0, div_cg) * div_cg.d), c = lc * 8;
@@ -601,7 +601,7 @@ __global__ __launch_bounds__(NT) void bn_act_maxpool_bwd_s2_kernel(const u16* __
   for (int i = 0; i < 8; ++i) { sh_[0][threadIdx.x * 8 + i] = s1[i]; sh_[1][threadIdx.x * 8 + i] = s2[i] * k1[i]; }
   __syncthreads();
   const int lanes = NT / cg;
-  float* a = acc + (int64_t)(blockIdx.x % DV_STAT_SHARDS) * 2 * g.C;
+  float* a = stat_row(acc, det, blockIdx.x, g.C);
   for (int ch = threadIdx.x; ch < g.C; ch += NT) {
     const int gi = ch / 8, e = ch % 8;
     float t1 = 0.f, t2 = 0.f;
@@ -666,7 +666,8 @@ int dv_bn_act_maxpool_bwd(const void* dy, const uint8_t* idx, const void* x, voi
     const int64_t blocks = (int64_t)N * P * Q * (C / 8);
     const FastDiv dc = make_fastdiv(C / 8), dq = make_fastdiv(Q), dp = make_fastdiv(P);
     const int grid = (int)std::min<int64_t>((blocks + NT - 1) / NT, apply ? 256 * 32 : 2048);
-#define S2_ARGS <<<grid, NT, 0, st>>>((const u16*)dy, idx, (const u16*)x, (u16*)dx, g, dc, dq, dp, blocks, prm, coef, slope, acc)
+    const DetStats det(apply ? 0 : grid, C, st);
+#define S2_ARGS <<<grid, NT, 0, st>>>((const u16*)dy, idx, (const u16*)x, (u16*)dx, g, dc, dq, dp, blocks, prm, coef, slope, acc, det.slab)
 #define S2_ACT(A) do { if (act == 0) bn_act_maxpool_bwd_s2_kernel<A, 0> S2_ARGS; \
                        else if (act == 1) bn_act_maxpool_bwd_s2_kernel<A, 1> S2_ARGS; \
                        else bn_act_maxpool_bwd_s2_kernel<A, 2> S2_ARGS; } while (0)
@@ -674,12 +675,14 @@ int dv_bn_act_maxpool_bwd(const void* dy, const uint8_t* idx, const void* x, voi
     else S2_ACT(false);
 #undef S2_ACT
 #undef S2_ARGS
+    det.fold(acc);
     return 0;
   }
   const FastDiv dc = make_fastdiv(C / 8), dw = make_fastdiv(W), dh = make_fastdiv(H);
   // the reduction's atomics are one row per block: a bounded grid (~2k blocks) keeps them cheap
   const int grid = (int)std::min<int64_t>((total + NT - 1) / NT, apply ? 256 * 32 : 2048);
-#define BWD_ARGS <<<grid, NT, 0, st>>>((const u16*)dy, idx, (const u16*)x, (u16*)dx, g, dc, dw, dh, total, prm, coef, act, slope, acc)
+  const DetStats det(apply ? 0 : grid, C, st);
+#define BWD_ARGS <<<grid, NT, 0, st>>>((const u16*)dy, idx, (const u16*)x, (u16*)dx, g, dc, dw, dh, total, prm, coef, act, slope, acc, det.slab)
   const bool stem = stem_window(kh, kw, sh, sw);
   if (apply) {
     if (stem) bn_act_maxpool_bwd_kernel<true, 3, 3, 2, 2> BWD_ARGS;
@@ -689,6 +692,7 @@ int dv_bn_act_maxpool_bwd(const void* dy, const uint8_t* idx, const void* x, voi
     else bn_act_maxpool_bwd_kernel<false, 0, 0, 0, 0> BWD_ARGS;
   }
 #undef BWD_ARGS
+  det.fold(acc);
   return 0;
 }
 void dv_avgpool_fwd(const void* x, void* y, int N, int H, int W, int C, int P, int Q, int kh, int kw, int sh, int sw,

@@ -43,6 +43,7 @@ struct StemParams {
   float* slab;       // weight gradient partials [blocks][64][R][32]
   const float* bias;
   float* stats;      // [SHARDS][2][64] + shift row, or nullptr
+  float* sdet;       // deterministic mode: per-block slab rows (kernels.h DetStats), or nullptr
   int act; float slope;
   int Hp, Wp, P, Q, sh, sw;
   int rowbytes;      // Wp * 8
@@ -305,7 +306,7 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_kernel(StemParams p) {
     float a = 0.f, b = 0.f;
 #pragma unroll
     for (int w = 0; w < 4; ++w) { a += red[(w * OC + n) * 2]; b += red[(w * OC + n) * 2 + 1]; }
-    float* sh = p.stats + (int64_t)(blockIdx.x % DV_STAT_SHARDS) * 2 * OC;
+    float* sh = stat_row(p.stats, p.sdet, blockIdx.x, OC);
     atomicAdd(sh + n, a);
     atomicAdd(sh + OC + n, b);
   }
@@ -519,6 +520,8 @@ int dv_stem_fwd(const void* xp, const void* w, void* y, const float* bias, float
   p.act = act; p.slope = slope;
   const bool full = bias || act, fq = Q % 16 == 0;
   const dim3 grid(N * p.chunks);
+  const DetStats det(stats ? grid.x : 0, OC, st);
+  p.sdet = det.slab;
   if (p.rowbytes <= 2048) {
     if (full) { if (fq) launch_fwd<SE_FULL, true, 2048>(p, grid, st); else launch_fwd<SE_FULL, false, 2048>(p, grid, st); }
     else { if (fq) launch_fwd<SE_STATS, true, 2048>(p, grid, st); else launch_fwd<SE_STATS, false, 2048>(p, grid, st); }
@@ -526,6 +529,7 @@ int dv_stem_fwd(const void* xp, const void* w, void* y, const float* bias, float
     if (full) { if (fq) launch_fwd<SE_FULL, true, 3072>(p, grid, st); else launch_fwd<SE_FULL, false, 3072>(p, grid, st); }
     else { if (fq) launch_fwd<SE_STATS, true, 3072>(p, grid, st); else launch_fwd<SE_STATS, false, 3072>(p, grid, st); }
   }
+  det.fold(stats);
   return 0;
 }
 
@@ -546,7 +550,8 @@ int dv_stem_wgrad(const void* xp, const void* dy, int ldy, float* dw, int N, int
   if (!p.slab) return -1;
   if (Q % 16 == 0) launch_wg<true>(p, nblk, lds, st);
   else launch_wg<false>(p, nblk, lds, st);
-  const int per = 16;
+  // deterministic mode: one y-block sums every block's slab in order (one atomic per element)
+  const int per = dv_deterministic() ? nblk : 16;
   const dim3 rg((OC * SR * 32 + 255) / 256, (nblk + per - 1) / per);
   stem_wgrad_reduce_kernel<<<rg, 256, 0, st>>>(p.slab, nblk, per, dw, C, S);
   return 0;

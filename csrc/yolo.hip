@@ -93,6 +93,7 @@ struct YoloArgs {
   int g, C;
   float aw[3], ah[3];
   float grad_scale, lambda_coord, lambda_noobj, ignore_thresh;
+  float* det;
 };
 
 __global__ __launch_bounds__(NT) void yolo_loss_kernel(YoloArgs a) {
@@ -179,7 +180,8 @@ __global__ __launch_bounds__(NT) void yolo_loss_kernel(YoloArgs a) {
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < NT / 64; ++i) s += red[threadIdx.x][i];
-    atomicAdd(a.losses + n * 4 + threadIdx.x, s);
+    // deterministic mode: this block's own slab row (kernels.h dv_det_sum folds them in order)
+    atomicAdd((a.det ? a.det + (int64_t)blockIdx.x * gridDim.y * 4 : a.losses) + n * 4 + threadIdx.x, s);
   }
 }
 
@@ -284,7 +286,9 @@ void dv_yolo_loss(const void* pred, int ldp, const float* y_true, const float* b
   a.ignore_thresh = ignore_thresh;
   const int cells = g * g;
   const int bx = std::max(1, std::min((cells + 3) / 4, 2048 / std::max(N, 1) + 1));
+  a.det = (losses && dv_deterministic()) ? dv_det_workspace((size_t)bx * N * 4, st) : nullptr;
   yolo_loss_kernel<<<dim3(bx, N), NT, 0, st>>>(a);
+  if (a.det) dv_det_sum(a.det, bx, (int64_t)N * 4, losses, st);
 }
 
 void dv_yolo_decode(const void* pred, int ldp, int N, int g, int C, const float* anchors6, float* out, int rows_total,

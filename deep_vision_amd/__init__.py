@@ -10,9 +10,16 @@ from . import ops  # noqa: F401,E402
 
 
 def set_deterministic(on: bool = True) -> None:
-    """Bitwise-reproducible weight gradients: split-K wgrad partials go through per-split slabs
-    summed in a fixed order instead of fp32 atomics (also ``DV_DETERMINISTIC=1``). BatchNorm
-    statistics keep their sharded atomics (order effects at the fp32 ulp level)."""
+    """Whole-step deterministic mode (also ``DV_DETERMINISTIC=1``): the same training step run twice
+    from the same state gives bitwise-equal losses, gradients and weights.
+
+    Every cross-block accumulation of the training path stops using float atomics in arbitrary
+    order: split-K / depthwise / grouped / stem weight gradients go through per-block fp32 slabs
+    summed in a fixed order; BatchNorm statistics and backward sums (conv / dgrad / depthwise /
+    grouped / stem / fused-pool epilogues, the separate reduction passes, bias channel sums) write
+    one partial row per block into a per-stream slab that a fold kernel adds, in block order, into
+    the 64 accumulator shards (csrc/kernels.h DetStats); loss totals likewise (dv_det_sum). Costs
+    one extra small launch per statistics producer (profiles/deterministic_cost.txt)."""
     from ._ext import lib
 
     lib().set_deterministic(bool(on))
