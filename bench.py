@@ -28,8 +28,9 @@ Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--model
 Reported besides the contract fields: ``per_gpu`` images/s, ``comm_exposed_ms`` (compute-stream
 time blocked on the gradient all-reduces per step, HIP events around DataParallel.finish) and
 ``vs_same_box_miopen`` (ratio to the PyTorch/MIOpen eager run on the same MI355X, read from the
-record ``bench.py --backend torch --write-comparator`` measured, profiles/bench_<model>_1gpu_torch_miopen.json,
-scaled by N; the file is named in ``vs_same_box_miopen_src``). ``vs_baseline`` divides by the
+record ``bench.py --backend torch --write-comparator`` measured, bench/comparators/bench_<model>_1gpu_torch_miopen.json
+-- outside the gpurun-ignored profiles/, so it travels to the GPU box -- scaled by N; the file is
+named in ``vs_same_box_miopen_src``). ``vs_baseline`` divides by the
 BASELINE.md proxy (~376 img/s per 8-GPU node, fp32 K80-era); it is NOT a like-for-like ratio.
 """
 from __future__ import annotations
@@ -42,7 +43,9 @@ import time
 # Reference-derived comparators, images/sec per node:
 #   ResNet-50-equivalent proxy ~376 (8 GPUs), YOLOv3 ~179 (8x V100), LeNet-5 PT ~906.
 BASELINES = {"resnet50": 376.0, "yolov3": 179.0, "lenet5": 906.0}
-PROFILES = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.abspath(__file__)), "profiles")
+ROOT = __import__("os").path.dirname(__import__("os").path.abspath(__file__))
+PROFILES = __import__("os").path.join(ROOT, "profiles")
+COMPARATORS = __import__("os").path.join(ROOT, "bench", "comparators")
 
 
 def comparator_path(model):
@@ -51,7 +54,7 @@ def comparator_path(model):
     arm for ``vs_same_box_miopen``."""
     import os
 
-    return os.path.join(PROFILES, f"bench_{model}_1gpu_torch_miopen.json")
+    return os.path.join(COMPARATORS, f"bench_{model}_1gpu_torch_miopen.json")
 
 
 def same_box_miopen(model):
@@ -66,7 +69,7 @@ def same_box_miopen(model):
             rec = json.loads(f.read().strip().splitlines()[-1])
         if rec.get("config", {}).get("backend") != "torch" or not rec.get("per_gpu"):
             return None, None
-        return float(rec["per_gpu"]), os.path.relpath(path, os.path.dirname(PROFILES))
+        return float(rec["per_gpu"]), os.path.relpath(path, ROOT)
     except (OSError, ValueError, KeyError, IndexError):
         return None, None
 

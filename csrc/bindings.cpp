@@ -191,7 +191,10 @@ PYBIND11_MODULE(_C, m) {
     check_last("act_bwd_rows");
   });
   m.def("add", [](uptr a, uptr b, uptr y, int64_t n, float alpha, float beta, int act, float slope, uptr st) { dv_add(CP(a), CP(b), P(y), n, alpha, beta, act, slope, ST(st)); check_last("add"); });
-  m.def("dropout", [](uptr x, uptr y, int64_t n, float p, uint64_t seed, uptr st) { dv_dropout(CP(x), P(y), n, p, seed, ST(st)); check_last("dropout"); });
+  m.def("dropout", [](uptr x, uptr y, int64_t n, float p, uint64_t seed, uptr st, uptr step) {
+    dv_dropout(CP(x), P(y), n, p, seed, (const uint32_t*)step, ST(st));
+    check_last("dropout");
+  }, py::arg("x"), py::arg("y"), py::arg("n"), py::arg("p"), py::arg("seed"), py::arg("st"), py::arg("step") = 0);
   m.def("wprep", [](uptr w, uptr out, int G, int Og, int Ig, int R, int S, int Ipad, int mode, int Sp, uptr st) { dv_wprep(CFP(w), P(out), G, Og, Ig, R, S, Ipad, mode, Sp, ST(st)); check_last("wprep"); });
   m.def("stem_fwd", [](uptr xp, uptr w, uptr y, uptr bias, uptr stats, int act, float slope, int N, int Hp, int Wp,
                        int P_, int Q, int R, int Sp, int K, int sh, int sw, uptr st) {

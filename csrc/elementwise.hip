@@ -112,9 +112,17 @@ DV_DEVICE uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
   return h;
 }
 
-// y = x * mask / (1-p);   mask_i = hash(seed, i) >= p*2^32
+// y = x * mask / (1-p);   mask_i = hash(seed, i) >= p*2^32. `step` (optional, device): a per-step
+// counter mixed into the key -- a captured graph bakes the host seed into the launch, and the
+// replayer advances the counter so every replay draws fresh masks (train/graph.py)
 __global__ __launch_bounds__(NT) void dropout_kernel(const u16* __restrict__ x, u16* __restrict__ y, int64_t n, uint32_t thr,
-                                                       float scale, uint32_t seed_lo, uint32_t seed_hi) {
+                                                       float scale, uint32_t seed_lo, uint32_t seed_hi,
+                                                       const uint32_t* __restrict__ step) {
+  if (step) {
+    const uint32_t k = step[0];
+    seed_lo ^= k * 0x9E3779B9u;
+    seed_hi += k;
+  }
   for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
     const uint32_t h = hash3(seed_lo, seed_hi, (uint32_t)i ^ (uint32_t)(i >> 32) * 0x27D4EB2Fu);
     y[i] = (h >= thr) ? f2bf(bf2f(x[i]) * scale) : (u16)0;
@@ -427,11 +435,12 @@ int dv_act_bwd_rows(const void* dy, int lddy, const void* y, int ldy, void* dx, 
 void dv_add(const void* a, const void* b, void* y, int64_t n, float alpha, float beta, int act, float slope, hipStream_t st) {
   add_kernel<<<grid_for(n, 8), NT, 0, st>>>((const u16*)a, (const u16*)b, (u16*)y, n, alpha, beta, act, slope);
 }
-void dv_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, hipStream_t st) {
+void dv_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, const uint32_t* step, hipStream_t st) {
   const double thr = (double)p * 4294967296.0;
   const uint32_t t = thr >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)thr;
   const float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
-  dropout_kernel<<<grid_for(n), NT, 0, st>>>((const u16*)x, (u16*)y, n, t, scale, (uint32_t)seed, (uint32_t)(seed >> 32));
+  dropout_kernel<<<grid_for(n), NT, 0, st>>>((const u16*)x, (u16*)y, n, t, scale, (uint32_t)seed, (uint32_t)(seed >> 32),
+                                             step);
 }
 void dv_wprep(const float* w, void* out, int G, int Og, int Ig, int R, int S, int pad, int mode, int Sp, hipStream_t st) {
   const int64_t total = (int64_t)G * (mode != 1 ? Og : Ig) * pad * R * (mode == 2 ? Sp : S);

@@ -185,7 +185,7 @@ void dv_act_bwd(const void* dy, const void* y, void* dx, int64_t n, int act, flo
 int dv_act_bwd_rows(const void* dy, int lddy, const void* y, int ldy, void* dx, int lddx, int64_t rows, int C, int act,
                     float slope, hipStream_t st);
 void dv_add(const void* a, const void* b, void* y, int64_t n, float alpha, float beta, int act, float slope, hipStream_t st);
-void dv_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, hipStream_t st);
+void dv_dropout(const void* x, void* y, int64_t n, float p, uint64_t seed, const uint32_t* step, hipStream_t st);
 void dv_wprep(const float* w, void* out, int G, int Og, int Ig, int R, int S, int Ipad, int mode, int Sp, hipStream_t st);
 // NHWC channel-slice copy (16-B vectors; concat into a slice of a wider buffer) or, with an index
 // table, a channel gather (ShuffleNet channel shuffle / its inverse). -1: unsupported geometry.

@@ -95,7 +95,7 @@ __global__ __launch_bounds__(NT) void pw_loss_kernel(int kind, const TP* __restr
     ls = block_sum<NT>(ls, sh);
     if (kind == K_FOCAL) ps = block_sum<NT>(ps, sh);
     if (threadIdx.x == 0) {
-      float* d = det ? det + blockIdx.x * 2 : sums;  // deterministic mode: this block's own slab row
+      float* d = det ? det + blockIdx.x * (kind == K_FOCAL ? 2 : 1) : sums;  // deterministic mode: this block's slab row
       atomicAdd(d, ls);
       if (kind == K_FOCAL) atomicAdd(d + 1, ps);
     }

@@ -108,10 +108,11 @@ def add(a, b, act=None, slope=0.0):
 
 class _DropoutFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, p, seed):
+    def forward(ctx, x, p, seed, step):
         y = torch.empty_like(x)
-        lib().dropout(ptr(x), ptr(y), x.numel(), float(p), seed, stream_handle())
+        lib().dropout(ptr(x), ptr(y), x.numel(), float(p), seed, stream_handle(), step=ptr(step))
         ctx.cfg = (p, seed, x.stride())
+        ctx.step = step
         return y
 
     @staticmethod
@@ -121,11 +122,32 @@ class _DropoutFn(torch.autograd.Function):
         if dy.stride() != stride:  # the mask is indexed by flat position: match the forward layout
             dy = torch.empty_strided(dy.shape, stride, dtype=dy.dtype, device=dy.device).copy_(dy)
         dx = torch.empty_like(dy)
-        lib().dropout(ptr(dy), ptr(dx), dy.numel(), float(p), seed, stream_handle())  # same mask
-        return dx, None, None
+        lib().dropout(ptr(dy), ptr(dx), dy.numel(), float(p), seed, stream_handle(), step=ptr(ctx.step))  # same mask
+        return dx, None, None, None
 
 
-_seed_counter = [0x5EED]
+# Per-device step counters of captured steps: a HIP graph bakes the host seed of every dropout call
+# into its launch, so inside a capture the kernels also read this counter, which the replayer
+# advances before every replay (train/graph.py CapturedStep) -- fresh masks per replayed step.
+_STEP = {}
+
+
+def step_counter(device):
+    dev = torch.device(device) if not isinstance(device, int) else torch.device("cuda", device)
+    if dev.type == "cuda" and dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    t = _STEP.get(dev)
+    if t is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("dropout step counter created inside a capture (CapturedStep makes it first)")
+        t = _STEP[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
+    return t
+
+
+def advance_dropout_step():
+    """Advance every device's dropout step counter (one tiny kernel each): called per replay."""
+    for t in _STEP.values():
+        t.add_(1)
 
 
 def dropout(x, p=0.5, training=True):
@@ -134,6 +156,8 @@ def dropout(x, p=0.5, training=True):
     if not native(x):
         return TF.dropout(x, p, training)
     x = _prep(x)
-    _seed_counter[0] += 1
-    seed = (int(torch.initial_seed()) * 1000003 + _seed_counter[0]) & 0xFFFFFFFFFFFFFFFF
-    return _DropoutFn.apply(x, p, seed)
+    # the host seed comes from torch's global CPU generator: torch.manual_seed makes masks
+    # reproducible (deterministic mode)
+    seed = int(torch.randint(0, 2**62, (1,)).item())
+    step = step_counter(x.device) if torch.cuda.is_current_stream_capturing() else None
+    return _DropoutFn.apply(x, p, seed, step)

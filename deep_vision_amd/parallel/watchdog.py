@@ -46,6 +46,18 @@ def install_backend_error_handling(timeout_s: int | None = None) -> None:
         os.environ.setdefault("DV_COMM_TIMEOUT", str(int(timeout_s)))
 
 
+# Held by a watchdog while it queries its events, and by a HIP-graph capture for its whole
+# duration (train/graph.py): event queries from another thread during a global-mode capture are
+# illegal, so polling pauses while a step is being captured.
+_POLL_LOCK = threading.Lock()
+
+
+@contextlib.contextmanager
+def suspend_polling():
+    with _POLL_LOCK:
+        yield
+
+
 class CommWatchdog:
     def __init__(self, timeout: float | None = None, on_timeout=None, poll: float | None = None):
         self.timeout = float(timeout if timeout is not None else os.environ.get("DV_COMM_TIMEOUT", "600"))
@@ -104,7 +116,8 @@ class CommWatchdog:
                     return None
                 name, ev, t0 = self._events[0]
             try:
-                done = bool(ev.query())
+                with _POLL_LOCK:
+                    done = bool(ev.query())
             except Exception as e:  # a failed stream (aborted communicator): report it as a comm error
                 return name, t0, f"{type(e).__name__}: {e}"
             if not done:

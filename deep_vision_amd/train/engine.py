@@ -135,7 +135,11 @@ class Engine:
         """GPU-side completion of the step just enqueued, watched by the comm watchdog: an RCCL
         all-reduce that never completes (dead / wedged peer) ends this rank even though the host
         only enqueued it (eager ``work.wait()`` is a stream wait; graph replays are one launch)."""
-        if self.comm_watchdog is not None and self.device.type == "cuda":
+        # not while a graph is being captured: an event recorded in a capture cannot be queried,
+        # and the watchdog thread would poll the warm-up events mid-capture (CapturedStep tracks
+        # the replays instead, train_step below)
+        if (self.comm_watchdog is not None and self.device.type == "cuda"
+                and not torch.cuda.is_current_stream_capturing()):
             ev = torch.cuda.Event()
             ev.record()
             self.comm_watchdog.track(f"{name} {self.step_count}", ev)

@@ -80,6 +80,9 @@ class CapturedStep:
             for _ in range(max(1, warmup)):  # real steps: allocator warm-up, first-step optimizer state
                 self.warmup_outputs = self.step_fn(*self.static_inputs)
         torch.cuda.current_stream().wait_stream(s)
+        from ..ops.act import step_counter
+
+        step_counter(torch.cuda.current_device())  # exists before the capture (captured dropouts read it)
         torch.cuda.synchronize()
         self.opt.use_device_hparams(True)
         host = [(f["step"], f["first"]) if f else None for f in self.opt._flat]
@@ -87,7 +90,9 @@ class CapturedStep:
         # captured on the warm-up stream: the per-stream scratch the warm-up sized (split-K slabs,
         # channel sums) is what the captured kernels use -- a fresh capture stream would find none
         # and could not allocate it mid-capture
-        with torch.cuda.graph(self.graph, stream=s):
+        from ..parallel.watchdog import suspend_polling
+
+        with suspend_polling(), torch.cuda.graph(self.graph, stream=s):  # no event queries mid-capture
             self.outputs = self.step_fn(*self.static_inputs)
         # the capture executed nothing: undo its host-side bookkeeping
         for f, h in zip(self.opt._flat, host):
@@ -104,6 +109,9 @@ class CapturedStep:
         self.opt.graph_tick()
         for m in self._counted:
             m._dv_nbt_pending = m.__dict__.get("_dv_nbt_pending", 0) + 1
+        from ..ops.act import advance_dropout_step
+
+        advance_dropout_step()  # fresh dropout masks per replay (ops/act.py)
         self.graph.replay()
         return self.outputs
 

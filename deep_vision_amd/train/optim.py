@@ -253,15 +253,18 @@ class _FlatOptimizer(torch.optim.Optimizer):
                 loss = closure()
         self._check_binding()
         guard = self._guard_active()
+        # the active segments of every group, taken once: _sync_grads binds a None .grad to its
+        # (zeroed) flat view, so a second call would report every parameter active and the update
+        # would apply weight decay / momentum to parameters that got no gradient this step
+        segs_all = [self._sync_grads(group, f) if f is not None else None
+                    for group, f in zip(self.param_groups, self._flat)]
         if guard:  # flag any non-finite gradient of any group before the first update launch
-            for group, f in zip(self.param_groups, self._flat):
+            for f in self._flat:
                 if f is not None:
-                    self._sync_grads(group, f)
                     lib().nonfinite_check(ptr(f["grad"]), f["grad"].numel(), ptr(self._dguard), stream_handle())
-        for group, f in zip(self.param_groups, self._flat):
+        for group, f, segs in zip(self.param_groups, self._flat, segs_all):
             if f is None:
                 continue
-            segs = self._sync_grads(group, f)
             f["step"] += 1
             # device hyperparameters: an eager step writes its own; inside a graph capture the
             # values come from graph_tick() before each replay (a captured copy would replay stale)

@@ -297,3 +297,71 @@ def test_captured_dp_step_skips_nonfinite_on_device():
     assert c1 == (1, 1, True)
     assert c2 == (1, 0, False)
     assert moved and finite
+
+
+def test_captured_dropout_draws_fresh_masks_per_replay():
+    """A captured step bakes each dropout call's host seed into the graph; the per-device step
+    counter (ops/act.py, advanced by CapturedStep before each replay) still gives every replay its
+    own masks, and the backward reuses its forward's mask."""
+    from deep_vision_amd import nn, ops as F
+    from deep_vision_amd.train.graph import CapturedStep
+    from deep_vision_amd.train.optim import FusedSGD
+
+    torch.manual_seed(0)
+    lin = nn.Linear(64, 64).to(DEV)
+    opt = FusedSGD(lin.parameters(), lr=0.0)
+    x = torch.randn(32, 64, device=DEV)
+    outs = []
+
+    def step(xx):
+        opt.zero_grad()
+        y = F.dropout(lin(xx), 0.5, True)
+        y.float().sum().backward()
+        opt.step()
+        return y.detach().float().clone(), lin.weight.grad.detach().clone()
+
+    cap = CapturedStep(step, opt, (x,), model=lin, warmup=1)
+    for _ in range(3):
+        y, g = cap(x)
+        outs.append((y.clone(), g.clone()))
+    torch.cuda.synchronize()
+    (y0, g0), (y1, g1) = outs[0], outs[1]
+    assert not torch.equal(y0 != 0, y1 != 0), "replays reused the captured dropout mask"
+    assert 0.4 < (y0 != 0).float().mean().item() < 0.6
+    # the weight gradient is sum over kept outputs of x: consistent with the forward's mask
+    keep = (y1 != 0).float() * 2.0
+    ref = keep.t() @ x
+    assert torch.allclose(g1, ref, rtol=2e-2, atol=2e-1)
+
+
+def test_engine_graph_step_with_comm_watchdog():
+    """Engine.train_step(graph=True) with a comm watchdog attached (as on a multi-rank job): the
+    capture records no watched event (an event recorded in a capture cannot be queried) and the
+    watchdog does not poll while the capture runs; the replays are tracked and complete."""
+    from deep_vision_amd import ops as F
+    from deep_vision_amd.parallel.watchdog import CommWatchdog
+    from deep_vision_amd.train.engine import Engine
+    from deep_vision_amd.train.optim import FusedSGD
+
+    eng = Engine(device="cuda", graph=True)
+    fired = []
+    eng.comm_watchdog = CommWatchdog(timeout=60, poll=0.01, on_timeout=lambda c, why: fired.append((c, why))).start()
+    try:
+        model = _net()
+        opt = FusedSGD(model.parameters(), lr=0.01, momentum=0.9)
+        x = torch.randn(16, 8, 20, 20, device=DEV)
+        y = torch.randint(0, 10, (16,), device=DEV)
+
+        def fl(xx, yy):
+            return F.cross_entropy(model(xx), yy), None
+
+        losses = [eng.train_step(model, opt, fl, x, y)[0].item() for _ in range(5)]
+        torch.cuda.synchronize()
+        import time
+
+        time.sleep(0.2)  # a few polls after the last replay
+        assert not fired, fired
+        assert all(v == v for v in losses)
+        assert eng.comm_watchdog.pending() <= 1
+    finally:
+        eng.comm_watchdog.stop()
