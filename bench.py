@@ -216,6 +216,11 @@ def main():
 
         sys.exit(spawn(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
 
+    if "WORLD_SIZE" in os.environ:  # a rank: its own NUMA-local CPU set before any GPU / thread-pool use
+        from deep_vision_amd.launch import pin_rank_cpus
+
+        pin_rank_cpus()
+
     import threading
 
     def heartbeat():  # long silent phases (MIOpen kernel search of the torch arm) print to stderr

@@ -46,7 +46,24 @@ from ..ops.conv import GradJoin
 import os
 
 BRANCH_STREAMS = {"1": True, "0": False}.get(os.environ.get("DV_BRANCH_STREAMS", "graph"), "graph")
+# Side streams: one per recursion depth, or -- when RCCL is active (a process group of > 1 rank) --
+# two shared by depth parity (depth % side_streams()), so that with the main / capture stream and
+# RCCL's own stream the process stays within GPU_MAX_HW_QUEUES = 4 hardware queues (streams beyond
+# that share queues and serialise: an all-reduce could queue behind branch compute). Nested levels
+# of one parity then share a stream (a level joins after the outer level's up1 too), each still
+# overlapping the main stream's low branch. DV_BRANCH_SIDE_STREAMS overrides.
+SIDE_STREAMS = int(os.environ.get("DV_BRANCH_SIDE_STREAMS", "0"))
 _STREAMS = {}
+
+
+def side_streams() -> int:
+    if SIDE_STREAMS > 0:
+        return SIDE_STREAMS
+    import torch.distributed as dist
+
+    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    return 2 if multi else 4
+_FORKED = set()  # recursion depths whose up1 branch was forked (tests)
 HANDOFF_STATS = True  # a block's conv3 epilogue accumulates the next block's pre-activation BN statistics
 
 
@@ -63,7 +80,8 @@ def _fork(x):
 def _side_stream(device, depth):
     import torch
 
-    key = (str(device), depth)
+    _FORKED.add(depth)
+    key = (str(device), depth % side_streams())
     st = _STREAMS.get(key)
     if st is None:
         st = _STREAMS[key] = torch.cuda.Stream(device=device)

@@ -303,7 +303,9 @@ def add_common_args(ap: argparse.ArgumentParser):
                     help="timer: per-phase HIP-event step timing; rocprof: re-run this command under "
                          "rocprofv3 --kernel-trace --stats (counters are collected in separate runs)")
     ap.add_argument("--tensorboard-dir", default=None, help="TensorBoard root (Keras configs: ./tensorboard)")
-    ap.add_argument("--nproc", type=int, default=None, help="spawn N ranks (one per GPU) via torch.distributed.run")
+    ap.add_argument("--nproc", type=int, default=None,
+                    help="spawn N ranks (one per GPU) via torch.distributed.run; default: every visible GPU "
+                         "(the reference wraps the net in nn.DataParallel whenever > 1 GPU is visible)")
     ap.add_argument("--graph", action="store_true",
                     help="capture the training step as a HIP graph and replay it (single GPU; train/graph.py)")
     return ap
@@ -330,7 +332,7 @@ def main(argv=None, choices=None, default=None):
         from ..profiling import run_under_rocprof
 
         run_under_rocprof(argv)  # exits with the profiled child's status
-    maybe_spawn(a.nproc)
+    maybe_spawn(a.nproc, a.device)
     cfg = get_config(a.model)
     ck = resolve_checkpoint(a.checkpoint, cfg, a.checkpoint_dir)
     run_epochs(cfg, ck, device=a.device, data_dir=a.data_dir, synthetic=a.synthetic, epochs=a.epochs,

@@ -273,6 +273,8 @@ def train(cfg: TrainConfig, checkpoint=None, *, train_glob=None, val_glob=None, 
           epochs=None, max_steps=None, val_steps=None, device=None, workers=2, log_every=10, checkpoint_dir=None,
           seed=None, batch_size=None, profile=False, tensorboard_dir=None, graph=False):
     eng = Engine(device=device, log_every=log_every, profile=profile, graph=graph)
+    if eng.world > 1:  # MirroredStrategy's replica report (R/YOLO/tensorflow/train.py:282)
+        eng.log(f"Using {eng.world} GPUs" if eng.device.type == "cuda" else f"Using {eng.world} ranks (gloo)")
     seed_everything(cfg.extras.get("seed", 0) if seed is None else seed, eng.rank)
     if batch_size:
         cfg = cfg.replace(batch_size=batch_size)
@@ -309,10 +311,15 @@ def add_args(ap):
     ap.add_argument("--log-every", type=int, default=10)
     ap.add_argument("--checkpoint-dir", default=None)
     ap.add_argument("--batch-size", type=int, default=None, help="per-replica batch")
+    ap.add_argument("--input-size", type=int, default=None, help="square input size (default: the config's)")
     ap.add_argument("--profile", nargs="?", const="timer", default=None, choices=["timer", "rocprof"])
     ap.add_argument("--tensorboard-dir", default=None)
-    ap.add_argument("--nproc", type=int, default=None)
-    ap.add_argument("--graph", action="store_true", help="HIP-graph replay of the training step (single GPU)")
+    ap.add_argument("--nproc", type=int, default=None,
+                    help="processes (one per GPU); default: every visible GPU, like MirroredStrategy")
+    ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=True,
+                    help="HIP-graph replay of the whole training step, data-parallel all-reduces included "
+                         "(default on: the captured step replays the eager one bit for bit in deterministic "
+                         "mode, tests/test_branch_streams_gpu.py); --no-graph runs eagerly")
     return ap
 
 
@@ -329,8 +336,10 @@ def main(family_config: str, argv=None, tfrecords_default="./dataset/tfrecords")
         from ..profiling import run_under_rocprof
 
         run_under_rocprof(argv)
-    maybe_spawn(a.nproc)
+    maybe_spawn(a.nproc, a.device)
     cfg = get_config(family_config)
+    if a.input_size:
+        cfg = cfg.replace(input_shape=(cfg.input_shape[0], a.input_size, a.input_size))
     return train(cfg, a.checkpoint, train_glob=os.path.join(a.tfrecords, "train*"),
                  val_glob=os.path.join(a.tfrecords, "val*"), synthetic=a.synthetic, synthetic_size=a.synthetic_size,
                  epochs=a.epochs, max_steps=a.max_steps, val_steps=a.val_steps, device=a.device, workers=a.workers,

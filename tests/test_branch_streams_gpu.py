@@ -101,7 +101,8 @@ def _six_steps(base, xs, hms, captured, lr=1e-4):
     losses = [cap.warmup_outputs.detach().float().clone()]
     losses += [cap(xs[i], hms[i]).detach().float().clone() for i in range(2, 6)]
     torch.cuda.synchronize()
-    assert any(k[1] == 4 for k in H._STREAMS), "capture did not fork the up1 branches"
+    assert 4 in H._FORKED, "capture did not fork the up1 branches"
+    assert len({k[1] for k in H._STREAMS}) <= H.side_streams()
     return torch.stack(losses), _params(m)
 
 
