@@ -118,7 +118,8 @@ def main():
         syn = make_jpegs(imgdir, a.images)
         rec["jpeg_gen_s"] = round(time.perf_counter() - t0, 2)
         arms = {"reference_fp32": ImageNet2012Dataset(imgdir, syn, T.imagenet_train_transform(device_normalize=False)),
-                "device_normalize_u8": ImageNet2012Dataset(imgdir, syn, T.imagenet_train_transform(device_normalize=True))}
+                "device_normalize_u8": ImageNet2012Dataset(imgdir, syn, T.imagenet_train_transform(device_normalize=True),
+                                                           decode_min_side=256)}
         for name, ds in arms.items():
             r, b = per_worker_rate(ds, a.per_worker)
             rec[name] = {"per_worker_img_s": round(r, 1), "bytes_per_img": int(b), "loader_img_s": {}}

@@ -118,6 +118,30 @@ static void normalize_batch(py::array_t<uint8_t, py::array::c_style> src, py::ar
   dvio::normalize_batch(s, d, N, H, W, C, mean, stdv, scale, threads);
 }
 
+// (H, W, C) uint8 -> the (ch, cw, C) crop of its bilinear rescale to (outH, outW), GIL released
+static py::array_t<uint8_t> resize_crop(py::array_t<uint8_t, py::array::c_style | py::array::forcecast> src,
+                                        int64_t outH, int64_t outW, int64_t cy, int64_t cx, int64_t ch, int64_t cw) {
+  if (src.ndim() != 3) throw std::runtime_error("resize_crop: expected an HWC array");
+  const int64_t H = src.shape(0), W = src.shape(1), C = src.shape(2);
+  py::array_t<uint8_t> out({ch, cw, C});
+  const uint8_t* s = src.data();
+  uint8_t* d = out.mutable_data();
+  {
+    py::gil_scoped_release nogil;
+    dvio::resize_crop_bilinear(s, H, W, C, outH, outW, cy, cx, ch, cw, d);
+  }
+  return out;
+}
+
+static void color_jitter(py::array_t<uint8_t, py::array::c_style> img, std::vector<float> f, std::vector<int> order) {
+  if (img.ndim() != 3 || img.shape(2) != 3 || f.size() != 3 || order.size() != 3)
+    throw std::runtime_error("color_jitter: expected an HWC RGB uint8 array, 3 factors and an order");
+  uint8_t* p = img.mutable_data();
+  const int64_t n = img.shape(0) * img.shape(1);
+  py::gil_scoped_release nogil;
+  dvio::color_jitter(p, n, f.data(), order.data());
+}
+
 PYBIND11_MODULE(_io, m) {
   m.doc() = "deep_vision_amd native input-pipeline runtime (TFRecord IO, Example decoding, batch collation)";
   m.def("crc32c", [](py::bytes b) { std::string s = b; return dvio::crc32c((const uint8_t*)s.data(), s.size()); });
@@ -134,6 +158,9 @@ PYBIND11_MODULE(_io, m) {
       .def("reset", &RecordReader::reset);
   m.def("index_file", &dvio::index_file);
   m.def("parse_example", &parse_example);
+  m.def("resize_crop", &resize_crop, py::arg("src"), py::arg("out_h"), py::arg("out_w"), py::arg("cy"), py::arg("cx"),
+        py::arg("ch"), py::arg("cw"));
+  m.def("color_jitter", &color_jitter, py::arg("img"), py::arg("factors"), py::arg("order"));
   m.def("normalize_batch", &normalize_batch, py::arg("src"), py::arg("dst"), py::arg("mean"), py::arg("std"),
         py::arg("scale") = 255.f, py::arg("threads") = 8);
 }

@@ -257,4 +257,83 @@ inline void normalize_batch(const uint8_t* s, float* d, int64_t N, int64_t H, in
   for (auto& th : pool) th.join();
 }
 
+// ---- image augmentation (the ImageNet train / val transforms, data/transforms.py) ----
+// Rescale(shorter side -> S, new size truncated by int() like R/ResNet/pytorch/data_load.py:85-101)
+// followed by a crop, computed in one pass for the crop window only: bilinear sampling with
+// cv2.resize INTER_LINEAR's geometry (src = (dst + 0.5) * in/out - 0.5, clamped to the border, no
+// antialiasing) -- the reference decodes and resizes with cv2 -- in 11-bit fixed point per axis
+// like cv2's uint8 path. src: [H][W][C] uint8, dst: [ch][cw][C].
+inline void resize_crop_bilinear(const uint8_t* src, int64_t H, int64_t W, int64_t C, int64_t outH, int64_t outW,
+                                 int64_t cy, int64_t cx, int64_t ch, int64_t cw, uint8_t* dst) {
+  if (H <= 0 || W <= 0 || outH <= 0 || outW <= 0 || cy < 0 || cx < 0 || cy + ch > outH || cx + cw > outW)
+    throw std::runtime_error("resize_crop_bilinear: bad geometry");
+  constexpr int BITS = 11, ONE = 1 << BITS;
+  const double fy = (double)H / outH, fx = (double)W / outW;
+  std::vector<int32_t> x0(cw), x1(cw), wx(cw);
+  for (int64_t j = 0; j < cw; ++j) {
+    double sx = (cx + j + 0.5) * fx - 0.5;
+    if (sx < 0) sx = 0;
+    int64_t a = (int64_t)sx;
+    if (a > W - 1) a = W - 1;
+    const double f = sx - a;
+    x0[j] = (int32_t)(a * C);
+    x1[j] = (int32_t)(std::min<int64_t>(a + 1, W - 1) * C);
+    wx[j] = (int32_t)(f * ONE + 0.5);
+  }
+  for (int64_t i = 0; i < ch; ++i) {
+    double sy = (cy + i + 0.5) * fy - 0.5;
+    if (sy < 0) sy = 0;
+    int64_t a = (int64_t)sy;
+    if (a > H - 1) a = H - 1;
+    const int32_t wy = (int32_t)((sy - a) * ONE + 0.5);
+    const uint8_t* r0 = src + a * W * C;
+    const uint8_t* r1 = src + std::min<int64_t>(a + 1, H - 1) * W * C;
+    uint8_t* d = dst + i * cw * C;
+    for (int64_t j = 0; j < cw; ++j) {
+      const int32_t w1 = wx[j], w0 = ONE - w1;
+      for (int64_t c = 0; c < C; ++c) {
+        const int32_t top = r0[x0[j] + c] * w0 + r0[x1[j] + c] * w1;
+        const int32_t bot = r1[x0[j] + c] * w0 + r1[x1[j] + c] * w1;
+        const int64_t v = ((int64_t)top * (ONE - wy) + (int64_t)bot * wy + ((int64_t)1 << (2 * BITS - 1))) >> (2 * BITS);
+        d[j * C + c] = (uint8_t)(v > 255 ? 255 : v);
+      }
+    }
+  }
+}
+
+// ColorJitter's PIL enhancers on an RGB uint8 [n][3] image, in place, in the given order
+// (0 brightness, 1 contrast, 2 saturation; factors f[0..2], a factor of exactly 1 is skipped):
+// each is Image.blend(degenerate, image, f) = degenerate + f * (image - degenerate), rounded and
+// clipped to uint8 after every enhancer like PIL. Degenerates: black; the mean of the image's
+// ITU-R 601-2 luma (L = (299 R + 587 G + 114 B) / 1000, rounded) as a flat gray; the per-pixel luma.
+inline uint8_t clip_round(float v) {  // branch-free: the loops below vectorise
+  return (uint8_t)(int)std::min(255.f, std::max(0.f, v));  // PIL ImagingBlend truncates
+}
+inline uint8_t luma(const uint8_t* p) { return (uint8_t)((p[0] * 19595 + p[1] * 38470 + p[2] * 7471 + 0x8000) >> 16); }
+inline void color_jitter(uint8_t* img, int64_t n, const float* f, const int* order) {
+  std::vector<float> g;
+  for (int k = 0; k < 3; ++k) {
+    const int op = order[k];
+    const float a = f[op];
+    if (a == 1.f) continue;
+    if (op == 0) {
+      for (int64_t i = 0; i < n * 3; ++i) img[i] = clip_round(img[i] * a);
+    } else if (op == 1) {
+      int64_t sum = 0;
+      for (int64_t i = 0; i < n; ++i) sum += luma(img + 3 * i);
+      const float m = (float)(int64_t)((double)sum / (double)n + 0.5);
+      for (int64_t i = 0; i < n * 3; ++i) img[i] = clip_round(m + a * ((float)img[i] - m));
+    } else {
+      g.resize(n);
+      for (int64_t i = 0; i < n; ++i) g[i] = (float)luma(img + 3 * i);
+      for (int64_t i = 0; i < n; ++i) {
+        uint8_t* p = img + 3 * i;
+        p[0] = clip_round(g[i] + a * ((float)p[0] - g[i]));
+        p[1] = clip_round(g[i] + a * ((float)p[1] - g[i]));
+        p[2] = clip_round(g[i] + a * ((float)p[2] - g[i]));
+      }
+    }
+  }
+}
+
 }  // namespace dvio

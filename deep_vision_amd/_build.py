@@ -116,7 +116,8 @@ def build_host(force: bool = False, verbose: bool = True) -> str:
 
     srcs = sorted(os.path.join(CSRC, "host", f) for f in os.listdir(os.path.join(CSRC, "host")) if f.endswith(".cpp"))
     out = io_ext_path()
-    if not force and os.path.exists(out) and all(os.path.getmtime(s) <= os.path.getmtime(out) for s in srcs):
+    deps = srcs + [os.path.join(CSRC, "host", f) for f in os.listdir(os.path.join(CSRC, "host")) if f.endswith(".h")]
+    if not force and os.path.exists(out) and all(os.path.getmtime(s) <= os.path.getmtime(out) for s in deps):
         return out
     cmd = ["g++", "-O3", "-msse4.2", "-std=c++17", "-shared", "-fPIC", "-pthread", *srcs, "-o", out,
            f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]

@@ -100,9 +100,17 @@ def read_synsets(labels_file: str | None = None):
     return label_to_idx, idx_to_name
 
 
-def load_rgb(path: str) -> np.ndarray:
-    """Decode to HWC uint8 RGB (alpha dropped; grayscale stays 2-D for ToTensor to expand)."""
+def load_rgb(path: str, min_side: int | None = None) -> np.ndarray:
+    """Decode to HWC uint8 RGB (alpha dropped; grayscale stays 2-D for ToTensor to expand).
+    ``min_side``: a JPEG is decoded at the smallest DCT scale (1/2, 1/4, 1/8) whose shorter side is
+    still >= min_side (PIL draft): the pipeline rescales to that side next anyway, and large images
+    decode several times faster."""
     with Image.open(path) as im:
+        if min_side and im.format == "JPEG":
+            w, h = im.size
+            s = min(w, h)
+            if s >= 2 * min_side:
+                im.draft("RGB", (-(-w * min_side // s), -(-h * min_side // s)))
         if im.mode in ("RGBA", "P", "CMYK", "LA"):
             im = im.convert("RGB")
         arr = np.asarray(im)
@@ -114,8 +122,9 @@ def load_rgb(path: str) -> np.ndarray:
 class ImageNet2012Dataset(Dataset):
     """A flattened directory (``nXXXXXXXX_<file>.JPEG``, T1c) with labels from the synset prefix."""
 
-    def __init__(self, root_dir, labels_file=None, transform=None):
+    def __init__(self, root_dir, labels_file=None, transform=None, decode_min_side=None):
         self.root_dir = root_dir
+        self.decode_min_side = decode_min_side  # load_rgb min_side: reduced-scale JPEG decode
         self.images = sorted(f for f in os.listdir(root_dir) if isfile(join(root_dir, f)))
         self.transform = transform
         self.label_to_idx, self.idx_to_name = read_synsets(labels_file)
@@ -125,7 +134,8 @@ class ImageNet2012Dataset(Dataset):
 
     def __getitem__(self, idx):
         name = self.images[idx]
-        sample = {"image": load_rgb(join(self.root_dir, name)), "annotation": self.label_to_idx[name.split("_")[0]]}
+        sample = {"image": load_rgb(join(self.root_dir, name), self.decode_min_side),
+                  "annotation": self.label_to_idx[name.split("_")[0]]}
         return self.transform(sample) if self.transform else sample
 
 

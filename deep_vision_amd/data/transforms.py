@@ -147,6 +147,69 @@ class ColorJitter:
         return {**sample, "image": np.asarray(image)}
 
 
+def _io():
+    try:
+        from .. import _io as io
+
+        return io if hasattr(io, "resize_crop") else None
+    except ImportError:
+        return None
+
+
+class RescaleCrop:
+    """``Rescale(size)`` then ``RandomCrop(crop)`` (train) or ``CenterCrop(crop)`` as ONE native pass
+    over the crop window only (deep_vision_amd._io resize_crop: cv2 INTER_LINEAR geometry, the
+    reference's cv2.resize, instead of PIL's antialiased bilinear). Same size truncation and crop
+    draws as the two-step form (the randint exclusive upper bound quirk included)."""
+
+    def __init__(self, size, crop, random_crop=True):
+        self.size, self.crop, self.random_crop = size, _pair(crop), random_crop
+
+    def __call__(self, sample):
+        image = sample["image"]
+        if image.ndim == 2:
+            image = np.stack((image,) * 3, axis=-1)
+        h, w = image.shape[:2]
+        if h > w:
+            nh, nw = int(self.size * h / w), self.size
+        else:
+            nh, nw = self.size, int(self.size * w / h)
+        ch, cw = self.crop
+        if self.random_crop:
+            top = np.random.randint(0, nh - ch) if nh > ch else 0
+            left = np.random.randint(0, nw - cw) if nw > cw else 0
+        else:
+            top, left = (nh - ch) // 2, (nw - cw) // 2
+        io = _io()
+        if io is None:  # the two-step form
+            r = _resize(image, nh, nw)
+            return {**sample, "image": np.ascontiguousarray(r[top:top + ch, left:left + cw])}
+        return {**sample, "image": io.resize_crop(np.ascontiguousarray(image), nh, nw, top, left, ch, cw)}
+
+
+class FastColorJitter(ColorJitter):
+    """ColorJitter (brightness / contrast / saturation, random order, the same factor draws) with
+    PIL's enhancer arithmetic in one native in-place call per image (deep_vision_amd._io
+    color_jitter); hue jitter falls back to PIL."""
+
+    def __call__(self, sample):
+        io = _io()
+        if io is None or self.hue > 0:
+            return super().__call__(sample)
+        f, order = [1.0, 1.0, 1.0], []
+        for k, amt in enumerate((self.brightness, self.contrast, self.saturation)):
+            if amt > 0:
+                f[k] = random.uniform(max(0, 1 - amt), 1 + amt)
+                order.append(k)
+        random.shuffle(order)
+        order += [k for k in range(3) if k not in order]
+        image = sample["image"]
+        if not (image.flags.writeable and image.flags.c_contiguous):
+            image = np.ascontiguousarray(image).copy()
+        io.color_jitter(image, f, order)
+        return {**sample, "image": image}
+
+
 class ToUint8:
     """Final step of the device-normalised pipeline (data/device_input.py): the HWC uint8 crop
     as a tensor (grayscale expanded to 3 channels) plus the horizontal-flip draw, which the device
@@ -169,8 +232,8 @@ class ToUint8:
 def imagenet_train_transform(device_normalize=False):
     """R/ResNet/pytorch/train.py:315-324. ``device_normalize``: stop at the uint8 crop + flip
     draw; flip, ToTensor and Normalize run on the GPU (data.device_input)."""
-    if device_normalize:
-        return Compose([Rescale(256), RandomCrop(224), ColorJitter(brightness=0.2, contrast=0.2, saturation=0.2, hue=0),
+    if device_normalize:  # native resize-crop + jitter (deep_vision_amd._io)
+        return Compose([RescaleCrop(256, 224), FastColorJitter(brightness=0.2, contrast=0.2, saturation=0.2, hue=0),
                         ToUint8(flip_p=0.5)])
     return Compose([Rescale(256), RandomHorizontalFlip(0.5), RandomCrop(224),
                     ColorJitter(brightness=0.2, contrast=0.2, saturation=0.2, hue=0), ToTensor(),
@@ -180,5 +243,5 @@ def imagenet_train_transform(device_normalize=False):
 def imagenet_val_transform(device_normalize=False):
     """R/ResNet/pytorch/train.py:326-331."""
     if device_normalize:
-        return Compose([Rescale(256), CenterCrop(224), ToUint8()])
+        return Compose([RescaleCrop(256, 224, random_crop=False), ToUint8()])
     return Compose([Rescale(256), CenterCrop(224), ToTensor(), Normalize(IMAGENET_MEAN, IMAGENET_STD)])

@@ -90,8 +90,9 @@ def build_datasets(cfg: TrainConfig, data_dir=None, synthetic=False, synthetic_s
             labels = None  # the packaged ImageNet-2012 synset list (data.imagenet_meta)
         if os.path.isdir(tr):
             dn = bool(cfg.extras.get("device_normalize", True))  # uint8 crops, normalised on the GPU
-            return (ImageNet2012Dataset(tr, labels, T.imagenet_train_transform(device_normalize=dn)),
-                    ImageNet2012Dataset(va, labels, T.imagenet_val_transform(device_normalize=dn)))
+            ms = 256 if dn else None  # the native pipeline also decodes large JPEGs at a reduced DCT scale
+            return (ImageNet2012Dataset(tr, labels, T.imagenet_train_transform(device_normalize=dn), decode_min_side=ms),
+                    ImageNet2012Dataset(va, labels, T.imagenet_val_transform(device_normalize=dn), decode_min_side=ms))
     return (SyntheticClassification(synthetic_size, cfg.input_shape, nc, key, seed=1),
             SyntheticClassification(max(64, synthetic_size // 4), cfg.input_shape, nc, key, seed=2))
 
