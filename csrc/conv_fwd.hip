@@ -287,13 +287,6 @@ void dispatch_res(const FwdParams& p, hipStream_t st) {
       // 128-row wave tiles (a wave = 128 pixels x 64 channels)
       case 12: return launch_fwd<256, 128, 64, KMODE, RES, 2, 0, EPI_FULL, 128>(p, st);  // 4 waves
       case 14: return launch_fwd<256, 256, 64, KMODE, RES, 2, 0, EPI_FULL, 128>(p, st);  // 8 waves
-      // register-staged operand loads (conv_fwd_core.h LD = 1)
-      case 30: return launch_fwd<128, 128, 32, KMODE, RES, 2, 0, EPI_FULL, 64, 1>(p, st);
-      case 31: return launch_fwd<256, 64, 32, KMODE, RES, 2, 0, EPI_FULL, 64, 1>(p, st);
-      case 32: return launch_fwd<128, 128, 64, KMODE, RES, 2, 0, EPI_FULL, 64, 1>(p, st);
-      case 33: return launch_fwd<256, 64, 64, KMODE, RES, 2, 0, EPI_FULL, 64, 1>(p, st);
-      case 34: return launch_fwd<256, 256, 64, KMODE, RES, 2, 0, EPI_FULL, 128, 1>(p, st);
-      case 35: return launch_fwd<256, 128, 64, KMODE, RES, 2, 0, EPI_FULL, 64, 1>(p, st);
       default: break;
     }
     const bool full = p.bias || p.act || p.ypart;  // split-K slabs are written by the FULL form

@@ -187,11 +187,8 @@ enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_FULL = 2 };
 // 256 threads (4 waves: one per SIMD, two blocks per CU) or 512 threads (8 waves: two per SIMD
 // from one block, whose deep LDS ring then holds one CU); __launch_bounds__' second argument is
 // waves per SIMD, so both forms get up to 256 VGPRs.
-// LD (operand staging): 0 = LDS-DMA (global_load_lds_dwordx4, one 1-KB piece per wave-instruction),
-// 1 = through registers (global_load_dwordx4 of tile t+1 issued before tile t's MFMAs, ds_write_b128
-// of the same bytes to the same swizzled LDS image after them: one barrier per K-tile, double buffer)
 template <int BM_, int BN_, int BK_, int KMODE, bool RES, int STAGES, int BNR = 0, int EPI = EPI_FULL,
-          int WMT = 64, int LD = 0>
+          int WMT = 64>
 __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_kernel(FwdParams p) {
   constexpr int WN = BN_ / 64, WM = BM_ / WMT;
   constexpr int NW = WN * WM;
@@ -208,9 +205,6 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
   constexpr int KK = BK_ / 32;         // 32-deep MFMA steps per K-tile
   constexpr int STAGE = stage_bytes<BM_, BN_, BK_>();
   constexpr int IPT = MI + NI;         // DMA instructions per wave per K-tile
-  static_assert(LD == 0 || STAGES == 2, "register staging: double buffer");
-  typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
-  u32x4v rstg[LD ? IPT : 1];           // LD 1: this wave's pieces of the next K-tile
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -273,10 +267,8 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
     const int k0 = kt0 * BK_, rs = k0 / p.Cg;
     t_c = k0 - rs * p.Cg; t_r = rs / p.S; t_s = rs - t_r * p.S;
   }
-  // one 16-B piece per lane of wave-instruction `slot`: LDS-DMA straight into the image, or (LD 1)
-  // a register load committed by commit() below
-  // the source is chosen by integer select (v_cndmask), not a branch: a divergent branch around the
-  // address would put the register-staged pieces in scratch
+  // one 16-B piece per lane of wave-instruction `slot`, LDS-DMA straight into the image; the source
+  // (operand or zero row) is chosen by integer select (v_cndmask), not a branch around the load
   auto sel = [](bool ok, const void* a, const void* z) {
     const uint64_t ia = reinterpret_cast<uint64_t>(a), iz = reinterpret_cast<uint64_t>(z);
     return reinterpret_cast<const void*>(ok ? ia : iz);
@@ -293,8 +285,7 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
       // fast loader: the weight offset of this K-tile's tap (equal to k0 for a whole filter)
       const int64_t wo = KMODE == KM_FAST ? (int64_t)t_r * p.wkr + t_s * p.wks + t_c : k0;
       const void* src = sel(ok, wrow[j] + wo, zero);
-      if constexpr (LD == 0) glds16(src, img_n + (wid * NI + j) * 1024);
-      else rstg[j] = *reinterpret_cast<const u32x4v*>(src);
+      glds16(src, img_n + (wid * NI + j) * 1024);
     }
     if (KMODE == KM_FAST) {
       const int64_t koff = ((int64_t)(t_r * p.dh) * p.Win + t_s * p.dw) * p.ldx + t_c;
@@ -303,8 +294,7 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
       for (int j = 0; j < MI; ++j) {
         const bool ok = (tapmask[j] >> sh_r) & (tapmask[j] >> sh_s) & 1u;
         const void* src = sel(ok, xrow[j] + koff, zero);
-        if constexpr (LD == 0) glds16(src, img_m + (wid * MI + j) * 1024);
-        else rstg[NI + j] = *reinterpret_cast<const u32x4v*>(src);
+        glds16(src, img_m + (wid * MI + j) * 1024);
       }
     } else {
 #pragma unroll
@@ -327,21 +317,8 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
         ok = ok && h >= 0 && h < p.Hin && w >= 0 && w < p.Win;
         const void* src = zero;
         if (ok) src = p.x + (pixbase[j] + (int64_t)h * p.Win + w) * p.ldx + goff_x + c;
-        if constexpr (LD == 0) glds16(src, img_m + (wid * MI + j) * 1024);
-        else rstg[NI + j] = *reinterpret_cast<const u32x4v*>(src);
+        glds16(src, img_m + (wid * MI + j) * 1024);
       }
-    }
-  };
-  // LD 1: the staged pieces -> the LDS image of `buf` (lane i's 16 B at piece base + 16 i, the
-  // bytes and positions the LDS-DMA form writes)
-  auto commit = [&](int buf) {
-    if constexpr (LD == 1) {
-      char* img_n = smem + buf * STAGE;
-      char* img_m = img_n + BN_ * BK_ * 2;
-#pragma unroll
-      for (int j = 0; j < NI; ++j) *reinterpret_cast<u32x4v*>(img_n + (wid * NI + j) * 1024 + lane * 16) = rstg[j];
-#pragma unroll
-      for (int j = 0; j < MI; ++j) *reinterpret_cast<u32x4v*>(img_m + (wid * MI + j) * 1024 + lane * 16) = rstg[NI + j];
     }
   };
   auto advance = [&]() {
@@ -376,25 +353,7 @@ __global__ __launch_bounds__((64 * n_waves<BM_, BN_, WMT>()), 2) void conv_fwd_k
           acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[j], fb[i], acc[j][i], 0, 0, 0);
     }
   };
-  if constexpr (LD == 1) {
-    // register-staged double buffer: tile t+1's global loads are in flight during tile t's MFMAs,
-    // their ds_writes go to the other buffer after them; one barrier per K-tile. The loads and
-    // the commit run every iteration (the last one re-reads tile nt-1 into the idle buffer): no
-    // control flow between a load and its use, which would make the compiler wait on it early.
-    stage(kt0, 0);
-    commit(0);
-    __syncthreads();
-    for (int t = 0; t < nt; ++t) {
-      const int cur = t & 1;
-      if (t + 1 < nt) advance();  // the walker (scalar) moves to tile t+1, or stays on the last one
-      stage(kt0 + min(t + 1, nt - 1), cur ^ 1);
-      __builtin_amdgcn_sched_barrier(0);
-      compute(cur, kt0 + t);
-      __builtin_amdgcn_sched_barrier(0);
-      commit(cur ^ 1);
-      __syncthreads();
-    }
-  } else if constexpr (STAGES == 2) {
+  if constexpr (STAGES == 2) {
     // double buffer, one barrier per K-tile: the DMA of tile t+1 overlaps the MFMAs of tile t
     stage(kt0, 0);
     advance();
@@ -784,11 +743,11 @@ constexpr int lds_bytes(int stages) {
 constexpr size_t LDS_MAX = 160 * 1024;
 
 template <int BM_, int BN_, int BK_, int KMODE, bool RES, int STAGES, int BNR = 0, int EPI = EPI_FULL,
-          int WMT = 64, int LD = 0>
+          int WMT = 64>
 void launch_fwd(const FwdParams& p, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES, BNR, EPI, WMT, LD>,
+    hipFuncSetAttribute((const void*)conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES, BNR, EPI, WMT>,
                         hipFuncAttributeMaxDynamicSharedMemorySize,
                         lds_bytes<BM_, BN_, BK_, WMT>(STAGES));
     attr = true;
@@ -801,7 +760,7 @@ void launch_fwd(const FwdParams& p, hipStream_t st) {
   const int nt = q.kt_per;
   const size_t lds = lds_bytes<BM_, BN_, BK_, WMT>(nt < STAGES ? nt : STAGES);
   const int blocks = ((p.M + BM_ - 1) / BM_) * ((p.N + BN_ - 1) / BN_) * p.G * q.ksplit;
-  conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES, BNR, EPI, WMT, LD>
+  conv_fwd_kernel<BM_, BN_, BK_, KMODE, RES, STAGES, BNR, EPI, WMT>
       <<<dim3(blocks), dim3(64 * n_waves<BM_, BN_, WMT>()), lds, st>>>(q);
   if (p.ypart) dv_g_last_ksplit = q.ksplit;
 }
