@@ -128,13 +128,13 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("acc"), py::arg("C"), py::arg("count"), py::arg("gamma"), py::arg("mean"), py::arg("invstd"), py::arg("dgamma"),
      py::arg("dbeta"), py::arg("accumulate"), py::arg("kA"), py::arg("kB"), py::arg("kC"), py::arg("st"), py::arg("xsum") = 0);
   m.def("bn_bwd_apply", [](uptr dout, uptr out, uptr x, uptr dx, uptr dres, int64_t n, int C, uptr kA, uptr kB, uptr kC,
-                           uptr mscale, uptr mshift, int act, float slope, int mask_bits, uptr st, uptr addend) {
+                           uptr mscale, uptr mshift, int act, float slope, int mask_bits, uptr st, uptr addend, uptr addend2) {
     dv_bn_bwd_apply(CP(dout), CP(out), CP(x), P(dx), P(dres), n, C, CFP(kA), CFP(kB), CFP(kC), CFP(mscale), CFP(mshift), act, slope,
-                    mask_bits, CP(addend), ST(st));
+                    mask_bits, CP(addend), CP(addend2), ST(st));
     check_last("bn_bwd_apply");
   }, py::arg("dout"), py::arg("out"), py::arg("x"), py::arg("dx"), py::arg("dres"), py::arg("n"), py::arg("C"), py::arg("kA"),
      py::arg("kB"), py::arg("kC"), py::arg("mscale"), py::arg("mshift"), py::arg("act"), py::arg("slope"),
-     py::arg("mask_bits"), py::arg("st"), py::arg("addend") = 0);
+     py::arg("mask_bits"), py::arg("st"), py::arg("addend") = 0, py::arg("addend2") = 0);
   m.def("bn_bwd_apply_dual", [](uptr dout, uptr bits, uptr x, uptr x2, uptr dx, uptr dx2, int64_t n, int C, uptr k,
                                 uptr k2, int act, float slope, uptr st) {
     if (C % 8 || n % C) throw std::runtime_error("bn_bwd_apply_dual: channels must be a multiple of 8");

@@ -397,17 +397,19 @@ __global__ void bn_bwd_finalize_kernel(float* __restrict__ acc, int C, double co
   }
 }
 
-// dx = kA*dz + kB*x + kC (+ addend) ; optionally dres = dz. ``addend``: another gradient of the
-// same input (e.g. a pre-activation block's residual path, models/hourglass.py) summed in this pass
-// instead of a separate add; it may alias dx (each element is read before it is written by the
-// same thread), hence no __restrict__ on the two.
+// dx = kA*dz + kB*x + kC (+ addend + addend2) ; optionally dres = dz. ``addend`` / ``addend2``:
+// other gradients of the same input (a pre-activation block's residual path, an hourglass level's
+// pooled branch -- models/hourglass.py) summed in this pass instead of separate adds; ``addend``
+// may alias dx (each element is read before it is written by the same thread), hence no
+// __restrict__ on the two.
 template <int VEC, int MM, int UNR = 2, bool NTL = false>
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const u16* __restrict__ dout, const u16* __restrict__ out,
                                                             const u16* __restrict__ x, u16* dx, u16* __restrict__ dres,
                                                             int64_t rows, int C, int64_t rows_per_block, const float* __restrict__ kA,
                                                             const float* __restrict__ kB, const float* __restrict__ kC,
                                                             const float* __restrict__ mscale, const float* __restrict__ mshift,
-                                                            int act, float slope, const u16* addend) {
+                                                            int act, float slope, const u16* addend,
+                                                            const u16* __restrict__ addend2) {
   RowTile t(C, VEC);
   if (t.lane_r >= t.rpi) return;
   const int64_t r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
@@ -422,11 +424,12 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const u16* __restrict_
 #pragma unroll UNR
     for (int64_t r = r0 + t.lane_r; r < r1; r += t.rpi) {
       const int64_t o = r * C + g * VEC;
-      float d[VEC], ov[VEC], xv[VEC], rr[VEC], av[VEC];
+      float d[VEC], ov[VEC], xv[VEC], rr[VEC], av[VEC], a2[VEC];
       ldv<NTL, VEC>(dout + o, d);
       ldv<NTL, VEC>(x + o, xv);
       if constexpr (MM == MM_OUT) ldv<NTL, VEC>(out + o, ov);
       if (addend) ldv<NTL, VEC>(addend + o, av);
+      if (addend2) ldv<NTL, VEC>(addend2 + o, a2);
       uint32_t mb = 0;
       if constexpr (MM == MM_BITS) mb = reinterpret_cast<const uint8_t*>(out)[o >> 3];
 #pragma unroll
@@ -438,6 +441,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const u16* __restrict_
         rr[k] = dz;
         d[k] = fmaf(a[k], dz, fmaf(b[k], xv[k], cc[k]));
         if (addend) d[k] += av[k];
+        if (addend2) d[k] += a2[k];
       }
       VecIO<VEC>::store(dx + o, d);
       if (dres) VecIO<VEC>::store(dres + o, rr);
@@ -776,8 +780,9 @@ void dv_bn_bwd_finalize(float* acc, int C, double count, const float* gamma, con
 template <int MM, bool NTL>
 static void bwd_apply_launch(int g, const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t rows,
                              int C, int64_t rpb, const float* kA, const float* kB, const float* kC, const float* mscale,
-                             const float* mshift, int act, float slope, const void* addend, hipStream_t st) {
-#define BA_ARGS <<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, (u16*)dx, (u16*)dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, (const u16*)addend)
+                             const float* mshift, int act, float slope, const void* addend, const void* addend2,
+                             hipStream_t st) {
+#define BA_ARGS <<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, (u16*)dx, (u16*)dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, (const u16*)addend, (const u16*)addend2)
   switch (vec_for(C)) {
     case 8: bn_bwd_apply_kernel<8, MM, 2, NTL> BA_ARGS; break;
     case 4: bn_bwd_apply_kernel<4, MM, 2, NTL> BA_ARGS; break;
@@ -791,7 +796,7 @@ template <bool NTL>
 static void bwd_apply_dispatch(const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t n, int C,
                                const float* kA, const float* kB, const float* kC, const float* mscale,
                                const float* mshift, int act, float slope, int mask_bits, const void* addend,
-                               hipStream_t st) {
+                               const void* addend2, hipStream_t st) {
   const int v = vec_for(C);
   const int64_t rows = n / C;
   const int64_t rpb = apply_rows_per_block(rows, C, v);
@@ -799,27 +804,27 @@ static void bwd_apply_dispatch(const void* dout, const void* out, const void* x,
   if (act && mask_bits && v == 8 && g_apply_unroll == 4) {
     bn_bwd_apply_kernel<8, MM_BITS, 4, NTL><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, (u16*)dx,
                                                            (u16*)dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope,
-                                                           (const u16*)addend);
+                                                           (const u16*)addend, (const u16*)addend2);
     return;
   }
   if (act && mask_bits && v == 8) {
     bn_bwd_apply_kernel<8, MM_BITS, 2, NTL><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, (u16*)dx,
                                                         (u16*)dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope,
-                                                        (const u16*)addend);
+                                                        (const u16*)addend, (const u16*)addend2);
     return;
   }
-  if (!act) bwd_apply_launch<MM_NONE, NTL>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, addend, st);
-  else if (out) bwd_apply_launch<MM_OUT, NTL>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, addend, st);
-  else bwd_apply_launch<MM_X, NTL>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, addend, st);
+  if (!act) bwd_apply_launch<MM_NONE, NTL>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, addend, addend2, st);
+  else if (out) bwd_apply_launch<MM_OUT, NTL>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, addend, addend2, st);
+  else bwd_apply_launch<MM_X, NTL>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, addend, addend2, st);
 }
 
 void dv_bn_bwd_apply(const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t n, int C,
                      const float* kA, const float* kB, const float* kC, const float* mscale, const float* mshift, int act,
-                     float slope, int mask_bits, const void* addend, hipStream_t st) {
+                     float slope, int mask_bits, const void* addend, const void* addend2, hipStream_t st) {
   if (n >= NT_LOAD_MIN_ELEMS)
-    bwd_apply_dispatch<true>(dout, out, x, dx, dres, n, C, kA, kB, kC, mscale, mshift, act, slope, mask_bits, addend, st);
+    bwd_apply_dispatch<true>(dout, out, x, dx, dres, n, C, kA, kB, kC, mscale, mshift, act, slope, mask_bits, addend, addend2, st);
   else
-    bwd_apply_dispatch<false>(dout, out, x, dx, dres, n, C, kA, kB, kC, mscale, mshift, act, slope, mask_bits, addend, st);
+    bwd_apply_dispatch<false>(dout, out, x, dx, dres, n, C, kA, kB, kC, mscale, mshift, act, slope, mask_bits, addend, addend2, st);
 }
 
 void dv_bn_bwd_apply_dual(const void* dout, const void* bits, const void* x, const void* x2, void* dx, void* dx2,

@@ -148,7 +148,7 @@ void dv_bn_bwd_finalize(float* acc, int C, double count, const float* gamma, con
                         float* xsum = nullptr);
 void dv_bn_bwd_apply(const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t n, int C,
                      const float* kA, const float* kB, const float* kC, const float* mscale, const float* mshift, int act,
-                     float slope, int mask_bits, const void* addend, hipStream_t st);
+                     float slope, int mask_bits, const void* addend, const void* addend2, hipStream_t st);
 // both BatchNorms of a residual block's output join (main + folded projection BN, one mask):
 // dz = act'(z)*dout from the mask bits, dx = kA*dz + kB*x + kC, dx2 = kA2*dz + kB2*x2 + kC2
 void dv_bn_bwd_apply_dual(const void* dout, const void* bits, const void* x, const void* x2, void* dx, void* dx2,

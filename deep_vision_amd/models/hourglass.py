@@ -65,6 +65,7 @@ def side_streams() -> int:
     return 2 if multi else 4
 _FORKED = set()  # recursion depths whose up1 branch was forked (tests)
 HANDOFF_STATS = True  # a block's conv3 epilogue accumulates the next block's pre-activation BN statistics
+LEVEL_JOIN = True  # an hourglass level input's three gradients are summed in one BN backward pass
 
 
 def _fork(x):
@@ -122,10 +123,11 @@ class BottleneckBlock(tnn.Module):
         self.bn3 = _bn(filters // 2)
         self.conv3 = nn.Conv2d(filters // 2, filters, 1)
 
-    def forward(self, x, next_bn=None):
+    def forward(self, x, next_bn=None, join=None):
         # identity blocks: x's two gradients (the residual path's dy and BN1's dx) meet in BN1's
-        # backward apply pass (GradJoin) instead of an autograd add -- 73 add passes per step
-        j = GradJoin() if self.downsample is None and F.native(x) else None
+        # backward apply pass (GradJoin) instead of an autograd add -- 73 add passes per step.
+        # ``join``: the hourglass level's (its pooled branch stashes a third gradient of x there)
+        j = (join or GradJoin()) if self.downsample is None and F.native(x) else None
         identity = self.downsample(x) if self.downsample is not None else x
         y = F.batch_norm_act(x, self.bn1, "relu", input_join=j, stats=_take_block_stats(self.bn1, x))
         y = F.conv_bn_act(y, self.conv1, self.bn2, "relu")
@@ -168,12 +170,13 @@ def _entry_bn(m):
     return None
 
 
-def _run_blocks(blocks, x, next_bn=None):
+def _run_blocks(blocks, x, next_bn=None, join=None):
     """A block sequence, each block handing the next one's BN statistics over (see
-    BottleneckBlock.forward); the last block hands over to ``next_bn``."""
+    BottleneckBlock.forward); the last block hands over to ``next_bn``. ``join``: the first
+    block's input gradient join (HourglassModule.forward)."""
     n = len(blocks)
     for i, b in enumerate(blocks):
-        x = b(x, next_bn=blocks[i + 1].bn1 if i + 1 < n else next_bn)
+        x = b(x, next_bn=blocks[i + 1].bn1 if i + 1 < n else next_bn, join=join if i == 0 else None)
     return x
 
 
@@ -189,25 +192,28 @@ class HourglassModule(tnn.Module):
             self.low2 = tnn.Sequential(*[BottleneckBlock(filters, filters) for _ in range(num_residual)])
         self.low3 = tnn.Sequential(*[BottleneckBlock(filters, filters) for _ in range(num_residual)])
 
-    def _low(self, x):
-        low = _run_blocks(self.low1, F.max_pool2d(x, 2, 2), next_bn=_entry_bn(self.low2))
+    def _low(self, x, join=None):
+        low = _run_blocks(self.low1, F.max_pool2d(x, 2, 2, input_join=join), next_bn=_entry_bn(self.low2))
         low = self.low2(low) if isinstance(self.low2, HourglassModule) else _run_blocks(self.low2, low)
         return _run_blocks(self.low3, low)
 
     def forward(self, x):
+        # x's gradients from up1 (block 0's BN1 and identity shortcut) and from the pool of the low
+        # branch all meet in block 0's BN1 backward apply pass: no autograd add at the level input
+        j = GradJoin() if LEVEL_JOIN and F.native(x) and self.up1[0].downsample is None else None
         if _fork(x):
             main = torch.cuda.current_stream(x.device)
             side = _side_stream(x.device, self.order)
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                up1 = _BranchEdge.apply(_run_blocks(self.up1, _BranchEdge.apply(x, main)), main)
-            low = self._low(x)
+                up1 = _BranchEdge.apply(_run_blocks(self.up1, _BranchEdge.apply(x, main), join=j), main)
+            low = self._low(x, j)
             main.wait_stream(side)
             x.record_stream(side)  # caching allocator: x is read on the side stream
             up1.record_stream(main)
             return F.upsample_add(low, up1, 2)
-        up1 = _run_blocks(self.up1, x)
-        return F.upsample_add(self._low(x), up1, 2)
+        up1 = _run_blocks(self.up1, x, join=j)
+        return F.upsample_add(self._low(x, j), up1, 2)
 
 
 class StackedHourglassNetwork(tnn.Module):
@@ -238,8 +244,14 @@ class StackedHourglassNetwork(tnn.Module):
             x = _run_blocks(self.residual[i], self.hourglass[i](x))
             lin = self.linear[i]
             x = F.conv_bn_act(x, lin["conv"], lin["bn"], "relu")
-            y = self.heatmap[i](x)
+            # x feeds the heatmap conv and (but for the last stack) the re-injection conv: the
+            # latter's input gradient is summed in the heatmap conv's dgrad epilogue (GradJoin)
+            j = GradJoin() if i < self.num_stack - 1 and F.native(x) else None
+            hm = self.heatmap[i]
+            y = F.conv2d(x, hm.weight, hm.bias, join=j, join_role="consumer") if j is not None else hm(x)
             ys.append(y)
             if i < self.num_stack - 1:
-                x = F.add(self.inter_x[i](x), self.inter_y[i](y))
+                ix = self.inter_x[i]
+                xi = F.conv2d(x, ix.weight, ix.bias, join=j, join_role="producer") if j is not None else ix(x)
+                x = F.add(xi, self.inter_y[i](y))
         return ys

@@ -27,7 +27,8 @@ FUSE_BWD_STATS = True  # fold the backward reduction into the consumer conv's dg
 LAZY_SHORTCUT = True   # identity-shortcut gradient masked inside the consumer's dgrad epilogue
 FOLD_RESIDUAL_BN = True  # projection-shortcut BN applied inside the block's last BN pass
 DUAL_BWD = True  # ...and its backward: reduction in the consumer dgrad's epilogue, one dual apply pass
-COUNTERS = {"bwd_reduce_fused": 0, "bwd_reduce_pass": 0, "shortcut_lazy": 0, "dual_apply": 0, "dual_fused": 0}
+COUNTERS = {"bwd_reduce_fused": 0, "bwd_reduce_pass": 0, "shortcut_lazy": 0, "dual_apply": 0, "dual_fused": 0,
+            "bwd_apply_two_addends": 0}
 
 
 class BNRef:
@@ -158,13 +159,21 @@ class _BNActFn(torch.autograd.Function):
         dev = x.device
         st = stream_handle()
         L = lib()
-        xg = ctx.xjoin.take() if ctx.xjoin is not None else None
+        xg, xg2 = ctx.xjoin.take2() if ctx.xjoin is not None else (None, None)
         pb_sink = pb_grad = None
         if xg is not None and not isinstance(xg, torch.Tensor):
             xg = xg.materialize()
-        # the other consumer's gradient is summed inside the apply pass, written over its own buffer
-        fold_x = (xg is not None and training and xg.dtype == BF16 and tuple(xg.shape) == tuple(x.shape)
-                  and xg.is_contiguous(memory_format=torch.channels_last))
+        if xg2 is not None and not isinstance(xg2, torch.Tensor):
+            xg2 = xg2.materialize()
+        foldable = lambda t: (t is not None and training and t.dtype == BF16  # noqa: E731
+                              and tuple(t.shape) == tuple(x.shape) and t.is_contiguous(memory_format=torch.channels_last))
+        # the other consumers' gradients are summed inside the apply pass, written over the first's buffer
+        fold_x = foldable(xg)
+        fold_x2 = fold_x and foldable(xg2)
+        if xg2 is not None and not fold_x2:
+            xg = xg2 if xg is None else xg + xg2
+            fold_x = foldable(xg)
+        COUNTERS["bwd_apply_two_addends"] += int(fold_x2)
         dx = xg if fold_x else torch.empty_like(x)
         # identity shortcut of a residual block: hand the shortcut consumer's dgrad the raw dout +
         # mask bits instead of writing dres = act'(z)*dout (csrc/conv_fwd.hip resbits epilogue)
@@ -207,7 +216,7 @@ class _BNActFn(torch.autograd.Function):
         if training and not dual:
             L.bn_bwd_apply(ptr(dout), ptr(out), ptr(x), ptr(dx), ptr(dres), x.numel(), C, ptr(coef[0]), ptr(coef[1]),
                            ptr(coef[2]), ptr(scale), ptr(shift), act, float(slope), int(ctx.bits), st,
-                           addend=ptr(xg) if fold_x else 0)
+                           addend=ptr(xg) if fold_x else 0, addend2=ptr(xg2) if fold_x2 else 0)
         elif not training:
             if act and out is None:  # eval backward needs the mask: rebuild the output
                 out = torch.empty_like(x)

@@ -328,29 +328,65 @@ class GradJoin:
     """Meeting point of two gradients of one tensor (a block input used by a conv and by a
     residual add / projection conv). Whichever backward runs first stashes or announces itself;
     the second folds the sum into the consumer conv's dgrad epilogue (no separate add pass).
-    Order-independent: the producer only stashes while the consumer has not run yet."""
+    Order-independent: the producer only stashes while the consumer has not run yet.
 
-    __slots__ = ("grad", "consumer_done")
+    Two producers (an hourglass level input: the block's identity shortcut and the pooled low
+    branch, models/hourglass.py) fill two slots that a BN backward apply pass sums together
+    (take2); a producer on another HIP stream than the consumer (the level's up1 branch runs on a
+    side stream) is ordered before it by a stream wait at take time."""
+
+    __slots__ = ("grad", "grad2", "consumer_done", "streams")
 
     def __init__(self):
-        self.grad = None
+        self.grad = self.grad2 = None
         self.consumer_done = False
+        self.streams = []
 
     def produce(self, g):
         """Producer side: returns the gradient to hand to autograd (None when stashed)."""
         if g is None or self.consumer_done:
             return g.materialize() if isinstance(g, MaskedGrad) else g
-        self.grad = g if self.grad is None else self.grad + g
+        t = g.grad if isinstance(g, MaskedGrad) else g
+        if t.is_cuda:
+            self.streams.append(torch.cuda.current_stream(t.device))
+        if self.grad is None:
+            self.grad = g
+        elif self.grad2 is None:
+            self.grad2 = g
+        else:
+            self.grad = self.grad + g
         return None
 
     def can_stash(self):
         """True when a produced gradient would be stashed (not handed to autograd)."""
         return not self.consumer_done and self.grad is None
 
-    def take(self):
-        """Consumer side: the stashed gradient (or None), marking the consumer as done."""
-        g, self.grad = self.grad, None
+    def _sync(self, *gs):
+        """Order the producers' streams before the current one; the stashed buffers are then in
+        use on the current stream too (caching allocator)."""
+        for s in self.streams:
+            cur = torch.cuda.current_stream(s.device)
+            if s != cur:
+                cur.wait_stream(s)
+                for g in gs:
+                    for t in ((g.grad, g.bits) if isinstance(g, MaskedGrad) else (g,)):
+                        if isinstance(t, torch.Tensor) and t.is_cuda:
+                            t.record_stream(cur)
+        self.streams = []
+
+    def take2(self):
+        """Consumer side: both stashed gradients (either may be None), marking the consumer done."""
+        g, g2 = self.grad, self.grad2
+        self.grad = self.grad2 = None
         self.consumer_done = True
+        self._sync(*(t for t in (g, g2) if t is not None))
+        return g, g2
+
+    def take(self):
+        """Consumer side: the (summed) stashed gradient or None, marking the consumer as done."""
+        g, g2 = self.take2()
+        if g2 is not None:
+            g = g + g2
         return g
 
 

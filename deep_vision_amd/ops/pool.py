@@ -39,7 +39,7 @@ def _dense(x):
 
 class _MaxPoolFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, k, s, p, ceil_mode):
+    def forward(ctx, x, k, s, p, ceil_mode, join=None):
         N, C, H, W = x.shape
         P = pool_out(H, k[0], s[0], p[0], ceil_mode)
         Q = pool_out(W, k[1], s[1], p[1], ceil_mode)
@@ -48,6 +48,7 @@ class _MaxPoolFn(torch.autograd.Function):
         lib().maxpool_fwd(ptr(x), ptr(y), ptr(idx), N, H, W, C, P, Q, k[0], k[1], s[0], s[1], p[0], p[1], stream_handle())
         ctx.save_for_backward(idx)
         ctx.cfg = (x.shape, k, s, p, P, Q)
+        ctx.join = join
         return y
 
     @staticmethod
@@ -58,17 +59,22 @@ class _MaxPoolFn(torch.autograd.Function):
         dy = _dense(grad_nhwc(dy))
         dx = torch.empty((N, C, H, W), dtype=BF16, device=dy.device, memory_format=CL)
         lib().maxpool_bwd(ptr(dy), ptr(idx), ptr(dx), N, H, W, C, P, Q, k[0], k[1], s[0], s[1], p[0], p[1], stream_handle())
-        return dx, None, None, None, None
+        if ctx.join is not None:
+            dx = ctx.join.produce(dx)
+        return dx, None, None, None, None, None
 
 
-def max_pool2d(x, kernel_size, stride=None, padding=0, ceil_mode=False):
+def max_pool2d(x, kernel_size, stride=None, padding=0, ceil_mode=False, input_join=None):
+    """``input_join`` (conv.GradJoin): x's gradient is stashed there for another consumer of x to
+    sum in its own backward pass (an hourglass level input, models/hourglass.py) -- only when x
+    is used as is (no layout copy in between)."""
     k = _pair(kernel_size)
     s = _pair(stride if stride is not None else kernel_size)
     p = _pair(padding)
     if not native(x):
         return TF.max_pool2d(x, k, s, p, ceil_mode=ceil_mode)
-    x = _dense(as_nhwc(x, pad_to8=False))
-    return _MaxPoolFn.apply(x, k, s, p, ceil_mode)
+    xd = _dense(as_nhwc(x, pad_to8=False))
+    return _MaxPoolFn.apply(xd, k, s, p, ceil_mode, input_join if xd is x else None)
 
 
 class _AvgPoolFn(torch.autograd.Function):

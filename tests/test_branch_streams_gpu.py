@@ -178,3 +178,40 @@ def test_block_statistics_handoff_matches_separate_pass():
     cos = lambda a, b: torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()
     assert cos(dx0, dx1) > 0.999 and cos(g0, g1) > 0.999
     assert not any("_dv_block_stats" in b.__dict__ for b in blocks.modules())
+
+
+@pytest.mark.parametrize("forked", [False, True])
+def test_level_gradient_join_matches_autograd_adds(forked):
+    """An hourglass level input's three gradients (block 0's BN1, its identity shortcut, the pooled
+    low branch) summed in block 0's BN1 backward apply pass (models/hourglass.py LEVEL_JOIN) give
+    the autograd-add gradients -- single stream, and with up1 on a side stream (the pooled
+    gradient then crosses streams through the join)."""
+    from deep_vision_amd.models import hourglass as H
+    from deep_vision_amd.ops.bn import COUNTERS
+
+    torch.manual_seed(0)
+    level = H.HourglassModule(2, 128, 1).to(DEV)
+    x32 = torch.randn(8, 128, 16, 16, device=DEV)
+    res = {}
+    saved = H.BRANCH_STREAMS
+    try:
+        H.BRANCH_STREAMS = forked
+        for on in (False, True):
+            H.LEVEL_JOIN = on
+            m = copy.deepcopy(level)
+            x = x32.to(torch.bfloat16).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+            n0 = COUNTERS["bwd_apply_two_addends"]
+            y = m(x)
+            g = torch.randn(y.shape, device=DEV, generator=torch.Generator(device=DEV).manual_seed(1))
+            y.backward(g.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+            torch.cuda.synchronize()
+            res[on] = (y.detach().float(), x.grad.float(), _grads(m), COUNTERS["bwd_apply_two_addends"] - n0)
+    finally:
+        H.LEVEL_JOIN = True
+        H.BRANCH_STREAMS = saved
+    (y0, dx0, g0, n_off), (y1, dx1, g1, n_on) = res[False], res[True]
+    assert n_off == 0 and n_on == 2, (n_off, n_on)  # both levels folded their pooled gradient
+    assert torch.equal(y0, y1)
+    rel = lambda a, b: ((a - b).norm() / a.norm()).item()  # noqa: E731
+    assert rel(dx0, dx1) < 1e-2, rel(dx0, dx1)
+    assert rel(g0, g1) < 1e-2, rel(g0, g1)
