@@ -16,7 +16,6 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 typedef short i16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned short u16;
 
 #define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))

@@ -59,30 +59,20 @@ DV_DEVICE void glds16(const void* src, uint32_t dst) {  // dst: wave-uniform LDS
 // 16-byte-chunk XOR key of pixel row k (multiples of 2 chunks = 32-B blocks). Rows of >= 256 B
 // take 8 keys; 128-B rows (64 columns) take 4 keys and rely on the row parity for the other
 // half of the bank row. Both verified conflict-free for the tr-read lane groups.
-// W32 (32x32x16 fragments): a 32-lane half reads 4 consecutive rows x 32 columns (two 16-lane
-// groups side by side), so the 4 rows must land in different 64-B bank quarters: key (k & 3) * 4
-// chunks on >= 256-B rows; on 128-B rows (two per bank row) ((k >> 1) & 1) * 4 chunks.
-template <int COLS, bool W32 = false>
+template <int COLS>
 DV_DEVICE int mn_swz(int k) {
-  if constexpr (W32) {
-    if constexpr (COLS >= 128) return (k & 3) << 2;
-    else return ((k >> 1) & 1) << 2;
-  }
   if constexpr (COLS >= 128) return ((k & 3) | ((k >> 1) & 4)) << 1;
   else return (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 1;
 }
 
-// 8-element MFMA fragment from an MN image [64 k][COLS] via two transposed reads. Each 16-lane
-// group reads a 4-row x 16-column block and gets one column per lane, rows k..k+3 / k+4..k+7.
-// 16x16x32 operand (W32 false): lane = column col0 + lane % 16, k = kbase + 8 * (lane / 16) + 0..7;
-// 32x32x16 operand (W32): lane = column col0 + lane % 32, k = kbase + 8 * (lane / 32) + 0..7.
-template <int COLS, bool W32 = false>
+// 8-element MFMA fragment from an MN image [64 k][COLS] via two transposed reads.
+template <int COLS>
 DV_DEVICE bf16x8 read_mn(const char* img, int col0, int kbase, int lane) {
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const int k1 = kbase + (W32 ? 8 * (g >> 1) : 8 * g) + q, k2 = k1 + 4;
-  const int u = ((col0 + (W32 ? (g & 1) * 16 : 0)) >> 2) + p;
-  const char* a1 = img + k1 * (COLS * 2) + ((u ^ (mn_swz<COLS, W32>(k1) << 1)) << 3);
-  const char* a2 = img + k2 * (COLS * 2) + ((u ^ (mn_swz<COLS, W32>(k2) << 1)) << 3);
+  const int k1 = kbase + 8 * g + q, k2 = k1 + 4;
+  const int u = (col0 >> 2) + p;
+  const char* a1 = img + k1 * (COLS * 2) + ((u ^ (mn_swz<COLS>(k1) << 1)) << 3);
+  const char* a2 = img + k2 * (COLS * 2) + ((u ^ (mn_swz<COLS>(k2) << 1)) << 3);
   i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((i16x4 __attribute__((address_space(3)))*)LDS_PTR(a1));
   i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((i16x4 __attribute__((address_space(3)))*)LDS_PTR(a2));
   i16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -103,13 +93,11 @@ constexpr int wg_waves() { return (BM_ / WMT) * (BN_ / 64); }
 template <int BM_, int BN_>
 constexpr int wg_epi_rows() { return BM_ * (BN_ + F32_PAD) * 4 > 96 * 1024 ? BM_ / 2 : BM_; }
 
-// MF32: the wave tile as 32x32x16 MFMAs (2 x WMT/32 accumulators of 16) instead of 16x16x32
-// (4 x WMT/16 of 4): the same fragment bytes per K, half the MFMA instructions.
-template <int BM_, int BN_, bool PLAIN, int BK = 64, int STAGES = 2, int WMT = 64, bool MF32 = false>
+template <int BM_, int BN_, bool PLAIN, int BK = 64, int STAGES = 2, int WMT = 64>
 __global__ __launch_bounds__((64 * wg_waves<BM_, BN_, WMT>()), 2) void conv_wgrad_kernel(WgParams p) {
   constexpr int WN = BN_ / 64, WM = BM_ / WMT;
   constexpr int NW = WN * WM;
-  constexpr int FM = WMT / 16, FM2 = WMT / 32;
+  constexpr int FM = WMT / 16;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   constexpr int MCH = BM_ / 8, NCH = BN_ / 8;        // 16-B chunks per image row
   constexpr int MRPI = 64 / MCH, NRPI = 64 / NCH;    // image rows per 1-KB DMA instruction
@@ -140,7 +128,7 @@ __global__ __launch_bounds__((64 * wg_waves<BM_, BN_, WMT>()), 2) void conv_wgra
 #pragma unroll
   for (int j = 0; j < MI; ++j) {
     const int row = (wid * MI + j) * MRPI + lane / MCH;
-    const int lc = (lane % MCH) ^ mn_swz<BM_, MF32>(row);
+    const int lc = (lane % MCH) ^ mn_swz<BM_>(row);
     const int m = m0 + lc * 8;
     mok[j] = m < p.M;
     mrow[j] = p.dy + (int64_t)row * p.ldm + (int64_t)grp * p.M + (mok[j] ? m : 0);
@@ -159,7 +147,7 @@ __global__ __launch_bounds__((64 * wg_waves<BM_, BN_, WMT>()), 2) void conv_wgra
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
     const int row = (wid * NI + j) * NRPI + lane / NCH;
-    const int lc = (lane % NCH) ^ mn_swz<BN_, MF32>(row);
+    const int lc = (lane % NCH) ^ mn_swz<BN_>(row);
     const int n = n0 + lc * 8;
     nok[j] = n < p.N;
     const int nn = nok[j] ? n : 0;
@@ -236,21 +224,11 @@ __global__ __launch_bounds__((64 * wg_waves<BM_, BN_, WMT>()), 2) void conv_wgra
     }
   };
 
-  f32x4 acc[MF32 ? 1 : 4][MF32 ? 1 : FM];
-  f32x16 acc32[MF32 ? 2 : 1][MF32 ? FM2 : 1];
-  if constexpr (MF32) {
+  f32x4 acc[4][FM];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int b = 0; b < FM2; ++b)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc32[a][b][r] = 0.f;
-  } else {
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int b = 0; b < FM; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
+    for (int b = 0; b < FM; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // every fragment of the tile is read before the first MFMA (sched_barrier): left to itself the
   // scheduler recycled one fragment register per 4 MFMAs and waited on each re-read, exposing
@@ -263,27 +241,6 @@ __global__ __launch_bounds__((64 * wg_waves<BM_, BN_, WMT>()), 2) void conv_wgra
     if (!live) return;
     const char* img_m = smem + buf * STAGE;
     const char* img_n = img_m + MBYTES;
-    if constexpr (MF32) {
-      constexpr int K16 = BK / 16;
-      bf16x8 fa[K16][2], fb[K16][FM2];
-#pragma unroll
-      for (int kk = 0; kk < K16; ++kk) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) fa[kk][j] = read_mn<BN_, true>(img_n, wave_n * 64 + j * 32, kk * 16, lane);
-#pragma unroll
-        for (int i = 0; i < FM2; ++i) fb[kk][i] = read_mn<BM_, true>(img_m, wave_m * WMT + i * 32, kk * 16, lane);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int kk = 0; kk < K16; ++kk)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int i = 0; i < FM2; ++i)
-            acc32[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[kk][j], fb[kk][i], acc32[j][i], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      return;
-    }
     constexpr int KK = BK / 32;
     bf16x8 fa[KK][4], fb[KK][FM];
 #pragma unroll
@@ -364,20 +321,7 @@ __global__ __launch_bounds__((64 * wg_waves<BM_, BN_, WMT>()), 2) void conv_wgra
 #pragma unroll
   for (int pass = 0; pass < BM_ / ER; ++pass) {
     if (pass) __syncthreads();  // the previous pass's rows have been read back
-    if (MF32 && wave_m * WMT / ER == pass) {
-      // acc32[j][i][r]: n_local = wave_n*64 + j*32 + 8*(r/4) + 4*(lane/32) + r%4, m_local = wave_m*WMT + i*32 + lane%32
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int i = 0; i < FM2; ++i)
-#pragma unroll
-          for (int g4 = 0; g4 < 4; ++g4) {
-            const int nl = wave_n * 64 + j * 32 + 8 * g4 + 4 * (lane >> 5);
-            const int ml = wave_m * WMT + i * 32 + (lane & 31) - pass * ER;
-            *reinterpret_cast<f32x4*>(&T[ml * LD + nl]) =
-                f32x4{acc32[j][i][4 * g4], acc32[j][i][4 * g4 + 1], acc32[j][i][4 * g4 + 2], acc32[j][i][4 * g4 + 3]};
-          }
-    } else if (wave_m * WMT / ER == pass) {
+    if (wave_m * WMT / ER == pass) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -411,17 +355,17 @@ constexpr int wg_lds_bytes() {
 }
 
 // p.ktiles_per_split arrives in 64-pixel units; BKW = 32 kernels walk twice as many tiles
-template <int BM_, int BN_, bool PLAIN, int BKW = 64, int STAGES = 2, int WMT = 64, bool MF32 = false>
+template <int BM_, int BN_, bool PLAIN, int BKW = 64, int STAGES = 2, int WMT = 64>
 void launch_wg(WgParams p, int blocks, hipStream_t st) {
   static bool attr = false;
   constexpr int lds = wg_lds_bytes<BM_, BN_, BKW, STAGES>();
   if (!attr) {
-    hipFuncSetAttribute((const void*)conv_wgrad_kernel<BM_, BN_, PLAIN, BKW, STAGES, WMT, MF32>,
+    hipFuncSetAttribute((const void*)conv_wgrad_kernel<BM_, BN_, PLAIN, BKW, STAGES, WMT>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
   p.ktiles_per_split *= BK / BKW;
-  conv_wgrad_kernel<BM_, BN_, PLAIN, BKW, STAGES, WMT, MF32>
+  conv_wgrad_kernel<BM_, BN_, PLAIN, BKW, STAGES, WMT>
       <<<dim3(blocks), dim3(64 * wg_waves<BM_, BN_, WMT>()), lds, st>>>(p);
 }
 
@@ -449,11 +393,6 @@ void dispatch_wg(const WgParams& p, int blocks_narrow, int blocks_wide, hipStrea
     case 5: return launch_wg<128, 128, PLAIN, 32, 4>(p, blocks_wide, st);
     case 6: return launch_wg<64, 256, PLAIN, 32, 4>(p, blocks_narrow, st);
     case 7: return launch_wg<128, 128, PLAIN, 64, 3>(p, blocks_wide, st);
-    // 32x32x16 MFMA wave tiles
-    case 10: return launch_wg<128, 128, PLAIN, 64, 2, 64, true>(p, blocks_wide, st);
-    case 11: return launch_wg<64, 256, PLAIN, 64, 2, 64, true>(p, blocks_narrow, st);
-    case 12: return launch_wg<128, 128, PLAIN, 32, 2, 64, true>(p, blocks_wide, st);
-    case 13: return launch_wg<256, 256, PLAIN, 64, 2, 128, true>(p, blocks_big, st);
     default: break;
   }
   if (wg_narrow(p.M, p.N)) launch_wg<64, 256, PLAIN>(p, blocks_narrow, st);
@@ -592,12 +531,12 @@ void dv_conv_wgrad_slab(int on) { g_wg_slab = on; }
 
 int dv_conv_wgrad_splits(const ConvWgradArgs& a) {
   const int M = a.Kout, N = a.R * a.S * a.Cg, K = a.Nb * a.P * a.Q;
-  const bool narrow = g_wg_variant == 2 || g_wg_variant == 4 || g_wg_variant == 6 || g_wg_variant == 11 ||
+  const bool narrow = g_wg_variant == 2 || g_wg_variant == 4 || g_wg_variant == 6 ||
                       (g_wg_variant == 0 && wg_narrow(M, N));
   // narrow 64x256 tiles (64-output-channel layers, few tiles): twice the blocks (s1 3x3x64 at
   // 56x56: 195 vs 214 us, profiles/wgbench_asm_dma.txt; the 1x1 narrow layers are flat)
   int tm = narrow ? 64 : 128, tn = narrow ? 256 : 128, target = narrow ? 768 : 384;
-  if (g_wg_variant == 8 || g_wg_variant == 13) { tm = 256; tn = 256; target = 256; }  // one 8-wave block per CU
+  if (g_wg_variant == 8) { tm = 256; tn = 256; target = 256; }  // one 8-wave block per CU
   if (g_wg_variant == 9) { tm = 256; tn = 128; target = 384; }
   const int tiles = cdiv(M, tm) * cdiv(N, tn) * a.G;
   const int ktiles = cdiv(K, BK);
