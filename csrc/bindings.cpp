@@ -128,13 +128,14 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("acc"), py::arg("C"), py::arg("count"), py::arg("gamma"), py::arg("mean"), py::arg("invstd"), py::arg("dgamma"),
      py::arg("dbeta"), py::arg("accumulate"), py::arg("kA"), py::arg("kB"), py::arg("kC"), py::arg("st"), py::arg("xsum") = 0);
   m.def("bn_bwd_apply", [](uptr dout, uptr out, uptr x, uptr dx, uptr dres, int64_t n, int C, uptr kA, uptr kB, uptr kC,
-                           uptr mscale, uptr mshift, int act, float slope, int mask_bits, uptr st, uptr addend, uptr addend2) {
+                           uptr mscale, uptr mshift, int act, float slope, int mask_bits, uptr st, uptr addend, uptr addend2,
+                           uptr colsum) {
     dv_bn_bwd_apply(CP(dout), CP(out), CP(x), P(dx), P(dres), n, C, CFP(kA), CFP(kB), CFP(kC), CFP(mscale), CFP(mshift), act, slope,
-                    mask_bits, CP(addend), CP(addend2), ST(st));
+                    mask_bits, CP(addend), CP(addend2), FP(colsum), ST(st));
     check_last("bn_bwd_apply");
   }, py::arg("dout"), py::arg("out"), py::arg("x"), py::arg("dx"), py::arg("dres"), py::arg("n"), py::arg("C"), py::arg("kA"),
      py::arg("kB"), py::arg("kC"), py::arg("mscale"), py::arg("mshift"), py::arg("act"), py::arg("slope"),
-     py::arg("mask_bits"), py::arg("st"), py::arg("addend") = 0, py::arg("addend2") = 0);
+     py::arg("mask_bits"), py::arg("st"), py::arg("addend") = 0, py::arg("addend2") = 0, py::arg("colsum") = 0);
   m.def("bn_bwd_apply_dual", [](uptr dout, uptr bits, uptr x, uptr x2, uptr dx, uptr dx2, int64_t n, int C, uptr k,
                                 uptr k2, int act, float slope, uptr st) {
     if (C % 8 || n % C) throw std::runtime_error("bn_bwd_apply_dual: channels must be a multiple of 8");
@@ -146,9 +147,14 @@ PYBIND11_MODULE(_C, m) {
   });
 
   m.def("maxpool_fwd", [](uptr x, uptr y, uptr idx, int N, int H, int W, int C, int P_, int Q, int kh, int kw, int sh, int sw,
-                          int ph, int pw, uptr st) {
-    dv_maxpool_fwd(CP(x), P(y), reinterpret_cast<uint8_t*>(idx), N, H, W, C, P_, Q, kh, kw, sh, sw, ph, pw, ST(st)); check_last("maxpool_fwd");
-  });
+                          int ph, int pw, uptr st, uptr stats) {
+    const int r = dv_maxpool_fwd(CP(x), P(y), reinterpret_cast<uint8_t*>(idx), N, H, W, C, P_, Q, kh, kw, sh, sw, ph, pw,
+                                 FP(stats), ST(st));
+    check_last("maxpool_fwd");
+    return r;
+  }, py::arg("x"), py::arg("y"), py::arg("idx"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("P"),
+     py::arg("Q"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("st"),
+     py::arg("stats") = 0);
   m.def("maxpool_bwd", [](uptr dy, uptr idx, uptr dx, int N, int H, int W, int C, int P_, int Q, int kh, int kw, int sh,
                           int sw, int ph, int pw, uptr st) {
     dv_maxpool_bwd(CP(dy), reinterpret_cast<const uint8_t*>(idx), P(dx), N, H, W, C, P_, Q, kh, kw, sh, sw, ph, pw, ST(st)); check_last("maxpool_bwd");
@@ -179,7 +185,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("gap_fwd", [](uptr x, uptr y, int N, int HW, int C, uptr st) { dv_gap_fwd(CP(x), P(y), N, HW, C, ST(st)); check_last("gap_fwd"); });
   m.def("gap_bwd", [](uptr dy, uptr dx, int N, int HW, int C, uptr st) { dv_gap_bwd(CP(dy), P(dx), N, HW, C, ST(st)); check_last("gap_bwd"); });
   m.def("upsample_fwd", [](uptr x, uptr y, int N, int H, int W, int C, int f, uptr st) { dv_upsample_fwd(CP(x), P(y), N, H, W, C, f, ST(st)); check_last("upsample_fwd"); });
-  m.def("upsample_add", [](uptr x, uptr r, uptr y, int N, int H, int W, int C, int f, uptr st) { dv_upsample_add(CP(x), CP(r), P(y), N, H, W, C, f, ST(st)); check_last("upsample_add"); });
+  m.def("upsample_add", [](uptr x, uptr r, uptr y, int N, int H, int W, int C, int f, uptr st, uptr stats) {
+    const int rc = dv_upsample_add(CP(x), CP(r), P(y), N, H, W, C, f, FP(stats), ST(st));
+    check_last("upsample_add");
+    return rc;
+  }, py::arg("x"), py::arg("r"), py::arg("y"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("f"),
+     py::arg("st"), py::arg("stats") = 0);
   m.def("upsample_bwd", [](uptr dy, uptr dx, int N, int H, int W, int C, int f, uptr st) { dv_upsample_bwd(CP(dy), P(dx), N, H, W, C, f, ST(st)); check_last("upsample_bwd"); });
 
   m.def("act_fwd", [](uptr x, uptr y, int64_t n, int act, float slope, uptr st) { dv_act_fwd(CP(x), P(y), n, act, slope, ST(st)); check_last("act_fwd"); });
@@ -315,6 +326,10 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("sumsq", [](uptr x, int64_t n, uptr out, uptr st) { dv_sumsq(CFP(x), n, FP(out), ST(st)); check_last("sumsq"); });
 
+  m.def("channel_sum_finalize", [](uptr acc, int ld, int C, uptr out, int accumulate, uptr st) {
+    dv_channel_sum_finalize(FP(acc), ld, C, FP(out), accumulate, ST(st));
+    check_last("channel_sum_finalize");
+  }, py::arg("acc"), py::arg("ld"), py::arg("C"), py::arg("out"), py::arg("accumulate"), py::arg("st"));
   m.def("channel_sum", [](uptr x, int64_t rows, int ld, int C, uptr acc, uptr out, int accumulate, uptr st) {
     dv_channel_sum(CP(x), rows, ld, C, FP(acc), FP(out), accumulate, ST(st));
     check_last("channel_sum");

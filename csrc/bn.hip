@@ -401,7 +401,9 @@ __global__ void bn_bwd_finalize_kernel(float* __restrict__ acc, int C, double co
 // other gradients of the same input (a pre-activation block's residual path, an hourglass level's
 // pooled branch -- models/hourglass.py) summed in this pass instead of separate adds; ``addend``
 // may alias dx (each element is read before it is written by the same thread), hence no
-// __restrict__ on the two.
+// __restrict__ on the two. ``colsum``: per-channel sums of dx into a [SHARDS][2][C] accumulator --
+// the bias gradient of the conv that produced x when dx is x's whole gradient (models/hourglass.py
+// block outputs), instead of a separate reduction pass over it. Host: C / VEC <= NT.
 template <int VEC, int MM, int UNR = 2, bool NTL = false>
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const u16* __restrict__ dout, const u16* __restrict__ out,
                                                             const u16* __restrict__ x, u16* dx, u16* __restrict__ dres,
@@ -409,11 +411,15 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const u16* __restrict_
                                                             const float* __restrict__ kB, const float* __restrict__ kC,
                                                             const float* __restrict__ mscale, const float* __restrict__ mshift,
                                                             int act, float slope, const u16* addend,
-                                                            const u16* __restrict__ addend2) {
+                                                            const u16* __restrict__ addend2, float* __restrict__ colsum) {
   RowTile t(C, VEC);
-  if (t.lane_r >= t.rpi) return;
+  const bool live = t.lane_r < t.rpi;
+  if (!live && !colsum) return;
   const int64_t r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
-  for (int g = t.lane_c; g < t.cg; g += t.tpr) {
+  float cs[VEC];
+#pragma unroll
+  for (int k = 0; k < VEC; ++k) cs[k] = 0.f;
+  for (int g = live ? t.lane_c : t.cg; g < t.cg; g += t.tpr) {
     float a[VEC], b[VEC], cc[VEC], ms[VEC], mh[VEC];
 #pragma unroll
     for (int k = 0; k < VEC; ++k) {
@@ -442,9 +448,24 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const u16* __restrict_
         d[k] = fmaf(a[k], dz, fmaf(b[k], xv[k], cc[k]));
         if (addend) d[k] += av[k];
         if (addend2) d[k] += a2[k];
+        cs[k] += d[k];
       }
       VecIO<VEC>::store(dx + o, d);
       if (dres) VecIO<VEC>::store(dres + o, rr);
+    }
+  }
+  if (colsum) {  // [row lane][channel] partials -> one coalesced atomic row per block
+    __shared__ float csh[NT * VEC];
+    if (live) {
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) csh[t.lane_r * C + t.lane_c * VEC + k] = cs[k];
+    }
+    __syncthreads();
+    float* a = stat_row(colsum, nullptr, blockIdx.x, C);
+    for (int ch = threadIdx.x; ch < C; ch += NT) {
+      float v = 0.f;
+      for (int rr = 0; rr < t.rpi; ++rr) v += csh[rr * C + ch];
+      atomicAdd(a + ch, v);
     }
   }
 }
@@ -673,6 +694,10 @@ void dv_channel_sum(const void* x, int64_t rows, int ld, int C, float* acc, floa
   channel_sum_finalize_kernel<<<(ld + 63) / 64, 256, 0, st>>>(acc, ld, C, out, accumulate);
 }
 
+void dv_channel_sum_finalize(float* acc, int ld, int C, float* out, int accumulate, hipStream_t st) {
+  channel_sum_finalize_kernel<<<(ld + 63) / 64, 256, 0, st>>>(acc, ld, C, out, accumulate);
+}
+
 void dv_bn_finalize(float* acc, int C, double count, float eps, float momentum, const float* gamma,
                     const float* beta, float* rm, float* rv, float* save_mean, float* save_invstd, float* scale,
                     float* shift, hipStream_t st) {
@@ -781,8 +806,8 @@ template <int MM, bool NTL>
 static void bwd_apply_launch(int g, const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t rows,
                              int C, int64_t rpb, const float* kA, const float* kB, const float* kC, const float* mscale,
                              const float* mshift, int act, float slope, const void* addend, const void* addend2,
-                             hipStream_t st) {
-#define BA_ARGS <<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, (u16*)dx, (u16*)dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, (const u16*)addend, (const u16*)addend2)
+                             float* colsum, hipStream_t st) {
+#define BA_ARGS <<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, (u16*)dx, (u16*)dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, (const u16*)addend, (const u16*)addend2, colsum)
   switch (vec_for(C)) {
     case 8: bn_bwd_apply_kernel<8, MM, 2, NTL> BA_ARGS; break;
     case 4: bn_bwd_apply_kernel<4, MM, 2, NTL> BA_ARGS; break;
@@ -796,7 +821,7 @@ template <bool NTL>
 static void bwd_apply_dispatch(const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t n, int C,
                                const float* kA, const float* kB, const float* kC, const float* mscale,
                                const float* mshift, int act, float slope, int mask_bits, const void* addend,
-                               const void* addend2, hipStream_t st) {
+                               const void* addend2, float* colsum, hipStream_t st) {
   const int v = vec_for(C);
   const int64_t rows = n / C;
   const int64_t rpb = apply_rows_per_block(rows, C, v);
@@ -804,27 +829,29 @@ static void bwd_apply_dispatch(const void* dout, const void* out, const void* x,
   if (act && mask_bits && v == 8 && g_apply_unroll == 4) {
     bn_bwd_apply_kernel<8, MM_BITS, 4, NTL><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, (u16*)dx,
                                                            (u16*)dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope,
-                                                           (const u16*)addend, (const u16*)addend2);
+                                                           (const u16*)addend, (const u16*)addend2, colsum);
     return;
   }
   if (act && mask_bits && v == 8) {
     bn_bwd_apply_kernel<8, MM_BITS, 2, NTL><<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, (u16*)dx,
                                                         (u16*)dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope,
-                                                        (const u16*)addend, (const u16*)addend2);
+                                                        (const u16*)addend, (const u16*)addend2, colsum);
     return;
   }
-  if (!act) bwd_apply_launch<MM_NONE, NTL>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, addend, addend2, st);
-  else if (out) bwd_apply_launch<MM_OUT, NTL>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, addend, addend2, st);
-  else bwd_apply_launch<MM_X, NTL>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, addend, addend2, st);
+  if (!act) bwd_apply_launch<MM_NONE, NTL>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, addend, addend2, colsum, st);
+  else if (out) bwd_apply_launch<MM_OUT, NTL>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, addend, addend2, colsum, st);
+  else bwd_apply_launch<MM_X, NTL>(g, dout, out, x, dx, dres, rows, C, rpb, kA, kB, kC, mscale, mshift, act, slope, addend, addend2, colsum, st);
 }
 
 void dv_bn_bwd_apply(const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t n, int C,
                      const float* kA, const float* kB, const float* kC, const float* mscale, const float* mshift, int act,
-                     float slope, int mask_bits, const void* addend, const void* addend2, hipStream_t st) {
+                     float slope, int mask_bits, const void* addend, const void* addend2, float* colsum,
+                     hipStream_t st) {
+  if (colsum && C / vec_for(C) > NT) throw std::runtime_error("bn_bwd_apply colsum: C / VEC must be <= 256");
   if (n >= NT_LOAD_MIN_ELEMS)
-    bwd_apply_dispatch<true>(dout, out, x, dx, dres, n, C, kA, kB, kC, mscale, mshift, act, slope, mask_bits, addend, addend2, st);
+    bwd_apply_dispatch<true>(dout, out, x, dx, dres, n, C, kA, kB, kC, mscale, mshift, act, slope, mask_bits, addend, addend2, colsum, st);
   else
-    bwd_apply_dispatch<false>(dout, out, x, dx, dres, n, C, kA, kB, kC, mscale, mshift, act, slope, mask_bits, addend, addend2, st);
+    bwd_apply_dispatch<false>(dout, out, x, dx, dres, n, C, kA, kB, kC, mscale, mshift, act, slope, mask_bits, addend, addend2, colsum, st);
 }
 
 void dv_bn_bwd_apply_dual(const void* dout, const void* bits, const void* x, const void* x2, void* dx, void* dx2,

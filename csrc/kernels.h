@@ -148,7 +148,8 @@ void dv_bn_bwd_finalize(float* acc, int C, double count, const float* gamma, con
                         float* xsum = nullptr);
 void dv_bn_bwd_apply(const void* dout, const void* out, const void* x, void* dx, void* dres, int64_t n, int C,
                      const float* kA, const float* kB, const float* kC, const float* mscale, const float* mshift, int act,
-                     float slope, int mask_bits, const void* addend, const void* addend2, hipStream_t st);
+                     float slope, int mask_bits, const void* addend, const void* addend2, float* colsum,
+                     hipStream_t st);
 // both BatchNorms of a residual block's output join (main + folded projection BN, one mask):
 // dz = act'(z)*dout from the mask bits, dx = kA*dz + kB*x + kC, dx2 = kA2*dz + kB2*x2 + kC2
 void dv_bn_bwd_apply_dual(const void* dout, const void* bits, const void* x, const void* x2, void* dx, void* dx2,
@@ -157,8 +158,9 @@ void dv_bn_bwd_eval(const void* dout, const void* out, void* dx, void* dres, int
                     int act, float slope, hipStream_t st);
 
 // ---- pooling (pool.hip) ----
-void dv_maxpool_fwd(const void* x, void* y, uint8_t* idx, int N, int H, int W, int C, int P, int Q, int kh, int kw,
-                    int sh, int sw, int ph, int pw, hipStream_t st);
+// stats: fused BatchNorm statistics of y into a [SHARDS][2][C] + shift accumulator (-1: unsupported C)
+int dv_maxpool_fwd(const void* x, void* y, uint8_t* idx, int N, int H, int W, int C, int P, int Q, int kh, int kw,
+                   int sh, int sw, int ph, int pw, float* stats, hipStream_t st);
 void dv_maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, int N, int H, int W, int C, int P, int Q, int kh,
                     int kw, int sh, int sw, int ph, int pw, hipStream_t st);
 // fused BatchNorm apply + activation + max pool (ResNet stem); -1 = shape not covered
@@ -175,7 +177,8 @@ void dv_avgpool_bwd(const void* dy, void* dx, int N, int H, int W, int C, int P,
 void dv_gap_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st);
 void dv_gap_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st);
 void dv_upsample_fwd(const void* x, void* y, int N, int H, int W, int C, int f, hipStream_t st);
-void dv_upsample_add(const void* x, const void* r, void* y, int N, int H, int W, int C, int f, hipStream_t st);
+int dv_upsample_add(const void* x, const void* r, void* y, int N, int H, int W, int C, int f, float* stats,
+                    hipStream_t st);
 void dv_upsample_bwd(const void* dy, void* dx, int N, int H, int W, int C, int f, hipStream_t st);
 
 // ---- elementwise / layout (elementwise.hip) ----
@@ -279,3 +282,5 @@ void dv_heatmaps(const int* px, const int* py, const int* vis, int N, int J, int
 // per-channel fp32 sum of a bf16 [rows][ld] tensor into out[C] (accumulate: +=); acc is a
 // zeroed [SHARDS][2][ld] workspace that the call leaves zeroed
 void dv_channel_sum(const void* x, int64_t rows, int ld, int C, float* acc, float* out, int accumulate, hipStream_t st);
+// the fold half of dv_channel_sum: shards (filled by a fused producer, e.g. dv_bn_bwd_apply colsum) -> out
+void dv_channel_sum_finalize(float* acc, int ld, int C, float* out, int accumulate, hipStream_t st);

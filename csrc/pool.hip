@@ -29,10 +29,43 @@ template <> struct V<1> {
 
 struct PoolGeo { int N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw; };
 
+// Fused BatchNorm statistics of a grid-stride kernel's output (the consumer BN then skips its own
+// statistics pass; models/hourglass.py pooled / upsampled block inputs): with C / VEC dividing NT
+// a thread keeps one channel group for the whole grid-stride loop, sums d = v - K and d^2 (K: the
+// BN's shift row, ops.bn) of the stored bf16 values, and the block's NT / cg threads of a channel
+// group meet in LDS -> one coalesced atomic row per block into the [SHARDS][2][C] accumulator.
+struct PoolStats {
+  float* acc;  // nullptr: no statistics
+  float* det;  // deterministic mode: this launch's per-block rows
+};
+template <int VEC>
+DV_DEVICE void pool_stats_commit(const float* s, const float* q, const PoolStats& ps, int C) {
+  __shared__ float sh[2][NT * VEC];
+  const int tid = threadIdx.x, cg = C / VEC, rpi = NT / cg;
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) { sh[0][tid * VEC + i] = s[i]; sh[1][tid * VEC + i] = q[i]; }
+  __syncthreads();
+  float* a = stat_row(ps.acc, ps.det, blockIdx.x, C);
+  for (int ch = tid; ch < C; ch += NT) {
+    const int gi = ch / VEC, i = ch - gi * VEC;
+    float ss = 0.f, qq = 0.f;
+    for (int r = 0; r < rpi; ++r) { ss += sh[0][(r * cg + gi) * VEC + i]; qq += sh[1][(r * cg + gi) * VEC + i]; }
+    atomicAdd(a + ch, ss);
+    atomicAdd(a + C + ch, qq);
+  }
+}
+
 template <int VEC>
 __global__ __launch_bounds__(NT) void maxpool_fwd_kernel(const u16* __restrict__ x, u16* __restrict__ y,
-                                                           uint8_t* __restrict__ idx, PoolGeo g, int64_t total) {
+                                                           uint8_t* __restrict__ idx, PoolGeo g, int64_t total,
+                                                           PoolStats ps) {
   const int cg = g.C / VEC;
+  float ss[VEC], sq[VEC], kq[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    ss[i] = 0.f; sq[i] = 0.f;
+    kq[i] = ps.acc ? stat_shift(ps.acc, g.C)[(threadIdx.x % cg) * VEC + i] : 0.f;
+  }
   for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < total; t += (int64_t)gridDim.x * NT) {
     const int c = (int)(t % cg) * VEC;
     int64_t pix = t / cg;
@@ -59,7 +92,12 @@ __global__ __launch_bounds__(NT) void maxpool_fwd_kernel(const u16* __restrict__
 #pragma unroll
       for (int i = 0; i < VEC; ++i) idx[o + i] = (uint8_t)bi[i];
     }
+    if (ps.acc) {  // the window maxima are bf16 values already
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) { const float d = best[i] - kq[i]; ss[i] += d; sq[i] = fmaf(d, d, sq[i]); }
+    }
   }
+  if (ps.acc) pool_stats_commit<VEC>(ss, sq, ps, g.C);
 }
 
 template <int VEC>
@@ -223,9 +261,16 @@ __global__ __launch_bounds__(NT) void upsample_fwd_kernel(const u16* __restrict_
 // instead of an upsample pass + an add pass over the upsampled tensor (16 per step)
 template <int VEC>
 __global__ __launch_bounds__(NT) void upsample_add_kernel(const u16* __restrict__ x, const u16* __restrict__ r,
-                                                            u16* __restrict__ y, int N, int H, int W, int C, int f) {
+                                                            u16* __restrict__ y, int N, int H, int W, int C, int f,
+                                                            PoolStats ps) {
   const int cg = C / VEC, OH = H * f, OW = W * f;
   const int64_t total = (int64_t)N * OH * OW * cg;
+  float ss[VEC], sq[VEC], kq[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    ss[i] = 0.f; sq[i] = 0.f;
+    kq[i] = ps.acc ? stat_shift(ps.acc, C)[(threadIdx.x % cg) * VEC + i] : 0.f;
+  }
   for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < total; t += (int64_t)gridDim.x * NT) {
     const int c = (int)(t % cg) * VEC; int64_t pix = t / cg;
     const int ow = (int)(pix % OW); pix /= OW; const int oh = (int)(pix % OH); const int n = (int)(pix / OH);
@@ -236,7 +281,15 @@ __global__ __launch_bounds__(NT) void upsample_add_kernel(const u16* __restrict_
 #pragma unroll
     for (int i = 0; i < VEC; ++i) a[i] += b[i];
     V<VEC>::st(y + o, a);
+    if (ps.acc) {  // statistics of the stored (bf16-rounded) sums
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        const float d = bf2f(f2bf(a[i])) - kq[i];
+        ss[i] += d; sq[i] = fmaf(d, d, sq[i]);
+      }
+    }
   }
+  if (ps.acc) pool_stats_commit<VEC>(ss, sq, ps, C);
 }
 
 template <int VEC>
@@ -622,12 +675,26 @@ inline int grid_for(int64_t total) {
 
 #define VDISPATCH(C, K, ...) do { if ((C) % 8 == 0) K<8> __VA_ARGS__; else K<1> __VA_ARGS__; } while (0)
 
-void dv_maxpool_fwd(const void* x, void* y, uint8_t* idx, int N, int H, int W, int C, int P, int Q, int kh, int kw,
-                    int sh, int sw, int ph, int pw, hipStream_t st) {
+// statistics-fused launches (stats != nullptr): C % 8 == 0 with C / 8 dividing NT (else -1, no
+// launch), a grid of at most 1,024 blocks (one atomic row each)
+static bool pool_stats_ok(int C) { return C % 8 == 0 && NT % (C / 8) == 0; }
+static int stats_grid(int64_t total) { return (int)std::min<int64_t>(grid_for(total), 1024); }
+
+int dv_maxpool_fwd(const void* x, void* y, uint8_t* idx, int N, int H, int W, int C, int P, int Q, int kh, int kw,
+                   int sh, int sw, int ph, int pw, float* stats, hipStream_t st) {
   PoolGeo g{N, H, W, C, P, Q, kh, kw, sh, sw, ph, pw};
   const int v = C % 8 == 0 ? 8 : 1;
   const int64_t total = (int64_t)N * P * Q * (C / v);
-  VDISPATCH(C, maxpool_fwd_kernel, <<<grid_for(total), NT, 0, st>>>((const u16*)x, (u16*)y, idx, g, total));
+  if (stats) {
+    if (!pool_stats_ok(C)) return -1;
+    const int grid = stats_grid(total);
+    DetStats d(grid, C, st);
+    maxpool_fwd_kernel<8><<<grid, NT, 0, st>>>((const u16*)x, (u16*)y, idx, g, total, PoolStats{stats, d.slab});
+    d.fold(stats);
+    return 0;
+  }
+  VDISPATCH(C, maxpool_fwd_kernel, <<<grid_for(total), NT, 0, st>>>((const u16*)x, (u16*)y, idx, g, total, PoolStats{nullptr, nullptr}));
+  return 0;
 }
 void dv_maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, int N, int H, int W, int C, int P, int Q, int kh,
                     int kw, int sh, int sw, int ph, int pw, hipStream_t st) {
@@ -721,9 +788,20 @@ void dv_upsample_fwd(const void* x, void* y, int N, int H, int W, int C, int f, 
   const int v = C % 8 == 0 ? 8 : 1;
   VDISPATCH(C, upsample_fwd_kernel, <<<grid_for((int64_t)N * H * W * f * f * C / v), NT, 0, st>>>((const u16*)x, (u16*)y, N, H, W, C, f));
 }
-void dv_upsample_add(const void* x, const void* r, void* y, int N, int H, int W, int C, int f, hipStream_t st) {
+int dv_upsample_add(const void* x, const void* r, void* y, int N, int H, int W, int C, int f, float* stats,
+                    hipStream_t st) {
   const int v = C % 8 == 0 ? 8 : 1;
-  VDISPATCH(C, upsample_add_kernel, <<<grid_for((int64_t)N * H * W * f * f * C / v), NT, 0, st>>>((const u16*)x, (const u16*)r, (u16*)y, N, H, W, C, f));
+  const int64_t total = (int64_t)N * H * W * f * f * C / v;
+  if (stats) {
+    if (!pool_stats_ok(C)) return -1;
+    const int grid = stats_grid(total);
+    DetStats d(grid, C, st);
+    upsample_add_kernel<8><<<grid, NT, 0, st>>>((const u16*)x, (const u16*)r, (u16*)y, N, H, W, C, f, PoolStats{stats, d.slab});
+    d.fold(stats);
+    return 0;
+  }
+  VDISPATCH(C, upsample_add_kernel, <<<grid_for(total), NT, 0, st>>>((const u16*)x, (const u16*)r, (u16*)y, N, H, W, C, f, PoolStats{nullptr, nullptr}));
+  return 0;
 }
 void dv_upsample_bwd(const void* dy, void* dx, int N, int H, int W, int C, int f, hipStream_t st) {
   const int v = C % 8 == 0 ? 8 : 1;

@@ -40,7 +40,7 @@ from .. import nn
 from .. import ops as F
 from ..ops.bn import STAT_ROWS, STAT_SHARDS
 from ..ops.common import workspace
-from ..ops.conv import GradJoin
+from ..ops.conv import ColsumBox, GradJoin
 
 
 import os
@@ -66,6 +66,7 @@ def side_streams() -> int:
 _FORKED = set()  # recursion depths whose up1 branch was forked (tests)
 HANDOFF_STATS = True  # a block's conv3 epilogue accumulates the next block's pre-activation BN statistics
 LEVEL_JOIN = True  # an hourglass level input's three gradients are summed in one BN backward pass
+BIAS_COLSUM = True  # conv3's bias gradient from the next block's BN1 backward apply pass
 
 
 def _fork(x):
@@ -129,33 +130,38 @@ class BottleneckBlock(tnn.Module):
         # ``join``: the hourglass level's (its pooled branch stashes a third gradient of x there)
         j = (join or GradJoin()) if self.downsample is None and F.native(x) else None
         identity = self.downsample(x) if self.downsample is not None else x
-        y = F.batch_norm_act(x, self.bn1, "relu", input_join=j, stats=_take_block_stats(self.bn1, x))
+        stats, box = _take_block_stats(self.bn1, x)
+        y = F.batch_norm_act(x, self.bn1, "relu", input_join=j, stats=stats, colsum=box)
         y = F.conv_bn_act(y, self.conv1, self.bn2, "relu")
         y = F.conv_bn_act(y, self.conv2, self.bn3, "relu")
         # the residual add rides in conv3's store epilogue (ops.conv2d residual=); when the next
         # block's pre-activation BN is known, the same epilogue accumulates that BN's batch
         # statistics of the block output (no separate statistics pass over it)
         if HANDOFF_STATS and next_bn is not None and next_bn.training and F.native(y):
-            sbuf = workspace(next_bn, "bn_fwd", (STAT_ROWS, self.conv3.out_channels), y.device)
+            C = self.conv3.out_channels
+            sbuf = workspace(next_bn, "bn_fwd", (STAT_ROWS, C), y.device)
+            # ... and the next block's BN1 backward sums this conv's output gradient for its bias
+            box = (ColsumBox(workspace(next_bn, "bias_colsum", (STAT_ROWS, C), y.device))
+                   if BIAS_COLSUM and self.conv3.bias is not None else None)
             out, st = F.conv2d(y, self.conv3.weight, self.conv3.bias, residual=identity, residual_join=j,
-                               want_stats=True, stats_buf=sbuf)
+                               want_stats=True, stats_buf=sbuf, bias_colsum=box)
             if st is not None:
-                next_bn.__dict__["_dv_block_stats"] = (out.data_ptr(), out._version, tuple(out.shape), st)
+                next_bn.__dict__["_dv_block_stats"] = (out.data_ptr(), out._version, tuple(out.shape), st, box)
             return out
         return F.conv2d(y, self.conv3.weight, self.conv3.bias, residual=identity, residual_join=j)
 
 
 def _take_block_stats(bn, x):
-    """The statistics a producing block's conv3 epilogue accumulated for ``bn`` -- if they are of
-    exactly ``x``; otherwise their shards are cleared (the workspace must be clean for the
-    statistics pass the BN then runs itself)."""
+    """(statistics, bias-colsum box) a producing block's conv3 handed ``bn`` -- if they are of
+    exactly ``x``; otherwise the statistics shards are cleared (the workspace must be clean for the
+    statistics pass the BN then runs itself) and the conv reduces its own bias gradient."""
     pre = bn.__dict__.pop("_dv_block_stats", None)
     if pre is None:
-        return None
+        return None, None
     if pre[:3] == (x.data_ptr(), x._version, tuple(x.shape)):
-        return pre[3]
+        return pre[3], pre[4]
     pre[3][: 2 * STAT_SHARDS].zero_()
-    return None
+    return None, None
 
 
 def _entry_bn(m):
@@ -193,11 +199,15 @@ class HourglassModule(tnn.Module):
         self.low3 = tnn.Sequential(*[BottleneckBlock(filters, filters) for _ in range(num_residual)])
 
     def _low(self, x, join=None):
-        low = _run_blocks(self.low1, F.max_pool2d(x, 2, 2, input_join=join), next_bn=_entry_bn(self.low2))
-        low = self.low2(low) if isinstance(self.low2, HourglassModule) else _run_blocks(self.low2, low)
+        low = _run_blocks(self.low1, _pool(x, join, self.low1[0].bn1), next_bn=_entry_bn(self.low2))
+        if isinstance(self.low2, HourglassModule):
+            low = self.low2(low, next_bn=self.low3[0].bn1)
+        else:
+            low = _run_blocks(self.low2, low, next_bn=self.low3[0].bn1)
         return _run_blocks(self.low3, low)
 
-    def forward(self, x):
+    def forward(self, x, next_bn=None):
+        # next_bn: the BN that reads this level's output (its statistics come from the merge pass)
         # x's gradients from up1 (block 0's BN1 and identity shortcut) and from the pool of the low
         # branch all meet in block 0's BN1 backward apply pass: no autograd add at the level input
         j = GradJoin() if LEVEL_JOIN and F.native(x) and self.up1[0].downsample is None else None
@@ -211,9 +221,39 @@ class HourglassModule(tnn.Module):
             main.wait_stream(side)
             x.record_stream(side)  # caching allocator: x is read on the side stream
             up1.record_stream(main)
-            return F.upsample_add(low, up1, 2)
+            return _merge(low, up1, next_bn)
         up1 = _run_blocks(self.up1, x, join=j)
-        return F.upsample_add(self._low(x, j), up1, 2)
+        return _merge(self._low(x, j), up1, next_bn)
+
+
+def _handoff(bn, like):
+    """bn's statistics workspace when a producer pass can accumulate them (bn trains, native path)."""
+    if HANDOFF_STATS and bn is not None and bn.training and F.native(like):
+        return workspace(bn, "bn_fwd", (STAT_ROWS, like.shape[1]), like.device)
+    return None
+
+
+def _hand_over(bn, y, st):
+    if st is not None:
+        bn.__dict__["_dv_block_stats"] = (y.data_ptr(), y._version, tuple(y.shape), st, None)
+    return y
+
+
+def _pool(x, join, bn):
+    """2x2 max pool of a level input; the pass also accumulates the statistics of the first low1
+    block's pre-activation BN (csrc/pool.hip maxpool_fwd stats) -- no separate statistics pass."""
+    sbuf = _handoff(bn, x)
+    if sbuf is None:
+        return F.max_pool2d(x, 2, 2, input_join=join)
+    return _hand_over(bn, *F.max_pool2d(x, 2, 2, input_join=join, stats_buf=sbuf))
+
+
+def _merge(low, up1, next_bn):
+    """The level merge upsample(low) + up1, accumulating next_bn's statistics when known."""
+    sbuf = _handoff(next_bn, up1)
+    if sbuf is None:
+        return F.upsample_add(low, up1, 2)
+    return _hand_over(next_bn, *F.upsample_add(low, up1, 2, stats_buf=sbuf))
 
 
 class StackedHourglassNetwork(tnn.Module):
@@ -237,11 +277,11 @@ class StackedHourglassNetwork(tnn.Module):
     def forward(self, x):
         x = F.conv_bn_act(x, self.stem, self.stem_bn, "relu")
         x = _run_blocks(self.pre, x)
-        x = F.max_pool2d(x, 2, 2)
+        x = _pool(x, None, self.pre2[0].bn1)
         x = _run_blocks(self.pre2, x, next_bn=_entry_bn(self.hourglass[0]))
         ys = []
         for i in range(self.num_stack):
-            x = _run_blocks(self.residual[i], self.hourglass[i](x))
+            x = _run_blocks(self.residual[i], self.hourglass[i](x, next_bn=self.residual[i][0].bn1))
             lin = self.linear[i]
             x = F.conv_bn_act(x, lin["conv"], lin["bn"], "relu")
             # x feeds the heatmap conv and (but for the last stack) the re-injection conv: the

@@ -76,7 +76,7 @@ class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, stats, weight, bias, running_mean, running_var, residual, training, momentum, eps, act,
                 slope, ws_fwd, ws_bwd, join=None, refbox=None, r_stats=None, r_weight=None, r_bias=None, r_rm=None,
-                r_rv=None, r_cfg=None, xjoin=None, prod_bias=None, post_res=False):
+                r_rv=None, r_cfg=None, xjoin=None, prod_bias=None, post_res=False, colsum=None):
         # xjoin (conv.GradJoin): another consumer of ``x`` stashes its gradient there (e.g. the
         # identity path of a pre-activation block); the backward apply pass adds it in place
         # r_*: a second, training-mode BatchNorm applied to ``residual`` inside the same pass
@@ -134,6 +134,7 @@ class _BNActFn(torch.autograd.Function):
         ctx.ws_bwd = ws_bwd
         ctx.join = join
         ctx.xjoin = xjoin
+        ctx.colsum = colsum if (training and C % 8 == 0 and C <= 2048) else None
         ctx.has_prod_bias = prod_bias is not None
         ctx.prod_bias_param = prod_bias  # leaf parameter (not saved): its gradient may sink in place
         ctx.bnref = None
@@ -213,10 +214,18 @@ class _BNActFn(torch.autograd.Function):
         # residual join with the projection BN folded in: both input gradients from one pass
         dual = (DUAL_BWD and training and rprm is not None and ctx.bits and not fold_x and ctx.needs_input_grad[6]
                 and dout.is_contiguous(memory_format=torch.channels_last))
+        # the producing conv's bias gradient from this pass (conv.ColsumBox): only when dx is all of
+        # x's gradient this pass knows of (every joined gradient folded in)
+        box = ctx.colsum if (training and not dual and (xg is None or fold_x) and (xg2 is None or fold_x2)
+                             and not L.deterministic()) else None
         if training and not dual:
             L.bn_bwd_apply(ptr(dout), ptr(out), ptr(x), ptr(dx), ptr(dres), x.numel(), C, ptr(coef[0]), ptr(coef[1]),
                            ptr(coef[2]), ptr(scale), ptr(shift), act, float(slope), int(ctx.bits), st,
-                           addend=ptr(xg) if fold_x else 0, addend2=ptr(xg2) if fold_x2 else 0)
+                           addend=ptr(xg) if fold_x else 0, addend2=ptr(xg2) if fold_x2 else 0,
+                           colsum=ptr(box.acc) if box is not None else 0)
+            if box is not None:
+                box.pending, box.version = True, dx._version
+                dx._dv_colsum = box
         elif not training:
             if act and out is None:  # eval backward needs the mask: rebuild the output
                 out = torch.empty_like(x)
@@ -250,7 +259,7 @@ class _BNActFn(torch.autograd.Function):
 
             pb_grad = _channel_sum(dx if dx.shape[1] == C else dx.contiguous(memory_format=torch.channels_last))
         return (dx, None, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None, None, None,
-                None, r_dgamma, r_dbeta, None, None, None, None, pb_grad, None)
+                None, r_dgamma, r_dbeta, None, None, None, None, pb_grad, None, None)
 
 
 def _residual_bn_coef(ctx, dout, bits, r_x, rprm, r_weight, r_bias, act, slope, fused):
@@ -461,10 +470,12 @@ def bn_momentum(bn) -> float:
 
 
 def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None, residual_join=None, residual_bn=None,
-                   input_join=None, prod_bias=None, residual_post=False):
+                   input_join=None, prod_bias=None, residual_post=False, colsum=None):
     """act(BN(x) (+ residual)) with ``bn`` an nn.BatchNorm2d (parameters, buffers, mode).
     ``input_join`` (conv.GradJoin): x's gradient from another consumer, stashed there by its
     producer, is added inside this BN's backward apply pass.
+    ``colsum`` (conv.ColsumBox): x is a conv output with a bias; the backward apply pass sums x's
+    gradient per channel for that bias (see conv2d bias_colsum).
     ``residual_bn=(bn_r, stats_r)``: ``residual`` is a raw conv output still to be normalised by
     ``bn_r`` (training mode, batch statistics ``stats_r`` from its conv epilogue); the two BNs,
     the add and the activation run as one pass (see conv_bn_deferred)."""
@@ -508,7 +519,7 @@ def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None, residu
         rargs = (None,) * 6
     y = _BN_APPLY(x, stats, bn.weight, bn.bias, rm, rv, residual, training, mom,
                        bn.eps, ACT_IDS[act], float(slope), ws_fwd, ws_bwd, residual_join, refbox, *rargs, input_join,
-                       prod_bias, bool(residual_post and residual_bn is None))
+                       prod_bias, bool(residual_post and residual_bn is None), colsum)
     if refbox:
         y._dv_bnref = refbox[0]  # read by the consumer conv (ops.conv._ConvFn)
     return y

@@ -95,9 +95,36 @@ def _channel_sum(dy: torch.Tensor, out=None) -> torch.Tensor:
     return dst
 
 
-def _bias_grad(bias, dy):
+class ColsumBox:
+    """Bias-gradient hand-off from a consumer BatchNorm's backward apply pass (ops.bn, csrc/bn.hip
+    bn_bwd_apply colsum): the BN of a conv output sums its input gradient per channel while writing
+    it, into ``acc`` (self-cleaning shards), and tags the gradient tensor; the producing conv's
+    backward folds the shards into its bias gradient when the gradient it receives is exactly that
+    tensor (same object, same version -- no other gradient was added to it), instead of a reduction
+    pass over it. Otherwise the shards are cleared and the conv reduces dy itself."""
+
+    __slots__ = ("acc", "pending", "version")
+
+    def __init__(self, acc):
+        self.acc, self.pending, self.version = acc, False, -1
+
+
+COUNTERS_BIAS = {"colsum_fused": 0, "colsum_pass": 0}
+
+
+def _bias_grad(bias, dy, box=None):
     """Bias gradient straight into the live gradient buffer when there is one (None to autograd)."""
     sink = grad_sink(bias)
+    if box is not None and box.pending:
+        box.pending = False
+        if getattr(dy, "_dv_colsum", None) is box and dy._version == box.version:
+            COUNTERS_BIAS["colsum_fused"] += 1
+            C = dy.shape[1]
+            db = sink if sink is not None else torch.empty(C, dtype=F32, device=dy.device)
+            lib().channel_sum_finalize(ptr(box.acc), C, C, ptr(db), int(sink is not None), stream_handle())
+            return None if sink is not None else db
+        box.acc.zero_()
+    COUNTERS_BIAS["colsum_pass"] += 1
     db = _channel_sum(dy, out=sink)
     return None if sink is not None else db
 
@@ -437,7 +464,8 @@ class _ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, stride, padding, dilation, groups, act, slope, want_stats, stats_buf=None,
                 extra=(0, 0), join=None, join_role=None, reflect=False, out_box=None, residual=None, residual_join=None,
-                bias_via_bn=False):
+                bias_via_bn=False, bias_colsum=None):
+        ctx.colsum_box = bias_colsum
         N, Cx, H, W = x.shape
         O, Ig, R, S = weight.shape
         G = groups
@@ -489,8 +517,8 @@ class _ConvFn(torch.autograd.Function):
                 g = join.take()  # nothing to add to: hand a stashed shortcut gradient through
                 if isinstance(g, MaskedGrad):
                     g = g.materialize()
-                return (g, None, None) + (None,) * 16
-            return (None,) * 19
+                return (g, None, None) + (None,) * 17
+            return (None,) * 20
         dy = grad_nhwc(dy)
         if act:  # y and dy may be channel-slice views of concat buffers: strided rows kernel
             dy = act_grad(dy, y, act, slope)
@@ -513,11 +541,11 @@ class _ConvFn(torch.autograd.Function):
             if sink is not None:
                 dw = None
         if has_bias and ctx.needs_input_grad[2]:
-            db = _bias_grad(ctx.bias_param, dy)
+            db = _bias_grad(ctx.bias_param, dy, ctx.colsum_box)
         dres = dy if ctx.has_residual and ctx.needs_input_grad[16] else None  # y = ... + residual
         if dres is not None and ctx.rjoin is not None:
             dres = ctx.rjoin.produce(dres)
-        return dx, dw, db, None, None, None, None, None, None, None, None, None, None, None, None, None, dres, None, None
+        return dx, dw, db, None, None, None, None, None, None, None, None, None, None, None, None, None, dres, None, None, None
 
 
 # ---------------------------------------------------------------------------------------
@@ -643,8 +671,11 @@ class _StemConvFn(torch.autograd.Function):
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=None, slope=0.0,
            want_stats=False, stats_buf=None, join=None, join_role=None, pad_mode="zeros", out=None, residual=None,
-           residual_join=None, shuffle=0, bias_via_bn=False):
+           residual_join=None, shuffle=0, bias_via_bn=False, bias_colsum=None):
     """Conv2d (+fused bias/activation). Returns y, or (y, stats) when want_stats (GPU only).
+
+    ``bias_colsum`` (ColsumBox): the BN consuming y sums y's gradient per channel in its backward
+    apply pass; the bias gradient is folded from those sums (models/hourglass.py).
 
     ``shuffle=g`` (> 1): the output channels are channel-shuffled in g groups (ShuffleNet V1;
     fused into the grouped 1x1 kernel's store on the native path, csrc/gconv.hip).
@@ -748,7 +779,7 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=
         residual_join = None
     return _CONV_APPLY(xn, weight, bias, stride, padding, dilation, groups, ACT_IDS[act], float(slope), want_stats,
                          stats_buf, extra, join, join_role, reflect, [out] if out is not None else None, res,
-                         residual_join, bool(bias_via_bn and bias is not None and not act))
+                         residual_join, bool(bias_via_bn and bias is not None and not act), bias_colsum)
 
 
 def _gconv_ok(x, weight, bias, stride, padding, dilation, groups, act, join=None, out=None, residual=None,

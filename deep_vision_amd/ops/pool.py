@@ -39,13 +39,16 @@ def _dense(x):
 
 class _MaxPoolFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, k, s, p, ceil_mode, join=None):
+    def forward(ctx, x, k, s, p, ceil_mode, join=None, stats_box=None):
         N, C, H, W = x.shape
         P = pool_out(H, k[0], s[0], p[0], ceil_mode)
         Q = pool_out(W, k[1], s[1], p[1], ceil_mode)
         y = torch.empty((N, C, P, Q), dtype=BF16, device=x.device, memory_format=CL)
         idx = torch.empty((N, P, Q, C), dtype=torch.uint8, device=x.device) if x.requires_grad else None
-        lib().maxpool_fwd(ptr(x), ptr(y), ptr(idx), N, H, W, C, P, Q, k[0], k[1], s[0], s[1], p[0], p[1], stream_handle())
+        rc = lib().maxpool_fwd(ptr(x), ptr(y), ptr(idx), N, H, W, C, P, Q, k[0], k[1], s[0], s[1], p[0], p[1],
+                               stream_handle(), stats=ptr(stats_box[0]) if stats_box else 0)
+        if stats_box:
+            stats_box[1] = rc == 0
         ctx.save_for_backward(idx)
         ctx.cfg = (x.shape, k, s, p, P, Q)
         ctx.join = join
@@ -61,20 +64,24 @@ class _MaxPoolFn(torch.autograd.Function):
         lib().maxpool_bwd(ptr(dy), ptr(idx), ptr(dx), N, H, W, C, P, Q, k[0], k[1], s[0], s[1], p[0], p[1], stream_handle())
         if ctx.join is not None:
             dx = ctx.join.produce(dx)
-        return dx, None, None, None, None, None
+        return dx, None, None, None, None, None, None
 
 
-def max_pool2d(x, kernel_size, stride=None, padding=0, ceil_mode=False, input_join=None):
+def max_pool2d(x, kernel_size, stride=None, padding=0, ceil_mode=False, input_join=None, stats_buf=None):
     """``input_join`` (conv.GradJoin): x's gradient is stashed there for another consumer of x to
     sum in its own backward pass (an hourglass level input, models/hourglass.py) -- only when x
-    is used as is (no layout copy in between)."""
+    is used as is (no layout copy in between). ``stats_buf``: as upsample_add (returns (y, stats
+    or None))."""
     k = _pair(kernel_size)
     s = _pair(stride if stride is not None else kernel_size)
     p = _pair(padding)
+    box = [stats_buf, False] if stats_buf is not None else None
     if not native(x):
-        return TF.max_pool2d(x, k, s, p, ceil_mode=ceil_mode)
+        y = TF.max_pool2d(x, k, s, p, ceil_mode=ceil_mode)
+        return (y, None) if box is not None else y
     xd = _dense(as_nhwc(x, pad_to8=False))
-    return _MaxPoolFn.apply(xd, k, s, p, ceil_mode, input_join if xd is x else None)
+    y = _MaxPoolFn.apply(xd, k, s, p, ceil_mode, input_join if xd is x else None, box)
+    return (y, stats_buf if box[1] else None) if box is not None else y
 
 
 class _AvgPoolFn(torch.autograd.Function):
@@ -162,10 +169,13 @@ class _UpsampleFn(torch.autograd.Function):
 
 class _UpsampleAddFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, r, f):
+    def forward(ctx, x, r, f, stats_box=None):
         N, C, H, W = x.shape
         y = torch.empty_like(r)
-        lib().upsample_add(ptr(x), ptr(r), ptr(y), N, H, W, C, f, stream_handle())
+        rc = lib().upsample_add(ptr(x), ptr(r), ptr(y), N, H, W, C, f, stream_handle(),
+                                stats=ptr(stats_box[0]) if stats_box else 0)
+        if stats_box:
+            stats_box[1] = rc == 0
         ctx.cfg = (x.shape, f)
         return y
 
@@ -177,25 +187,32 @@ class _UpsampleAddFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.empty((N, C, H, W), dtype=BF16, device=dy.device, memory_format=CL)
             lib().upsample_bwd(ptr(dy), ptr(dx), N, H, W, C, f, stream_handle())
-        return dx, dy, None
+        return dx, dy, None, None
 
 
-def upsample_add(x, r, scale_factor=2):
+def upsample_add(x, r, scale_factor=2, stats_buf=None):
     """upsample_nearest(x, scale_factor) + r in one native pass (the Hourglass level merge,
-    R/Hourglass/tensorflow/hourglass104.py:95-97); r's gradient is the incoming one unchanged."""
+    R/Hourglass/tensorflow/hourglass104.py:95-97); r's gradient is the incoming one unchanged.
+    ``stats_buf`` (a BN's [STAT_ROWS, C] statistics workspace): the pass also accumulates the
+    batch statistics of its output for the BN that consumes it; returns (y, statistics or None)."""
     f = int(scale_factor)
+    box = [stats_buf, False] if stats_buf is not None else None
+
+    def ret(y):
+        return (y, stats_buf if box[1] else None) if box is not None else y
+
     if not native(x) or f != scale_factor:
         from .act import add
 
-        return add(upsample_nearest(x, scale_factor), r)
+        return ret(add(upsample_nearest(x, scale_factor), r))
     x = _dense(as_nhwc(x, pad_to8=False))
     r = _dense(as_nhwc(r, pad_to8=False))
     N, C, H, W = x.shape
     if tuple(r.shape) != (N, C, H * f, W * f) or r.dtype != BF16 or x.dtype != BF16:
         from .act import add
 
-        return add(upsample_nearest(x, scale_factor), r)
-    return _UpsampleAddFn.apply(x, r, f)
+        return ret(add(upsample_nearest(x, scale_factor), r))
+    return ret(_UpsampleAddFn.apply(x, r, f, box))
 
 
 def upsample_nearest(x, scale_factor=2):

@@ -215,3 +215,98 @@ def test_level_gradient_join_matches_autograd_adds(forked):
     rel = lambda a, b: ((a - b).norm() / a.norm()).item()  # noqa: E731
     assert rel(dx0, dx1) < 1e-2, rel(dx0, dx1)
     assert rel(g0, g1) < 1e-2, rel(g0, g1)
+
+
+def test_bias_gradient_from_bn_backward_matches_reduction_pass():
+    """conv3's bias gradient folded from the next block's BN1 backward apply pass (the pass sums
+    the gradient it writes, csrc/bn.hip bn_bwd_apply colsum; models/hourglass.py BIAS_COLSUM) equals
+    the separate per-channel reduction of that gradient; every other gradient is unchanged."""
+    from deep_vision_amd.models import hourglass as H
+    from deep_vision_amd.ops.conv import COUNTERS_BIAS
+
+    torch.manual_seed(0)
+    blocks = torch.nn.Sequential(*[H.BottleneckBlock(128, 128) for _ in range(3)]).to(DEV)
+    x32 = torch.randn(8, 128, 24, 24, device=DEV)
+    res = {}
+    try:
+        for on in (False, True):
+            H.BIAS_COLSUM = on
+            m = copy.deepcopy(blocks)
+            x = x32.to(torch.bfloat16).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+            n0 = COUNTERS_BIAS["colsum_fused"]
+            y = H._run_blocks(m, x)
+            g = torch.randn(y.shape, device=DEV, generator=torch.Generator(device=DEV).manual_seed(1))
+            y.backward(g.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+            torch.cuda.synchronize()
+            res[on] = ([p.grad.float().clone() for p in m.parameters()], x.grad.float(),
+                       COUNTERS_BIAS["colsum_fused"] - n0)
+    finally:
+        H.BIAS_COLSUM = True
+    (g0, dx0, n_off), (g1, dx1, n_on) = res[False], res[True]
+    assert n_off == 0 and n_on == 2, (n_off, n_on)  # blocks 0 and 1 hand their bias gradient over
+    assert torch.equal(dx0, dx1)
+    for i, (a, b) in enumerate(zip(g0, g1)):
+        rel = ((a - b).norm() / a.norm().clamp_min(1e-12)).item()
+        assert rel < 1e-3, (i, rel)
+
+
+@pytest.mark.parametrize("op", ["maxpool", "upsample_add"])
+def test_pool_fused_bn_statistics(op):
+    """max pool / upsample-add passes accumulating the consumer BN's statistics of their output
+    (csrc/pool.hip PoolStats): the shard sums equal the fp32 per-channel sum and sum of squares of
+    the stored output (shift row zero)."""
+    from deep_vision_amd import ops as F
+    from deep_vision_amd.ops.bn import STAT_ROWS, STAT_SHARDS
+
+    g = torch.Generator(device=DEV).manual_seed(4)
+    x = torch.randn(8, 256, 32, 32, device=DEV, generator=g).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    buf = torch.zeros((STAT_ROWS, 256), device=DEV)
+    if op == "maxpool":
+        y, st = F.max_pool2d(x, 2, 2, stats_buf=buf)
+        ref = torch.nn.functional.max_pool2d(x.float(), 2, 2)
+    else:
+        low = torch.randn(8, 256, 16, 16, device=DEV, generator=g).to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        y, st = F.upsample_add(low, x, 2, stats_buf=buf)
+        ref = (torch.nn.functional.interpolate(low.float(), scale_factor=2, mode="nearest") + x.float())
+    torch.cuda.synchronize()
+    assert st is not None
+    assert torch.allclose(y.float(), ref.to(torch.bfloat16).float())
+    sh = buf[: 2 * STAT_SHARDS].view(STAT_SHARDS, 2, 256).sum(0)
+    yf = y.float()
+    s_ref, q_ref = yf.sum((0, 2, 3)), (yf * yf).sum((0, 2, 3))
+    assert torch.allclose(sh[0], s_ref, rtol=1e-4, atol=1e-2), (sh[0] - s_ref).abs().max().item()
+    assert torch.allclose(sh[1], q_ref, rtol=1e-4, atol=1e-2), (sh[1] - q_ref).abs().max().item()
+
+
+def test_level_statistics_handoff_matches_separate_passes():
+    """A whole hourglass level with every pre-activation BN statistic handed over (conv3 epilogues,
+    the pool and the merge pass) trains like the level with separate statistics passes."""
+    from deep_vision_amd.models import hourglass as H
+
+    torch.manual_seed(0)
+    level = H.HourglassModule(2, 128, 1).to(DEV)
+    nxt = H.BottleneckBlock(128, 128).to(DEV)
+    x32 = torch.randn(8, 128, 16, 16, device=DEV) * 2 + 0.5
+    res = {}
+    try:
+        for on in (False, True):
+            H.HANDOFF_STATS = on
+            m, b = copy.deepcopy(level), copy.deepcopy(nxt)
+            x = x32.to(torch.bfloat16).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+            y = H._run_blocks([b], m(x, next_bn=b.bn1))
+            g = torch.randn(y.shape, device=DEV, generator=torch.Generator(device=DEV).manual_seed(1))
+            y.backward(g.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+            torch.cuda.synchronize()
+            res[on] = (y.detach().float(), x.grad.float(), _grads(m), torch.cat([bf.float() for bf in m.buffers()]),
+                       b.bn1.running_mean.clone())
+    finally:
+        H.HANDOFF_STATS = True
+    (y0, dx0, g0, b0, r0), (y1, dx1, g1, b1, r1) = res[False], res[True]
+    assert torch.allclose(r0, r1, rtol=1e-3, atol=1e-4)
+    assert ((b0 - b1).norm() / b0.norm()).item() < 1e-4
+    assert ((y0 - y1).norm() / y0.norm()).item() < 1e-2
+    cos = lambda a, b: torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()  # noqa: E731
+    assert cos(dx0, dx1) > 0.999 and cos(g0, g1) > 0.999
+    assert not any("_dv_block_stats" in mm.__dict__ for mm in list(m.modules()) + list(b.modules()))
