@@ -448,7 +448,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(const u16* __restrict_
         d[k] = fmaf(a[k], dz, fmaf(b[k], xv[k], cc[k]));
         if (addend) d[k] += av[k];
         if (addend2) d[k] += a2[k];
-        cs[k] += d[k];
+        cs[k] += bf2f(f2bf(d[k]));  // the stored value: the sum a reduction pass over dx would take
       }
       VecIO<VEC>::store(dx + o, d);
       if (dres) VecIO<VEC>::store(dres + o, rr);

@@ -299,7 +299,7 @@ def test_level_statistics_handoff_matches_separate_passes():
             g = torch.randn(y.shape, device=DEV, generator=torch.Generator(device=DEV).manual_seed(1))
             y.backward(g.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
             torch.cuda.synchronize()
-            res[on] = (y.detach().float(), x.grad.float(), _grads(m), torch.cat([bf.float() for bf in m.buffers()]),
+            res[on] = (y.detach().float(), x.grad.float(), _grads(m), torch.cat([bf.float().flatten() for bf in m.buffers() if bf.is_floating_point()]),
                        b.bn1.running_mean.clone())
     finally:
         H.HANDOFF_STATS = True

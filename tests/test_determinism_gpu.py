@@ -163,13 +163,26 @@ def test_deterministic_mode_matches_default_per_block(name):
     mod, shape = _block(name)
     x = torch.randn(shape, device=DEV, generator=torch.Generator(device=DEV).manual_seed(3))
     x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last) if shape[1] != 3 else x
-    a = _run_block(mod, x, False)
+    runs = [_run_block(mod, x, False) for _ in range(3)]
     b = _run_block(mod, x, True)
+    a = runs[0]
     rel = lambda u, v: ((u - v).norm() / u.norm().clamp_min(1e-12)).item()  # noqa: E731
+    # Some gradients are ill-conditioned sums (a BN gamma whose dz * xhat terms nearly cancel: in
+    # the ShuffleNet units a 3e-5 relative change of the input gradient, from the order of the
+    # default mode's float atomics, moves bn1.weight's gradient by up to 9 %, run to run --
+    # tools/diag_shuffle_block.py). The deterministic result must then lie as close to one of
+    # three default runs as those lie to each other; every well-conditioned tensor within 2e-2.
+    def check(what, k, i=None):
+        ts = [r[k] if i is None else r[k][i] for r in runs]
+        v = b[k] if i is None else b[k][i]
+        spread = max(rel(ts[0], ts[1]), rel(ts[0], ts[2]), rel(ts[1], ts[2]))
+        err = min(rel(t, v) for t in ts)
+        assert err < max(2e-2, 4 * spread), (what, i, err, spread)
+
     assert rel(a[0], b[0]) < 2e-3, ("output", rel(a[0], b[0]))
-    assert rel(a[1], b[1]) < 2e-2, ("input grad", rel(a[1], b[1]))
-    for i, (u, v) in enumerate(zip(a[2], b[2])):
-        assert rel(u, v) < 2e-2, ("param grad", i, rel(u, v))
+    check("input grad", 1)
+    for i in range(len(a[2])):
+        check("param grad", 2, i)
     for i, (u, v) in enumerate(zip(a[3], b[3])):
         assert rel(u, v) < 1e-4, ("buffer", i, rel(u, v))
 
