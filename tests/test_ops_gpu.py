@@ -524,7 +524,8 @@ def test_batched_weight_prep_matches_per_layer():
     wcache.clear()
     cases = [((64, 32, 3, 3), 1, 32, 0), ((64, 32, 3, 3), 1, 64, 1), ((48, 24, 1, 1), 2, 24, 0),
              ((48, 24, 1, 1), 2, 24, 1), ((100, 3, 7, 7), 1, 8, 0), ((100, 3, 7, 7), 1, 104, 1),
-             ((1000, 2048, 1, 1), 1, 2048, 0), ((1000, 2048, 1, 1), 1, 1000, 1)]
+             ((1000, 2048, 1, 1), 1, 2048, 0), ((1000, 2048, 1, 1), 1, 1000, 1),
+             ((96, 100, 3, 3), 1, 104, 0), ((64, 16, 3, 3), 4, 16, 0), ((32, 8, 5, 5), 1, 8, 0)]
     params = []
     for shape, G, pad, mode in cases:
         p = torch.nn.Parameter(torch.randn(*shape, device=DEV))
