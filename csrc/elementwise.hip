@@ -194,25 +194,6 @@ __global__ __launch_bounds__(256) void wprep_batched_kernel(const WprepDesc* __r
     }
     return;
   }
-  if (d.mode == 0 && d.R * d.S > 1 && d.R * d.S <= 64) {
-    // forward layout of a spatial filter: per (g*Og + o) and 64 input channels, the contiguous
-    // [64][R*S] source run -> LDS -> [R*S][64] output rows (both sides coalesced; the per-element
-    // walk below reads R*S-strided floats)
-    const int RS = d.R * d.S, ni = (d.pad + 63) / 64;
-    const int go = ch.y / ni, i0 = (ch.y - go * ni) * 64;
-    const float* src = d.w + (int64_t)go * d.Ig * RS;
-    for (int e = threadIdx.x; e < 64 * RS; e += 256) {
-      const int i = e / RS, rs = e - i * RS;
-      tile[i][rs] = (i0 + i < d.Ig) ? src[(int64_t)(i0 + i) * RS + rs] : 0.f;
-    }
-    __syncthreads();
-    u16* out = d.out + (int64_t)go * RS * d.pad;
-    for (int e = threadIdx.x; e < RS * 64; e += 256) {
-      const int rs = e >> 6, c = e & 63;
-      if (i0 + c < d.pad) out[(int64_t)rs * d.pad + i0 + c] = f2bf(tile[c][rs]);
-    }
-    return;
-  }
   // forward layout: out[g][o][r][s][i] (i padded; s padded to Sp in mode 2) -- reads stay inside
   // one filter row (cached)
   const int SS = d.mode == 2 ? d.Sp : d.S;

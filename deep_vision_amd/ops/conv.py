@@ -375,7 +375,7 @@ class GradJoin:
             return g.materialize() if isinstance(g, MaskedGrad) else g
         t = g.grad if isinstance(g, MaskedGrad) else g
         if t.is_cuda:
-            self.streams.append(torch.cuda.current_stream(t.device))
+            self.streams.append(stream_handle())  # raw handle: no Stream object on the hot path
         if self.grad is None:
             self.grad = g
         elif self.grad2 is None:
@@ -391,15 +391,17 @@ class GradJoin:
     def _sync(self, *gs):
         """Order the producers' streams before the current one; the stashed buffers are then in
         use on the current stream too (caching allocator)."""
-        for s in self.streams:
-            cur = torch.cuda.current_stream(s.device)
-            if s != cur:
-                cur.wait_stream(s)
-                for g in gs:
-                    for t in ((g.grad, g.bits) if isinstance(g, MaskedGrad) else (g,)):
-                        if isinstance(t, torch.Tensor) and t.is_cuda:
-                            t.record_stream(cur)
-        self.streams = []
+        if self.streams:
+            here = stream_handle()
+            for h in self.streams:
+                if h != here:
+                    cur = torch.cuda.current_stream()
+                    cur.wait_stream(torch.cuda.ExternalStream(h))
+                    for g in gs:
+                        for t in ((g.grad, g.bits) if isinstance(g, MaskedGrad) else (g,)):
+                            if isinstance(t, torch.Tensor) and t.is_cuda:
+                                t.record_stream(cur)
+            self.streams = []
 
     def take2(self):
         """Consumer side: both stashed gradients (either may be None), marking the consumer done."""

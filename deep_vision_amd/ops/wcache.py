@@ -68,8 +68,6 @@ def _build_table(device):
         if mode == 1:  # 64x64 transpose tiles per group (wprep_batched_kernel)
             K = Ig * R * S
             ntiles = G * ((K + 63) // 64) * ((pad + 63) // 64)
-        elif mode == 0 and 1 < R * S <= 64:  # [64 channels][R*S] tiles per output channel
-            ntiles = G * Og * ((pad + 63) // 64)
         else:
             ntiles = (total + chunk - 1) // chunk
         chunks += [(di, c) for c in range(ntiles)]
