@@ -93,6 +93,11 @@ __global__ __launch_bounds__(NT) void adam_kernel(float* __restrict__ p, const f
                                                     const float* __restrict__ hp, const float* __restrict__ skip) {
   if (skip && *skip != 0.f) return;
   if (hp) { lr = hp[0]; bc1 = hp[1]; bc2 = hp[2]; }
+  if (hp && skip) {  // device guard: the bias corrections count the steps actually applied (guard[4])
+    const float t = skip[4] + 1.f;
+    bc1 = 1.f - powf(b1, t);
+    bc2 = 1.f - powf(b2, t);
+  }
   for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
     float pv = p[i];
     float gv = g[i] * gscale;
@@ -135,7 +140,7 @@ __global__ __launch_bounds__(NT) void sumsq_kernel(const float* __restrict__ x, 
 }
 
 // Device-side non-finite guard (graph-captured steps: no host sync). guard = [flag, skipped total,
-// consecutive skips, last step's flag]. nonfinite_check ORs "any non-finite gradient" into flag
+// consecutive skips, last step's flag, steps applied]. nonfinite_check ORs "any non-finite gradient" into flag
 // (every finder stores the same 1.0: plain vector stores, no atomics); the optimizer kernels
 // read flag and skip the whole update; nonfinite_tally, the step's last launch, folds flag into
 // the counters and re-arms it for the next step. In a data-parallel step the checked buffer is
@@ -163,6 +168,7 @@ __global__ void nonfinite_tally_kernel(float* __restrict__ guard) {
   guard[1] += f;
   guard[2] = f != 0.f ? guard[2] + 1.f : 0.f;
   guard[3] = f;
+  guard[4] += 1.f - f;  // Adam's bias corrections under the guard count applied steps only
   guard[0] = 0.f;
 }
 

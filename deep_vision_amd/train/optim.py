@@ -179,14 +179,22 @@ class _FlatOptimizer(torch.optim.Optimizer):
         nonfinite_check / nonfinite_tally): every step checks the flat gradients, the update
         kernels become no-ops when any is Inf/NaN, and device counters record the skips -- no host
         synchronisation, so it works inside a captured step. The guard
-        tensor [flag, skipped, consecutive, last] is allocated once and never replaced (graphs
-        bake its pointer in). In a data-parallel step the checked gradients are the all-reduced
-        ones, identical on every rank: the ranks skip together without an extra collective."""
+        tensor [flag, skipped, consecutive, last, applied] is allocated once and never replaced
+        (graphs bake its pointer in). In a data-parallel step the checked gradients are the
+        all-reduced ones, identical on every rank: the ranks skip together without an extra
+        collective.
+
+        ``applied`` counts the steps actually taken (it starts at the host step count): Adam's
+        bias corrections read it under the guard, so a skipped replay does not advance them -- as
+        an eager skipped step, which never calls step(), does not. The host step count
+        (graph_tick, state_dict) and LR schedules still count every replay; the applied count is
+        ``step - skipped``."""
         self._dguard_on = bool(on)
         if on and getattr(self, "_dguard", None) is None:
             dev = next((f["param"].device for f in self._flat if f is not None), None)
             if dev is not None and dev.type == "cuda":
-                self._dguard = torch.zeros(4, dtype=torch.float32, device=dev)
+                done = max((f["step"] for f in self._flat if f is not None), default=0)
+                self._dguard = torch.tensor([0.0, 0.0, 0.0, 0.0, float(done)], dtype=torch.float32, device=dev)
 
     def _guard_active(self):
         return getattr(self, "_dguard_on", False) and getattr(self, "_dguard", None) is not None
@@ -332,6 +340,8 @@ class _FlatOptimizer(torch.optim.Optimizer):
                         f["step"] = int(float(st["step"]))
                 idx += 1
             f["first"] = not any_state
+        if getattr(self, "_dguard", None) is not None:  # the device guard's applied-step count follows
+            self._dguard[4] = float(max((f["step"] for f in self._flat if f is not None), default=0))
 
 
 class FusedSGD(_FlatOptimizer):

@@ -365,3 +365,59 @@ def test_engine_graph_step_with_comm_watchdog():
         assert eng.comm_watchdog.pending() <= 1
     finally:
         eng.comm_watchdog.stop()
+
+
+def test_captured_adam_skipped_step_keeps_bias_correction():
+    """a replay the device guard skips must not advance Adam's bias corrections (an eager
+    skipped step never calls step()). Captured run: warm-up, replay(x1), replay(NaN batch),
+    replay(x3); it must match eager steps on the same batches without the NaN one, and differ
+    from a run whose step count did advance over the skip."""
+    from deep_vision_amd import nn
+    from deep_vision_amd.train.graph import CapturedStep
+    from deep_vision_amd.train.optim import FusedAdam
+
+    torch.manual_seed(0)
+    base = nn.Linear(32, 16).to(DEV)
+    xs = [torch.randn(64, 32, device=DEV) for _ in range(3)]
+    bad = xs[1].clone()
+    bad[5, 3] = float("nan")
+
+    def make():
+        m = copy.deepcopy(base)
+        return m, FusedAdam(m.parameters(), lr=1e-2, betas=(0.9, 0.999))
+
+    def step_fn(m, opt):
+        def step(x):
+            opt.zero_grad()
+            loss = (m(x).float() ** 2).mean()
+            loss.backward()
+            opt.step()
+            return loss
+        return step
+
+    m, opt = make()
+    opt.use_device_guard(True)
+    cap = CapturedStep(step_fn(m, opt), opt, (xs[0].clone(),), model=m, warmup=2)
+    for x in (xs[0], bad, xs[2]):
+        cap(x)
+    torch.cuda.synchronize()
+    assert opt.device_guard_counts()[0] == 1
+    got = torch.cat([p.detach().flatten() for p in m.parameters()])
+
+    def eager(skip_advances):
+        me, oe = make()
+        st = step_fn(me, oe)
+        for x in (xs[0], xs[0], xs[0]):  # the two warm-up steps, then replay 1
+            st(x)
+        if skip_advances:
+            for f in oe._flat:
+                if f is not None:
+                    f["step"] += 1
+        st(xs[2])
+        torch.cuda.synchronize()
+        return torch.cat([p.detach().flatten() for p in me.parameters()])
+
+    ref, wrong = eager(False), eager(True)
+    rel = lambda a, b: ((a - b).norm() / b.norm()).item()  # noqa: E731
+    assert rel(got, ref) < 1e-4, (rel(got, ref), rel(got, wrong))
+    assert rel(wrong, ref) > 10 * rel(got, ref)
