@@ -626,6 +626,368 @@ bool plane_wgrad(const void* x, const void* dy, float* dw, const DwGeo& g, hipSt
   return true;
 }
 
+// Benchmark override of (strip length QT, minimum waves per SIMD) for the 3x3 strip kernels:
+// 0 = heuristic, 1 = (4, 4), 2 = (2, 4), 3 = (8, 2), 4 = (4, 2), 5 = (2, 2); 60 = LDS-tiled
+// stride-1 kernels everywhere, 61 = the strip / plane kernels everywhere, 62 = tiled with 4 rows
+// per thread.
+int g_dw_variant = 0;
+
+// ---------------------------------------------------------------- LDS-tiled stride 1 (fwd, dgrad)
+// One block = one image x NG*8 channels x a tile of RB*TH output rows x TW output columns. The
+// input halo ((RB*TH + KS-1) x (TW + KS-1) pixels x NG*8 channels, bf16) is staged ONCE by LDS-DMA
+// (global_load_lds_dwordx4: no VGPR staging, the zero page for the padding, one piece = 16 B = 8
+// channels of one pixel, pieces in (row, column, group) order so each 1-KB wave-instruction is 64
+// consecutive pieces). Then thread = (8-channel group, output column of a row band) streams its TH
+// output rows down the tile: every input row's KS columns are read from LDS once (ds_read_b128)
+// and feed up to KS output rows held in registers. Per output and 8 channels: KS LDS reads, 4*KS
+// unpacks and 4*KS*KS packed FMAs -- against the strip kernel's 4.5 global loads per output, each
+// with its own bounds / 64-bit address VALU (1,368 VALU per wave there, VALU-issue- and
+// latency-bound at 2-3 TB/s: profiles/pmc_dw_r5.txt).
+struct DwTileGeo {
+  int TW, RB, LCOLS, pieces, ncolt, nrowt;
+  FastDiv fd_lcols;
+};
+
+template <int KS, bool FLIP, bool BNR, int NG, int TH>
+__global__ __launch_bounds__(NT) void dw_tile_kernel(const u16* __restrict__ x, const float* __restrict__ w,
+                                                     const float* __restrict__ bias, u16* __restrict__ y, DwGeo g,
+                                                     DwTileGeo tg, int act, float slope, float* __restrict__ stats,
+                                                     DwBnr bnr, float* __restrict__ sdet) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int CW = NG * 8;  // channels per block
+  const int cb = (int)blockIdx.y * CW;
+  const int ct = (int)blockIdx.x % tg.ncolt, rest = (int)blockIdx.x / tg.ncolt;
+  const int rt = rest % tg.nrowt, n = rest / tg.nrowt;
+  const int p0 = rt * tg.RB * TH, q0 = ct * tg.TW;
+  const int h0 = p0 - g.ph, w0 = q0 - g.pw;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // ---- stage the halo: chunk k = pieces [64k, 64k + 64), one LDS-DMA wave-instruction ----
+  {
+    const u16* xb = x + (int64_t)n * g.H * g.W * g.ldx + cb;
+    const int nchunks = (tg.pieces + 63) >> 6;
+    for (int k = wid; k < nchunks; k += NT / 64) {
+      const int piece = k * 64 + lane;
+      const int pix = piece / NG, gi = piece & (NG - 1);
+      const int lr = (int)fdiv((uint32_t)pix, tg.fd_lcols), lc = pix - lr * tg.LCOLS;
+      const int h = h0 + lr, ww = w0 + lc;
+      const bool ok = piece < tg.pieces && (unsigned)h < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
+      const u16* src = ok ? xb + ((int64_t)h * g.W + ww) * g.ldx + gi * 8 : reinterpret_cast<const u16*>(dv_zero_page);
+      __builtin_amdgcn_global_load_lds(GLB_PTR(src), LDS_PTR(smem + k * 1024), 16, 0, 0);
+    }
+  }
+  const int gi = threadIdx.x & (NG - 1), pl = threadIdx.x / NG;
+  const int band = pl / tg.TW, c = pl - band * tg.TW;
+  const bool active = band < tg.RB;
+  const int c0 = cb + gi * 8;
+  f32x2 wr[KS * KS][4];
+#pragma unroll
+  for (int tp = 0; tp < KS * KS; ++tp)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int wt = FLIP ? KS * KS - 1 - tp : tp;
+      wr[tp][k] = f32x2{w[(c0 + 2 * k) * KS * KS + wt], w[(c0 + 2 * k + 1) * KS * KS + wt]};
+    }
+  f32x2 bv[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) bv[k] = bias ? f32x2{bias[c0 + 2 * k], bias[c0 + 2 * k + 1]} : f32x2{0.f, 0.f};
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int q = q0 + c;
+  const int pb = p0 + band * TH;  // first output row of this thread's band
+  // BN input of the fused BN-backward reduction at this thread's outputs, in flight during the FMAs
+  uint4 bxv[BNR ? TH : 1];
+  if constexpr (BNR) {
+#pragma unroll
+    for (int i = 0; i < TH; ++i) {
+      const bool ok = active && pb + i < g.P && q < g.Q;
+      bxv[i] = ok ? *reinterpret_cast<const uint4*>(bnr.x + (((int64_t)n * g.P + pb + i) * g.Q + q) * g.ldy + c0)
+                  : uint4{0u, 0u, 0u, 0u};
+    }
+  }
+  f32x2 acc[TH][4];
+#pragma unroll
+  for (int i = 0; i < TH; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[i][k] = bv[k];
+  if (active) {
+    const char* rp = smem + ((band * TH * tg.LCOLS + c) * NG + gi) * 16;
+    const int rowb = tg.LCOLS * NG * 16;
+#pragma unroll
+    for (int ir = 0; ir < TH + KS - 1; ++ir) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        f32x2 v[4];
+        ld8p(reinterpret_cast<const u16*>(rp + s * NG * 16), v);
+#pragma unroll
+        for (int r = 0; r < KS; ++r) {
+          const int i = ir - r;  // compile-time
+          if (i >= 0 && i < TH) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc[i][k] = pfma(v[k], wr[r * KS + s][k], acc[i][k]);
+          }
+        }
+      }
+      rp += rowb;
+    }
+  }
+  f32x2 ssum[4], ssq[4], nkq[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    ssum[k] = f32x2{0.f, 0.f}; ssq[k] = f32x2{0.f, 0.f};
+    nkq[k] = stats ? -f32x2{stat_shift(stats, g.C)[c0 + 2 * k], stat_shift(stats, g.C)[c0 + 2 * k + 1]}
+                   : f32x2{0.f, 0.f};
+  }
+  DwBnrLane bl;
+  if constexpr (BNR) bl.init(bnr, g.C, c0);
+  if (active && q < g.Q) {
+#pragma unroll
+    for (int i = 0; i < TH; ++i) {
+      if (pb + i >= g.P) break;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        f32x2 v = acc[i][k];
+        if (act == 1) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); }
+        else if (act == 2) { v.x = v.x > 0.f ? v.x : v.x * slope; v.y = v.y > 0.f ? v.y : v.y * slope; }
+        acc[i][k] = v;
+        if (stats) { const f32x2 d = v + nkq[k]; ssum[k] += d; ssq[k] = pfma(d, d, ssq[k]); }
+      }
+      st8p(y + (((int64_t)n * g.P + pb + i) * g.Q + q) * g.ldy + c0, acc[i]);
+      if constexpr (BNR) bl.add(bnr, acc[i], bxv[i]);
+    }
+  }
+  if (!stats && !BNR) return;
+  // ---- per-channel block sums (the tile is no longer read) -> one coalesced atomic row ----
+  __syncthreads();
+  float* sh0 = reinterpret_cast<float*>(smem);
+  float* sh1 = sh0 + NT * 8;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const f32x2 a = BNR ? bl.s[k] : ssum[k], b = BNR ? bl.q[k] : ssq[k];
+    sh0[pl * CW + gi * 8 + 2 * k] = a.x; sh0[pl * CW + gi * 8 + 2 * k + 1] = a.y;
+    sh1[pl * CW + gi * 8 + 2 * k] = b.x; sh1[pl * CW + gi * 8 + 2 * k + 1] = b.y;
+  }
+  __syncthreads();
+  if (threadIdx.x < CW) {
+    const int ch = threadIdx.x;
+    float s1v = 0.f, s2v = 0.f;
+    for (int r = 0; r < NT / NG; ++r) { s1v += sh0[r * CW + ch]; s2v += sh1[r * CW + ch]; }
+    if constexpr (BNR) {
+      float* a = stat_row(bnr.acc, bnr.det, blockIdx.x, g.C);
+      atomicAdd(a + cb + ch, s1v);
+      atomicAdd(a + g.C + cb + ch, s2v * bnr.prm[3 * g.C + cb + ch]);  // sum dz*(x-mean) * invstd
+    } else {
+      float* a = stat_row(stats, sdet, blockIdx.x, g.C);
+      atomicAdd(a + cb + ch, s1v);
+      atomicAdd(a + g.C + cb + ch, s2v);
+    }
+  }
+}
+
+// Weight gradient on the same tiles: dw[c][r][s] += sum_{n,p,q} dy[n][p][q][c] * x[n][p-ph+r][q-pw+s][c].
+// A block walks `tpb` tiles; per tile the x halo and the dy tile are staged by LDS-DMA, then the
+// thread streams its column down the band: each input row's KS columns (read once) meet the dy of
+// the KS output rows that use them (a rolling 3-row dy window in registers), into KS*KS x 8
+// per-thread tap partials. One LDS reduction over the pixel lanes and one coalesced atomic row
+// (or, deterministic mode, one slab row) per block.
+template <int KS, int NG, int TH>
+__global__ __launch_bounds__(NT) void dw_tile_wgrad_kernel(const u16* __restrict__ x, const u16* __restrict__ dy,
+                                                           float* __restrict__ dw, DwGeo g, DwTileGeo tg, int tpb,
+                                                           float* __restrict__ slabs) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int CW = NG * 8;
+  const int cb = (int)blockIdx.y * CW;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int gi = threadIdx.x & (NG - 1), pl = threadIdx.x / NG;
+  const int band = pl / tg.TW, c = pl - band * tg.TW;
+  const bool active = band < tg.RB;
+  const int xchunks = (tg.pieces + 63) >> 6;
+  const int dpieces = tg.RB * TH * tg.TW * NG, dchunks = (dpieces + 63) >> 6;
+  char* dimg = smem + xchunks * 1024;
+  const int ntiles = g.N * tg.nrowt * tg.ncolt;
+  f32x2 acc[KS * KS][4];
+#pragma unroll
+  for (int tp = 0; tp < KS * KS; ++tp)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[tp][k] = f32x2{0.f, 0.f};
+  const int t0 = (int)blockIdx.x * tpb, t1 = min(ntiles, t0 + tpb);
+  for (int t = t0; t < t1; ++t) {
+    const int ct = t % tg.ncolt, rest = t / tg.ncolt;
+    const int rt = rest % tg.nrowt, n = rest / tg.nrowt;
+    const int p0 = rt * tg.RB * TH, q0 = ct * tg.TW;
+    const int h0 = p0 - g.ph, w0 = q0 - g.pw;
+    if (t != t0) __syncthreads();  // the previous tile's LDS reads are done
+    const u16* xb = x + (int64_t)n * g.H * g.W * g.ldx + cb;
+    for (int k = wid; k < xchunks; k += NT / 64) {
+      const int piece = k * 64 + lane;
+      const int pix = piece / NG, pg = piece & (NG - 1);
+      const int lr = (int)fdiv((uint32_t)pix, tg.fd_lcols), lc = pix - lr * tg.LCOLS;
+      const int h = h0 + lr, ww = w0 + lc;
+      const bool ok = piece < tg.pieces && (unsigned)h < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
+      const u16* src = ok ? xb + ((int64_t)h * g.W + ww) * g.ldx + pg * 8 : reinterpret_cast<const u16*>(dv_zero_page);
+      __builtin_amdgcn_global_load_lds(GLB_PTR(src), LDS_PTR(smem + k * 1024), 16, 0, 0);
+    }
+    const u16* db = dy + (int64_t)n * g.P * g.Q * g.ldy + cb;
+    for (int k = wid; k < dchunks; k += NT / 64) {
+      const int piece = k * 64 + lane;
+      const int pix = piece / NG, pg = piece & (NG - 1);
+      const int lr = pix / tg.TW, lc = pix - lr * tg.TW;
+      const int p = p0 + lr, q = q0 + lc;
+      const bool ok = piece < dpieces && p < g.P && q < g.Q;  // outside the output grid: zero gradient
+      const u16* src = ok ? db + ((int64_t)p * g.Q + q) * g.ldy + pg * 8 : reinterpret_cast<const u16*>(dv_zero_page);
+      __builtin_amdgcn_global_load_lds(GLB_PTR(src), LDS_PTR(dimg + k * 1024), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (active) {
+      const char* xp = smem + ((band * TH * tg.LCOLS + c) * NG + gi) * 16;
+      const char* dp = dimg + ((band * TH * tg.TW + c) * NG + gi) * 16;
+      const int xrowb = tg.LCOLS * NG * 16, drowb = tg.TW * NG * 16;
+      f32x2 d[KS][4];  // dy of output rows ir, ir-1, ..., ir-KS+1 (slot i % KS)
+#pragma unroll
+      for (int ir = 0; ir < TH + KS - 1; ++ir) {
+        if (ir < TH) ld8p(reinterpret_cast<const u16*>(dp + ir * drowb), d[ir % KS]);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          f32x2 v[4];
+          ld8p(reinterpret_cast<const u16*>(xp + s * NG * 16), v);
+#pragma unroll
+          for (int r = 0; r < KS; ++r) {
+            const int i = ir - r;  // compile-time
+            if (i >= 0 && i < TH) {
+#pragma unroll
+              for (int k = 0; k < 4; ++k) acc[r * KS + s][k] = pfma(v[k], d[i % KS][k], acc[r * KS + s][k]);
+            }
+          }
+        }
+        xp += xrowb;
+      }
+    }
+  }
+  // ---- per-tap sums over the pixel lanes (LDS, tap by tap) -> [CW][KS*KS] -> one row per block ----
+  __syncthreads();
+  float* sh = reinterpret_cast<float*>(smem);  // [NT/NG][CW]
+  float* red = sh + NT * 8;                    // [CW][KS*KS]
+#pragma unroll
+  for (int tp = 0; tp < KS * KS; ++tp) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      sh[pl * CW + gi * 8 + 2 * k] = acc[tp][k].x;
+      sh[pl * CW + gi * 8 + 2 * k + 1] = acc[tp][k].y;
+    }
+    __syncthreads();
+    if (threadIdx.x < CW) {
+      float sum = 0.f;
+      for (int r = 0; r < NT / NG; ++r) sum += sh[r * CW + threadIdx.x];
+      red[threadIdx.x * KS * KS + tp] = sum;
+    }
+    __syncthreads();
+  }
+  const int64_t coff = (int64_t)cb * KS * KS;
+  if (slabs) {
+    float* dst = slabs + (int64_t)blockIdx.x * g.C * KS * KS + coff;
+    for (int e = threadIdx.x; e < CW * KS * KS; e += NT) dst[e] = red[e];
+    return;
+  }
+  for (int e = threadIdx.x; e < CW * KS * KS; e += NT) atomicAdd(dw + coff + e, red[e]);
+}
+
+inline DwTileGeo make_tile_geo(const DwGeo& g, int NG, int TH, int KS) {
+  const int PL = NT / NG;
+  DwTileGeo tg{};
+  tg.TW = std::min(g.Q, PL);
+  tg.RB = PL / tg.TW;
+  tg.LCOLS = tg.TW + KS - 1;
+  tg.pieces = (tg.RB * TH + KS - 1) * tg.LCOLS * NG;
+  tg.ncolt = (g.Q + tg.TW - 1) / tg.TW;
+  tg.nrowt = (g.P + tg.RB * TH - 1) / (tg.RB * TH);
+  tg.fd_lcols = make_fastdiv((uint32_t)tg.LCOLS);
+  return tg;
+}
+
+template <int KS, int NG, int TH>
+void tile_wgrad_launch(const void* x, const void* dy, float* dw, const DwGeo& g, hipStream_t st) {
+  const DwTileGeo tg = make_tile_geo(g, NG, TH, KS);
+  const int ntiles = g.N * tg.nrowt * tg.ncolt, nslab = g.C / (NG * 8);
+  // ~768 blocks (3 per CU): every block ends in KS*KS LDS reductions + one atomic row, so a block
+  // walks several tiles
+  const int tpb = std::max(1, (ntiles * nslab + 767) / 768);
+  const dim3 grid((unsigned)((ntiles + tpb - 1) / tpb), (unsigned)nslab);
+  const size_t xb = (size_t)((tg.pieces + 63) / 64) * 1024;
+  const size_t db = (size_t)((tg.RB * TH * tg.TW * NG + 63) / 64) * 1024;
+  const size_t lds = std::max(xb + db, (size_t)(NT * 8 + NG * 8 * KS * KS) * 4);
+  float* ws = nullptr;
+  const int64_t n = (int64_t)g.C * KS * KS;
+  if (dv_deterministic()) ws = dv_slab_workspace((size_t)grid.x * n, st);
+  dw_tile_wgrad_kernel<KS, NG, TH><<<grid, NT, lds, st>>>((const u16*)x, (const u16*)dy, dw, g, tg, tpb, ws);
+  if (ws) dv_slab_reduce(ws, dw, n, (int)grid.x, 1, st);
+}
+
+template <int KS, bool FLIP, int NG, int TH>
+void tile_launch(const void* x, const float* w, const float* bias, void* y, const DwGeo& g, int act, float slope,
+                 float* stats, hipStream_t st, const DwBnr* bnr) {
+  const DwTileGeo tg = make_tile_geo(g, NG, TH, KS);
+  const dim3 grid((unsigned)(g.N * tg.nrowt * tg.ncolt), (unsigned)(g.C / (NG * 8)));
+  const size_t lds = std::max<size_t>((size_t)((tg.pieces + 63) / 64) * 1024, (size_t)2 * NT * 8 * 4);
+  const DetStats det((bnr || stats) ? grid.x : 0, g.C, st);
+  if (bnr) {
+    DwBnr b = *bnr;
+    b.det = det.slab;
+    dw_tile_kernel<KS, FLIP, true, NG, TH><<<grid, NT, lds, st>>>((const u16*)x, w, bias, (u16*)y, g, tg, act, slope,
+                                                                  stats, b, nullptr);
+    det.fold(bnr->acc);
+  } else {
+    dw_tile_kernel<KS, FLIP, false, NG, TH><<<grid, NT, lds, st>>>((const u16*)x, w, bias, (u16*)y, g, tg, act, slope,
+                                                                   stats, DwBnr{}, det.slab);
+    det.fold(stats);
+  }
+}
+// rows per thread: the candidate that covers P (in bands of RB rows) with the fewest idle rows
+inline int tile_th(int P, int Q, int NG) {
+  const int PL = NT / NG, TW = std::min(Q, PL), RB = PL / TW;
+  int best = 8, waste = 1 << 30;
+  for (int th : {8, 7, 4, 2}) {
+    const int rows = RB * th, wst = (P + rows - 1) / rows * rows - P;
+    if (wst < waste) { waste = wst; best = th; }
+  }
+  return best;
+}
+template <int KS, bool FLIP>
+bool tile_fwd(const void* x, const float* w, const float* bias, void* y, const DwGeo& g, int act, float slope,
+              float* stats, hipStream_t st, const DwBnr* bnr) {
+  if constexpr (KS != 3) {
+    return false;
+  } else {
+    if (g.sh != 1 || g.sw != 1 || g.ldx % 8 || g.ldy % 8) return false;
+    const int NG = g.C % 64 == 0 ? 8 : (g.C % 32 == 0 ? 4 : 0);
+    if (!NG) return false;
+    const int th = g_dw_variant == 62 ? 4 : tile_th(g.P, g.Q, NG);
+#define DW_TILE(NGV, THV) \
+  if (NG == NGV && th == THV) { tile_launch<KS, FLIP, NGV, THV>(x, w, bias, y, g, act, slope, stats, st, bnr); return true; }
+    DW_TILE(8, 8) DW_TILE(8, 7) DW_TILE(8, 4) DW_TILE(8, 2)
+    DW_TILE(4, 8) DW_TILE(4, 7) DW_TILE(4, 4) DW_TILE(4, 2)
+#undef DW_TILE
+    return false;
+  }
+}
+
+template <int KS>
+bool tile_wgrad(const void* x, const void* dy, float* dw, const DwGeo& g, hipStream_t st) {
+  if constexpr (KS != 3) {
+    return false;
+  } else {
+    if (g.sh != 1 || g.sw != 1 || g.ldx % 8 || g.ldy % 8) return false;
+    const int NG = g.C % 64 == 0 ? 8 : (g.C % 32 == 0 ? 4 : 0);
+    if (!NG) return false;
+    const int th = g_dw_variant == 62 ? 4 : tile_th(g.P, g.Q, NG);
+#define DW_TILE(NGV, THV) \
+  if (NG == NGV && th == THV) { tile_wgrad_launch<KS, NGV, THV>(x, dy, dw, g, st); return true; }
+    DW_TILE(8, 8) DW_TILE(8, 7) DW_TILE(8, 4) DW_TILE(8, 2)
+    DW_TILE(4, 8) DW_TILE(4, 7) DW_TILE(4, 4) DW_TILE(4, 2)
+#undef DW_TILE
+    return false;
+  }
+}
+
 int64_t per_block(int64_t nstrips, int rpi, int slabs, int64_t target_blocks) {
   // ~target blocks in total over the slabs, a whole number of strip passes per block
   int64_t spb = std::max<int64_t>(rpi, (nstrips * slabs + target_blocks - 1) / target_blocks);
@@ -642,9 +1004,6 @@ inline int rpi_of(int C) {
   const int cgn = C / 8, tpr = cgn < SLAB ? cgn : SLAB;
   return NT / tpr;
 }
-// Benchmark override of (strip length QT, minimum waves per SIMD) for the 3x3 kernels:
-// 0 = heuristic, 1 = (4, 4), 2 = (2, 4), 3 = (8, 2), 4 = (4, 2), 5 = (2, 2).
-int g_dw_variant = 0;
 
 template <int KS, int SW, bool FLIP, int QT, int OCC>
 void fwd_launch(const void* x, const float* w, const float* bias, void* y, const DwGeo& g, int act, float slope,
@@ -670,6 +1029,10 @@ void fwd_launch(const void* x, const float* w, const float* bias, void* y, const
 template <int KS, int SW, bool FLIP>
 void fwd_variants(const void* x, const float* w, const float* bias, void* y, const DwGeo& g, int act, float slope,
                   float* stats, hipStream_t st, const DwBnr* bnr = nullptr) {
+  // LDS-tiled for stride 1 down to 14x14 outputs (18-40 % faster than the strip kernel there); the
+  // strip kernel keeps 7x7 (the 9x9 halo of a 7x7 tile costs more than it saves: profiles/dw_tile_r5.txt)
+  const bool tiled = g_dw_variant == 60 || g_dw_variant == 62 || (g_dw_variant == 0 && g.P * g.Q >= 196);
+  if (tiled && tile_fwd<KS, FLIP>(x, w, bias, y, g, act, slope, stats, st, bnr)) return;
   if (bnr) return fwd_launch<KS, SW, FLIP, 4, 1>(x, w, bias, y, g, act, slope, stats, 4096, st, bnr);
   if constexpr (KS == 3) {
     switch (g_dw_variant) {
@@ -703,6 +1066,12 @@ void wgrad_launch(const void* x, const void* dy, float* dw, const DwGeo& g, int 
 }
 template <int KS, int SW>
 void wgrad_variants(const void* x, const void* dy, float* dw, const DwGeo& g, hipStream_t st) {
+  if constexpr (SW == 1) {
+    // tiled weight gradient for outputs up to 14x14 (28-30 % faster than the plane / strip kernels
+    // there); larger maps keep the strip kernel, whose blocks overlap loads with FMAs across strips
+    const bool tiled = g_dw_variant == 60 || g_dw_variant == 62 || (g_dw_variant == 0 && g.P * g.Q <= 196);
+    if (tiled && tile_wgrad<KS>(x, dy, dw, g, st)) return;
+  }
   if constexpr (KS == 3) {
     switch (g_dw_variant) {
       case 1: return wgrad_launch<KS, SW, 4, 4>(x, dy, dw, g, 2048, st);

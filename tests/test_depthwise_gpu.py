@@ -217,3 +217,41 @@ def test_depthwise_dgrad_fuses_bn_backward(s, act):
     assert nrel(fused[2], xr.grad) < 3e-2
     assert nrel(fused[4], ref[1].weight.grad) < 3e-2
     assert nrel(fused[5], ref[1].bias.grad) < 3e-2
+
+
+@pytest.mark.parametrize("C,H,W,act", [(32, 112, 112, "relu"), (96, 13, 20, None), (128, 9, 33, "leaky"),
+                                       (512, 14, 14, "relu"), (64, 5, 70, None)])
+def test_depthwise_tiled_matches_strip(C, H, W, act):
+    """The LDS-tiled stride-1 kernels (csrc/depthwise.hip dw_tile_kernel / dw_tile_wgrad_kernel) against
+    the strip kernels (benchmark variant 61) on ragged tiles: partial column / row tiles, several
+    row bands per block, a 32-channel-multiple slab (C = 96), with bias, activation and BN statistics.
+    The forward and data gradient sum the taps in the same order (bitwise equal); the weight gradient
+    and the statistics reduce in another order (fp32 rounding only)."""
+    from deep_vision_amd import ops as F
+    from deep_vision_amd._ext import lib
+
+    torch.manual_seed(C + H + W)
+    x32 = torch.randn(3, C, H, W, device=DEV).bfloat16().float()
+    w0 = torch.randn(C, 1, 3, 3, device=DEV) * 0.3
+    b0 = torch.randn(C, device=DEV) * 0.5
+    dy = _nhwc(torch.randn(3, C, H, W, device=DEV))
+
+    def run(variant):
+        lib().dw_variant(variant)
+        try:
+            x = _nhwc(x32).requires_grad_(True)
+            w = w0.clone().requires_grad_(True)
+            b = b0.clone().requires_grad_(True)
+            y, stats = F.conv2d(x, w, b, 1, 1, 1, C, act=act, slope=0.1, want_stats=True)
+            y.backward(dy)
+            torch.cuda.synchronize()
+            return y.detach(), stats[:128].reshape(64, 2, -1).sum(0)[:, :C], x.grad, w.grad, b.grad
+        finally:
+            lib().dw_variant(0)
+
+    tiled, strip = run(0), run(61)
+    assert torch.equal(tiled[0], strip[0]), "forward differs"
+    assert _rel(tiled[1], strip[1]) < 1e-5
+    assert torch.equal(tiled[2], strip[2]), "data gradient differs"
+    assert _rel(tiled[3], strip[3]) < 1e-5
+    assert _rel(tiled[4], strip[4]) < 1e-5

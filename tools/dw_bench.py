@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--variants", default="0,1,2,3,4,5")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--stats", action="store_true", help="forward with fused BN statistics (MobileNet's form)")
     a = ap.parse_args()
     vs = [int(v) for v in a.variants.split(",")]
     L = lib()
@@ -37,9 +38,11 @@ def main():
         y = torch.empty(N, C, P, P, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=CL)
         dx = torch.empty_like(x)
         dw = torch.zeros(C, 9, device="cuda")
+        acc = torch.zeros(129 * C, device="cuda")  # [64][2][C] shards + the shift row
+        sp = ptr(acc) if a.stats else 0
         bx, by = x.numel() * 2, y.numel() * 2
         ops = {
-            "fwd": (lambda: L.dw_fwd(ptr(x), ptr(w), 0, ptr(y), N, H, H, C, C, P, P, C, 3, s, s, 1, 1, 0, 0.0, 0, st),
+            "fwd": (lambda: L.dw_fwd(ptr(x), ptr(w), 0, ptr(y), N, H, H, C, C, P, P, C, 3, s, s, 1, 1, 0, 0.0, sp, st),
                     y, bx + by),
             "dgrad": (lambda: L.dw_dgrad(ptr(dy), ptr(w), ptr(dx), N, H, H, C, C, P, P, C, 3, s, s, 1, 1, st), dx,
                       bx + by),
