@@ -114,6 +114,23 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("x"), py::arg("res"), py::arg("out"), py::arg("n"), py::arg("C"), py::arg("scale"), py::arg("shift"),
      py::arg("act"), py::arg("slope"), py::arg("mask"), py::arg("st"), py::arg("rscale") = 0, py::arg("rshift") = 0,
      py::arg("post") = 0);
+  m.def("bn_fin_ok", [](int64_t n, int C) { return dv_bn_fin_ok(n, C); });
+  m.def("bn_fin_apply", [](uptr acc, double count, float eps, float mom, uptr gamma, uptr beta, uptr rm, uptr rv, uptr prm,
+                           uptr ticket, uptr x, uptr res, uptr out, int64_t n, int C, int act, float slope, uptr mask,
+                           int post, uptr st) {
+    dv_bn_fin_apply(FP(acc), count, eps, mom, CFP(gamma), CFP(beta), FP(rm), FP(rv), FP(prm), reinterpret_cast<int*>(ticket),
+                    CP(x), CP(res), P(out), n, C, act, slope, P(mask), post, ST(st));
+    check_last("bn_fin_apply");
+  });
+  m.def("bn_bwd_fin_apply", [](uptr acc, double count, uptr gamma, uptr mean, uptr invstd, uptr dgamma, uptr dbeta,
+                               int accumulate, uptr xsum, uptr ticket, uptr dout, uptr out, uptr x, uptr dx, uptr dres,
+                               int64_t n, int C, uptr mscale, uptr mshift, int act, float slope, int mask_bits, uptr addend,
+                               uptr addend2, uptr colsum, uptr st) {
+    dv_bn_bwd_fin_apply(FP(acc), count, CFP(gamma), CFP(mean), CFP(invstd), FP(dgamma), FP(dbeta), accumulate, FP(xsum),
+                        reinterpret_cast<int*>(ticket), CP(dout), CP(out), CP(x), P(dx), P(dres), n, C, CFP(mscale),
+                        CFP(mshift), act, slope, mask_bits, CP(addend), CP(addend2), FP(colsum), ST(st));
+    check_last("bn_bwd_fin_apply");
+  });
   m.def("bn_bwd_reduce", [](uptr dout, uptr out, uptr x, int64_t rows, int C, uptr mean, uptr invstd, uptr mscale,
                             uptr mshift, int act, float slope, uptr acc, int mask_bits, uptr st) {
     dv_bn_bwd_reduce(CP(dout), CP(out), CP(x), rows, C, CFP(mean), CFP(invstd), CFP(mscale), CFP(mshift), act, slope, FP(acc),

@@ -875,3 +875,274 @@ void dv_bn_bwd_eval(const void* dout, const void* out, void* dx, void* dres, int
   const int g = (int)((rows + rpb - 1) / rpb);
   DISPATCH_VEC(C, bn_bwd_eval_kernel, <<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (u16*)dx, (u16*)dres, rows, C, rpb, scale, act, slope))
 }
+
+// ---------------------------------------------------------------------------------------------
+// Small BatchNorms: the shard fold inside the apply pass (no finalize launch).
+// Hourglass-104 / YOLOv3 carry hundreds of BatchNorms over a few thousand rows each (the 16x16 ..
+// 4x4 hourglass levels at batch 32): there the separate finalize launch (~5 us of pure latency,
+// 230 + 230 of them per Hourglass step, profiles/hourglass_step_census.txt) cost as much as the
+// apply pass itself. These passes tile [row range] x [64-channel slab]: every block folds its
+// slab's SHARDS x 64 partial sums (32 KB, L2-resident: the producer just wrote them) in its
+// prologue, in the order of bn_finalize_kernel (same bits as the two-launch form), block (0, slab)
+// publishes the per-channel results (running statistics, save_mean / invstd / scale / shift, or
+// dgamma / dbeta / the producer's bias gradient), and the LAST block of the slab to finish (a
+// ticket counter) re-zeroes the slab's shards -- and, forward, stores the batch mean as the next
+// shift -- after every block of the slab has read them.
+namespace {
+constexpr int FIN_CH = 64;  // channels per slab
+struct FwdFin {
+  float* acc; double count; float eps, momentum;
+  const float* gamma; const float* beta; float* rm; float* rv;
+  float* prm;   // [4][C]: scale, shift, mean, invstd
+  int* ticket;  // [C / 64], zero between uses
+};
+struct BwdFin {
+  float* acc; double count;
+  const float* gamma; const float* mean; const float* invstd;
+  float* dgamma; float* dbeta; int accumulate; float* xsum;
+  int* ticket;
+};
+
+// fold channels [c0, c0 + 64) of a [SHARDS][2][C] accumulator (fold_shards' order, no zeroing):
+// every thread returns its channel's (c0 + tid % 64) totals
+DV_DEVICE void fold64(const float* __restrict__ acc, int C, int c0, double& s, double& q) {
+  __shared__ double red[2][4][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  constexpr int PER = SHARDS / 4;
+  float va[PER], vb[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const float* p = acc + (int64_t)(grp * PER + i) * 2 * C + c0 + cl;
+    va[i] = p[0]; vb[i] = p[C];
+  }
+  double a = 0.0, b = 0.0;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) { a += va[i]; b += vb[i]; }
+  red[0][grp][cl] = a; red[1][grp][cl] = b;
+  __syncthreads();
+  s = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
+  q = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+}
+
+// Ticket of the slab, taken by thread 0 right after fold64 (whose barrier follows every thread's
+// shard loads: the values are in registers, so the reads are complete -- no fence, nothing to
+// drain). The block that takes the last ticket re-zeroes the shards at its end; fin_last() there
+// broadcasts the answer to the block.
+DV_DEVICE void fin_ticket(int* ticket, int nblocks, int* last) {
+  if (threadIdx.x == 0) *last = atomicAdd(ticket, 1) == nblocks - 1;
+}
+DV_DEVICE bool fin_last(const int* last) {
+  __syncthreads();
+  return *last;
+}
+DV_DEVICE void fin_zero(float* __restrict__ acc, int C, int c0) {
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  constexpr int PER = SHARDS / 4;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    float* p = acc + (int64_t)(grp * PER + i) * 2 * C + c0 + cl;
+    p[0] = 0.f; p[C] = 0.f;
+  }
+}
+
+// 8 threads x 8 channels cover a row of the slab; 32 rows per iteration
+template <bool MB, bool POST, bool NTL>
+__global__ __launch_bounds__(NT) void bn_fin_apply_kernel(const u16* __restrict__ x, const u16* __restrict__ res,
+                                                          u16* __restrict__ out, int64_t rows, int C, int64_t rpb,
+                                                          int act, float slope, uint8_t* __restrict__ mask, FwdFin f) {
+  __shared__ float ssc[FIN_CH], ssf[FIN_CH];
+  const int c0 = (int)blockIdx.y * FIN_CH;
+  const int cl = threadIdx.x & 63, c = c0 + cl;
+  float* shiftp = stat_shift(f.acc, C) + c;
+  // per-channel operands before the fold (one round trip for both)
+  const float k = *shiftp;
+  const float g = f.gamma ? f.gamma[c] : 1.f, b = f.beta ? f.beta[c] : 0.f;
+  const bool pub = blockIdx.x == 0 && threadIdx.x < 64;
+  float rm0 = 0.f, rv0 = 0.f;
+  if (pub && f.rm) { rm0 = f.rm[c]; rv0 = f.rv[c]; }
+  double s, q;
+  fold64(f.acc, C, c0, s, q);
+  __shared__ int last;
+  fin_ticket(f.ticket + blockIdx.y, gridDim.x, &last);
+  const double dm = s / f.count;
+  const double mean = (double)k + dm;
+  double var = q / f.count - dm * dm;
+  if (var < 0) var = 0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
+  const float scale = g * invstd, shift = b - (float)mean * g * invstd;
+  if (threadIdx.x < 64) { ssc[cl] = scale; ssf[cl] = shift; }
+  if (pub) {  // bn_finalize_kernel's outputs
+    f.prm[c] = scale; f.prm[C + c] = shift; f.prm[2 * C + c] = (float)mean; f.prm[3 * C + c] = invstd;
+    if (f.rm && isfinite(mean) && isfinite(var)) {
+      const double unb = f.count > 1 ? var * f.count / (f.count - 1) : var;
+      f.rm[c] = (1.f - f.momentum) * rm0 + f.momentum * (float)mean;
+      f.rv[c] = (1.f - f.momentum) * rv0 + f.momentum * (float)unb;
+    }
+  }
+  __syncthreads();
+  const int lane_c = threadIdx.x & 7, lane_r = threadIdx.x >> 3;
+  float sc[8], sf[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { sc[e] = ssc[lane_c * 8 + e]; sf[e] = ssf[lane_c * 8 + e]; }
+  const int64_t r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
+#pragma unroll 2
+  for (int64_t r = r0 + lane_r; r < r1; r += NT / 8) {
+    const int64_t o = r * C + c0 + lane_c * 8;
+    float v[8], rv[8];
+    ldv<NTL, 8>(x + o, v);
+    if (res) ldv<NTL, 8>(res + o, rv);
+    uint32_t bits = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float z = fmaf(v[e], sc[e], sf[e]);
+      if (res && !POST) z += rv[e];
+      if constexpr (MB) bits |= (z > 0.f ? 1u : 0u) << e;
+      v[e] = act_fwd(z, act, slope);
+      if constexpr (POST) v[e] += rv[e];
+    }
+    VecIO<8>::store(out + o, v);
+    if constexpr (MB) {  // 4 lanes = 32 channels = one aligned 32-bit word of the mask (C % 64 == 0)
+      uint32_t w = bits << (8 * (lane_c & 3));
+      w |= __shfl_xor(w, 1, 64);
+      w |= __shfl_xor(w, 2, 64);
+      if ((lane_c & 3) == 0) *reinterpret_cast<uint32_t*>(mask + (o >> 3)) = w;
+    }
+  }
+  if (fin_last(&last)) {
+    fin_zero(f.acc, C, c0);
+    if (threadIdx.x < 64) *shiftp = isfinite(mean) ? (float)mean : 0.f;  // the next batch's shift
+    if (threadIdx.x == 0) f.ticket[blockIdx.y] = 0;
+  }
+}
+
+template <int MM, bool NTL>
+__global__ __launch_bounds__(NT) void bn_bwd_fin_apply_kernel(const u16* __restrict__ dout, const u16* __restrict__ out,
+                                                              const u16* __restrict__ x, u16* dx, u16* __restrict__ dres,
+                                                              int64_t rows, int C, int64_t rpb,
+                                                              const float* __restrict__ mscale, const float* __restrict__ mshift,
+                                                              int act, float slope, const u16* addend,
+                                                              const u16* __restrict__ addend2, float* __restrict__ colsum,
+                                                              BwdFin f) {
+  __shared__ float sk[3][FIN_CH];
+  const int c0 = (int)blockIdx.y * FIN_CH;
+  const int cl = threadIdx.x & 63, c = c0 + cl;
+  const bool pub = blockIdx.x == 0 && threadIdx.x < 64;
+  const float gm = f.gamma ? f.gamma[c] : 1.f, mu = f.mean[c], isd = f.invstd[c];
+  float db0 = 0.f, dg0 = 0.f, xs0 = 0.f;
+  if (pub) {
+    if (f.accumulate && f.dbeta) db0 = f.dbeta[c];
+    if (f.accumulate && f.dgamma) dg0 = f.dgamma[c];
+    if (f.xsum) xs0 = f.xsum[c];
+  }
+  double s, q;
+  fold64(f.acc, C, c0, s, q);
+  __shared__ int last;
+  fin_ticket(f.ticket + blockIdx.y, gridDim.x, &last);
+  // bn_bwd_finalize_kernel's coefficients of dx = kA*dz + kB*x + kC
+  const double mdz = s / f.count, mdzx = q / f.count;
+  const double is = isd, a = (double)gm * is;
+  const double kb = -a * is * mdzx, kc = a * ((double)mu * is * mdzx - mdz);
+  if (threadIdx.x < 64) { sk[0][cl] = (float)a; sk[1][cl] = (float)kb; sk[2][cl] = (float)kc; }
+  if (pub) {
+    if (f.dbeta) f.dbeta[c] = f.accumulate ? db0 + (float)s : (float)s;
+    if (f.dgamma) f.dgamma[c] = f.accumulate ? dg0 + (float)q : (float)q;
+    if (f.xsum) f.xsum[c] = xs0 + (float)(a * s + kb * f.count * (double)mu + f.count * kc);
+  }
+  __syncthreads();
+  const int lane_c = threadIdx.x & 7, lane_r = threadIdx.x >> 3;
+  float ka[8], kbv[8], kcv[8], ms[8], mh[8], cs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int ch = lane_c * 8 + e;
+    ka[e] = sk[0][ch]; kbv[e] = sk[1][ch]; kcv[e] = sk[2][ch];
+    ms[e] = MM == MM_X ? mscale[c0 + ch] : 0.f;
+    mh[e] = MM == MM_X ? mshift[c0 + ch] : 0.f;
+    cs[e] = 0.f;
+  }
+  const int64_t r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
+#pragma unroll 2
+  for (int64_t r = r0 + lane_r; r < r1; r += NT / 8) {
+    const int64_t o = r * C + c0 + lane_c * 8;
+    float d[8], ov[8], xv[8], rr[8], av[8], a2[8];
+    ldv<NTL, 8>(dout + o, d);
+    ldv<NTL, 8>(x + o, xv);
+    if constexpr (MM == MM_OUT) ldv<NTL, 8>(out + o, ov);
+    if (addend) ldv<NTL, 8>(addend + o, av);
+    if (addend2) ldv<NTL, 8>(addend2 + o, a2);
+    uint32_t mb = 0;
+    if constexpr (MM == MM_BITS) mb = reinterpret_cast<const uint8_t*>(out)[o >> 3];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float dz = d[e];
+      if constexpr (MM == MM_OUT) dz = act_bwd(d[e], ov[e], act, slope);
+      if constexpr (MM == MM_BITS) dz = ((mb >> e) & 1u) ? d[e] : (act == 2 ? d[e] * slope : 0.f);
+      if constexpr (MM == MM_X) dz = act_bwd(d[e], fmaf(xv[e], ms[e], mh[e]), act, slope);
+      rr[e] = dz;
+      d[e] = fmaf(ka[e], dz, fmaf(kbv[e], xv[e], kcv[e]));
+      if (addend) d[e] += av[e];
+      if (addend2) d[e] += a2[e];
+      cs[e] += bf2f(f2bf(d[e]));
+    }
+    VecIO<8>::store(dx + o, d);
+    if (dres) VecIO<8>::store(dres + o, rr);
+  }
+  if (colsum) {  // [row lane][slab channel] -> one coalesced atomic row of 64 channels per block
+    __shared__ float csh[NT / 8][FIN_CH];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) csh[lane_r][lane_c * 8 + e] = cs[e];
+    __syncthreads();
+    if (threadIdx.x < FIN_CH) {
+      float v = 0.f;
+      for (int rr = 0; rr < NT / 8; ++rr) v += csh[rr][threadIdx.x];
+      atomicAdd(stat_row(colsum, nullptr, blockIdx.x, C) + c0 + threadIdx.x, v);
+    }
+  }
+  if (fin_last(&last)) {
+    fin_zero(f.acc, C, c0);
+    if (threadIdx.x == 0) f.ticket[blockIdx.y] = 0;
+  }
+}
+
+// row blocks per 64-channel slab: 32 rows (one iteration) each up to ~1,024 blocks in all -- the
+// pass is latency-bound at these sizes, each block's shard fold is one round trip of 32 loads
+inline int fin_row_blocks(int64_t rows, int C, int64_t& rpb) {
+  const int slabs = C / FIN_CH;
+  int64_t nrb = std::max<int64_t>(1, std::min<int64_t>((rows + 31) / 32, std::max(1, 1024 / slabs)));
+  rpb = (rows + nrb - 1) / nrb;
+  rpb = (rpb + 31) / 32 * 32;
+  return (int)((rows + rpb - 1) / rpb);
+}
+}  // namespace
+
+bool dv_bn_fin_ok(int64_t n, int C) { return C % FIN_CH == 0 && C > 0 && n <= DV_BN_FIN_MAX_ELEMS; }
+
+void dv_bn_fin_apply(float* acc, double count, float eps, float momentum, const float* gamma, const float* beta,
+                     float* rm, float* rv, float* prm, int* ticket, const void* x, const void* res, void* out, int64_t n,
+                     int C, int act, float slope, void* mask, int post, hipStream_t st) {
+  const int64_t rows = n / C;
+  int64_t rpb;
+  const dim3 g((unsigned)fin_row_blocks(rows, C, rpb), (unsigned)(C / FIN_CH));
+  const FwdFin f{acc, count, eps, momentum, gamma, beta, rm, rv, prm, ticket};
+#define FA_ARGS <<<g, NT, 0, st>>>((const u16*)x, (const u16*)res, (u16*)out, rows, C, rpb, act, slope, (uint8_t*)mask, f)
+  if (post && res) bn_fin_apply_kernel<false, true, false> FA_ARGS;
+  else if (mask) bn_fin_apply_kernel<true, false, false> FA_ARGS;
+  else bn_fin_apply_kernel<false, false, false> FA_ARGS;
+#undef FA_ARGS
+}
+
+void dv_bn_bwd_fin_apply(float* acc, double count, const float* gamma, const float* mean, const float* invstd,
+                         float* dgamma, float* dbeta, int accumulate, float* xsum, int* ticket, const void* dout,
+                         const void* out, const void* x, void* dx, void* dres, int64_t n, int C, const float* mscale,
+                         const float* mshift, int act, float slope, int mask_bits, const void* addend,
+                         const void* addend2, float* colsum, hipStream_t st) {
+  const int64_t rows = n / C;
+  int64_t rpb;
+  const dim3 g((unsigned)fin_row_blocks(rows, C, rpb), (unsigned)(C / FIN_CH));
+  const BwdFin f{acc, count, gamma, mean, invstd, dgamma, dbeta, accumulate, xsum, ticket};
+#define FB_ARGS <<<g, NT, 0, st>>>((const u16*)dout, (const u16*)out, (const u16*)x, (u16*)dx, (u16*)dres, rows, C, rpb, mscale, mshift, act, slope, (const u16*)addend, (const u16*)addend2, colsum, f)
+  if (act && mask_bits) bn_bwd_fin_apply_kernel<MM_BITS, false> FB_ARGS;
+  else if (!act) bn_bwd_fin_apply_kernel<MM_NONE, false> FB_ARGS;
+  else if (out) bn_bwd_fin_apply_kernel<MM_OUT, false> FB_ARGS;
+  else bn_bwd_fin_apply_kernel<MM_X, false> FB_ARGS;
+#undef FB_ARGS
+}

@@ -134,6 +134,18 @@ void dv_bn_stats(const void* x, int64_t rows, int C, float* acc, hipStream_t st)
 void dv_bn_finalize(float* acc, int C, double count, float eps, float momentum, const float* gamma,
                     const float* beta, float* rm, float* rv, float* save_mean, float* save_invstd, float* scale,
                     float* shift, hipStream_t st);
+// Small BatchNorms (C % 64 == 0, at most DV_BN_FIN_MAX_ELEMS elements): the statistics fold inside
+// the apply pass, no finalize launch (bn.hip "Small BatchNorms"). ticket: [C / 64] zeroed ints.
+#define DV_BN_FIN_MAX_ELEMS (2ll << 20)
+bool dv_bn_fin_ok(int64_t n, int C);
+void dv_bn_fin_apply(float* acc, double count, float eps, float momentum, const float* gamma, const float* beta,
+                     float* rm, float* rv, float* prm, int* ticket, const void* x, const void* res, void* out, int64_t n,
+                     int C, int act, float slope, void* mask, int post, hipStream_t st);
+void dv_bn_bwd_fin_apply(float* acc, double count, const float* gamma, const float* mean, const float* invstd,
+                         float* dgamma, float* dbeta, int accumulate, float* xsum, int* ticket, const void* dout,
+                         const void* out, const void* x, void* dx, void* dres, int64_t n, int C, const float* mscale,
+                         const float* mshift, int act, float slope, int mask_bits, const void* addend,
+                         const void* addend2, float* colsum, hipStream_t st);
 void dv_bn_eval_prep(int C, float eps, const float* gamma, const float* beta, const float* rm, const float* rv,
                      float* scale, float* shift, hipStream_t st);
 // out = act(x*scale + shift (+ res [* rscale + rshift])): rscale/rshift fold a second BatchNorm

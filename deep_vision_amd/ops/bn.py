@@ -15,6 +15,8 @@ models (eps 1e-3, momentum 0.99 -> PyTorch momentum 0.01; Hourglass 0.9 -> 0.1).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as TF
 
@@ -27,8 +29,11 @@ FUSE_BWD_STATS = True  # fold the backward reduction into the consumer conv's dg
 LAZY_SHORTCUT = True   # identity-shortcut gradient masked inside the consumer's dgrad epilogue
 FOLD_RESIDUAL_BN = True  # projection-shortcut BN applied inside the block's last BN pass
 DUAL_BWD = True  # ...and its backward: reduction in the consumer dgrad's epilogue, one dual apply pass
+# small BatchNorms (C % 64 == 0, <= 2M elements): the statistics fold inside the apply passes instead
+# of a separate finalize launch, forward and backward (csrc/bn.hip "Small BatchNorms")
+FUSE_FINALIZE = os.environ.get("DV_FUSE_FIN", "1") != "0"
 COUNTERS = {"bwd_reduce_fused": 0, "bwd_reduce_pass": 0, "shortcut_lazy": 0, "dual_apply": 0, "dual_fused": 0,
-            "bwd_apply_two_addends": 0}
+            "bwd_apply_two_addends": 0, "bn_fin_fused": 0, "bn_bwd_fin_fused": 0}
 
 
 class BNRef:
@@ -76,7 +81,7 @@ class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, stats, weight, bias, running_mean, running_var, residual, training, momentum, eps, act,
                 slope, ws_fwd, ws_bwd, join=None, refbox=None, r_stats=None, r_weight=None, r_bias=None, r_rm=None,
-                r_rv=None, r_cfg=None, xjoin=None, prod_bias=None, post_res=False, colsum=None):
+                r_rv=None, r_cfg=None, xjoin=None, prod_bias=None, post_res=False, colsum=None, tickets=None):
         # xjoin (conv.GradJoin): another consumer of ``x`` stashes its gradient there (e.g. the
         # identity path of a pre-activation block); the backward apply pass adds it in place
         # r_*: a second, training-mode BatchNorm applied to ``residual`` inside the same pass
@@ -93,12 +98,15 @@ class _BNActFn(torch.autograd.Function):
         rows = N * H * W
         g = weight.detach() if weight is not None else None
         b = bias.detach() if bias is not None else None
+        # small BatchNorm: the shard fold runs inside the apply pass (csrc/bn.hip "Small BatchNorms")
+        fin = (training and tickets is not None and r_cfg is None and FUSE_FINALIZE and L.bn_fin_ok(x.numel(), C))
         if training:
             if stats is None:
                 stats = ws_fwd
                 L.bn_stats(ptr(x), rows, C, ptr(stats), st)
-            L.bn_finalize(ptr(stats), C, float(rows), float(eps), float(momentum), ptr(g), ptr(b), ptr(running_mean),
-                          ptr(running_var), ptr(mean), ptr(invstd), ptr(scale), ptr(shift), st)
+            if not fin:
+                L.bn_finalize(ptr(stats), C, float(rows), float(eps), float(momentum), ptr(g), ptr(b),
+                              ptr(running_mean), ptr(running_var), ptr(mean), ptr(invstd), ptr(scale), ptr(shift), st)
         else:
             L.bn_eval_prep(C, float(eps), ptr(g), ptr(b), ptr(running_mean), ptr(running_var), ptr(scale), ptr(shift), st)
             if weight is not None and weight.requires_grad:  # dgamma needs xhat of the running stats
@@ -121,9 +129,15 @@ class _BNActFn(torch.autograd.Function):
         mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=dev) if bits else None
         rsc, rsh = (rprm[0], rprm[1]) if rprm is not None else (None, None)
 
-        L.bn_apply(ptr(x), ptr(residual), ptr(out), x.numel(), C, ptr(scale), ptr(shift), act, float(slope), ptr(mask),
-                   st, rscale=ptr(rsc) if rsc is not None else 0, rshift=ptr(rsh) if rsh is not None else 0,
-                   post=int(post))
+        if fin:
+            COUNTERS["bn_fin_fused"] += 1
+            L.bn_fin_apply(ptr(stats), float(rows), float(eps), float(momentum), ptr(g), ptr(b), ptr(running_mean),
+                           ptr(running_var), ptr(prm), ptr(tickets[0]), ptr(x), ptr(residual), ptr(out), x.numel(), C,
+                           act, float(slope), ptr(mask), int(post), st)
+        else:
+            L.bn_apply(ptr(x), ptr(residual), ptr(out), x.numel(), C, ptr(scale), ptr(shift), act, float(slope),
+                       ptr(mask), st, rscale=ptr(rsc) if rsc is not None else 0,
+                       rshift=ptr(rsh) if rsh is not None else 0, post=int(post))
         keep_out = bool(act) and residual is not None and not bits and not post
         ctx.save_for_backward(x, mask if bits else (out if keep_out else None), weight, bias, prm,
                               residual if rprm is not None else None, rprm, r_weight, r_bias)
@@ -138,6 +152,7 @@ class _BNActFn(torch.autograd.Function):
         ctx.has_prod_bias = prod_bias is not None
         ctx.prod_bias_param = prod_bias  # leaf parameter (not saved): its gradient may sink in place
         ctx.bnref = None
+        ctx.tickets = tickets if fin else None
         if refbox is not None and training and ws_bwd is not None and C % 8 == 0 and (not act or bits or residual is None
                                                                                        or post):
             mode = 3 if bits else (2 if act else 1)
@@ -185,6 +200,8 @@ class _BNActFn(torch.autograd.Function):
         dgamma = dbeta = None
         want_affine = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
         direct = False
+        # small BatchNorm: the backward fold runs inside the apply pass (no bn_bwd_finalize launch)
+        bfin = (ctx.tickets is not None and training and rprm is None and L.bn_fin_ok(x.numel(), C))
         if training or want_affine:
             # sum dz and sum dz*xhat (xhat from the batch statistics, or the running ones in eval)
             rows = N * H * W
@@ -207,10 +224,11 @@ class _BNActFn(torch.autograd.Function):
                     pb_sink = grad_sink(ctx.prod_bias_param)
                     if pb_sink is None:
                         pb_grad = torch.zeros(C, dtype=F32, device=dev)
-            L.bn_bwd_finalize(ptr(acc), C, float(rows), ptr(weight.detach() if weight is not None else None), ptr(mean),
-                              ptr(invstd), ptr(sg if direct else dgamma), ptr(sb if direct else dbeta), int(direct),
-                              ptr(coef[0]), ptr(coef[1]), ptr(coef[2]), st,
-                              xsum=ptr(pb_sink if pb_sink is not None else pb_grad))
+            if not bfin:
+                L.bn_bwd_finalize(ptr(acc), C, float(rows), ptr(weight.detach() if weight is not None else None),
+                                  ptr(mean), ptr(invstd), ptr(sg if direct else dgamma), ptr(sb if direct else dbeta),
+                                  int(direct), ptr(coef[0]), ptr(coef[1]), ptr(coef[2]), st,
+                                  xsum=ptr(pb_sink if pb_sink is not None else pb_grad))
         # residual join with the projection BN folded in: both input gradients from one pass
         dual = (DUAL_BWD and training and rprm is not None and ctx.bits and not fold_x and ctx.needs_input_grad[6]
                 and dout.is_contiguous(memory_format=torch.channels_last))
@@ -218,7 +236,18 @@ class _BNActFn(torch.autograd.Function):
         # x's gradient this pass knows of (every joined gradient folded in)
         box = ctx.colsum if (training and not dual and (xg is None or fold_x) and (xg2 is None or fold_x2)
                              and not L.deterministic()) else None
-        if training and not dual:
+        if training and not dual and bfin:
+            COUNTERS["bn_bwd_fin_fused"] += 1
+            L.bn_bwd_fin_apply(ptr(acc), float(N * H * W), ptr(weight.detach() if weight is not None else None),
+                               ptr(mean), ptr(invstd), ptr(sg if direct else dgamma), ptr(sb if direct else dbeta),
+                               int(direct), ptr(pb_sink if pb_sink is not None else pb_grad), ptr(ctx.tickets[1]),
+                               ptr(dout), ptr(out), ptr(x), ptr(dx), ptr(dres), x.numel(), C, ptr(scale), ptr(shift),
+                               act, float(slope), int(ctx.bits), ptr(xg) if fold_x else 0,
+                               ptr(xg2) if fold_x2 else 0, ptr(box.acc) if box is not None else 0, st)
+            if box is not None:
+                box.pending, box.version = True, dx._version
+                dx._dv_colsum = box
+        elif training and not dual:
             L.bn_bwd_apply(ptr(dout), ptr(out), ptr(x), ptr(dx), ptr(dres), x.numel(), C, ptr(coef[0]), ptr(coef[1]),
                            ptr(coef[2]), ptr(scale), ptr(shift), act, float(slope), int(ctx.bits), st,
                            addend=ptr(xg) if fold_x else 0, addend2=ptr(xg2) if fold_x2 else 0,
@@ -259,7 +288,7 @@ class _BNActFn(torch.autograd.Function):
 
             pb_grad = _channel_sum(dx if dx.shape[1] == C else dx.contiguous(memory_format=torch.channels_last))
         return (dx, None, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None, None, None,
-                None, r_dgamma, r_dbeta, None, None, None, None, pb_grad, None, None)
+                None, r_dgamma, r_dbeta, None, None, None, None, pb_grad, None, None, None)
 
 
 def _residual_bn_coef(ctx, dout, bits, r_x, rprm, r_weight, r_bias, act, slope, fused):
@@ -519,7 +548,9 @@ def batch_norm_act(x, bn, act=None, slope=0.0, residual=None, stats=None, residu
         rargs = (None,) * 6
     y = _BN_APPLY(x, stats, bn.weight, bn.bias, rm, rv, residual, training, mom,
                        bn.eps, ACT_IDS[act], float(slope), ws_fwd, ws_bwd, residual_join, refbox, *rargs, input_join,
-                       prod_bias, bool(residual_post and residual_bn is None), colsum)
+                       prod_bias, bool(residual_post and residual_bn is None), colsum,
+                       workspace(bn, "bn_fin_ticket", (2, C // 64), x.device, torch.int32)
+                       if training and C % 64 == 0 else None)
     if refbox:
         y._dv_bnref = refbox[0]  # read by the consumer conv (ops.conv._ConvFn)
     return y

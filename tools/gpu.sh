@@ -12,7 +12,7 @@
 #   tools/gpu.sh host            Python host profiles of the eager launch-bound models
 #   tools/gpu.sh convergence     ResNet-50 1,000-step native vs torch-bf16 curves, 2 seeds
 #   tools/gpu.sh overlap         DP bucket overlap test + force-DP kernel timeline
-#   AB=VAR tools/gpu.sh ab       bench + kernel-trace A/B of an env toggle (DV_DEFER)
+#   AB=VAR [MODEL=m ARGS=..] tools/gpu.sh ab   same-box bench + kernel-trace A/B of an env toggle
 #   tools/gpu.sh abtree          same-box bench A/B of ./ab_old (tools/ab_tree.sh <commit>) vs the tree
 # Every GPU step has its own time limit and the steps are chained with &&: after a fault,
 # abort or timeout nothing else runs on the GPU in that call.
@@ -132,23 +132,25 @@ case "$mode" in
     [ -n "$t" ] && python tools/comm_timeline.py "$t" > gpurun_out/comm_timeline.txt 2>&1; rm -f "$t"
     grep -E "PASS|FAIL|backward .* ms" gpurun_out/overlap_test.log | head; head -40 gpurun_out/comm_timeline.txt 2>/dev/null ;;
   ab)
-    # A/B of an environment toggle on the ResNet-50 bench + kernel traces of both arms:
-    #   AB="DV_DEFER" (BN apply deferred into the consumer conv, tests/test_defer_gpu.py first)
-    v=${AB:-DV_DEFER}; t=tests/test_defer_gpu.py
-    timeout -k 10 600 $PYT $t > gpurun_out/ab_tests.log 2>&1 && \
-    env $v=0 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/ab_off.log 2>&1 && \
-    env $v=1 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/ab_on.log 2>&1 && \
-    cd /tmp && export TMPDIR=/tmp && \
-    env $v=0 timeout -k 10 300 rocprofv3 --kernel-trace -d "$R/gpurun_out/ab_prof_off" -o run --output-format csv -- \
-      python3 "$R/bench.py" --steps 6 --warmup 2 > "$R/gpurun_out/ab_prof_off.log" 2>&1 && \
-    env $v=1 timeout -k 10 300 rocprofv3 --kernel-trace -d "$R/gpurun_out/ab_prof_on" -o run --output-format csv -- \
-      python3 "$R/bench.py" --steps 6 --warmup 2 > "$R/gpurun_out/ab_prof_on.log" 2>&1
+    # same-box A/B of an environment toggle: bench.py alternating off / on twice, then a kernel
+    # trace of each arm:  AB=DV_FUSE_FIN MODEL=hourglass ARGS=--graph tools/gpu.sh ab
+    v=${AB:?set AB=VAR}; m=${MODEL:-resnet50}; args=${ARGS:-}
+    rc=0
+    for i in 1 2; do for s in 0 1; do
+      [ $rc -eq 0 ] && { env $v=$s timeout -k 10 300 python bench.py --model $m $args --steps 10 --warmup 3 > gpurun_out/ab_${s}_$i.log 2>&1 || rc=$?; }
+    done; done
+    [ $rc -eq 0 ] && cd /tmp && export TMPDIR=/tmp && \
+    env $v=0 timeout -k 10 300 rocprofv3 --kernel-trace -d "$R/gpurun_out/ab_prof_0" -o run --output-format csv -- \
+      python3 "$R/bench.py" --model $m $args --steps 6 --warmup 2 > "$R/gpurun_out/ab_prof_0.log" 2>&1 && \
+    env $v=1 timeout -k 10 300 rocprofv3 --kernel-trace -d "$R/gpurun_out/ab_prof_1" -o run --output-format csv -- \
+      python3 "$R/bench.py" --model $m $args --steps 6 --warmup 2 > "$R/gpurun_out/ab_prof_1.log" 2>&1
     rc=$?; cd "$R"
-    for a in off on; do
-      t=$(find gpurun_out/ab_prof_$a -name '*kernel_trace.csv' -print -quit 2>/dev/null)
-      [ -n "$t" ] && python tools/step_table.py "$t" --steps 4 --title "resnet50 $v=$a" > gpurun_out/ab_step_$a.txt 2>&1
+    for s in 0 1; do
+      t=$(find gpurun_out/ab_prof_$s -name '*kernel_trace.csv' -print -quit 2>/dev/null)
+      [ -n "$t" ] && python tools/step_table.py "$t" --steps 4 --title "$m $args $v=$s" > gpurun_out/ab_step_$s.txt 2>&1
       rm -f "$t"
-      echo "$v=$a: $(grep '^{' gpurun_out/ab_$a.log | tail -1 | cut -c1-120)"; sed -n 3,12p gpurun_out/ab_step_$a.txt 2>/dev/null
+      for i in 1 2; do echo "$v=$s run $i: $(grep '^{' gpurun_out/ab_${s}_$i.log | tail -1 | cut -c1-110)"; done
+      sed -n 1,14p gpurun_out/ab_step_$s.txt 2>/dev/null
     done ;;
   abtree)
     # same-box A/B of the tree in ./ab_old (tools/ab_tree.sh <commit>) against the working tree:
