@@ -29,8 +29,8 @@ FUSE_BWD_STATS = True  # fold the backward reduction into the consumer conv's dg
 LAZY_SHORTCUT = True   # identity-shortcut gradient masked inside the consumer's dgrad epilogue
 FOLD_RESIDUAL_BN = True  # projection-shortcut BN applied inside the block's last BN pass
 DUAL_BWD = True  # ...and its backward: reduction in the consumer dgrad's epilogue, one dual apply pass
-# small BatchNorms (C % 64 == 0, <= 2M elements): the statistics fold inside the apply passes instead
-# of a separate finalize launch, forward and backward (csrc/bn.hip "Small BatchNorms")
+# small BatchNorms (C % 64 == 0, <= 2M elements), eager steps: the statistics fold inside the apply
+# passes instead of a separate finalize launch, forward and backward (csrc/bn.hip "Small BatchNorms")
 FUSE_FINALIZE = os.environ.get("DV_FUSE_FIN", "1") != "0"
 COUNTERS = {"bwd_reduce_fused": 0, "bwd_reduce_pass": 0, "shortcut_lazy": 0, "dual_apply": 0, "dual_fused": 0,
             "bwd_apply_two_addends": 0, "bn_fin_fused": 0, "bn_bwd_fin_fused": 0}
@@ -99,7 +99,11 @@ class _BNActFn(torch.autograd.Function):
         g = weight.detach() if weight is not None else None
         b = bias.detach() if bias is not None else None
         # small BatchNorm: the shard fold runs inside the apply pass (csrc/bn.hip "Small BatchNorms")
-        fin = (training and tickets is not None and r_cfg is None and FUSE_FINALIZE and L.bn_fin_ok(x.numel(), C))
+        # eager only: it removes two launches per BatchNorm from the host's issue path (Hourglass eager
+        # +3 %); inside a captured graph the launches cost nothing on the host and the two-kernel form
+        # measured 1.4 % faster (profiles/bn_fin_ab.txt). Both forms leave the shards zeroed.
+        fin = (training and tickets is not None and r_cfg is None and FUSE_FINALIZE and L.bn_fin_ok(x.numel(), C)
+               and not torch.cuda.is_current_stream_capturing())
         if training:
             if stats is None:
                 stats = ws_fwd
