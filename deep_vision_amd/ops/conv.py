@@ -11,6 +11,8 @@ R/ResNet/pytorch/models/resnet50.py:20-27 (7x7 s2 stem), :101-133 (bottleneck 1x
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as TF
 
@@ -419,6 +421,55 @@ class GradJoin:
         return g
 
 
+# ---- weight gradients on a side stream ------------------------------------------------------
+# A layer's weight gradient is needed only by the optimizer (and the bucket all-reduce); its data
+# gradient feeds the next BatchNorm backward pass. With the weight gradient written straight into
+# ``.grad`` (grad_sink) it can run on a side HIP stream, concurrently with the HBM-bound BatchNorm
+# passes and the data gradients of the layers below. The side stream waits for the origin stream
+# at each launch (dy and x are ready), the caching allocator keeps dy / x alive until the side
+# stream is done with them, and the origin stream waits for the side stream at the end of the
+# backward pass (an autograd final callback) and before every gradient bucket's all-reduce
+# (parallel.ddp). DV_WGRAD_SIDE=0 keeps every launch on the origin stream.
+WGRAD_SIDE = os.environ.get("DV_WGRAD_SIDE", "1") != "0"
+_SIDE = {"streams": {}, "active": None}  # active: (origin stream, side stream) of this backward
+
+
+def _side_stream(device):
+    s = _SIDE["streams"].get(device)
+    if s is None:
+        s = _SIDE["streams"][device] = torch.cuda.Stream(device=device)
+    return s
+
+
+def wgrad_side_join():
+    """End of backward: the origin stream waits for every weight gradient queued on the side stream."""
+    a = _SIDE["active"]
+    if a is not None:
+        _SIDE["active"] = None
+        a[0].wait_stream(a[1])
+
+
+def wgrad_side_flush():
+    """Before reading ``.grad`` mid-backward (a bucket all-reduce): the current stream waits for the
+    weight gradients queued so far."""
+    a = _SIDE["active"]
+    if a is not None:
+        torch.cuda.current_stream(a[1].device).wait_stream(a[1])
+
+
+def _on_side(fn, device, *keep):
+    origin = torch.cuda.current_stream(device)
+    side = _side_stream(device)
+    if _SIDE["active"] is None:
+        _SIDE["active"] = (origin, side)
+        torch.autograd.Variable._execution_engine.queue_callback(wgrad_side_join)
+    side.wait_stream(origin)
+    with torch.cuda.stream(side):
+        fn()
+    for t in keep:
+        t.record_stream(side)
+
+
 def _wgrad(x, dy, weight, Cg_x, G, stride, padding, dilation, out=None, reflect=False):
     """Weight gradient (OIHW fp32). With ``out`` the result is ADDED into ``out`` (live grad).
     ``reflect``: the forward padded by reflection (im2col taps outside the image are mirrored)."""
@@ -539,7 +590,11 @@ class _ConvFn(torch.autograd.Function):
                 dx = join.produce(dx)
         if ctx.needs_input_grad[1]:
             sink = grad_sink(weight)
-            dw = _wgrad(x, dy, weight, Cg_x, G, stride, padding, dilation, out=sink, reflect=ctx.reflect)
+            if sink is not None and WGRAD_SIDE and dy.is_cuda:
+                _on_side(lambda: _wgrad(x, dy, weight, Cg_x, G, stride, padding, dilation, out=sink,
+                                        reflect=ctx.reflect), dy.device, x, dy)
+            else:
+                dw = _wgrad(x, dy, weight, Cg_x, G, stride, padding, dilation, out=sink, reflect=ctx.reflect)
             if sink is not None:
                 dw = None
         if has_bias and ctx.needs_input_grad[2]:

@@ -47,6 +47,10 @@ import torch.distributed as dist
 from .flat import flatten_parameters
 
 
+def t_cuda(t):
+    return t.is_cuda
+
+
 class DoubleReadyError(RuntimeError):
     """A parameter reported a complete gradient twice in one backward (its bucket may already be
     in flight), e.g. a second ``backward(retain_graph=True)`` without a new forward / prepare."""
@@ -159,6 +163,10 @@ class DataParallel(torch.nn.Module):
 
     # ------------------------------------------------------------------ communication
     def _issue(self, b: _Bucket, where: str = "finish"):
+        if t_cuda(self.gflat):  # weight gradients still queued on the side stream (ops.conv)
+            from ..ops.conv import wgrad_side_flush
+
+            wgrad_side_flush()
         t = self.gflat[b.start:b.end]
         b.issued = True
         self.comm_stats["allreduce_calls"] += 1
