@@ -40,7 +40,7 @@ from .. import nn
 from .. import ops as F
 from ..ops.bn import STAT_ROWS, STAT_SHARDS
 from ..ops.common import workspace
-from ..ops.conv import ColsumBox, GradJoin
+from ..ops.conv import ColsumBox, GradJoin, no_wgrad_side
 
 
 import os
@@ -275,6 +275,12 @@ class StackedHourglassNetwork(tnn.Module):
         self.inter_y = tnn.ModuleList(nn.Conv2d(num_heatmap, 256, 1) for _ in range(num_stack - 1))
 
     def forward(self, x):
+        if _fork(x):  # branch streams this step: weight gradients stay on their origin streams
+            with no_wgrad_side():
+                return self._forward(x)
+        return self._forward(x)
+
+    def _forward(self, x):
         x = F.conv_bn_act(x, self.stem, self.stem_bn, "relu")
         x = _run_blocks(self.pre, x)
         x = _pool(x, None, self.pre2[0].bn1)

@@ -15,6 +15,7 @@ import torch.nn as tnn
 
 from .. import nn
 from .. import ops as F
+from ..ops.conv import no_wgrad_side
 
 
 def _ch(c, alpha):
@@ -71,7 +72,8 @@ class MobileNetV1(tnn.Module):
         self.linear = nn.Linear(_ch(1024, alpha), num_classes)
 
     def forward(self, x):
-        return self.linear(torch.flatten(self.features(x), 1))
+        with no_wgrad_side():  # pointwise wgrads gain nothing on a side stream here (ops/conv.py WGRAD_SIDE)
+            return self.linear(torch.flatten(self.features(x), 1))
 
 
 class _SeparableConvTF(tnn.Module):
@@ -102,8 +104,9 @@ class MobileNetV1TF(tnn.Module):
         self.fc = nn.Linear(1024, num_classes)
 
     def forward(self, x):
-        x = self.blocks(self.conv1(x))
-        return self.fc(torch.flatten(self.pool(x), 1))
+        with no_wgrad_side():
+            x = self.blocks(self.conv1(x))
+            return self.fc(torch.flatten(self.pool(x), 1))
 
 
 # ------------------------------------ ShuffleNet V1 ------------------------------------

@@ -11,6 +11,7 @@ R/ResNet/pytorch/models/resnet50.py:20-27 (7x7 s2 stem), :101-133 (bottleneck 1x
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -430,8 +431,24 @@ class GradJoin:
 # stream is done with them, and the origin stream waits for the side stream at the end of the
 # backward pass (an autograd final callback) and before every gradient bucket's all-reduce
 # (parallel.ddp). DV_WGRAD_SIDE=0 keeps every launch on the origin stream.
-WGRAD_SIDE = os.environ.get("DV_WGRAD_SIDE", "1") != "0"
-_SIDE = {"streams": {}, "active": None}  # active: (origin stream, side stream) of this backward
+# DV_WGRAD_SIDE=0 keeps every launch on the origin stream, "3x3" moves only the im2col (R*S > 1)
+# ones. Same-box, ResNet-50: origin stream 13,152 img/s, 3x3 only 13,342, every wgrad 13,837
+# (profiles/wgrad_side_stream_ab.txt); MobileNet V1 lost 1.8 % with its pointwise wgrads moved (they
+# overlap its HBM-bound depthwise / BN passes, nothing gains) and opts out (models/mobilenet.py).
+WGRAD_SIDE = {"0": False, "3x3": "3x3"}.get(os.environ.get("DV_WGRAD_SIDE", "1"), "all")
+_SIDE = {"streams": {}, "active": None, "suspend": 0}  # active: (origin, side stream) of this backward
+
+
+@contextlib.contextmanager
+def no_wgrad_side():
+    """Convolutions built inside keep their weight gradients on the origin stream (a model that
+    forks its own branch streams: models/hourglass.py, where a fifth stream would share a hardware
+    queue with the branches)."""
+    _SIDE["suspend"] += 1
+    try:
+        yield
+    finally:
+        _SIDE["suspend"] -= 1
 
 
 def _side_stream(device):
@@ -519,6 +536,8 @@ class _ConvFn(torch.autograd.Function):
                 extra=(0, 0), join=None, join_role=None, reflect=False, out_box=None, residual=None, residual_join=None,
                 bias_via_bn=False, bias_colsum=None):
         ctx.colsum_box = bias_colsum
+        R_, S_ = weight.shape[2], weight.shape[3]
+        ctx.wside = bool(WGRAD_SIDE) and _SIDE["suspend"] == 0 and (WGRAD_SIDE == "all" or R_ * S_ > 1)
         N, Cx, H, W = x.shape
         O, Ig, R, S = weight.shape
         G = groups
@@ -590,7 +609,7 @@ class _ConvFn(torch.autograd.Function):
                 dx = join.produce(dx)
         if ctx.needs_input_grad[1]:
             sink = grad_sink(weight)
-            if sink is not None and WGRAD_SIDE and dy.is_cuda:
+            if sink is not None and ctx.wside and dy.is_cuda:
                 _on_side(lambda: _wgrad(x, dy, weight, Cg_x, G, stride, padding, dilation, out=sink,
                                         reflect=ctx.reflect), dy.device, x, dy)
             else:
