@@ -436,6 +436,7 @@ class GradJoin:
 # (profiles/wgrad_side_stream_ab.txt); MobileNet V1 lost 1.8 % with its pointwise wgrads moved (they
 # overlap its HBM-bound depthwise / BN passes, nothing gains) and opts out (models/mobilenet.py).
 WGRAD_SIDE = {"0": False, "3x3": "3x3"}.get(os.environ.get("DV_WGRAD_SIDE", "1"), "all")
+SIDE_COMM = os.environ.get("DV_WGRAD_SIDE_COMM", "side")
 _SIDE = {"streams": {}, "active": None, "suspend": 0}  # active: (origin, side stream) of this backward
 
 
@@ -458,6 +459,12 @@ def _side_stream(device):
     return s
 
 
+def _dist_active():
+    import torch.distributed as dist
+
+    return dist.is_available() and dist.is_initialized()
+
+
 def wgrad_side_join():
     """End of backward: the origin stream waits for every weight gradient queued on the side stream."""
     a = _SIDE["active"]
@@ -466,12 +473,20 @@ def wgrad_side_join():
         a[0].wait_stream(a[1])
 
 
-def wgrad_side_flush():
-    """Before reading ``.grad`` mid-backward (a bucket all-reduce): the current stream waits for the
-    weight gradients queued so far."""
+def wgrad_side_comm_stream():
+    """For a consumer of ``.grad`` mid-backward (a bucket all-reduce): the side stream, made to wait
+    for the current stream, when weight gradients are queued on it (the consumer then issues from
+    it: ordered after both streams' work so far, and the origin stream does not stall); else None."""
     a = _SIDE["active"]
-    if a is not None:
-        torch.cuda.current_stream(a[1].device).wait_stream(a[1])
+    if a is None:
+        return None
+    side = a[1]
+    cur = torch.cuda.current_stream(side.device)
+    if SIDE_COMM == "flush":  # the current stream waits for the queued weight gradients instead
+        cur.wait_stream(side)
+        return None
+    side.wait_stream(cur)
+    return side
 
 
 def _on_side(fn, device, *keep):
@@ -537,7 +552,11 @@ class _ConvFn(torch.autograd.Function):
                 bias_via_bn=False, bias_colsum=None):
         ctx.colsum_box = bias_colsum
         R_, S_ = weight.shape[2], weight.shape[3]
-        ctx.wside = bool(WGRAD_SIDE) and _SIDE["suspend"] == 0 and (WGRAD_SIDE == "all" or R_ * S_ > 1)
+        # not under a process group: with RCCL's streams present the side stream shared the compute
+        # stream's hardware queue (GPU_MAX_HW_QUEUES = 4) and serialised behind it -- world-1 RCCL
+        # ResNet-50 13,000 -> 12,300 img/s (profiles/wgrad_side_stream_ab.txt)
+        ctx.wside = (bool(WGRAD_SIDE) and _SIDE["suspend"] == 0 and (WGRAD_SIDE == "all" or R_ * S_ > 1)
+                     and not _dist_active())
         N, Cx, H, W = x.shape
         O, Ig, R, S = weight.shape
         G = groups

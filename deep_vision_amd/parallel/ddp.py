@@ -47,10 +47,6 @@ import torch.distributed as dist
 from .flat import flatten_parameters
 
 
-def t_cuda(t):
-    return t.is_cuda
-
-
 class DoubleReadyError(RuntimeError):
     """A parameter reported a complete gradient twice in one backward (its bucket may already be
     in flight), e.g. a second ``backward(retain_graph=True)`` without a new forward / prepare."""
@@ -163,10 +159,17 @@ class DataParallel(torch.nn.Module):
 
     # ------------------------------------------------------------------ communication
     def _issue(self, b: _Bucket, where: str = "finish"):
-        if t_cuda(self.gflat):  # weight gradients still queued on the side stream (ops.conv)
-            from ..ops.conv import wgrad_side_flush
+        side = None
+        if self.gflat.is_cuda:  # weight gradients still queued on the side stream (ops.conv)
+            from ..ops.conv import wgrad_side_comm_stream
 
-            wgrad_side_flush()
+            side = wgrad_side_comm_stream()
+        if side is not None:
+            with torch.cuda.stream(side):
+                return self._issue_on(b, where)
+        return self._issue_on(b, where)
+
+    def _issue_on(self, b: _Bucket, where: str):
         t = self.gflat[b.start:b.end]
         b.issued = True
         self.comm_stats["allreduce_calls"] += 1
