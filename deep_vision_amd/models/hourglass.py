@@ -275,10 +275,12 @@ class StackedHourglassNetwork(tnn.Module):
         self.inter_y = tnn.ModuleList(nn.Conv2d(num_heatmap, 256, 1) for _ in range(num_stack - 1))
 
     def forward(self, x):
-        if _fork(x):  # branch streams this step: weight gradients stay on their origin streams
-            with no_wgrad_side():
-                return self._forward(x)
-        return self._forward(x)
+        # weight gradients stay on their origin streams: a captured step forks its own branch streams
+        # (a fifth stream shared their hardware queues: 1,428 -> 1,233 img/s), and the eager step is
+        # host-bound (each side-stream launch adds event records / waits on the host: 913 / 771 vs
+        # 682 / 770 img/s, profiles/wgrad_side_stream_ab.txt)
+        with no_wgrad_side():
+            return self._forward(x)
 
     def _forward(self, x):
         x = F.conv_bn_act(x, self.stem, self.stem_bn, "relu")
