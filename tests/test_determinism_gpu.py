@@ -172,19 +172,22 @@ def test_deterministic_mode_matches_default_per_block(name):
     # default mode's float atomics, moves bn1.weight's gradient by up to 9 %, run to run --
     # tools/diag_shuffle_block.py). The deterministic result must then lie as close to one of
     # three default runs as those lie to each other; every well-conditioned tensor within 2e-2.
-    def check(what, k, i=None):
+    def check(what, k, i=None, floor=2e-2):
         ts = [r[k] if i is None else r[k][i] for r in runs]
         v = b[k] if i is None else b[k][i]
         spread = max(rel(ts[0], ts[1]), rel(ts[0], ts[2]), rel(ts[1], ts[2]))
         err = min(rel(t, v) for t in ts)
-        assert err < max(2e-2, 4 * spread), (what, i, err, spread)
+        assert err < max(floor, 4 * spread), (what, i, err, spread)
 
     assert rel(a[0], b[0]) < 2e-3, ("output", rel(a[0], b[0]))
     check("input grad", 1)
     for i in range(len(a[2])):
         check("param grad", 2, i)
-    for i, (u, v) in enumerate(zip(a[3], b[3])):
-        assert rel(u, v) < 1e-4, ("buffer", i, rel(u, v))
+    # running statistics: 1e-4, or the default mode's own spread for a running mean near zero (the
+    # ShuffleNet units' grouped-conv outputs: |mean| ~ 1e-5, where the float-atomic order of the
+    # batch sums moves it by several percent run to run)
+    for i in range(len(a[3])):
+        check("buffer", 3, i, floor=1e-4)
 
 
 def test_deterministic_loss_totals_match_default():
