@@ -40,6 +40,14 @@ import json
 import sys
 import time
 
+# Eight hardware queues per process (HIP's default is 4), set before HIP initialises: the compute
+# stream, the weight-gradient side stream (deep_vision_amd/ops/conv.py) and RCCL's streams each get a
+# queue of their own. With 4, the side stream shared the compute stream's queue under RCCL and
+# serialised (world-1 RCCL ResNet-50: 12,960 img/s without the side stream, 13,690 with it and 8
+# queues; profiles/wgrad_side_stream_ab.txt). A larger value already set is kept.
+if int(__import__("os").environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+    __import__("os").environ["GPU_MAX_HW_QUEUES"] = "8"
+
 # Reference-derived comparators, images/sec per node:
 #   ResNet-50-equivalent proxy ~376 (8 GPUs), YOLOv3 ~179 (8x V100), LeNet-5 PT ~906.
 BASELINES = {"resnet50": 376.0, "yolov3": 179.0, "lenet5": 906.0}

@@ -176,6 +176,9 @@ def spawn(nproc: int, argv, module: str | None = None) -> int:
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env.setdefault("OMP_NUM_THREADS", "4")
+    # a hardware queue each for the compute, weight-gradient side and RCCL streams (ops/conv.py)
+    if int(env.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+        env["GPU_MAX_HW_QUEUES"] = "8"
     return subprocess.call(cmd, env=env)
 
 

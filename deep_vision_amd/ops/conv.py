@@ -459,7 +459,24 @@ def _side_stream(device):
     return s
 
 
+def _hw_queues():
+    try:
+        return int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    except ValueError:
+        return 4
+
+
+# Under a process group the side stream needs hardware queues of its own: with HIP's default 4 it
+# shared the compute stream's queue beside RCCL's streams and serialised behind it (world-1 RCCL
+# ResNet-50 13,000 -> 12,300 img/s); with GPU_MAX_HW_QUEUES >= 8 (bench.py sets 8) it overlaps
+# (12,960 -> 13,690). DV_WGRAD_SIDE_DP=0 / 1 forces it off / on under a process group.
+_SIDE_DP = {"0": False, "1": True}.get(os.environ.get("DV_WGRAD_SIDE_DP", ""), _hw_queues() >= 8)
+
+
 def _dist_active():
+    """True when a process group is up and the side stream must stay off (see _SIDE_DP)."""
+    if _SIDE_DP:
+        return False
     import torch.distributed as dist
 
     return dist.is_available() and dist.is_initialized()
@@ -552,9 +569,7 @@ class _ConvFn(torch.autograd.Function):
                 bias_via_bn=False, bias_colsum=None):
         ctx.colsum_box = bias_colsum
         R_, S_ = weight.shape[2], weight.shape[3]
-        # not under a process group: with RCCL's streams present the side stream shared the compute
-        # stream's hardware queue (GPU_MAX_HW_QUEUES = 4) and serialised behind it -- world-1 RCCL
-        # ResNet-50 13,000 -> 12,300 img/s (profiles/wgrad_side_stream_ab.txt)
+        # under a process group only with >= 8 hardware queues (_SIDE_DP)
         ctx.wside = (bool(WGRAD_SIDE) and _SIDE["suspend"] == 0 and (WGRAD_SIDE == "all" or R_ * S_ > 1)
                      and not _dist_active())
         N, Cx, H, W = x.shape
