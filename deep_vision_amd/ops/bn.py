@@ -475,10 +475,21 @@ def _torch_bn_act(x, bn, act, slope, residual):
 
 
 def _flush_batch_count(bn):
-    n = bn.__dict__.get("_dv_nbt_pending", 0)
+    d = bn.__dict__
+    n = d.get("_dv_nbt_pending", 0)
     if n:
-        bn.num_batches_tracked.add_(n)
-        bn._dv_nbt_pending = 0
+        if not _nbt_rewritten(bn):
+            bn.num_batches_tracked.add_(n)
+        d["_dv_nbt_pending"] = 0
+
+
+def _nbt_rewritten(bn) -> bool:
+    """Was ``num_batches_tracked`` written in place since the pending count started
+    (reset_running_stats' zero_, load_state_dict's copy_)? Those writes replace the count. A
+    different tensor object (deepcopy, module.to / cuda) carries the count over."""
+    t = bn.num_batches_tracked
+    ref = bn.__dict__.get("_dv_nbt_ver")
+    return ref is not None and ref[0] == id(t) and ref[1] != t._version
 
 
 def _count_batch(bn):
@@ -492,7 +503,17 @@ def _count_batch(bn):
     d = bn.__dict__  # plain instance attributes: no nn.Module.__setattr__ on the per-call path
     if "_dv_nbt_hook" not in d:
         d["_dv_nbt_hook"] = bn.register_state_dict_pre_hook(lambda m, *a, **k: _flush_batch_count(m))
-    d["_dv_nbt_pending"] = d.get("_dv_nbt_pending", 0) + 1
+    add_pending_batches(bn, 1)
+
+
+def add_pending_batches(bn, k):
+    """Count ``k`` more training batches against ``bn.num_batches_tracked`` (host side, lazy)."""
+    d = bn.__dict__
+    t = bn.num_batches_tracked
+    if d.get("_dv_nbt_pending", 0) and _nbt_rewritten(bn):
+        d["_dv_nbt_pending"] = 0  # the buffer was rewritten since: earlier pending steps are void
+    d["_dv_nbt_pending"] = d.get("_dv_nbt_pending", 0) + k
+    d["_dv_nbt_ver"] = (id(t), t._version)
 
 
 def bn_momentum(bn) -> float:

@@ -107,8 +107,10 @@ class CapturedStep:
             if src is not dst:
                 dst.copy_(src, non_blocking=True)
         self.opt.graph_tick()
+        from ..ops.bn import add_pending_batches
+
         for m in self._counted:
-            m._dv_nbt_pending = m.__dict__.get("_dv_nbt_pending", 0) + 1
+            add_pending_batches(m, 1)
         from ..ops.act import advance_dropout_step
 
         advance_dropout_step()  # fresh dropout masks per replay (ops/act.py)
