@@ -109,6 +109,18 @@ class BatchNorm2d(tnn.BatchNorm2d):
             return super().forward(x)
         return F.batch_norm_act(x, self)
 
+    # the native path counts num_batches_tracked on the host and writes it lazily (ops/bn.py
+    # _count_batch): a copy or pickle takes the exact count, a reset drops the pending steps
+    def __getstate__(self):
+        from ..ops.bn import _flush_batch_count
+
+        _flush_batch_count(self)
+        return super().__getstate__()
+
+    def reset_running_stats(self):
+        self.__dict__["_dv_nbt_pending"] = 0
+        super().reset_running_stats()
+
 
 class ReLU(tnn.ReLU):
     def forward(self, x):

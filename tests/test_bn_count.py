@@ -57,3 +57,19 @@ def test_deepcopy_carries_pending_steps():
     assert bn_momentum(cp) == 1.0  # cumulative average restarts after a reset
     _count_batch(cp)
     assert bn_momentum(cp) == 0.5
+
+
+def test_framework_batchnorm_copy_then_reset():
+    """deep_vision_amd.nn.BatchNorm2d: a deepcopy flushes the pending count into the copy, and
+    reset_running_stats on the copy drops everything (tools/diag_eval_gap.py's recalibration)."""
+    from deep_vision_amd import nn
+
+    bn = nn.BatchNorm2d(4)
+    _count_batch(bn)
+    _count_batch(bn)
+    cp = copy.deepcopy(bn)
+    assert int(cp.num_batches_tracked) == 2 and _n(bn) == 2
+    cp.reset_running_stats()
+    cp.momentum = None
+    _count_batch(cp)
+    assert bn_momentum(cp) == 1.0
