@@ -118,17 +118,22 @@ static void normalize_batch(py::array_t<uint8_t, py::array::c_style> src, py::ar
   dvio::normalize_batch(s, d, N, H, W, C, mean, stdv, scale, threads);
 }
 
-// (H, W, C) uint8 -> the (ch, cw, C) crop of its bilinear rescale to (outH, outW), GIL released
-static py::array_t<uint8_t> resize_crop(py::array_t<uint8_t, py::array::c_style | py::array::forcecast> src,
-                                        int64_t outH, int64_t outW, int64_t cy, int64_t cx, int64_t ch, int64_t cw) {
+// (H, W, C) uint8 -> the (ch, cw, C) crop of its bilinear rescale to (outH, outW), GIL released.
+// ``src`` may be a strided view with unit channel stride (e.g. the RGB channels of a decoder's
+// RGBX buffer, exported without a copy: data/datasets.py load_rgb).
+static py::array_t<uint8_t> resize_crop(py::array_t<uint8_t, py::array::forcecast> src, int64_t outH, int64_t outW,
+                                        int64_t cy, int64_t cx, int64_t ch, int64_t cw) {
   if (src.ndim() != 3) throw std::runtime_error("resize_crop: expected an HWC array");
   const int64_t H = src.shape(0), W = src.shape(1), C = src.shape(2);
+  if (src.strides(2) != 1 || src.strides(1) < C || src.strides(0) < W * src.strides(1))  // e.g. a flipped view
+    src = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>::ensure(src);
+  const int64_t ps = src.strides(1), rs = src.strides(0);
   py::array_t<uint8_t> out({ch, cw, C});
   const uint8_t* s = src.data();
   uint8_t* d = out.mutable_data();
   {
     py::gil_scoped_release nogil;
-    dvio::resize_crop_bilinear(s, H, W, C, outH, outW, cy, cx, ch, cw, d);
+    dvio::resize_crop_bilinear(s, H, W, C, outH, outW, cy, cx, ch, cw, d, ps, rs);
   }
   return out;
 }

@@ -262,11 +262,16 @@ inline void normalize_batch(const uint8_t* s, float* d, int64_t N, int64_t H, in
 // followed by a crop, computed in one pass for the crop window only: bilinear sampling with
 // cv2.resize INTER_LINEAR's geometry (src = (dst + 0.5) * in/out - 0.5, clamped to the border, no
 // antialiasing) -- the reference decodes and resizes with cv2 -- in 11-bit fixed point per axis
-// like cv2's uint8 path. src: [H][W][C] uint8, dst: [ch][cw][C].
+// like cv2's uint8 path. src: [H][W][C] uint8 with pixel stride ps >= C and row stride rs (a
+// decoder's RGBX image read in place: ps = 4), dst: [ch][cw][C] contiguous.
 inline void resize_crop_bilinear(const uint8_t* src, int64_t H, int64_t W, int64_t C, int64_t outH, int64_t outW,
-                                 int64_t cy, int64_t cx, int64_t ch, int64_t cw, uint8_t* dst) {
+                                 int64_t cy, int64_t cx, int64_t ch, int64_t cw, uint8_t* dst, int64_t ps = 0,
+                                 int64_t rs = 0) {
   if (H <= 0 || W <= 0 || outH <= 0 || outW <= 0 || cy < 0 || cx < 0 || cy + ch > outH || cx + cw > outW)
     throw std::runtime_error("resize_crop_bilinear: bad geometry");
+  if (ps == 0) ps = C;
+  if (rs == 0) rs = W * ps;
+  if (ps < C || rs < W * ps) throw std::runtime_error("resize_crop_bilinear: bad strides");
   constexpr int BITS = 11, ONE = 1 << BITS;
   const double fy = (double)H / outH, fx = (double)W / outW;
   std::vector<int32_t> x0(cw), x1(cw), wx(cw);
@@ -276,8 +281,8 @@ inline void resize_crop_bilinear(const uint8_t* src, int64_t H, int64_t W, int64
     int64_t a = (int64_t)sx;
     if (a > W - 1) a = W - 1;
     const double f = sx - a;
-    x0[j] = (int32_t)(a * C);
-    x1[j] = (int32_t)(std::min<int64_t>(a + 1, W - 1) * C);
+    x0[j] = (int32_t)(a * ps);
+    x1[j] = (int32_t)(std::min<int64_t>(a + 1, W - 1) * ps);
     wx[j] = (int32_t)(f * ONE + 0.5);
   }
   for (int64_t i = 0; i < ch; ++i) {
@@ -286,8 +291,8 @@ inline void resize_crop_bilinear(const uint8_t* src, int64_t H, int64_t W, int64
     int64_t a = (int64_t)sy;
     if (a > H - 1) a = H - 1;
     const int32_t wy = (int32_t)((sy - a) * ONE + 0.5);
-    const uint8_t* r0 = src + a * W * C;
-    const uint8_t* r1 = src + std::min<int64_t>(a + 1, H - 1) * W * C;
+    const uint8_t* r0 = src + a * rs;
+    const uint8_t* r1 = src + std::min<int64_t>(a + 1, H - 1) * rs;
     uint8_t* d = dst + i * cw * C;
     for (int64_t j = 0; j < cw; ++j) {
       const int32_t w1 = wx[j], w0 = ONE - w1;

@@ -184,7 +184,7 @@ class RescaleCrop:
         if io is None:  # the two-step form
             r = _resize(image, nh, nw)
             return {**sample, "image": np.ascontiguousarray(r[top:top + ch, left:left + cw])}
-        return {**sample, "image": io.resize_crop(np.ascontiguousarray(image), nh, nw, top, left, ch, cw)}
+        return {**sample, "image": io.resize_crop(image, nh, nw, top, left, ch, cw)}  # strided views read in place
 
 
 class FastColorJitter(ColorJitter):

@@ -99,3 +99,33 @@ def test_rescale_crop_transform_and_draft_decode(tmp_path):
     small = load_rgb(p, min_side=256)
     assert min(small.shape[:2]) >= 256 and small.shape[0] < 1100
     assert load_rgb(p).shape[:2] == (1100, 1500)
+
+
+def test_resize_crop_reads_strided_views_and_zero_copy_decode(tmp_path):
+    """_io.resize_crop reads an RGBX-strided view (the decoder's buffer, data/datasets.py load_rgb
+    zero_copy) in place and a flipped view through a copy, with the contiguous result; the zero-copy
+    decode equals the copying one and stays valid after its image is closed."""
+    import gc
+
+    import numpy as np
+    from PIL import Image
+
+    from deep_vision_amd import _io
+    from deep_vision_amd.data.datasets import load_rgb
+
+    rng = np.random.RandomState(2)
+    rgbx = rng.randint(0, 256, (41, 57, 4)).astype(np.uint8)
+    view = rgbx[:, :, :3]
+    for v in (view, view[:, ::-1], view[::-1]):
+        a = _io.resize_crop(v, 36, 50, 3, 4, 30, 40)
+        assert np.array_equal(a, _io.resize_crop(np.ascontiguousarray(v), 36, 50, 3, 4, 30, 40))
+    paths = []
+    for i in range(4):
+        p = str(tmp_path / f"im{i}.jpg")
+        Image.fromarray(rng.randint(0, 256, (300 + i, 420, 3)).astype(np.uint8)).save(p, quality=90)
+        paths.append(p)
+    views = [load_rgb(p, 128, zero_copy=True) for p in paths]
+    gc.collect()
+    _ = [np.full((300, 420, 4), 9, np.uint8) for _ in range(20)]  # reuse freed memory, if any was freed
+    for v, p in zip(views, paths):
+        assert v.shape[2] == 3 and np.array_equal(v, load_rgb(p, 128))
