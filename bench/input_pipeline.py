@@ -121,9 +121,9 @@ def main():
         arms = {"reference_fp32": ImageNet2012Dataset(imgdir, syn, T.imagenet_train_transform(device_normalize=False)),
                 "device_normalize_u8": ImageNet2012Dataset(imgdir, syn, T.imagenet_train_transform(device_normalize=True),
                                                            decode_min_side=256),
-                "device_normalize_u8_copying_decode": ImageNet2012Dataset(
+                "device_normalize_u8_zero_copy_decode": ImageNet2012Dataset(
                     imgdir, syn, T.imagenet_train_transform(device_normalize=True), decode_min_side=256,
-                    zero_copy=False)}
+                    zero_copy=True)}
         for name, ds in arms.items():
             r, b = per_worker_rate(ds, a.per_worker)
             rec[name] = {"per_worker_img_s": round(r, 1), "bytes_per_img": int(b), "loader_img_s": {}}
