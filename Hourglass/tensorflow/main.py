@@ -46,7 +46,7 @@ def main(epochs, start_epoch, learning_rate, tensorboard_dir, checkpoint, num_he
          num_stack):
     from deep_vision_amd.launch import maybe_spawn
 
-    maybe_spawn(nproc, device)  # parent: spawns one rank per GPU and exits; ranks: CPU pinning
+    maybe_spawn(nproc, device, graph=graph)  # parent: spawns one rank per GPU and exits; ranks: CPU pinning
     cfg = get_config("hourglass")
     cfg = cfg.replace(optimizer_params={"lr": learning_rate}, batch_size=batch_size, total_epochs=epochs,
                       model_params={**cfg.model_params, "num_heatmap": num_heatmap},

@@ -40,12 +40,15 @@ import json
 import sys
 import time
 
-# Eight hardware queues per process (HIP's default is 4), set before HIP initialises: the compute
-# stream, the weight-gradient side stream (deep_vision_amd/ops/conv.py) and RCCL's streams each get a
-# queue of their own. With 4, the side stream shared the compute stream's queue under RCCL and
-# serialised (world-1 RCCL ResNet-50: 12,960 img/s without the side stream, 13,690 with it and 8
-# queues; profiles/wgrad_side_stream_ab.txt). A larger value already set is kept.
-if int(__import__("os").environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+# Eager steps: eight hardware queues per process (HIP's default is 4), set before HIP initialises:
+# the compute stream, the weight-gradient side stream (deep_vision_amd/ops/conv.py) and RCCL's
+# streams each get a queue of their own. With 4, the side stream shared the compute stream's queue
+# under RCCL and serialised (world-1 RCCL ResNet-50: 12,960 img/s without the side stream, 13,690
+# with it and 8 queues). Captured steps (--graph) keep HIP's default: they use no side stream, and
+# Hourglass's captured branch streams replayed 2.7 % slower with 8 (profiles/wgrad_side_stream_ab.txt).
+# A larger value already set is kept; DV_KEEP_HW_QUEUES=1 keeps any value (A/B runs).
+if ("--graph" not in __import__("sys").argv and __import__("os").environ.get("DV_KEEP_HW_QUEUES") != "1"
+        and int(__import__("os").environ.get("GPU_MAX_HW_QUEUES", "4")) < 8):
     __import__("os").environ["GPU_MAX_HW_QUEUES"] = "8"
 
 # Reference-derived comparators, images/sec per node:
@@ -222,7 +225,7 @@ def main():
         # self-launch N ranks; this parent never initialises the GPU
         from deep_vision_amd.launch import spawn
 
-        sys.exit(spawn(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
+        sys.exit(spawn(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:], graph=args.graph))
 
     if "WORLD_SIZE" in os.environ:  # a rank: its own NUMA-local CPU set before any GPU / thread-pool use
         from deep_vision_amd.launch import pin_rank_cpus

@@ -169,20 +169,28 @@ def pin_rank_cpus() -> None:
         pass
 
 
-def spawn(nproc: int, argv, module: str | None = None) -> int:
+def hw_queues_env(env, graph: bool) -> None:
+    """Eager steps: a hardware queue each for the compute, weight-gradient side and RCCL streams
+    (ops/conv.py; 4, HIP's default, serialised the side stream under RCCL). Captured steps keep
+    HIP's default: they use no side stream, and the Hourglass branch streams of a captured step
+    replayed 2.7 % slower with 8 (profiles/wgrad_side_stream_ab.txt). A larger value already set
+    is kept; DV_KEEP_HW_QUEUES=1 keeps any value."""
+    if not graph and env.get("DV_KEEP_HW_QUEUES") != "1" and int(env.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+        env["GPU_MAX_HW_QUEUES"] = "8"
+
+
+def spawn(nproc: int, argv, module: str | None = None, graph: bool = False) -> int:
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr=127.0.0.1", f"--master-port={free_port()}"]
     cmd += (["-m", module] if module else []) + list(argv)
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env.setdefault("OMP_NUM_THREADS", "4")
-    # a hardware queue each for the compute, weight-gradient side and RCCL streams (ops/conv.py)
-    if int(env.get("GPU_MAX_HW_QUEUES", "4")) < 8:
-        env["GPU_MAX_HW_QUEUES"] = "8"
+    hw_queues_env(env, graph)
     return subprocess.call(cmd, env=env)
 
 
-def maybe_spawn(nproc, device=None) -> None:
+def maybe_spawn(nproc, device=None, graph: bool = False) -> None:
     """Called first thing by the entry points: with ``--nproc N > 1`` (or the default: every visible
     GPU, resolve_nproc) outside a torchrun world, re-launch this script N times and exit. Inside a
     world, pin this rank's CPUs (pin_rank_cpus)."""
@@ -205,7 +213,7 @@ def maybe_spawn(nproc, device=None) -> None:
         if a.startswith("--nproc="):
             continue
         out.append(a)
-    sys.exit(spawn(nproc, out))
+    sys.exit(spawn(nproc, out, graph=graph))
 
 
 def main(argv=None):

@@ -444,12 +444,27 @@ _SIDE = {"streams": {}, "active": None, "suspend": 0}  # active: (origin, side s
 def no_wgrad_side():
     """Convolutions built inside keep their weight gradients on the origin stream (a model that
     forks its own branch streams: models/hourglass.py, where a fifth stream would share a hardware
-    queue with the branches)."""
+    queue with the branches). DV_WGRAD_SIDE_OPTOUT=0 ignores it (same-box A/B)."""
+    if not _SIDE_OPTOUT:
+        yield
+        return
     _SIDE["suspend"] += 1
     try:
         yield
     finally:
         _SIDE["suspend"] -= 1
+
+
+_SIDE_OPTOUT = os.environ.get("DV_WGRAD_SIDE_OPTOUT", "1") != "0"
+# Captured steps with >= 8 hardware queues keep weight gradients on the origin stream: a graph
+# whose side-stream branches land on hardware queues of their own replayed 24-35 % slower
+# (ResNet-50 --graph 13,120 -> 10,010 img/s, YOLOv3 1,142 -> 750; profiles/wgrad_side_stream_ab.txt).
+# With HIP's default 4 (what bench.py / launch.spawn leave to captured steps) the side stream is kept
+# (YOLOv3 --graph +2 %, ResNet-50 +0.3 %). DV_WGRAD_SIDE_GRAPH=0 / 1 forces it.
+
+
+def _capturing():
+    return not _SIDE_GRAPH and torch.cuda.is_current_stream_capturing()
 
 
 def _side_stream(device):
@@ -471,6 +486,7 @@ def _hw_queues():
 # ResNet-50 13,000 -> 12,300 img/s); with GPU_MAX_HW_QUEUES >= 8 (bench.py sets 8) it overlaps
 # (12,960 -> 13,690). DV_WGRAD_SIDE_DP=0 / 1 forces it off / on under a process group.
 _SIDE_DP = {"0": False, "1": True}.get(os.environ.get("DV_WGRAD_SIDE_DP", ""), _hw_queues() >= 8)
+_SIDE_GRAPH = {"0": False, "1": True}.get(os.environ.get("DV_WGRAD_SIDE_GRAPH", ""), _hw_queues() < 8)
 
 
 def _dist_active():
@@ -571,7 +587,7 @@ class _ConvFn(torch.autograd.Function):
         R_, S_ = weight.shape[2], weight.shape[3]
         # under a process group only with >= 8 hardware queues (_SIDE_DP)
         ctx.wside = (bool(WGRAD_SIDE) and _SIDE["suspend"] == 0 and (WGRAD_SIDE == "all" or R_ * S_ > 1)
-                     and not _dist_active())
+                     and not _dist_active() and not _capturing())
         N, Cx, H, W = x.shape
         O, Ig, R, S = weight.shape
         G = groups

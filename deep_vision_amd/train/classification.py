@@ -333,7 +333,7 @@ def main(argv=None, choices=None, default=None):
         from ..profiling import run_under_rocprof
 
         run_under_rocprof(argv)  # exits with the profiled child's status
-    maybe_spawn(a.nproc, a.device)
+    maybe_spawn(a.nproc, a.device, graph=a.graph)
     cfg = get_config(a.model)
     ck = resolve_checkpoint(a.checkpoint, cfg, a.checkpoint_dir)
     run_epochs(cfg, ck, device=a.device, data_dir=a.data_dir, synthetic=a.synthetic, epochs=a.epochs,

@@ -336,7 +336,7 @@ def main(family_config: str, argv=None, tfrecords_default="./dataset/tfrecords")
         from ..profiling import run_under_rocprof
 
         run_under_rocprof(argv)
-    maybe_spawn(a.nproc, a.device)
+    maybe_spawn(a.nproc, a.device, graph=a.graph)
     cfg = get_config(family_config)
     if a.input_size:
         cfg = cfg.replace(input_shape=(cfg.input_shape[0], a.input_size, a.input_size))

@@ -97,3 +97,23 @@ def test_hourglass_main_cli_cpu(tmp_path):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "Hourglass/tensorflow/main.py"), "--help"],
                        capture_output=True, text=True, env=env, timeout=120)
     assert "--nproc" in r.stdout and "--graph / --no-graph" in r.stdout
+
+
+def test_hw_queue_budget_eager_vs_captured():
+    """Eager ranks get 8 hardware queues (weight-gradient side stream beside RCCL's); captured steps
+    keep HIP's default 4 (no side stream in a graph; Hourglass's captured branches replay faster)."""
+    from deep_vision_amd.launch import hw_queues_env
+
+    for start in ({}, {"GPU_MAX_HW_QUEUES": "4"}):
+        env = dict(start)
+        hw_queues_env(env, graph=False)
+        assert env["GPU_MAX_HW_QUEUES"] == "8"
+        env = dict(start)
+        hw_queues_env(env, graph=True)
+        assert env.get("GPU_MAX_HW_QUEUES", "4") == "4"
+    env = {"GPU_MAX_HW_QUEUES": "16"}
+    hw_queues_env(env, graph=False)
+    assert env["GPU_MAX_HW_QUEUES"] == "16"
+    env = {"GPU_MAX_HW_QUEUES": "4", "DV_KEEP_HW_QUEUES": "1"}
+    hw_queues_env(env, graph=False)
+    assert env["GPU_MAX_HW_QUEUES"] == "4"
