@@ -107,8 +107,16 @@ def _sample_cls(i, cin, size, ncls):
     global batch is the same whatever the world size: rank r holds samples [r*B, (r+1)*B))."""
     import torch
 
+    # learnable, so the reported loss_first_last shows the step training: the label is one of
+    # min(100, ncls) classes and the image that class's smooth template (an 8x8 Gaussian field,
+    # upsampled) plus N(0, 0.5^2) noise -- same shapes and dtypes as random inputs
+    k = min(100, ncls)
+    c = i % k
+    gt = torch.Generator().manual_seed(104729 * c + 3)
+    t = torch.nn.functional.interpolate(torch.randn(1, cin, 8, 8, generator=gt), size=(size, size), mode="bilinear",
+                                        align_corners=False)[0]
     g = torch.Generator().manual_seed(7919 * i + 17)
-    return torch.randn(cin, size, size, generator=g), int(torch.randint(0, ncls, (1,), generator=g))
+    return t / t.std() + 0.5 * torch.randn(cin, size, size, generator=g), c * (ncls // k)
 
 
 def build_step_for_profile(model_name, batch=0):
@@ -378,7 +386,8 @@ def main():
             "per_gpu": round(imgs / max(1, world), 2),
             "comm_exposed_ms": round(comm_ms, 3),
             "dtype": "bf16" if cuda else "fp32",
-            "data": "synthetic (random inputs / labels of the config's shapes, random-init weights)",
+            "data": ("synthetic (classification: 100 class templates + noise, a learnable fixed batch; "
+                     "others: random inputs / labels of the config's shapes; random-init weights)"),
             "config": {
                 "model": args.model,
                 "global_batch": B * world,
