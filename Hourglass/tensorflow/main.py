@@ -37,7 +37,8 @@ from deep_vision_amd.train.detection import train  # noqa: E402
 @click.option("--synthetic", is_flag=True, help="Synthetic data (no TFRecords needed).")
 @click.option("--device", default=None)
 @click.option("--nproc", type=int, default=None, help="Processes, one per GPU (default: every visible GPU).")
-@click.option("--graph/--no-graph", default=True, help="HIP-graph replay of the training step (default on).")
+@click.option("--graph/--no-graph", default=None,
+              help="HIP-graph replay of the training step (default: on, Hourglass's measured-faster mode).")
 @click.option("--max_steps", type=int, default=None, help="Stop after this many training steps (smoke runs).")
 @click.option("--input_size", type=int, default=None, help="Square input size (default 256).")
 @click.option("--num_stack", type=int, default=None, help="Hourglass stacks (default 4).")
@@ -46,7 +47,7 @@ def main(epochs, start_epoch, learning_rate, tensorboard_dir, checkpoint, num_he
          num_stack):
     from deep_vision_amd.launch import maybe_spawn
 
-    maybe_spawn(nproc, device, graph=graph)  # parent: spawns one rank per GPU and exits; ranks: CPU pinning
+    graph = maybe_spawn(nproc, device, graph=graph, model="hourglass")  # parent: spawns one rank per GPU and exits; ranks: CPU pinning
     cfg = get_config("hourglass")
     cfg = cfg.replace(optimizer_params={"lr": learning_rate}, batch_size=batch_size, total_epochs=epochs,
                       model_params={**cfg.model_params, "num_heatmap": num_heatmap},

@@ -40,16 +40,21 @@ import json
 import sys
 import time
 
-# Eager steps: eight hardware queues per process (HIP's default is 4), set before HIP initialises:
-# the compute stream, the weight-gradient side stream (deep_vision_amd/ops/conv.py) and RCCL's
-# streams each get a queue of their own. With 4, the side stream shared the compute stream's queue
-# under RCCL and serialised (world-1 RCCL ResNet-50: 12,960 img/s without the side stream, 13,690
-# with it and 8 queues). Captured steps (--graph) keep HIP's default: they use no side stream, and
-# Hourglass's captured branch streams replayed 2.7 % slower with 8 (profiles/wgrad_side_stream_ab.txt).
-# A larger value already set is kept; DV_KEEP_HW_QUEUES=1 keeps any value (A/B runs).
-if ("--graph" not in __import__("sys").argv and __import__("os").environ.get("DV_KEEP_HW_QUEUES") != "1"
-        and int(__import__("os").environ.get("GPU_MAX_HW_QUEUES", "4")) < 8):
-    __import__("os").environ["GPU_MAX_HW_QUEUES"] = "8"
+# The process's step mode and hardware-queue count (deep_vision_amd/policy.py: eager steps get 8
+# queues, captured steps HIP's default 4; the mode defaults to the model's measured-faster one),
+# decided before torch / HIP initialise -- in this process and in every rank torchrun starts.
+def _pre_args(argv):
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=None)
+    return ap.parse_known_args(argv)[0]
+
+
+_PRE = _pre_args(sys.argv[1:])
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+from deep_vision_amd import policy as _policy  # noqa: E402  (imports no torch)
+
+GRAPH = _policy.configure(_PRE.model, _PRE.graph)
 
 # Reference-derived comparators, images/sec per node:
 #   ResNet-50-equivalent proxy ~376 (8 GPUs), YOLOv3 ~179 (8x V100), LeNet-5 PT ~906.
@@ -222,10 +227,20 @@ def main():
     ap.add_argument("--force-dp", action="store_true",
                     help="wrap in DataParallel and all-reduce over a process group even at world size 1 "
                          "(exercises the RCCL bucket path on one GPU)")
-    ap.add_argument("--graph", action="store_true",
+    ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=None,
                     help="capture the training step (data-parallel all-reduces included) as a HIP graph and "
-                         "replay it (deep_vision_amd/train/graph.py) -- for launch-bound models")
+                         "replay it (deep_vision_amd/train/graph.py); default: the model's measured-faster "
+                         "mode (deep_vision_amd/policy.py PREFERRED)")
+    ap.add_argument("--policy", action="store_true",
+                    help="print this process's resolved stream / queue policy as JSON and exit (no GPU use)")
     args = ap.parse_args()
+    # an explicit --graph stands; the per-model default applies to the native GPU path only
+    args.graph = GRAPH and (_PRE.graph is not None or (args.backend == "native" and args.device != "cpu"))
+    if args.policy:
+        rec = _policy.describe()
+        rec["rank"] = int(__import__("os").environ.get("RANK", "0"))
+        print(json.dumps(rec), flush=True)
+        return
 
     import os
 

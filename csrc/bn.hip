@@ -924,12 +924,16 @@ DV_DEVICE void fold64(const float* __restrict__ acc, int C, int c0, double& s, d
   q = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
 }
 
-// Ticket of the slab, taken by thread 0 right after fold64 (whose barrier follows every thread's
-// shard loads: the values are in registers, so the reads are complete -- no fence, nothing to
-// drain). The block that takes the last ticket re-zeroes the shards at its end; fin_last() there
-// broadcasts the answer to the block.
+// Ticket of the slab, taken by thread 0 after every thread of the block has drained its global
+// loads (the shard values of fold64 AND the shift k read before it: the last block rewrites *shiftp
+// and re-zeroes the shards at its end, so no block may still have one of those loads in flight when
+// its ticket is counted). The ticket itself is acq_rel at agent scope. fin_last() broadcasts the
+// answer to the block.
 DV_DEVICE void fin_ticket(int* ticket, int nblocks, int* last) {
-  if (threadIdx.x == 0) *last = atomicAdd(ticket, 1) == nblocks - 1;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    *last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nblocks - 1;
 }
 DV_DEVICE bool fin_last(const int* last) {
   __syncthreads();

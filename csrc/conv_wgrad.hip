@@ -534,14 +534,14 @@ int dv_conv_wgrad_splits(const ConvWgradArgs& a) {
   const bool narrow = g_wg_variant == 2 || g_wg_variant == 4 || g_wg_variant == 6 ||
                       (g_wg_variant == 0 && wg_narrow(M, N));
   // narrow 64x256 tiles (64-output-channel layers, few tiles): twice the blocks (s1 3x3x64 at
-  // 56x56: 195 vs 214 us, profiles/wgbench_asm_dma.txt; the 1x1 narrow layers are flat)
+  // 56x56: 195 vs 214 us, profiles/archive/wgbench_asm_dma.txt; the 1x1 narrow layers are flat)
   int tm = narrow ? 64 : 128, tn = narrow ? 256 : 128, target = narrow ? 768 : 384;
   if (g_wg_variant == 8) { tm = 256; tn = 256; target = 256; }  // one 8-wave block per CU
   if (g_wg_variant == 9) { tm = 256; tn = 128; target = 384; }
   const int tiles = cdiv(M, tm) * cdiv(N, tn) * a.G;
   const int ktiles = cdiv(K, BK);
   // ~1.5 blocks per CU: measured 5-15 % faster than 3 per CU on the ResNet-50 3x3 / strided
-  // layers (half the atomic epilogues), equal on the rest (profiles/wgbench_variants.txt)
+  // layers (half the atomic epilogues), equal on the rest (profiles/archive/wgbench_variants.txt)
   int splits = cdiv(target * g_wg_split_pct / 100, tiles);
   // im2col layers (3x3, strided 1x1, stems): a grid of whole waves of the 512 block slots (2 per
   // CU for both tile shapes) instead of ~1.5 blocks per CU, which left a tail of half-empty CUs:

@@ -435,7 +435,7 @@ __global__ __launch_bounds__(NT, OCC) void dw_wgrad_kernel(const u16* __restrict
 // ((P-1)*sh + KS rows x (Q-1)*SW + KS columns, zero outside the image) is staged once in LDS with
 // 16-B loads issued all at once; every tap is then an LDS read. The strip kernels above re-read
 // each input pixel ~4.5x through L1/L2 and, on 14x14 / 7x7 layers, ran at 1.2-2 TB/s
-// (profiles/dw_bench_r2.txt). Thread = 8 channels (cg = tid % 8) x output pixels pl, pl + 32, ...
+// (profiles/archive/dw_bench_r2.txt). Thread = 8 channels (cg = tid % 8) x output pixels pl, pl + 32, ...
 constexpr int PL_CH = 64;              // channels per block
 constexpr int PL_LANES = NT / 8;       // pixel lanes
 constexpr int PLANE_MAX_OUT = 196;     // 14 x 14
@@ -1045,7 +1045,7 @@ void fwd_variants(const void* x, const float* w, const float* bias, void* y, con
     }
   }
   // the whole-plane forward measured no faster on 14x14 and slower on 7x7 outputs than the strip
-  // kernel (profiles/dw_bench_r3.txt): benchmark variant 51 only
+  // kernel (profiles/archive/dw_bench_r3.txt): benchmark variant 51 only
   if (g_dw_variant == 51 && !dv_deterministic() && plane_fwd<KS, SW, FLIP>(x, w, bias, y, g, act, slope, stats, st)) return;
   fwd_launch<KS, SW, FLIP, 4, 1>(x, w, bias, y, g, act, slope, stats, 4096, st);
 }

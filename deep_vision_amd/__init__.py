@@ -6,7 +6,15 @@ BatchNorm, pooling, loss, optimizers) and one-process-per-GPU data parallelism o
 """
 __version__ = "0.1.0"
 
-from . import ops  # noqa: F401,E402
+
+def __getattr__(name):
+    # subpackages load on first use, so ``deep_vision_amd.policy`` can be imported (and the launch
+    # environment set) before torch / HIP are touched
+    if name in ("ops", "nn", "models", "train", "data", "parallel", "utils", "profiling", "inference"):
+        import importlib
+
+        return importlib.import_module(f".{name}", __name__)
+    raise AttributeError(name)
 
 
 def set_deterministic(on: bool = True) -> None:

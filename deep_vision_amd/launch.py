@@ -170,13 +170,10 @@ def pin_rank_cpus() -> None:
 
 
 def hw_queues_env(env, graph: bool) -> None:
-    """Eager steps: a hardware queue each for the compute, weight-gradient side and RCCL streams
-    (ops/conv.py; 4, HIP's default, serialised the side stream under RCCL). Captured steps keep
-    HIP's default: they use no side stream, and the Hourglass branch streams of a captured step
-    replayed 2.7 % slower with 8 (profiles/wgrad_side_stream_ab.txt). A larger value already set
-    is kept; DV_KEEP_HW_QUEUES=1 keeps any value."""
-    if not graph and env.get("DV_KEEP_HW_QUEUES") != "1" and int(env.get("GPU_MAX_HW_QUEUES", "4")) < 8:
-        env["GPU_MAX_HW_QUEUES"] = "8"
+    """A child environment's hardware-queue count for a step mode (deep_vision_amd/policy.py)."""
+    from . import policy
+
+    policy.queues_env(env, graph)
 
 
 def spawn(nproc: int, argv, module: str | None = None, graph: bool = False) -> int:
@@ -190,16 +187,21 @@ def spawn(nproc: int, argv, module: str | None = None, graph: bool = False) -> i
     return subprocess.call(cmd, env=env)
 
 
-def maybe_spawn(nproc, device=None, graph: bool = False) -> None:
-    """Called first thing by the entry points: with ``--nproc N > 1`` (or the default: every visible
-    GPU, resolve_nproc) outside a torchrun world, re-launch this script N times and exit. Inside a
-    world, pin this rank's CPUs (pin_rank_cpus)."""
+def maybe_spawn(nproc, device=None, graph: bool | None = None, model: str | None = None) -> bool:
+    """Called first thing by the entry points, before HIP initialises. Resolves the process's step
+    mode and queue policy (policy.configure: ``graph`` None -> ``model``'s measured-faster mode) and
+    returns the graph decision. With ``--nproc N > 1`` (or the default: every visible GPU,
+    resolve_nproc) outside a torchrun world, re-launches this script N times and exits. Inside a
+    world (this script started by torchrun, ours or an external one), pins this rank's CPUs."""
+    from . import policy
+
+    graph = policy.configure(model, graph)
     if "WORLD_SIZE" in os.environ:
         pin_rank_cpus()
-        return
+        return graph
     nproc = resolve_nproc(nproc, device)
     if nproc <= 1:
-        return
+        return graph
     argv = list(sys.argv)
     # drop the --nproc flag so the children do not spawn again
     out, skip = [], False

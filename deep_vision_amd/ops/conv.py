@@ -17,6 +17,7 @@ import os
 import torch
 import torch.nn.functional as TF
 
+from .. import policy as _policy
 from . import wcache
 from .common import (ACT_IDS, BF16, CL, F32, act_grad, alloc_cl, as_nhwc, empty_nhwc, fast_apply, grad_nhwc, grad_sink, is_nhwc,
                      ld_of, lib,
@@ -435,8 +436,9 @@ class GradJoin:
 # ones. Same-box, ResNet-50: origin stream 13,152 img/s, 3x3 only 13,342, every wgrad 13,837
 # (profiles/wgrad_side_stream_ab.txt); MobileNet V1 lost 1.8 % with its pointwise wgrads moved (they
 # overlap its HBM-bound depthwise / BN passes, nothing gains) and opts out (models/mobilenet.py).
-WGRAD_SIDE = {"0": False, "3x3": "3x3"}.get(os.environ.get("DV_WGRAD_SIDE", "1"), "all")
-SIDE_COMM = os.environ.get("DV_WGRAD_SIDE_COMM", "side")
+_POLICY = _policy.side_policy()  # the A/B switches (deep_vision_amd/policy.py reads them all)
+WGRAD_SIDE = _POLICY["wgrad_side"]
+SIDE_COMM = _POLICY["comm"]
 _SIDE = {"streams": {}, "active": None, "suspend": 0}  # active: (origin, side stream) of this backward
 
 
@@ -455,7 +457,7 @@ def no_wgrad_side():
         _SIDE["suspend"] -= 1
 
 
-_SIDE_OPTOUT = os.environ.get("DV_WGRAD_SIDE_OPTOUT", "1") != "0"
+_SIDE_OPTOUT = _POLICY["optout"]
 # Captured steps with >= 8 hardware queues keep weight gradients on the origin stream: a graph
 # whose side-stream branches land on hardware queues of their own replayed 24-35 % slower
 # (ResNet-50 --graph 13,120 -> 10,010 img/s, YOLOv3 1,142 -> 750; profiles/wgrad_side_stream_ab.txt).
@@ -463,8 +465,18 @@ _SIDE_OPTOUT = os.environ.get("DV_WGRAD_SIDE_OPTOUT", "1") != "0"
 # (YOLOv3 --graph +2 %, ResNet-50 +0.3 %). DV_WGRAD_SIDE_GRAPH=0 / 1 forces it.
 
 
+def _queue_policy():
+    """(under_dp, in_capture) from the process's hardware-queue count, resolved at the first conv
+    (after HIP initialised: the queue count is fixed by then), not at import."""
+    qp = _SIDE.get("qp")
+    if qp is None:
+        sp = _policy.side_policy()
+        qp = _SIDE["qp"] = (sp["under_dp"], sp["in_capture"])
+    return qp
+
+
 def _capturing():
-    return not _SIDE_GRAPH and torch.cuda.is_current_stream_capturing()
+    return not _queue_policy()[1] and torch.cuda.is_current_stream_capturing()
 
 
 def _side_stream(device):
@@ -474,24 +486,15 @@ def _side_stream(device):
     return s
 
 
-def _hw_queues():
-    try:
-        return int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
-    except ValueError:
-        return 4
-
-
 # Under a process group the side stream needs hardware queues of its own: with HIP's default 4 it
 # shared the compute stream's queue beside RCCL's streams and serialised behind it (world-1 RCCL
-# ResNet-50 13,000 -> 12,300 img/s); with GPU_MAX_HW_QUEUES >= 8 (bench.py sets 8) it overlaps
-# (12,960 -> 13,690). DV_WGRAD_SIDE_DP=0 / 1 forces it off / on under a process group.
-_SIDE_DP = {"0": False, "1": True}.get(os.environ.get("DV_WGRAD_SIDE_DP", ""), _hw_queues() >= 8)
-_SIDE_GRAPH = {"0": False, "1": True}.get(os.environ.get("DV_WGRAD_SIDE_GRAPH", ""), _hw_queues() < 8)
+# ResNet-50 13,000 -> 12,300 img/s); with GPU_MAX_HW_QUEUES >= 8 (policy.configure sets 8 for eager
+# steps) it overlaps (12,960 -> 13,690). DV_WGRAD_SIDE_DP=0 / 1 forces it off / on.
 
 
 def _dist_active():
-    """True when a process group is up and the side stream must stay off (see _SIDE_DP)."""
-    if _SIDE_DP:
+    """True when a process group is up and the side stream must stay off (see _queue_policy)."""
+    if _queue_policy()[0]:
         return False
     import torch.distributed as dist
 
@@ -585,9 +588,12 @@ class _ConvFn(torch.autograd.Function):
                 bias_via_bn=False, bias_colsum=None):
         ctx.colsum_box = bias_colsum
         R_, S_ = weight.shape[2], weight.shape[3]
-        # under a process group only with >= 8 hardware queues (_SIDE_DP)
+        # under a process group only with >= 8 hardware queues (_SIDE_DP). Never with a residual
+        # epilogue: its dy is handed on (dres / residual_join) to a consumer that may overwrite it in
+        # place on the origin stream (a BN backward folding the stashed gradient, dx = xg) while the
+        # side-stream weight gradient still reads it; record_stream only guards the free, not the write.
         ctx.wside = (bool(WGRAD_SIDE) and _SIDE["suspend"] == 0 and (WGRAD_SIDE == "all" or R_ * S_ > 1)
-                     and not _dist_active() and not _capturing())
+                     and residual is None and not _dist_active() and not _capturing())
         N, Cx, H, W = x.shape
         O, Ig, R, S = weight.shape
         G = groups
@@ -1224,7 +1230,7 @@ class _DWConvFn(torch.autograd.Function):
         # x is a BatchNorm output (MobileNet: pw -> BN -> ReLU -> dw): its backward reduction is
         # folded into this dgrad's epilogue (modes 1 / 2: no mask bits), cf. _ConvFn
         # (stride 1 only: the stride-2 dgrad writes 4x the pixels it reads, and reading the BN input
-        # there as well cost as much as the separate reduce pass it saved, profiles/dw_bench_r3b.txt)
+        # there as well cost as much as the separate reduce pass it saved, profiles/archive/dw_bench_r3b.txt)
         bnref = getattr(x, "_dv_bnref", None)
         ctx.bnref = (bnref if (bnref is not None and bnref.mode in (1, 2) and ld_of(x) == C and tuple(stride) == (1, 1))
                      else None)

@@ -307,8 +307,9 @@ def add_common_args(ap: argparse.ArgumentParser):
     ap.add_argument("--nproc", type=int, default=None,
                     help="spawn N ranks (one per GPU) via torch.distributed.run; default: every visible GPU "
                          "(the reference wraps the net in nn.DataParallel whenever > 1 GPU is visible)")
-    ap.add_argument("--graph", action="store_true",
-                    help="capture the training step as a HIP graph and replay it (single GPU; train/graph.py)")
+    ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=None,
+                    help="capture the training step as a HIP graph and replay it (train/graph.py); default: "
+                         "the model's measured-faster mode (deep_vision_amd/policy.py PREFERRED)")
     return ap
 
 
@@ -333,8 +334,11 @@ def main(argv=None, choices=None, default=None):
         from ..profiling import run_under_rocprof
 
         run_under_rocprof(argv)  # exits with the profiled child's status
-    maybe_spawn(a.nproc, a.device, graph=a.graph)
     cfg = get_config(a.model)
+    explicit = a.graph is not None
+    a.graph = maybe_spawn(a.nproc, a.device, graph=a.graph, model=cfg.name)
+    if a.graph and not explicit and (a.device == "cpu" or not torch.cuda.is_available()):
+        a.graph = False  # the per-model default applies to the GPU path only
     ck = resolve_checkpoint(a.checkpoint, cfg, a.checkpoint_dir)
     run_epochs(cfg, ck, device=a.device, data_dir=a.data_dir, synthetic=a.synthetic, epochs=a.epochs,
                max_steps=a.max_steps, val_steps=a.val_steps, synthetic_size=a.synthetic_size, num_workers=a.workers,

@@ -316,10 +316,11 @@ def add_args(ap):
     ap.add_argument("--tensorboard-dir", default=None)
     ap.add_argument("--nproc", type=int, default=None,
                     help="processes (one per GPU); default: every visible GPU, like MirroredStrategy")
-    ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=True,
+    ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=None,
                     help="HIP-graph replay of the whole training step, data-parallel all-reduces included "
-                         "(default on: the captured step replays the eager one bit for bit in deterministic "
-                         "mode, tests/test_branch_streams_gpu.py); --no-graph runs eagerly")
+                         "(default: the model's measured-faster mode, deep_vision_amd/policy.py -- on for YOLOv3 / "
+                         "CenterNet / Hourglass; the captured step replays the eager one bit for bit in "
+                         "deterministic mode, tests/test_branch_streams_gpu.py); --no-graph runs eagerly")
     return ap
 
 
@@ -336,7 +337,7 @@ def main(family_config: str, argv=None, tfrecords_default="./dataset/tfrecords")
         from ..profiling import run_under_rocprof
 
         run_under_rocprof(argv)
-    maybe_spawn(a.nproc, a.device, graph=a.graph)
+    a.graph = maybe_spawn(a.nproc, a.device, graph=a.graph, model=family_config)
     cfg = get_config(family_config)
     if a.input_size:
         cfg = cfg.replace(input_shape=(cfg.input_shape[0], a.input_size, a.input_size))

@@ -61,6 +61,41 @@ def test_branch_streams_match_single_stream():
         assert torch.equal(res[0][1], res[k][1]), (k, (res[0][1] - res[k][1]).abs().max().item())
 
 
+def test_side_stream_wgrad_with_optout_disabled_matches_origin_stream():
+    """with the Hourglass no_wgrad_side opt-out ignored (what DV_WGRAD_SIDE_OPTOUT=0
+    does), weight gradients run on the side stream. A residual-epilogue conv hands its dy on to a BN
+    backward that overwrites it in place on the origin stream, so such convs must keep their weight
+    gradient on the origin stream; deterministic mode, so the side-stream step must equal the
+    all-origin step bitwise."""
+    from deep_vision_amd import set_deterministic
+    from deep_vision_amd.models import hourglass as H
+    from deep_vision_amd.ops import conv as C
+
+    x = torch.randn(4, 3, 128, 128, device=DEV)
+    hm = torch.rand(4, 16, 32, 32, device=DEV)
+    base = _net()
+    res = []
+    saved = (C._SIDE_OPTOUT, C.WGRAD_SIDE, H.BRANCH_STREAMS)
+    set_deterministic(True)
+    try:
+        H.BRANCH_STREAMS = False
+        for side in (False, True, True):
+            C._SIDE_OPTOUT = not side
+            C.WGRAD_SIDE = saved[1] if side else 0
+            m = copy.deepcopy(base)
+            loss = _loss(m(x), hm)
+            loss.backward()
+            C.wgrad_side_join()
+            torch.cuda.synchronize()
+            res.append((loss.detach().float().clone(), _grads(m)))
+    finally:
+        C._SIDE_OPTOUT, C.WGRAD_SIDE, H.BRANCH_STREAMS = saved
+        set_deterministic(False)
+    for k in (1, 2):
+        assert torch.equal(res[0][0], res[k][0])
+        assert torch.equal(res[0][1], res[k][1]), (k, (res[0][1] - res[k][1]).abs().max().item())
+
+
 def _six_steps(base, xs, hms, captured, lr=1e-4):
     """6 SGD steps: eagerly on one stream, or as a captured step (2 eager warm-up steps on the capture
     stream consume the first two batches, then 4 replays) with the up1 branches forked."""

@@ -1,10 +1,19 @@
-"""100-step convergence of the native training step on a learnable synthetic task (SURVEY §7.3
-phase 2): ResNet-50 and MobileNet V1 from one initialisation, native kernels vs PyTorch under
-autocast bf16, SGD momentum 0.9 at lr 0.01 / 0.02 (16 classes, images = 0.5 * class template +
-0.3 * noise). Both arms must drive the cross-entropy from ln(1000) to ~0 within 100 steps, and
-the native curve must end in a band around the precision-matched reference (measured sweep:
-profiles/loss_curve_sweep.txt).
-The full three-arm curves are recorded by tools/loss_curve.py (profiles/loss_curve_*.json)."""
+"""Training-trajectory checks of the native step (SURVEY §7.3 phase 2), native HIP kernels vs
+PyTorch under autocast bf16 from one initialisation, SGD momentum 0.9 / wd 1e-4.
+
+The native arm runs in deterministic mode (``set_deterministic``): no float-atomic accumulation
+order, so its trajectory is bitwise reproducible run to run and box to box, and a bound that holds
+once holds always. Bounds are placed only where they are well-posed (profiles/agreement_r6.txt,
+tools/agreement.py, 3 seeds per regime):
+- per-step agreement with torch-bf16 over the first steps, before rounding differences are
+  amplified (max relative loss difference measured: 1.7 % over 20 steps at lr .01 / noise .3,
+  2.1 % over 10 steps at lr .02 / noise 1.0, 0.9 % over 20 steps for MobileNet) -- bounded at ~3x;
+- final convergence only in the well-conditioned regime (lr .01-.02 / noise .3), where the torch arm
+  itself clears the bound with a wide margin. The lr .02 / noise 1.0 and lr .1 streaming regimes are
+  chaotic in BOTH arms (per-step differences of 27-66 % by step 20 between two correct bf16
+  implementations), so there only agreement before the divergence and "it trains" are asserted.
+Reference oracle: a completed run that trains (R/ResNet/pytorch/logs/resnet34-yanjiali-010319.log).
+"""
 import math
 import os
 import sys
@@ -16,57 +25,57 @@ pytestmark = pytest.mark.gpu
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
 
 
+def _rel(a, b):
+    return [abs(x - y) / max(abs(y), 1e-3) for x, y in zip(a, b)]
+
+
 @pytest.mark.parametrize("name,bs,lr", [("resnet50", 64, 0.01), ("mobilenet1", 64, 0.02)])
 def test_learnable_task_converges(name, bs, lr):
+    """Well-conditioned regime: both arms drive the cross-entropy from ln(1000) to ~0 in 100 steps,
+    and the first 20 steps agree per step."""
     from loss_curve import run_curve
 
-    curves = run_curve(name, bs=bs, steps=100, lr=lr, task="learnable", noise=0.3)
+    curves = run_curve(name, bs=bs, steps=100, lr=lr, task="learnable", noise=0.3, deterministic=True)
     nat, ref = curves["native"], curves["torch-bf16"]
     assert all(math.isfinite(v) for v in nat)
     assert nat[0] > 5.0 and ref[0] > 5.0          # starts at ~ln(1000)
+    d = _rel(nat[:20], ref[:20])
+    assert max(d) < 0.05, [round(v, 4) for v in d]
     tail_n = sum(nat[-10:]) / 10
     tail_r = sum(ref[-10:]) / 10
     assert tail_r < 0.1, f"reference did not learn: {ref[::10]}"
     assert tail_n < 0.1, f"native did not learn: {nat[::10]}"
-    # the two bf16 trajectories differ only by rounding / accumulation order
-    assert abs(tail_n - tail_r) < 0.05, (tail_n, tail_r)
-
-
-def test_resnet50_high_noise_lr002():
-    """the lr .02 / noise 1.0 regime, where round 2's single-pass BN variance
-    left the native run at 0.09 against 1e-4 for torch-bf16. With shifted statistics both arms
-    reach ~0 (profiles/loss_curve_sweep.txt: medians over 3 seeds 1e-4 native, 0.09 torch-bf16).
-    The trajectories are chaotic, so the best of two seeds per arm is compared."""
-    from loss_curve import run_curve
-
-    fin = {"native": [], "torch-bf16": []}
-    for seed in (0, 1):
-        c = run_curve("resnet50", bs=64, steps=100, lr=0.02, task="learnable", noise=1.0, seed=seed)
-        for arm in fin:
-            assert all(math.isfinite(v) for v in c[arm])
-            fin[arm].append(sum(c[arm][-5:]) / 5)
-    n, r = min(fin["native"]), min(fin["torch-bf16"])
-    # both arms reach ~0 on their better seed; which seed gets there first is chaotic in BOTH arms
-    # (torch-bf16 itself ended at 0.196 and 1e-4 on the two seeds, native at 0.056 and 0.197 once the
-    # float-atomic order moved with concurrent side-stream work), so no tighter relative bound
-    assert n < 0.1 and r < 0.1, fin
 
 
 @pytest.mark.parametrize("seed", [0, 1])
-def test_resnet50_streaming_task_per_seed(seed):
-    """VERDICT r3 next #7, short form of profiles/convergence_resnet50.txt (1,000 steps, 2 seeds):
-    ResNet-50 with the reference SGD settings (lr .1, momentum .9, wd 1e-4) on the streaming
-    learnable task (a fresh batch every step), native vs torch-bf16 from one initialisation,
-    judged per seed (no best-of): after 200 steps both arms have left ln(1000) behind and the
-    native windowed training loss is within a factor 1.6 of the reference's (the 1,000-step runs
-    differ by up to 0.9 in loss while the task is being learned and by < 0.01 at the end)."""
+def test_resnet50_high_noise_early_agreement(seed):
+    """lr .02 / noise 1.0: the first 10 steps agree per step within 6 % (measured <= 2.1 %); after
+    that both arms pass through loss spikes whose timing is set by rounding. The native arm is
+    bitwise reproducible (two deterministic runs give the same 10 losses)."""
+    from loss_curve import run_curve
+
+    c = run_curve("resnet50", bs=64, steps=10, lr=0.02, task="learnable", noise=1.0, seed=seed, deterministic=True)
+    c2 = run_curve("resnet50", bs=64, steps=10, lr=0.02, task="learnable", noise=1.0, seed=seed, deterministic=True,
+                   arms=("native",))
+    assert all(math.isfinite(v) for v in c["native"])
+    assert c["native"] == c2["native"], (c["native"], c2["native"])
+    d = _rel(c["native"], c["torch-bf16"])
+    assert max(d) < 0.06, [round(v, 4) for v in d]
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_resnet50_streaming_task_trains(seed):
+    """The reference SGD settings (lr .1, momentum .9, wd 1e-4) on the streaming learnable task (a
+    fresh batch every step; profiles/convergence_resnet50.txt has the 1,000-step curves): the
+    initial losses agree, and over 200 steps the native run leaves ln(1000) ~ 6.9 well behind (the
+    trajectory itself is chaotic from step ~2 in both arms: 14-19 % apart at step 5)."""
     from convergence import run
 
-    r = run("resnet50", bs=128, steps=200, lr=0.1, seed=seed, every=100, n_eval=256, log=lambda s: None)
+    r = run("resnet50", bs=128, steps=200, lr=0.1, seed=seed, every=100, n_eval=256, log=lambda s: None,
+            deterministic=True)
     nat, ref = r["native"], r["torch-bf16"]
     assert all(math.isfinite(v) for v in nat["loss"])
+    assert abs(nat["loss"][0] - ref["loss"][0]) / ref["loss"][0] < 0.01, (nat["loss"][:3], ref["loss"][:3])
     ln, lr_ = nat["checkpoints"][-1]["train_loss"], ref["checkpoints"][-1]["train_loss"]
-    first = sum(nat["loss"][:5]) / 5
-    assert first > 6.0, first  # ~ln(1000) at initialisation
-    assert ln < 5.5 and lr_ < 5.5, (ln, lr_)
-    assert 1 / 1.6 <= ln / lr_ <= 1.6, (ln, lr_)
+    assert lr_ < 6.0, f"reference did not train: {lr_}"
+    assert ln < 5.5, (ln, lr_)

@@ -79,7 +79,9 @@ def _evaluate(arm, m, task, n_eval, bs):
 
 
 def run(model="resnet50", bs=256, steps=1000, lr=0.1, seed=0, every=100, n_eval=1024, arms=("native", "torch-bf16"),
-        log=print, **task_kw):
+        log=print, deterministic=False, **task_kw):
+    from deep_vision_amd import set_deterministic
+
     torch.manual_seed(seed)
     base = M.get_model(model).cuda()
     task = Task(seed=seed, **task_kw)
@@ -88,6 +90,7 @@ def run(model="resnet50", bs=256, steps=1000, lr=0.1, seed=0, every=100, n_eval=
         m = copy.deepcopy(base)
         opt = FusedSGD(m.parameters(), lr=lr, momentum=0.9, weight_decay=1e-4)
         set_backend("native" if arm == "native" else "torch")
+        set_deterministic(deterministic and arm == "native")
         losses, evals = [], []
         t0 = time.time()
         try:
@@ -108,6 +111,7 @@ def run(model="resnet50", bs=256, steps=1000, lr=0.1, seed=0, every=100, n_eval=
                         f"({time.time() - t0:.0f}s)")
         finally:
             set_backend("native")
+            set_deterministic(False)
         res[arm] = {"loss": [round(v, 4) for v in torch.stack(losses).float().tolist()], "checkpoints": evals}
     return res
 

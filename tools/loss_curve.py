@@ -38,7 +38,11 @@ def make_batch(bs, task="learnable", size=224, classes=16, seed=0, noise=1.0):
 
 
 def run_curve(name="resnet50", bs=128, steps=100, lr=0.05, task="learnable", arms=("native", "torch-bf16"), seed=0,
-              noise=1.0):
+              noise=1.0, deterministic=False):
+    """deterministic=True runs the native arm under set_deterministic (a reproducible trajectory on
+    any box: no float-atomic accumulation order); the torch arms are unaffected."""
+    from deep_vision_amd import set_deterministic
+
     torch.manual_seed(seed)
     base = M.get_model(name).cuda()
     x, y = make_batch(bs, task, noise=noise)
@@ -47,6 +51,7 @@ def run_curve(name="resnet50", bs=128, steps=100, lr=0.05, task="learnable", arm
         m = copy.deepcopy(base)
         opt = FusedSGD(m.parameters(), lr=lr, momentum=0.9, weight_decay=1e-4)
         set_backend("native" if arm == "native" else "torch")
+        set_deterministic(deterministic and arm == "native")
         ls = []
         try:
             for _ in range(steps):
@@ -64,6 +69,7 @@ def run_curve(name="resnet50", bs=128, steps=100, lr=0.05, task="learnable", arm
                 ls.append(round(loss.item(), 4))
         finally:
             set_backend("native")
+            set_deterministic(False)
         curves[arm] = ls
     return curves
 
