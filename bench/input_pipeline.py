@@ -71,6 +71,35 @@ def loader_rate(ds, workers, batch, batches):
     return k * batch / (time.perf_counter() - t0)
 
 
+def shm_loader_rate(ds, workers, batch, batches, device=None):
+    """The shared-memory batch ring (data/shm_loader.py), consumed like the trainer does: through
+    the DevicePrefetcher when a GPU is present (pinned ring -> async H2D), else on the host."""
+    from deep_vision_amd.data.loader import DevicePrefetcher
+    from deep_vision_amd.data.shm_loader import ShmBatchLoader
+
+    ld = ShmBatchLoader(ds, batch, num_workers=workers, shuffle=True, drop_last=True, rank=0, world=1)
+    try:
+        src = DevicePrefetcher(ld, device) if device else ld
+        it = iter(src)
+        next(it)  # worker start-up
+        t0 = time.perf_counter()
+        k = 0
+        for _ in range(batches):
+            try:
+                b = next(it)
+            except StopIteration:
+                it = iter(src)
+                b = next(it)
+            k += 1
+        if device:
+            import torch
+
+            torch.cuda.synchronize()
+        return k * batch / (time.perf_counter() - t0), ld.pinned
+    finally:
+        ld.close()
+
+
 def gpu_costs(batch, reps=20):
     import torch
 
@@ -130,6 +159,15 @@ def main():
             for w in [int(v) for v in a.workers.split(",") if v]:
                 if w <= (os.cpu_count() or 1):
                     rec[name]["loader_img_s"][w] = round(loader_rate(ds, w, a.batch, a.batches), 1)
+            if name == "device_normalize_u8":
+                import torch
+
+                dev = "cuda" if torch.cuda.is_available() else None
+                rec[name]["shm_loader_img_s"] = {}
+                for w in [int(v) for v in a.workers.split(",") if v]:
+                    r, pinned = shm_loader_rate(ds, w, a.batch, a.batches, dev)
+                    rec[name]["shm_loader_img_s"][w] = round(r, 1)
+                    rec[name]["shm_ring_pinned"] = pinned
             print(name, json.dumps(rec[name]), flush=True)
     rec["h2d_bytes_ratio_fp32_over_u8"] = round(rec["reference_fp32"]["bytes_per_img"] /
                                                 rec["device_normalize_u8"]["bytes_per_img"], 2)

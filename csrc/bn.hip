@@ -927,13 +927,13 @@ DV_DEVICE void fold64(const float* __restrict__ acc, int C, int c0, double& s, d
 // Ticket of the slab, taken by thread 0 after every thread of the block has drained its global
 // loads (the shard values of fold64 AND the shift k read before it: the last block rewrites *shiftp
 // and re-zeroes the shards at its end, so no block may still have one of those loads in flight when
-// its ticket is counted). The ticket itself is acq_rel at agent scope. fin_last() broadcasts the
-// answer to the block.
+// its ticket is counted). The ticket is a relaxed agent-scope atomic: an acq_rel one would emit an
+// L2 write-back (buffer_wbl2) and invalidate per block. fin_last() broadcasts the answer.
 DV_DEVICE void fin_ticket(int* ticket, int nblocks, int* last) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0)
-    *last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nblocks - 1;
+    *last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblocks - 1;
 }
 DV_DEVICE bool fin_last(const int* last) {
   __syncthreads();

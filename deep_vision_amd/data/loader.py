@@ -3,6 +3,8 @@
 * ``make_loader``: per-rank DataLoader; with a process group the dataset is sharded by a
   DistributedSampler (the reference's DataParallel split the *global* batch inside one process;
   here every rank loads its own ``global / world`` slice).
+* ``make_loader(..., shm=True)``: the shared-memory batch ring (data/shm_loader.py) instead of
+  the stock DataLoader -- workers write samples into pinned batch slots, nothing is pickled.
 * ``DevicePrefetcher``: host->device copies of the next batch on a side HIP stream (pinned
   memory, non_blocking) while the current step computes; the consumer stream waits on an event
   and the tensors are ``record_stream``-ed so the caching allocator never recycles them early.
@@ -14,9 +16,15 @@ from torch.utils.data import DataLoader
 from torch.utils.data.distributed import DistributedSampler
 
 
-def make_loader(dataset, batch_size, shuffle=True, num_workers=4, drop_last=False, seed=0, collate_fn=None):
+def make_loader(dataset, batch_size, shuffle=True, num_workers=4, drop_last=False, seed=0, collate_fn=None,
+                shm=False):
     import torch.distributed as dist
 
+    if shm and num_workers > 0 and collate_fn is None:
+        from .shm_loader import ShmBatchLoader
+
+        return ShmBatchLoader(dataset, batch_size, num_workers=num_workers, shuffle=shuffle, drop_last=drop_last,
+                              seed=seed)
     sampler = None
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         sampler = DistributedSampler(dataset, shuffle=shuffle, seed=seed, drop_last=drop_last)
@@ -27,6 +35,9 @@ def make_loader(dataset, batch_size, shuffle=True, num_workers=4, drop_last=Fals
 
 
 def set_epoch(loader, epoch):
+    if hasattr(loader, "set_epoch"):
+        loader.set_epoch(epoch)
+        return
     s = getattr(loader, "sampler", None)
     if isinstance(s, DistributedSampler):
         s.set_epoch(epoch)
@@ -82,8 +93,11 @@ class DevicePrefetcher:
             return None
         if not self.cuda:
             return b, None
+        owner, slot = getattr(b, "owner", None), getattr(b, "slot", -1)
         with torch.cuda.stream(self.stream):
             b = _to(b, self.device, True)
             ev = torch.cuda.Event()
             ev.record(self.stream)
+        if owner is not None:  # a shared-memory ring slot: recycled once this copy has completed
+            owner.copied(slot, ev)
         return b, ev

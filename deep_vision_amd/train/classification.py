@@ -90,9 +90,13 @@ def build_datasets(cfg: TrainConfig, data_dir=None, synthetic=False, synthetic_s
             labels = None  # the packaged ImageNet-2012 synset list (data.imagenet_meta)
         if os.path.isdir(tr):
             dn = bool(cfg.extras.get("device_normalize", True))  # uint8 crops, normalised on the GPU
-            ms = 256 if dn else None  # the native pipeline also decodes large JPEGs at a reduced DCT scale
+            # training crops: large JPEGs decoded at a reduced DCT scale (the pipeline rescales to 256
+            # next anyway; a pre-filtered input to the cv2-geometry resize, a documented deviation
+            # from the reference's full cv2.imread, README "Input pipeline"); validation keeps the
+            # full decode so eval accuracy is measured on the reference's pixels
+            ms = 256 if dn else None
             return (ImageNet2012Dataset(tr, labels, T.imagenet_train_transform(device_normalize=dn), decode_min_side=ms),
-                    ImageNet2012Dataset(va, labels, T.imagenet_val_transform(device_normalize=dn), decode_min_side=ms))
+                    ImageNet2012Dataset(va, labels, T.imagenet_val_transform(device_normalize=dn)))
     return (SyntheticClassification(synthetic_size, cfg.input_shape, nc, key, seed=1),
             SyntheticClassification(max(64, synthetic_size // 4), cfg.input_shape, nc, key, seed=2))
 
@@ -233,8 +237,11 @@ def run_epochs(config: TrainConfig, checkpoint_path=None, *, device=None, data_d
     bs = cfg.per_rank_batch(eng.world)
     train_ds, val_ds = build_datasets(cfg, data_dir, synthetic, synthetic_size)
     workers = cfg.num_workers if num_workers is None else num_workers
-    train_loader = make_loader(train_ds, bs, shuffle=True, num_workers=workers, seed=seed)
-    val_loader = make_loader(val_ds, bs, shuffle=False, num_workers=workers)
+    # decoded-image sets go through the shared-memory batch ring (data/shm_loader.py: scales with
+    # workers, no per-sample pickling); DV_SHM_LOADER=0 falls back to the stock DataLoader
+    shm = isinstance(train_ds, ImageNet2012Dataset) and os.environ.get("DV_SHM_LOADER", "1") != "0"
+    train_loader = make_loader(train_ds, bs, shuffle=True, num_workers=workers, seed=seed, shm=shm)
+    val_loader = make_loader(val_ds, bs, shuffle=False, num_workers=workers, shm=shm)
     model = eng.build_model(cfg.model, **cfg.model_params)
     eng.log(model_summary(model, cfg.input_shape))
     net = eng.wrap(model)

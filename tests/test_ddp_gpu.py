@@ -7,6 +7,7 @@
   parameter broadcast + every bucket issued exactly once + a never-used parameter.
 """
 import os
+import queue
 import socket
 
 import pytest
@@ -281,7 +282,15 @@ def test_bucket_allreduce_overlaps_backward():
     q = ctx.Queue()
     p = ctx.Process(target=_overlap_worker, args=(_port(), q))
     p.start()
-    rep, bwd_ms, nb = q.get(timeout=300)
+    rep = None
+    for _ in range(110):  # a worker that dies fails the test now, not at a 300 s queue timeout
+        try:
+            rep, bwd_ms, nb = q.get(timeout=1)
+            break
+        except queue.Empty:
+            if not p.is_alive():
+                break
+    assert rep is not None, f"worker exited with {p.exitcode} before reporting"
     p.join(timeout=60)
     assert p.exitcode == 0
     assert nb >= 8 and len(rep) == nb
