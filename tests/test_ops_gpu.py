@@ -541,6 +541,21 @@ def test_batched_weight_prep_matches_per_layer():
         lib().wprep(ptr(p.detach()), ptr(ref), G, O // G, Ig, R, S, pad, mode, 0, stream_handle())
         got = _prep_weight(p, G, pad, mode)  # cache hit
         assert torch.equal(got, ref), (p.shape, G, pad, mode)
+    # mode 2: the tap-packed stem layout (filter width padded to Sp, 4 channels)
+    from deep_vision_amd.ops.conv import _prep_stem_weight
+
+    stems = [(torch.nn.Parameter(torch.randn(64, 3, 7, 7, device=DEV)), 8),
+             (torch.nn.Parameter(torch.randn(96, 3, 11, 11, device=DEV)), 16)]
+    for p, Sp in stems:
+        _prep_stem_weight(p, Sp)
+        with torch.no_grad():
+            p.mul_(0.5)
+    wcache.after_step()
+    for p, Sp in stems:
+        O, I, R, S = p.shape
+        ref = torch.empty(O * R * Sp * 4, dtype=torch.bfloat16, device=DEV)
+        lib().wprep(ptr(p.detach()), ptr(ref), 1, O, I, R, S, 4, 2, Sp, stream_handle())
+        assert torch.equal(_prep_stem_weight(p, Sp), ref), (p.shape, Sp)
     wcache.clear()
 
 
