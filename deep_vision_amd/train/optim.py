@@ -193,7 +193,9 @@ class _FlatOptimizer(torch.optim.Optimizer):
         if on and getattr(self, "_dguard", None) is None:
             dev = next((f["param"].device for f in self._flat if f is not None), None)
             if dev is not None and dev.type == "cuda":
-                done = max((f["step"] for f in self._flat if f is not None), default=0)
+                done = getattr(self, "_loaded_applied", None)
+                if done is None:
+                    done = max((f["step"] for f in self._flat if f is not None), default=0)
                 self._dguard = torch.tensor([0.0, 0.0, 0.0, 0.0, float(done)], dtype=torch.float32, device=dev)
 
     def _guard_active(self):
@@ -313,15 +315,24 @@ class _FlatOptimizer(torch.optim.Optimizer):
                     state[idx] = st
                 idx += 1
         sd["state"] = state
+        # the device guard's applied-step count (steps whose update ran; Adam's bias corrections
+        # follow it) and skips: a captured run's "step" also counts skipped replays, an eager run's
+        # does not, so the applied count is saved explicitly
+        applied = skipped = None
+        if getattr(self, "_dguard", None) is not None:
+            v = self._dguard.tolist()
+            skipped, applied = int(v[1]), int(v[4])
         for g, f in zip(sd["param_groups"], self._flat):
             g["_dv_step"] = f["step"] if f else 0
+            if applied is not None:
+                g["_dv_applied"], g["_dv_skipped"] = applied, skipped
         return sd
 
     def load_state_dict(self, state_dict):
         groups = state_dict["param_groups"]
         for g, sg in zip(self.param_groups, groups):
             for k, v in sg.items():
-                if k not in ("params", "_dv_step"):
+                if k not in ("params", "_dv_step", "_dv_applied", "_dv_skipped"):
                     g[k] = v
         idx = 0
         for sg, group, f in zip(groups, self.param_groups, self._flat):
@@ -340,8 +351,12 @@ class _FlatOptimizer(torch.optim.Optimizer):
                         f["step"] = int(float(st["step"]))
                 idx += 1
             f["first"] = not any_state
-        if getattr(self, "_dguard", None) is not None:  # the device guard's applied-step count follows
-            self._dguard[4] = float(max((f["step"] for f in self._flat if f is not None), default=0))
+        # the device guard's applied-step count: saved by a guarded run, else every saved step applied
+        saved = [sg["_dv_applied"] for sg in groups if "_dv_applied" in sg]
+        self._loaded_applied = (int(saved[0]) if saved else
+                                max((f["step"] for f in self._flat if f is not None), default=0))
+        if getattr(self, "_dguard", None) is not None:
+            self._dguard[4] = float(self._loaded_applied)
 
 
 class FusedSGD(_FlatOptimizer):
