@@ -158,6 +158,21 @@ def conv_ksplit(M, O, K, G=1):
     return max(1, min(16, 192 // tiles, K // 128))
 
 
+DGRAD_SPLIT = os.environ.get("DV_DGRAD_SPLIT", "1") != "0"
+
+
+def dgrad_ksplit(M, O, K, G=1):
+    """Split-K factor of a stride-1 dgrad whose 128x128 tile grid fills less than half of the 256
+    CUs and whose K is long (>= 2048): up to 4 splits, >= 1024 of K each (profiles/conv_bench_
+    yolov3_vs_miopen.txt: the 13x13 3x3 dgrads)."""
+    if not DGRAD_SPLIT or G != 1 or O % 4 or K < 2048:
+        return 1
+    tiles = -(-M // 128) * -(-O // 128)
+    if tiles >= 128:
+        return 1
+    return max(1, min(4, 256 // tiles, K // 1024))
+
+
 def conv_fwd_raw(x, wk, y, bias, stats, N, H, W, Cg, ldx, G, Kout, P, Q, R, S, stride, padding, dilation,
                  act=0, slope=0.0, tgather=0, omap=None, ldy=None, res=None, bnref=None, resmask=None, reflect=False,
                  ksplit=1, zfill=0, wlayout=None):
@@ -246,9 +261,14 @@ def _dgrad(dy, weight, x_shape, Cg_x, G, stride, padding, dilation, device, accu
         zfill = int(scatter and Cg_x == Ig and G == 1 and Ig % 8 == 0 and H <= P * sh and W <= Q * sw)
         dX, res = alloc_cl((N, G * Cg_x, H, W), zero=((scatter and not zfill) or Cg_x != Ig), device=device), None
     if (sh, sw) == (1, 1):
-        fuse = bnref if (bnref is not None and G == 1 and Cg_x == Ig and (res is not None or accum is None)) else None
+        # an under-filled grid (small maps, long K: YOLOv3's 13x13 3x3 dgrads, 88 tiles of 128x128 on
+        # 256 CUs, K = 9216) splits K across blocks; the BatchNorm-backward sums then come from the
+        # BN's own (small) reduce pass instead of this epilogue
+        ks = dgrad_ksplit(N * H * W, Ig, R * S * Cg_dy, G) if resmask is None else 1
+        fuse = (bnref if (bnref is not None and G == 1 and Cg_x == Ig and (res is not None or accum is None)
+                          and ks == 1) else None)
         if conv_fwd_raw(dy, wd, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, H, W, R, S, (1, 1), (-ph, -pw),
-                        (-dh, -dw), ldy=G * Cg_x, res=res, bnref=fuse, resmask=resmask):
+                        (-dh, -dw), ldy=G * Cg_x, res=res, bnref=fuse, resmask=resmask, ksplit=ks):
             fuse.mark_fused(dX)
     elif scatter:
         # the BatchNorm-backward sums ride on the scatter too (the unwritten pixels' zero gradient

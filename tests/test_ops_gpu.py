@@ -833,3 +833,36 @@ def test_darknet_residual_post_activation_add():
     assert _cos(x.grad, xr.grad) > 0.999
     for (n, p), (_, q) in zip(blk.named_parameters(), ref.named_parameters()):
         assert _cos(p.grad, q.grad) > 0.998, n
+
+
+@pytest.mark.parametrize("C,O,H,bnfuse", [(512, 1024, 13, False), (1024, 512, 13, True), (256, 256, 9, False)])
+def test_dgrad_split_k_small_grid(C, O, H, bnfuse):
+    """Stride-1 3x3 dgrads on under-filled grids split K across blocks (ops.conv.dgrad_ksplit:
+    YOLOv3's 13x13 layers): against fp32 torch, with and without a BatchNorm in front (its
+    backward sums then come from its own reduce pass, not the dgrad epilogue)."""
+    from deep_vision_amd import nn, ops as F
+    from deep_vision_amd.ops import conv as Cv
+
+    torch.manual_seed(C + O)
+    N = 2
+    assert Cv.dgrad_ksplit(N * H * H, C, 9 * O) > 1
+    x = torch.randn(N, C, H, H, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    conv = nn.Conv2d(C, O, 3, padding=1, bias=False).to(DEV)
+    dy = torch.randn(N, O, H, H, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    xi = x.clone().requires_grad_(True)
+    if bnfuse:
+        bn = nn.BatchNorm2d(C).to(DEV)
+        h = F.batch_norm_act(xi, bn, "relu")
+        y = F.conv2d(h, conv.weight, None, 1, 1)
+        y.backward(dy)
+        xr = x.float().requires_grad_(True)
+        hr = torch.relu(torch.nn.functional.batch_norm(xr, None, None, bn.weight.float(), bn.bias.float(), True))
+        yr = torch.nn.functional.conv2d(hr.to(torch.bfloat16).float(), conv.weight.to(torch.bfloat16).float(), None, 1, 1)
+    else:
+        y = F.conv2d(xi, conv.weight, None, 1, 1)
+        y.backward(dy)
+        xr = x.float().requires_grad_(True)
+        yr = torch.nn.functional.conv2d(xr, conv.weight.to(torch.bfloat16).float(), None, 1, 1)
+    yr.backward(dy.float())
+    err = ((xi.grad.float() - xr.grad).norm() / xr.grad.norm()).item()
+    assert err < 2e-2, err
