@@ -75,6 +75,14 @@ class Engine:
         if graph and not self.graph:
             self.log("[dv] --graph needs a GPU: running eagerly")
         self._graphed = {}
+        # eager steps run on a high-priority stream (as bench.py's): the weight-gradient side stream
+        # then fills the CUs the main path leaves idle (profiles/main_stream_priority_ab.txt);
+        # DV_MAIN_PRIO=0 keeps the default stream
+        self.main_stream = None
+        if self.device.type == "cuda" and not self.graph and os.environ.get("DV_MAIN_PRIO", "1") == "1":
+            self.main_stream = torch.cuda.Stream(device=self.device, priority=-1)
+            self.main_stream.wait_stream(torch.cuda.current_stream(self.device))
+            torch.cuda.set_stream(self.main_stream)
 
     def log(self, *a, **kw):
         if self.is_main:
