@@ -628,7 +628,7 @@ bool plane_wgrad(const void* x, const void* dy, float* dw, const DwGeo& g, hipSt
 
 // Benchmark override of (strip length QT, minimum waves per SIMD) for the 3x3 strip kernels:
 // 0 = heuristic, 1 = (4, 4), 2 = (2, 4), 3 = (8, 2), 4 = (4, 2), 5 = (2, 2); 60 = LDS-tiled
-// stride-1 kernels everywhere, 61 = the strip / plane kernels everywhere, 62 = tiled with 4 rows
+// kernels everywhere (stride 1 and 2), 61 = the strip / plane kernels everywhere, 62 = tiled with 4 rows
 // per thread.
 int g_dw_variant = 0;
 
@@ -643,12 +643,29 @@ int g_dw_variant = 0;
 // unpacks and 4*KS*KS packed FMAs -- against the strip kernel's 4.5 global loads per output, each
 // with its own bounds / 64-bit address VALU (1,368 VALU per wave there, VALU-issue- and
 // latency-bound at 2-3 TB/s: profiles/pmc_dw_r5.txt).
+//
+// Stride 2 (STR = 2, forward and weight gradient): the halo is (RB*TH-1)*2 + KS rows x (TW-1)*2 + KS
+// columns, and each staged row keeps its even input columns first and its odd ones after them (NE
+// even positions): thread column c reads input columns 2c + s at positions c + s/2 (even s) and
+// NE + c + s/2 (odd s), so the 16 lanes of one ds_read_b128 cycle hit 256 consecutive bytes.
 struct DwTileGeo {
-  int TW, RB, LCOLS, pieces, ncolt, nrowt;
+  int TW, RB, LCOLS, pieces, ncolt, nrowt, NE;
   FastDiv fd_lcols;
 };
+// LDS column position -> input column offset in the halo (the even / odd split of stride 2)
+template <int STR>
+DV_DEVICE int halo_col(int lc, int NE) {
+  if constexpr (STR == 1) return lc;
+  else return lc < NE ? 2 * lc : 2 * (lc - NE) + 1;
+}
+// input column offset s of a thread's window -> LDS position offset (from the thread's base c)
+template <int STR>
+DV_DEVICE int halo_pos(int s, int NE) {
+  if constexpr (STR == 1) return s;
+  else return (s & 1) ? NE + (s >> 1) : (s >> 1);
+}
 
-template <int KS, bool FLIP, bool BNR, int NG, int TH>
+template <int KS, bool FLIP, bool BNR, int NG, int TH, int STR = 1>
 __global__ __launch_bounds__(NT) void dw_tile_kernel(const u16* __restrict__ x, const float* __restrict__ w,
                                                      const float* __restrict__ bias, u16* __restrict__ y, DwGeo g,
                                                      DwTileGeo tg, int act, float slope, float* __restrict__ stats,
@@ -659,7 +676,7 @@ __global__ __launch_bounds__(NT) void dw_tile_kernel(const u16* __restrict__ x, 
   const int ct = (int)blockIdx.x % tg.ncolt, rest = (int)blockIdx.x / tg.ncolt;
   const int rt = rest % tg.nrowt, n = rest / tg.nrowt;
   const int p0 = rt * tg.RB * TH, q0 = ct * tg.TW;
-  const int h0 = p0 - g.ph, w0 = q0 - g.pw;
+  const int h0 = p0 * STR - g.ph, w0 = q0 * STR - g.pw;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   // ---- stage the halo: chunk k = pieces [64k, 64k + 64), one LDS-DMA wave-instruction ----
   {
@@ -669,7 +686,7 @@ __global__ __launch_bounds__(NT) void dw_tile_kernel(const u16* __restrict__ x, 
       const int piece = k * 64 + lane;
       const int pix = piece / NG, gi = piece & (NG - 1);
       const int lr = (int)fdiv((uint32_t)pix, tg.fd_lcols), lc = pix - lr * tg.LCOLS;
-      const int h = h0 + lr, ww = w0 + lc;
+      const int h = h0 + lr, ww = w0 + halo_col<STR>(lc, tg.NE);
       const bool ok = piece < tg.pieces && (unsigned)h < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
       const u16* src = ok ? xb + ((int64_t)h * g.W + ww) * g.ldx + gi * 8 : reinterpret_cast<const u16*>(dv_zero_page);
       __builtin_amdgcn_global_load_lds(GLB_PTR(src), LDS_PTR(smem + k * 1024), 16, 0, 0);
@@ -710,18 +727,18 @@ __global__ __launch_bounds__(NT) void dw_tile_kernel(const u16* __restrict__ x, 
 #pragma unroll
     for (int k = 0; k < 4; ++k) acc[i][k] = bv[k];
   if (active) {
-    const char* rp = smem + ((band * TH * tg.LCOLS + c) * NG + gi) * 16;
+    const char* rp = smem + ((band * TH * STR * tg.LCOLS + c) * NG + gi) * 16;
     const int rowb = tg.LCOLS * NG * 16;
 #pragma unroll
-    for (int ir = 0; ir < TH + KS - 1; ++ir) {
+    for (int ir = 0; ir < (TH - 1) * STR + KS; ++ir) {
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         f32x2 v[4];
-        ld8p(reinterpret_cast<const u16*>(rp + s * NG * 16), v);
+        ld8p(reinterpret_cast<const u16*>(rp + halo_pos<STR>(s, tg.NE) * NG * 16), v);
 #pragma unroll
         for (int r = 0; r < KS; ++r) {
-          const int i = ir - r;  // compile-time
-          if (i >= 0 && i < TH) {
+          const int i = (ir - r) / STR;  // compile-time
+          if (ir >= r && (ir - r) % STR == 0 && i < TH) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) acc[i][k] = pfma(v[k], wr[r * KS + s][k], acc[i][k]);
           }
@@ -789,7 +806,7 @@ __global__ __launch_bounds__(NT) void dw_tile_kernel(const u16* __restrict__ x, 
 // the KS output rows that use them (a rolling 3-row dy window in registers), into KS*KS x 8
 // per-thread tap partials. One LDS reduction over the pixel lanes and one coalesced atomic row
 // (or, deterministic mode, one slab row) per block.
-template <int KS, int NG, int TH>
+template <int KS, int NG, int TH, int STR = 1>
 __global__ __launch_bounds__(NT) void dw_tile_wgrad_kernel(const u16* __restrict__ x, const u16* __restrict__ dy,
                                                            float* __restrict__ dw, DwGeo g, DwTileGeo tg, int tpb,
                                                            float* __restrict__ slabs) {
@@ -814,14 +831,14 @@ __global__ __launch_bounds__(NT) void dw_tile_wgrad_kernel(const u16* __restrict
     const int ct = t % tg.ncolt, rest = t / tg.ncolt;
     const int rt = rest % tg.nrowt, n = rest / tg.nrowt;
     const int p0 = rt * tg.RB * TH, q0 = ct * tg.TW;
-    const int h0 = p0 - g.ph, w0 = q0 - g.pw;
+    const int h0 = p0 * STR - g.ph, w0 = q0 * STR - g.pw;
     if (t != t0) __syncthreads();  // the previous tile's LDS reads are done
     const u16* xb = x + (int64_t)n * g.H * g.W * g.ldx + cb;
     for (int k = wid; k < xchunks; k += NT / 64) {
       const int piece = k * 64 + lane;
       const int pix = piece / NG, pg = piece & (NG - 1);
       const int lr = (int)fdiv((uint32_t)pix, tg.fd_lcols), lc = pix - lr * tg.LCOLS;
-      const int h = h0 + lr, ww = w0 + lc;
+      const int h = h0 + lr, ww = w0 + halo_col<STR>(lc, tg.NE);
       const bool ok = piece < tg.pieces && (unsigned)h < (unsigned)g.H && (unsigned)ww < (unsigned)g.W;
       const u16* src = ok ? xb + ((int64_t)h * g.W + ww) * g.ldx + pg * 8 : reinterpret_cast<const u16*>(dv_zero_page);
       __builtin_amdgcn_global_load_lds(GLB_PTR(src), LDS_PTR(smem + k * 1024), 16, 0, 0);
@@ -838,7 +855,33 @@ __global__ __launch_bounds__(NT) void dw_tile_wgrad_kernel(const u16* __restrict
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (active) {
+    if (STR != 1 && active) {
+      // stride 2: the TH dy rows of the band in registers (TH <= 4), each input row meets the
+      // (up to two) output rows whose taps reach it
+      const char* xp = smem + ((band * TH * STR * tg.LCOLS + c) * NG + gi) * 16;
+      const char* dp = dimg + ((band * TH * tg.TW + c) * NG + gi) * 16;
+      const int xrowb = tg.LCOLS * NG * 16, drowb = tg.TW * NG * 16;
+      f32x2 d[TH][4];
+#pragma unroll
+      for (int i = 0; i < TH; ++i) ld8p(reinterpret_cast<const u16*>(dp + i * drowb), d[i]);
+#pragma unroll
+      for (int ir = 0; ir < (TH - 1) * STR + KS; ++ir) {
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          f32x2 v[4];
+          ld8p(reinterpret_cast<const u16*>(xp + halo_pos<STR>(s, tg.NE) * NG * 16), v);
+#pragma unroll
+          for (int r = 0; r < KS; ++r) {
+            const int i = (ir - r) / STR;  // compile-time
+            if (ir >= r && (ir - r) % STR == 0 && i < TH) {
+#pragma unroll
+              for (int k = 0; k < 4; ++k) acc[r * KS + s][k] = pfma(v[k], d[i][k], acc[r * KS + s][k]);
+            }
+          }
+        }
+        xp += xrowb;
+      }
+    } else if (active) {
       const char* xp = smem + ((band * TH * tg.LCOLS + c) * NG + gi) * 16;
       const char* dp = dimg + ((band * TH * tg.TW + c) * NG + gi) * 16;
       const int xrowb = tg.LCOLS * NG * 16, drowb = tg.TW * NG * 16;
@@ -891,22 +934,23 @@ __global__ __launch_bounds__(NT) void dw_tile_wgrad_kernel(const u16* __restrict
   for (int e = threadIdx.x; e < CW * KS * KS; e += NT) atomicAdd(dw + coff + e, red[e]);
 }
 
-inline DwTileGeo make_tile_geo(const DwGeo& g, int NG, int TH, int KS) {
+inline DwTileGeo make_tile_geo(const DwGeo& g, int NG, int TH, int KS, int STR = 1) {
   const int PL = NT / NG;
   DwTileGeo tg{};
   tg.TW = std::min(g.Q, PL);
   tg.RB = PL / tg.TW;
-  tg.LCOLS = tg.TW + KS - 1;
-  tg.pieces = (tg.RB * TH + KS - 1) * tg.LCOLS * NG;
+  tg.LCOLS = (tg.TW - 1) * STR + KS;
+  tg.NE = (tg.LCOLS + 1) / 2;
+  tg.pieces = ((tg.RB * TH - 1) * STR + KS) * tg.LCOLS * NG;
   tg.ncolt = (g.Q + tg.TW - 1) / tg.TW;
   tg.nrowt = (g.P + tg.RB * TH - 1) / (tg.RB * TH);
   tg.fd_lcols = make_fastdiv((uint32_t)tg.LCOLS);
   return tg;
 }
 
-template <int KS, int NG, int TH>
+template <int KS, int NG, int TH, int STR = 1>
 void tile_wgrad_launch(const void* x, const void* dy, float* dw, const DwGeo& g, hipStream_t st) {
-  const DwTileGeo tg = make_tile_geo(g, NG, TH, KS);
+  const DwTileGeo tg = make_tile_geo(g, NG, TH, KS, STR);
   const int ntiles = g.N * tg.nrowt * tg.ncolt, nslab = g.C / (NG * 8);
   // ~768 blocks (3 per CU): every block ends in KS*KS LDS reductions + one atomic row, so a block
   // walks several tiles
@@ -918,25 +962,25 @@ void tile_wgrad_launch(const void* x, const void* dy, float* dw, const DwGeo& g,
   float* ws = nullptr;
   const int64_t n = (int64_t)g.C * KS * KS;
   if (dv_deterministic()) ws = dv_slab_workspace((size_t)grid.x * n, st);
-  dw_tile_wgrad_kernel<KS, NG, TH><<<grid, NT, lds, st>>>((const u16*)x, (const u16*)dy, dw, g, tg, tpb, ws);
+  dw_tile_wgrad_kernel<KS, NG, TH, STR><<<grid, NT, lds, st>>>((const u16*)x, (const u16*)dy, dw, g, tg, tpb, ws);
   if (ws) dv_slab_reduce(ws, dw, n, (int)grid.x, 1, st);
 }
 
-template <int KS, bool FLIP, int NG, int TH>
+template <int KS, bool FLIP, int NG, int TH, int STR = 1>
 void tile_launch(const void* x, const float* w, const float* bias, void* y, const DwGeo& g, int act, float slope,
                  float* stats, hipStream_t st, const DwBnr* bnr) {
-  const DwTileGeo tg = make_tile_geo(g, NG, TH, KS);
+  const DwTileGeo tg = make_tile_geo(g, NG, TH, KS, STR);
   const dim3 grid((unsigned)(g.N * tg.nrowt * tg.ncolt), (unsigned)(g.C / (NG * 8)));
   const size_t lds = std::max<size_t>((size_t)((tg.pieces + 63) / 64) * 1024, (size_t)2 * NT * 8 * 4);
   const DetStats det((bnr || stats) ? grid.x : 0, g.C, st);
   if (bnr) {
     DwBnr b = *bnr;
     b.det = det.slab;
-    dw_tile_kernel<KS, FLIP, true, NG, TH><<<grid, NT, lds, st>>>((const u16*)x, w, bias, (u16*)y, g, tg, act, slope,
+    dw_tile_kernel<KS, FLIP, true, NG, TH, STR><<<grid, NT, lds, st>>>((const u16*)x, w, bias, (u16*)y, g, tg, act, slope,
                                                                   stats, b, nullptr);
     det.fold(bnr->acc);
   } else {
-    dw_tile_kernel<KS, FLIP, false, NG, TH><<<grid, NT, lds, st>>>((const u16*)x, w, bias, (u16*)y, g, tg, act, slope,
+    dw_tile_kernel<KS, FLIP, false, NG, TH, STR><<<grid, NT, lds, st>>>((const u16*)x, w, bias, (u16*)y, g, tg, act, slope,
                                                                    stats, DwBnr{}, det.slab);
     det.fold(stats);
   }
@@ -951,6 +995,53 @@ inline int tile_th(int P, int Q, int NG) {
   }
   return best;
 }
+// stride 2: rows per thread (4 or 2) with the fewest idle rows whose tile fits `cap` bytes of LDS
+// (the halo is ~4x the output tile); 0 = none fits
+inline int tile_th2(const DwGeo& g, int NG, int KS, int cap, bool with_dy) {
+  const int PL = NT / NG, TW = std::min(g.Q, PL), RB = PL / TW, LCOLS = (TW - 1) * 2 + KS;
+  int best = 0, waste = 1 << 30;
+  for (int th : {4, 2}) {
+    const int rows = RB * th;
+    const int lds = (((rows - 1) * 2 + KS) * LCOLS * NG + (with_dy ? rows * TW * NG : 0)) * 16;
+    const int wst = (g.P + rows - 1) / rows * rows - g.P;
+    if (lds <= cap && wst < waste) { waste = wst; best = th; }
+  }
+  return best;
+}
+template <int KS>
+bool tile_fwd2(const void* x, const float* w, const float* bias, void* y, const DwGeo& g, int act, float slope,
+               float* stats, hipStream_t st) {
+  if constexpr (KS != 3) {
+    return false;
+  } else {
+    if (g.sh != 2 || g.sw != 2 || g.ldx % 8 || g.ldy % 8) return false;
+    const int NG = g.C % 64 == 0 ? 8 : (g.C % 32 == 0 ? 4 : 0);
+    if (!NG) return false;
+    const int th = tile_th2(g, NG, KS, 80 * 1024, false);
+    if (NG == 8 && th == 4) { tile_launch<KS, false, 8, 4, 2>(x, w, bias, y, g, act, slope, stats, st, nullptr); return true; }
+    if (NG == 8 && th == 2) { tile_launch<KS, false, 8, 2, 2>(x, w, bias, y, g, act, slope, stats, st, nullptr); return true; }
+    if (NG == 4 && th == 4) { tile_launch<KS, false, 4, 4, 2>(x, w, bias, y, g, act, slope, stats, st, nullptr); return true; }
+    if (NG == 4 && th == 2) { tile_launch<KS, false, 4, 2, 2>(x, w, bias, y, g, act, slope, stats, st, nullptr); return true; }
+    return false;
+  }
+}
+template <int KS>
+bool tile_wgrad2(const void* x, const void* dy, float* dw, const DwGeo& g, hipStream_t st) {
+  if constexpr (KS != 3) {
+    return false;
+  } else {
+    if (g.sh != 2 || g.sw != 2 || g.ldx % 8 || g.ldy % 8) return false;
+    const int NG = g.C % 64 == 0 ? 8 : (g.C % 32 == 0 ? 4 : 0);
+    if (!NG) return false;
+    const int th = tile_th2(g, NG, KS, 60 * 1024, true);
+    if (NG == 8 && th == 4) { tile_wgrad_launch<KS, 8, 4, 2>(x, dy, dw, g, st); return true; }
+    if (NG == 8 && th == 2) { tile_wgrad_launch<KS, 8, 2, 2>(x, dy, dw, g, st); return true; }
+    if (NG == 4 && th == 4) { tile_wgrad_launch<KS, 4, 4, 2>(x, dy, dw, g, st); return true; }
+    if (NG == 4 && th == 2) { tile_wgrad_launch<KS, 4, 2, 2>(x, dy, dw, g, st); return true; }
+    return false;
+  }
+}
+
 template <int KS, bool FLIP>
 bool tile_fwd(const void* x, const float* w, const float* bias, void* y, const DwGeo& g, int act, float slope,
               float* stats, hipStream_t st, const DwBnr* bnr) {
@@ -1033,6 +1124,12 @@ void fwd_variants(const void* x, const float* w, const float* bias, void* y, con
   // strip kernel keeps 7x7 (the 9x9 halo of a 7x7 tile costs more than it saves: profiles/dw_tile_r5.txt)
   const bool tiled = g_dw_variant == 60 || g_dw_variant == 62 || (g_dw_variant == 0 && g.P * g.Q >= 196);
   if (tiled && tile_fwd<KS, FLIP>(x, w, bias, y, g, act, slope, stats, st, bnr)) return;
+  // stride 2 on LDS tiles (the even / odd split halo), every map size; variant 63 = strip kernel
+  if constexpr (SW == 2 && !FLIP) {
+    // measured no faster than the strip kernel on any MobileNet stride-2 layer (the strip kernel
+    // already streams the big ones at ~4 TB/s; profiles/dw_tile_stride2.txt): variant 60 only
+    if (!bnr && g_dw_variant == 60 && tile_fwd2<KS>(x, w, bias, y, g, act, slope, stats, st)) return;
+  }
   if (bnr) return fwd_launch<KS, SW, FLIP, 4, 1>(x, w, bias, y, g, act, slope, stats, 4096, st, bnr);
   if constexpr (KS == 3) {
     switch (g_dw_variant) {
@@ -1071,6 +1168,11 @@ void wgrad_variants(const void* x, const void* dy, float* dw, const DwGeo& g, hi
     // there); larger maps keep the strip kernel, whose blocks overlap loads with FMAs across strips
     const bool tiled = g_dw_variant == 60 || g_dw_variant == 62 || (g_dw_variant == 0 && g.P * g.Q <= 196);
     if (tiled && tile_wgrad<KS>(x, dy, dw, g, st)) return;
+  } else {
+    // outputs up to 14x14: 12-20 % faster than the strip / plane kernels; the 56x56 and 28x28
+    // outputs keep the strip kernel (profiles/dw_tile_stride2.txt)
+    const bool tiled = g_dw_variant == 60 || (g_dw_variant == 0 && g.P * g.Q <= 196);
+    if (tiled && tile_wgrad2<KS>(x, dy, dw, g, st)) return;
   }
   if constexpr (KS == 3) {
     switch (g_dw_variant) {

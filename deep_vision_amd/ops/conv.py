@@ -318,6 +318,20 @@ def _subpixel_parts(H, W, P, Q, R, S, stride, padding):
     return parts
 
 
+# The parity parts write disjoint pixels and each fills a quarter of the grid: launched on streams of
+# their own they run side by side (YOLOv3's stride-2 3x3 dgrads; DV_SUBPIXEL_CONC=0: one stream).
+# Not in deterministic mode (the parts' BatchNorm-backward partial rows share one slab sequence).
+SUBPIXEL_CONC = os.environ.get("DV_SUBPIXEL_CONC", "1") != "0"
+_SUBPIX_STREAMS = {}
+
+
+def _subpix_streams(device, n):
+    lst = _SUBPIX_STREAMS.setdefault(device, [])
+    while len(lst) < n:
+        lst.append(torch.cuda.Stream(device=device))
+    return lst[:n]
+
+
 def _subpixel_dgrad(dy, wd, dX, res, bnref, N, H, W, P, Q, Cg_dy, ldy_in, G, Ig, Cg_x, R, S, stride, padding):
     sh, sw = stride
     parts = _subpixel_parts(H, W, P, Q, R, S, stride, padding)
@@ -327,14 +341,26 @@ def _subpixel_dgrad(dy, wd, dX, res, bnref, N, H, W, P, Q, Cg_dy, ldy_in, G, Ig,
     # the BatchNorm-backward sums ride on every part (disjoint pixels, together all of them), or
     # on none: a partial fusion would leave part of the sums in the accumulator
     fuse = bnref if (bnref is not None and G == 1 and Cg_x == Ig and len(live) == len(parts)) else None
+    conc = SUBPIXEL_CONC and dy.is_cuda and len(live) > 1 and not lib().deterministic()
+    if conc:
+        cur = torch.cuda.current_stream(dy.device)
+        sides = _subpix_streams(dy.device, len(live) - 1)
+        for st in sides:
+            st.wait_stream(cur)
     ok = []
-    for a, b, r0, s0, ra, sb, dh, dw, U, V in live:
+    for idx, (a, b, r0, s0, ra, sb, dh, dw, U, V) in enumerate(live):
         # the parity's taps (r0 + sh*i, s0 + sw*j) of the [G][Ig][R][S][Cg_dy] operand, read in place
         wsub = wd[(r0 * S + s0) * Cg_dy:]
         COUNTERS_DGRAD["subpixel"] += 1
-        ok.append(conv_fwd_raw(dy, wsub, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, U, V, ra, sb, (1, 1),
-                               (-dh, -dw), (-1, -1), omap=(H, W, sh, sw, a, b), ldy=G * Cg_x, res=res, bnref=fuse,
-                               wlayout=(R * S * Cg_dy, sh * S * Cg_dy, sw * Cg_dy)))
+        with (torch.cuda.stream(sides[idx - 1]) if conc and idx > 0 else contextlib.nullcontext()):
+            ok.append(conv_fwd_raw(dy, wsub, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, U, V, ra, sb, (1, 1),
+                                   (-dh, -dw), (-1, -1), omap=(H, W, sh, sw, a, b), ldy=G * Cg_x, res=res,
+                                   bnref=fuse, wlayout=(R * S * Cg_dy, sh * S * Cg_dy, sw * Cg_dy)))
+    if conc:
+        for st in sides:
+            cur.wait_stream(st)
+            for t in (dy, wd, dX):  # the caching allocator must not recycle them under a side stream
+                t.record_stream(st)
     if fuse is not None:
         if all(ok):
             fuse.mark_fused(dX)

@@ -219,14 +219,17 @@ def test_depthwise_dgrad_fuses_bn_backward(s, act):
     assert nrel(fused[5], ref[1].bias.grad) < 3e-2
 
 
-@pytest.mark.parametrize("C,H,W,act", [(32, 112, 112, "relu"), (96, 13, 20, None), (128, 9, 33, "leaky"),
-                                       (512, 14, 14, "relu"), (64, 5, 70, None)])
-def test_depthwise_tiled_matches_strip(C, H, W, act):
-    """The LDS-tiled stride-1 kernels (csrc/depthwise.hip dw_tile_kernel / dw_tile_wgrad_kernel) against
-    the strip kernels (benchmark variant 61) on ragged tiles: partial column / row tiles, several
-    row bands per block, a 32-channel-multiple slab (C = 96), with bias, activation and BN statistics.
-    The forward and data gradient sum the taps in the same order (bitwise equal); the weight gradient
-    and the statistics reduce in another order (fp32 rounding only)."""
+@pytest.mark.parametrize("C,H,W,act,s", [(32, 112, 112, "relu", 1), (96, 13, 20, None, 1), (128, 9, 33, "leaky", 1),
+                                         (512, 14, 14, "relu", 1), (64, 5, 70, None, 1),
+                                         (64, 112, 112, "relu", 2), (96, 13, 20, None, 2), (128, 9, 33, "leaky", 2),
+                                         (256, 28, 28, "relu", 2), (512, 14, 14, "relu", 2), (64, 5, 70, None, 2)])
+def test_depthwise_tiled_matches_strip(C, H, W, act, s):
+    """The LDS-tiled kernels (csrc/depthwise.hip dw_tile_kernel / dw_tile_wgrad_kernel; stride 2 with
+    the even / odd split halo) against the strip kernels (benchmark variant 61) on ragged tiles:
+    partial column / row tiles, several row bands per block, a 32-channel-multiple slab (C = 96),
+    odd maps, with bias, activation and BN statistics. The forward and data gradient sum the taps
+    in the same order (bitwise equal); the weight gradient and the statistics reduce in another
+    order (fp32 rounding only)."""
     from deep_vision_amd import ops as F
     from deep_vision_amd._ext import lib
 
@@ -234,7 +237,8 @@ def test_depthwise_tiled_matches_strip(C, H, W, act):
     x32 = torch.randn(3, C, H, W, device=DEV).bfloat16().float()
     w0 = torch.randn(C, 1, 3, 3, device=DEV) * 0.3
     b0 = torch.randn(C, device=DEV) * 0.5
-    dy = _nhwc(torch.randn(3, C, H, W, device=DEV))
+    P, Q = (H - 1) // s + 1, (W - 1) // s + 1
+    dy = _nhwc(torch.randn(3, C, P, Q, device=DEV))
 
     def run(variant):
         lib().dw_variant(variant)
@@ -242,14 +246,14 @@ def test_depthwise_tiled_matches_strip(C, H, W, act):
             x = _nhwc(x32).requires_grad_(True)
             w = w0.clone().requires_grad_(True)
             b = b0.clone().requires_grad_(True)
-            y, stats = F.conv2d(x, w, b, 1, 1, 1, C, act=act, slope=0.1, want_stats=True)
+            y, stats = F.conv2d(x, w, b, s, 1, 1, C, act=act, slope=0.1, want_stats=True)
             y.backward(dy)
             torch.cuda.synchronize()
             return y.detach(), stats[:128].reshape(64, 2, -1).sum(0)[:, :C], x.grad, w.grad, b.grad
         finally:
             lib().dw_variant(0)
 
-    tiled, strip = run(0), run(61)
+    tiled, strip = run(60), run(61)  # LDS tiles everywhere vs strip / plane kernels everywhere
     assert torch.equal(tiled[0], strip[0]), "forward differs"
     assert _rel(tiled[1], strip[1]) < 1e-5
     assert torch.equal(tiled[2], strip[2]), "data gradient differs"

@@ -91,6 +91,37 @@ def test_strided_dgrad_takes_subpixel_path():
     assert C.COUNTERS_DGRAD["subpixel"] - n0 == 4 and C.COUNTERS_DGRAD["tgather"] == t0
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_subpixel_parts_on_side_streams_match_one_stream(graph):
+    """The parity parts launched side by side (ops.conv.SUBPIXEL_CONC) write disjoint pixels: the
+    input gradient is bitwise the one-stream one, eager and inside a captured graph."""
+    from deep_vision_amd.ops import conv as C
+
+    dy = _nhwc(torch.randn(4, 128, 26, 26, device=DEV)).bfloat16()
+    w = torch.randn(128, 64, 3, 3, device=DEV) * 0.05
+
+    def run(conc):
+        old, C.SUBPIXEL_CONC = C.SUBPIXEL_CONC, conc
+        try:
+            if not graph:
+                return C._dgrad(dy, w, (4, 64, 52, 52), 64, 1, (2, 2), (1, 1), (1, 1), dy.device).clone()
+            C._dgrad(dy, w, (4, 64, 52, 52), 64, 1, (2, 2), (1, 1), (1, 1), dy.device)  # warm the weight cache
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(s), torch.cuda.graph(g, stream=s):
+                out = C._dgrad(dy, w, (4, 64, 52, 52), 64, 1, (2, 2), (1, 1), (1, 1), dy.device)
+            g.replay()
+            torch.cuda.synchronize()
+            return out.clone()
+        finally:
+            C.SUBPIXEL_CONC = old
+
+    a, b = run(False), run(True)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+
+
 def test_conv_bias_relu_epilogue():
     from deep_vision_amd import ops as F
 
