@@ -40,8 +40,14 @@ HOURGLASS = [
     ("hg16_3x3_128", 16, 128, 128, 3, 1), ("hg8_3x3_128", 8, 128, 128, 3, 1),
 ]
 
+# YOLOv3 (batch 16, 416) Darknet-53 3x3 convs at the under-filled 13x13 / 26x26 scales
+YOLOV3 = [
+    ("yl13_3x3_512_1024", 13, 512, 1024, 3, 1), ("yl26_3x3_256_512", 26, 256, 512, 3, 1),
+    ("yl52_3x3_128_256", 52, 128, 256, 3, 1), ("yl13_1x1_1024_512", 13, 1024, 512, 1, 1),
+]
 
-def run(name, H, Cin, Cout, k, s, N, variants, iters):
+
+def run(name, H, Cin, Cout, k, s, N, variants, iters, ksplits=(1,)):
     pad = k // 2
     P = (H + 2 * pad - k) // s + 1
     x = torch.randn(N, Cin, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
@@ -50,11 +56,12 @@ def run(name, H, Cin, Cout, k, s, N, variants, iters):
     flops = 2.0 * N * P * P * Cout * Cin * k * k
     nbytes = 2.0 * (N * H * H * Cin + N * P * P * Cout)
     res, ref = {}, None
-    for v in variants:
+    for v, ks in [(v, ks) for v in variants for ks in ksplits]:
         lib().conv_fwd_variant(v)
 
         def go():
-            conv_fwd_raw(x, w, y, None, None, N, H, H, Cin, Cin, 1, Cout, P, P, k, k, (s, s), (pad, pad), (1, 1))
+            conv_fwd_raw(x, w, y, None, None, N, H, H, Cin, Cin, 1, Cout, P, P, k, k, (s, s), (pad, pad), (1, 1),
+                         ksplit=ks)
 
         go()
         torch.cuda.synchronize()
@@ -70,8 +77,8 @@ def run(name, H, Cin, Cout, k, s, N, variants, iters):
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / iters
-        res[v] = (us, err)
-        print(f"{name:22s} v{v}  {us:8.1f} us  {flops / us / 1e6:7.1f} TF/s  {nbytes / us / 1e3:7.1f} GB/s  maxdiff {err:.3g}",
+        res[f"{v}/{ks}"] = (us, err)
+        print(f"{name:22s} v{v} ks{ks:2d} {us:8.1f} us  {flops / us / 1e6:7.1f} TF/s  {nbytes / us / 1e3:7.1f} GB/s  maxdiff {err:.3g}",
               flush=True)
     lib().conv_fwd_variant(0)
     return res
@@ -128,12 +135,13 @@ def main():
     ap.add_argument("--splits", default="100")
     ap.add_argument("--slab", default="1", help="wgrad split-K combine: 1 = ordered slabs, 0 = atomics, -1 = heuristic (e.g. 1,0)")
     ap.add_argument("--layers", default="", help="comma-separated layer names (default: all)")
-    ap.add_argument("--set", default="resnet50", choices=["resnet50", "hourglass"])
+    ap.add_argument("--set", default="resnet50", choices=["resnet50", "hourglass", "yolov3"])
+    ap.add_argument("--ksplit", default="1", help="forward split-K factors (e.g. 1,2,3)")
     a = ap.parse_args()
     keep = set(a.layers.split(",")) if a.layers else None
     vs = [int(v) for v in a.variants.split(",")]
     out = {}
-    for L in (HOURGLASS if a.set == "hourglass" else LAYERS):
+    for L in {"hourglass": HOURGLASS, "yolov3": YOLOV3}.get(a.set, LAYERS):
         if keep is not None and L[0] not in keep:
             continue
         if a.wgrad:
@@ -141,7 +149,7 @@ def main():
                 out[L[0]] = run_wgrad(*L, a.batch, vs, a.iters, [int(x) for x in a.splits.split(",")],
                                       [int(x) for x in a.slab.split(",")])
         else:
-            out[L[0]] = run(*L, a.batch, vs, a.iters)
+            out[L[0]] = run(*L, a.batch, vs, a.iters, [int(x) for x in a.ksplit.split(",")])
     if a.out:
         json.dump(out, open(a.out, "w"), indent=1)
 
