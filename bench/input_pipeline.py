@@ -71,9 +71,12 @@ def loader_rate(ds, workers, batch, batches):
     return k * batch / (time.perf_counter() - t0)
 
 
-def shm_loader_rate(ds, workers, batch, batches, device=None):
+def shm_loader_rate(ds, workers, batch, batches, device=None, consume=False):
     """The shared-memory batch ring (data/shm_loader.py), consumed like the trainer does: through
-    the DevicePrefetcher when a GPU is present (pinned ring -> async H2D), else on the host."""
+    the DevicePrefetcher when a GPU is present (pinned ring -> async H2D), else on the host.
+    ``consume``: also build the network input of every batch (device_input.batch_images: the GPU
+    jitter if the samples carry it, flip, normalise), as the trainer's step does."""
+    from deep_vision_amd.data.device_input import batch_images
     from deep_vision_amd.data.loader import DevicePrefetcher
     from deep_vision_amd.data.shm_loader import ShmBatchLoader
 
@@ -90,6 +93,8 @@ def shm_loader_rate(ds, workers, batch, batches, device=None):
             except StopIteration:
                 it = iter(src)
                 b = next(it)
+            if consume and device:
+                batch_images(b, device)
             k += 1
         if device:
             import torch
@@ -111,11 +116,16 @@ def gpu_costs(batch, reps=20):
     u8 = torch.randint(0, 256, (batch, 224, 224, 3), dtype=torch.uint8).pin_memory()
     f32 = torch.randn(batch, 3, 224, 224).pin_memory()
     flip = torch.randint(0, 2, (batch,), dtype=torch.bool).pin_memory()
+    jit = torch.cat([0.8 + 0.4 * torch.rand(batch, 3), torch.stack([torch.randperm(3) for _ in range(batch)]).float()],
+                    1).pin_memory()
     res = {}
     for name, fn in (("h2d_fp32_chw", lambda: f32.to(dev, non_blocking=True)),
                      ("h2d_u8_hwc", lambda: u8.to(dev, non_blocking=True)),
                      ("h2d_u8_plus_normalize", lambda: normalize_u8(u8.to(dev, non_blocking=True),
-                                                                    flip.to(dev, non_blocking=True)))):
+                                                                    flip.to(dev, non_blocking=True))),
+                     ("h2d_u8_plus_jitter_normalize", lambda: normalize_u8(u8.to(dev, non_blocking=True),
+                                                                           flip.to(dev, non_blocking=True),
+                                                                           jitter=jit.to(dev, non_blocking=True)))):
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
@@ -152,14 +162,18 @@ def main():
                                                            decode_min_side=256),
                 "device_normalize_u8_zero_copy_decode": ImageNet2012Dataset(
                     imgdir, syn, T.imagenet_train_transform(device_normalize=True), decode_min_side=256,
-                    zero_copy=True)}
+                    zero_copy=True),
+                # ColorJitter draws in the worker, the pixels jittered on the GPU (transforms.JitterDraw)
+                "device_normalize_u8_device_jitter": ImageNet2012Dataset(
+                    imgdir, syn, T.imagenet_train_transform(device_normalize=True, device_jitter=True),
+                    decode_min_side=256)}
         for name, ds in arms.items():
             r, b = per_worker_rate(ds, a.per_worker)
             rec[name] = {"per_worker_img_s": round(r, 1), "bytes_per_img": int(b), "loader_img_s": {}}
             for w in [int(v) for v in a.workers.split(",") if v]:
                 if w <= (os.cpu_count() or 1):
                     rec[name]["loader_img_s"][w] = round(loader_rate(ds, w, a.batch, a.batches), 1)
-            if name == "device_normalize_u8":
+            if name in ("device_normalize_u8", "device_normalize_u8_device_jitter"):
                 import torch
 
                 dev = "cuda" if torch.cuda.is_available() else None

@@ -238,6 +238,9 @@ PYBIND11_MODULE(_C, m) {
     return r;
   });
   m.def("stem_tuning", [](int blocks, int wg_blocks) { dv_stem_tuning(blocks, wg_blocks); });
+  m.def("u8_jitter", [](uptr x, uptr prm, int N, int64_t npix, uptr st) {
+    dv_u8_jitter(P(x), CFP(prm), N, npix, ST(st)); check_last("u8_jitter");
+  });
   m.def("u8_normalize", [](uptr x, uptr flip, uptr y, int N, int C, int H, int W, float scale, std::vector<float> mean,
                            std::vector<float> sd, uptr st) {
     if (C < 1 || C > 3 || (int)mean.size() < C || (int)sd.size() < C) throw std::runtime_error("u8_normalize: 1-3 channels");

@@ -354,6 +354,62 @@ __global__ void u8_normalize_kernel(const uint8_t* __restrict__ x, const uint8_t
   }
 }
 
+// ColorJitter on the device (the trainer's uint8 crops, before u8_normalize): the arithmetic of
+// csrc/host/io_core.h color_jitter, i.e. PIL's enhancers -- brightness / contrast / saturation in
+// the drawn order, each Image.blend(degenerate, image, f) truncated to uint8, luma
+// (19595 R + 38470 G + 7471 B + 0x8000) >> 16, the contrast gray = round(mean luma) -- so the
+// bytes equal the worker-side jitter's. One block per image; an image that fits the LDS (a
+// 224x224 crop is 147 KB of the 160 KB) is read once and written once, a larger one is worked in
+// place in global memory. prm[n] = {f_bright, f_contrast, f_sat, op0, op1, op2}; a factor of
+// exactly 1 is skipped, as on the host. No FMA contraction: the blends round like the host's
+// separate multiply and add (SSE, no FMA).
+DV_DEVICE uint8_t jit_clip(float v) { return (uint8_t)(int)fminf(255.f, fmaxf(0.f, v)); }
+DV_DEVICE int jit_luma(const uint8_t* q) { return (q[0] * 19595 + q[1] * 38470 + q[2] * 7471 + 0x8000) >> 16; }
+template <bool IN_LDS>
+__global__ __launch_bounds__(256) void u8_jitter_kernel(uint8_t* __restrict__ x, const float* __restrict__ prm,
+                                                        int64_t npix) {
+#pragma clang fp contract(off)
+  extern __shared__ __attribute__((aligned(16))) uint8_t jbuf[];
+  __shared__ long long red[4];
+  const int64_t nb = npix * 3;
+  uint8_t* gimg = x + (int64_t)blockIdx.x * nb;
+  uint8_t* img = IN_LDS ? jbuf : gimg;
+  const float* p = prm + (int64_t)blockIdx.x * 6;
+  if constexpr (IN_LDS) {
+    for (int64_t i = threadIdx.x; i < nb; i += 256) jbuf[i] = gimg[i];
+    __syncthreads();
+  }
+  for (int k = 0; k < 3; ++k) {
+    const int op = (int)p[3 + k];
+    const float a = p[op];
+    if (a == 1.f) continue;  // uniform over the block
+    if (op == 0) {
+      for (int64_t i = threadIdx.x; i < nb; i += 256) img[i] = jit_clip((float)img[i] * a);
+    } else if (op == 1) {
+      long long s = 0;
+      for (int64_t i = threadIdx.x; i < npix; i += 256) s += jit_luma(img + 3 * i);
+      for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o);
+      if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+      __syncthreads();
+      const long long tot = red[0] + red[1] + red[2] + red[3];
+      const float m = (float)(long long)((double)tot / (double)npix + 0.5);
+      for (int64_t i = threadIdx.x; i < nb; i += 256) img[i] = jit_clip(m + a * ((float)img[i] - m));
+    } else {
+      for (int64_t i = threadIdx.x; i < npix; i += 256) {
+        uint8_t* q = img + 3 * i;
+        const float g = (float)jit_luma(q);
+        const uint8_t r = jit_clip(g + a * ((float)q[0] - g)), gg = jit_clip(g + a * ((float)q[1] - g)),
+                      b = jit_clip(g + a * ((float)q[2] - g));
+        q[0] = r; q[1] = gg; q[2] = b;
+      }
+    }
+    __syncthreads();
+  }
+  if constexpr (IN_LDS) {
+    for (int64_t i = threadIdx.x; i < nb; i += 256) gimg[i] = jbuf[i];
+  }
+}
+
 // NHWC channel-slice copy / gather: dst[row][c] = src[row][idx ? idx[c] : c] for c < C.
 // Contiguous copies (concat into a channel slice) move 16-B vectors; gathers (channel shuffle
 // and its inverse) read 2-B elements through the index table.
@@ -488,6 +544,17 @@ void dv_u8_normalize(const void* x, const void* flip, void* y, int N, int C, int
                                                      C > 1 ? 1.f / std_[1] : 1.f, C > 2 ? 1.f / std_[2] : 1.f);
 }
 
+void dv_u8_jitter(void* x, const float* prm, int N, int64_t npix, hipStream_t st) {
+  const int64_t nb = npix * 3;
+  static const bool lds_ok = [] {
+    return hipFuncSetAttribute((const void*)u8_jitter_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               150 * 1024) == hipSuccess;
+  }();
+  if (lds_ok && nb <= 150 * 1024)
+    u8_jitter_kernel<true><<<N, 256, (size_t)((nb + 15) / 16 * 16), st>>>((uint8_t*)x, prm, npix);
+  else
+    u8_jitter_kernel<false><<<N, 256, 0, st>>>((uint8_t*)x, prm, npix);
+}
 void dv_to_nhwc(const void* x, int x_is_f32, void* y, int N, int C, int H, int W, int Cp, hipStream_t st) {
   const int64_t total = (int64_t)N * H * W * (Cp / 8);
   if (x_is_f32) to_nhwc_kernel<float><<<grid_for(total), NT, 0, st>>>((const float*)x, (u16*)y, N, C, H, W, Cp);

@@ -221,6 +221,7 @@ void dv_wgrad_unprep(float* src, float* dst, int G, int Og, int Ig, int R, int S
                      int accumulate, int zero_src, hipStream_t st);
 void dv_to_nhwc(const void* x, int x_is_f32, void* y, int N, int C, int H, int W, int Cp, hipStream_t st);
 // uint8 HWC input crops -> normalised bf16 NCHW (C <= 3, host mean / std), optional per-sample flip
+void dv_u8_jitter(void* x, const float* prm, int N, int64_t npix, hipStream_t st);
 void dv_u8_normalize(const void* x, const void* flip, void* y, int N, int C, int H, int W, float scale, const float* mean,
                      const float* std_, hipStream_t st);
 void dv_f32_to_bf16(const float* x, void* y, int64_t n, hipStream_t st);

@@ -23,11 +23,37 @@ from .transforms import IMAGENET_MEAN, IMAGENET_STD
 REFERENCE_NORM = (1.0, IMAGENET_MEAN, IMAGENET_STD)  # ToTensor without /255 (reference quirk)
 
 
-def normalize_u8(img, flip=None, norm=REFERENCE_NORM, out_dtype=None):
+def jitter_u8(img, jitter):
+    """ColorJitter of ``transforms.JitterDraw`` applied IN PLACE to a uint8 [N, H, W, 3] batch:
+    ``jitter`` float32 [N, 6] (factors, order). GPU: one native launch (csrc/elementwise.hip
+    u8_jitter); CPU: the worker-side native jitter (deep_vision_amd._io), per image. Both give the
+    bytes ``FastColorJitter`` gives."""
+    N, H, W, C = img.shape
+    if C != 3 or not img.is_contiguous():
+        raise ValueError("jitter_u8: a contiguous [N, H, W, 3] uint8 batch")
+    if native(img):
+        prm = jitter.to(device=img.device, dtype=torch.float32).contiguous()
+        lib().u8_jitter(ptr(img), ptr(prm), N, H * W, stream_handle())
+        return img
+    from .. import _io
+
+    host = img if img.device.type == "cpu" else img.cpu()
+    j = jitter.cpu()
+    for n in range(N):
+        _io.color_jitter(host[n].numpy(), [float(v) for v in j[n, :3]], [int(v) for v in j[n, 3:]])
+    if host is not img:
+        img.copy_(host)
+    return img
+
+
+def normalize_u8(img, flip=None, norm=REFERENCE_NORM, out_dtype=None, jitter=None):
     """``img`` uint8 [N, H, W, C] (on any device), ``flip`` bool/uint8 [N] or None ->
-    normalised NCHW: bf16 from the native kernel on the GPU, fp32 (or ``out_dtype``) on the CPU."""
+    normalised NCHW: bf16 from the native kernel on the GPU, fp32 (or ``out_dtype``) on the CPU.
+    ``jitter`` ([N, 6], ``transforms.JitterDraw``): ColorJitter first, in place on ``img``."""
     scale, mean, std = norm
     N, H, W, C = img.shape
+    if jitter is not None:
+        img = jitter_u8(img.contiguous(), jitter)
     if native(img):
         x = img.contiguous()
         f = flip.to(device=img.device, dtype=torch.uint8).contiguous() if flip is not None else None
@@ -51,8 +77,8 @@ def batch_images(data, device, non_blocking=True):
     img = data["image"]
     if img.dtype == torch.uint8 and img.dim() == 4:
         img = img.to(device, non_blocking=non_blocking)
-        flip = data.get("flip")
+        flip, jit = data.get("flip"), data.get("jitter")
         if flip is not None:
             flip = flip.to(device, non_blocking=non_blocking)
-        return normalize_u8(img, flip)
+        return normalize_u8(img, flip, jitter=jit)
     return img.to(device, non_blocking=non_blocking)

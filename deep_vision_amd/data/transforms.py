@@ -210,6 +210,27 @@ class FastColorJitter(ColorJitter):
         return {**sample, "image": image}
 
 
+class JitterDraw(ColorJitter):
+    """The draws of ``FastColorJitter`` (same factors, same order shuffle, same RNG calls in the
+    same place of the pipeline) without touching the pixels: the factors and order go with the
+    sample as ``jitter`` = float32 [f_brightness, f_contrast, f_saturation, op0, op1, op2], and the
+    GPU applies them to the uint8 batch (data.device_input.jitter_u8, csrc/elementwise.hip
+    u8_jitter: the same bytes as the worker-side jitter). Moves ~12 % of a loader worker's
+    per-image CPU time to the device."""
+
+    def __call__(self, sample):
+        if self.hue > 0:
+            raise ValueError("JitterDraw: hue jitter is host-only (FastColorJitter)")
+        f, order = [1.0, 1.0, 1.0], []
+        for k, amt in enumerate((self.brightness, self.contrast, self.saturation)):
+            if amt > 0:
+                f[k] = random.uniform(max(0, 1 - amt), 1 + amt)
+                order.append(k)
+        random.shuffle(order)
+        order += [k for k in range(3) if k not in order]
+        return {**sample, "jitter": torch.tensor(f + [float(k) for k in order], dtype=torch.float32)}
+
+
 class ToUint8:
     """Final step of the device-normalised pipeline (data/device_input.py): the HWC uint8 crop
     as a tensor (grayscale expanded to 3 channels) plus the horizontal-flip draw, which the device
@@ -229,11 +250,13 @@ class ToUint8:
         return {**sample, "image": torch.from_numpy(image), "flip": flip}
 
 
-def imagenet_train_transform(device_normalize=False):
+def imagenet_train_transform(device_normalize=False, device_jitter=False):
     """R/ResNet/pytorch/train.py:315-324. ``device_normalize``: stop at the uint8 crop + flip
-    draw; flip, ToTensor and Normalize run on the GPU (data.device_input)."""
+    draw; flip, ToTensor and Normalize run on the GPU (data.device_input). ``device_jitter``
+    (with it): the ColorJitter draws stay in the worker, the pixels are jittered on the GPU."""
     if device_normalize:  # native resize-crop + jitter (deep_vision_amd._io)
-        return Compose([RescaleCrop(256, 224), FastColorJitter(brightness=0.2, contrast=0.2, saturation=0.2, hue=0),
+        jit = JitterDraw if device_jitter else FastColorJitter
+        return Compose([RescaleCrop(256, 224), jit(brightness=0.2, contrast=0.2, saturation=0.2, hue=0),
                         ToUint8(flip_p=0.5)])
     return Compose([Rescale(256), RandomHorizontalFlip(0.5), RandomCrop(224),
                     ColorJitter(brightness=0.2, contrast=0.2, saturation=0.2, hue=0), ToTensor(),

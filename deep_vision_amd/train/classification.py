@@ -95,7 +95,10 @@ def build_datasets(cfg: TrainConfig, data_dir=None, synthetic=False, synthetic_s
             # from the reference's full cv2.imread, README "Input pipeline"); validation keeps the
             # full decode so eval accuracy is measured on the reference's pixels
             ms = 256 if dn else None
-            return (ImageNet2012Dataset(tr, labels, T.imagenet_train_transform(device_normalize=dn), decode_min_side=ms),
+            # ColorJitter draws in the worker, pixels jittered on the GPU (same bytes; README "Input pipeline")
+            dj = dn and bool(cfg.extras.get("device_jitter", True))
+            return (ImageNet2012Dataset(tr, labels, T.imagenet_train_transform(device_normalize=dn, device_jitter=dj),
+                                        decode_min_side=ms),
                     ImageNet2012Dataset(va, labels, T.imagenet_val_transform(device_normalize=dn)))
     return (SyntheticClassification(synthetic_size, cfg.input_shape, nc, key, seed=1),
             SyntheticClassification(max(64, synthetic_size // 4), cfg.input_shape, nc, key, seed=2))

@@ -264,3 +264,41 @@ def test_uint8_pipeline_matches_float_pipeline():
     pyrandom.seed(0)
     tr = T.imagenet_train_transform(device_normalize=True)({"image": img, "annotation": 1})
     assert tr["image"].dtype == torch.uint8 and isinstance(tr["flip"], bool)
+
+
+def test_device_jitter_draws_and_bytes_match_worker_jitter():
+    """transforms.JitterDraw + data.device_input.jitter_u8 (the pixels jittered after the batch
+    leaves the worker) give the same RNG draws, the same flip draw and the same bytes as the
+    worker-side FastColorJitter, for every order of the three enhancers."""
+    import random as pyrandom
+
+    import numpy as np
+
+    from deep_vision_amd.data import transforms as T
+    from deep_vision_amd.data.device_input import jitter_u8, normalize_u8
+
+    rng = np.random.RandomState(1)
+    imgs = [rng.randint(0, 256, (300 + 7 * k, 420 - 5 * k, 3), dtype=np.uint8) for k in range(6)]
+    host, dev = [], []
+    for k, img in enumerate(imgs):
+        pyrandom.seed(100 + k)
+        np.random.seed(100 + k)
+        host.append(T.imagenet_train_transform(device_normalize=True)({"image": img.copy(), "annotation": 0}))
+        pyrandom.seed(100 + k)
+        np.random.seed(100 + k)
+        dev.append(T.imagenet_train_transform(device_normalize=True, device_jitter=True)({"image": img.copy(),
+                                                                                          "annotation": 0}))
+    orders = {tuple(int(v) for v in d["jitter"][3:]) for d in dev}
+    assert len(orders) >= 3  # the seeds cover several enhancer orders
+    for h, d in zip(host, dev):
+        assert h["flip"] == d["flip"]
+        assert d["jitter"].dtype == torch.float32 and tuple(d["jitter"].shape) == (6,)
+    hb = torch.utils.data.default_collate(host)
+    db = torch.utils.data.default_collate(dev)
+    assert not torch.equal(hb["image"], db["image"])  # the device form has not jittered yet
+    jitter_u8(db["image"], db["jitter"])
+    assert torch.equal(hb["image"], db["image"])
+    a = normalize_u8(hb["image"], hb["flip"])
+    db2 = torch.utils.data.default_collate(dev)
+    b = normalize_u8(db2["image"], db2["flip"], jitter=db2["jitter"])
+    assert torch.equal(a, b)

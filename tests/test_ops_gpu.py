@@ -802,6 +802,30 @@ def test_u8_normalize_kernel(W):
     assert torch.allclose(out.float().cpu(), ref, rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize("H,W", [(224, 224), (320, 300), (9, 13)])
+def test_u8_jitter_kernel_matches_worker_bytes(H, W):
+    """csrc u8_jitter (ColorJitter on the GPU, in LDS for a 224x224 crop, in global memory above
+    150 KB) gives exactly the bytes of the worker-side native jitter (PIL enhancer arithmetic) for
+    every enhancer order, factors above / below 1 and a factor of exactly 1 (skipped)."""
+    import itertools
+
+    from deep_vision_amd.data.device_input import jitter_u8
+
+    g = torch.Generator().manual_seed(H * W)
+    orders = list(itertools.permutations(range(3)))
+    N = len(orders) + 2
+    x = torch.randint(0, 256, (N, H, W, 3), dtype=torch.uint8, generator=g)
+    x[0] = 255 - x[0] // 3  # a bright image: clipping above
+    f = 0.8 + 0.4 * torch.rand(N, 3, generator=g)
+    f[1, 1] = 1.0
+    o = torch.tensor(orders + [(0, 1, 2), (2, 0, 1)], dtype=torch.float32)
+    prm = torch.cat([f, o], 1)
+    ref = jitter_u8(x.clone(), prm)
+    out = jitter_u8(x.to(DEV), prm.to(DEV)).cpu()
+    assert not torch.equal(ref, x)
+    assert torch.equal(out, ref)
+
+
 @pytest.mark.parametrize("train", [True, False])
 def test_conv_bias_grad_via_bn(train):
     """A conv bias feeding a training BatchNorm gets its gradient from the BN's backward sums

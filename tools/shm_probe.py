@@ -25,12 +25,18 @@ def main():
         os.makedirs(imgdir)
         syn = make_jpegs(imgdir, 1536)
         ds = ImageNet2012Dataset(imgdir, syn, T.imagenet_train_transform(device_normalize=True), decode_min_side=256)
+        # the trainer's default: ColorJitter draws in the worker, the pixels jittered on the GPU
+        dsj = ImageNet2012Dataset(imgdir, syn, T.imagenet_train_transform(device_normalize=True, device_jitter=True),
+                                  decode_min_side=256)
         dev = "cuda" if torch.cuda.is_available() else None
         for w in workers:
             r = {"stock": round(loader_rate(ds, w, batch, 24), 1)}
             r["shm_host"] = round(shm_loader_rate(ds, w, batch, 24, None)[0], 1)
             if dev:
-                r["shm_device"] = round(shm_loader_rate(ds, w, batch, 24, dev)[0], 1)
+                r["shm_device"] = round(shm_loader_rate(ds, w, batch, 24, dev, consume=True)[0], 1)
+                r["shm_device_gpu_jitter"] = round(shm_loader_rate(dsj, w, batch, 24, dev, consume=True)[0], 1)
+            else:
+                r["shm_host_gpu_jitter_draws"] = round(shm_loader_rate(dsj, w, batch, 24, None)[0], 1)
             out[w] = r
             print(w, json.dumps(r), flush=True)
     print(json.dumps(out))
