@@ -326,7 +326,11 @@ _SUBPIX_STREAMS = {}
 
 
 def _subpix_streams(device, n):
+    """n side streams of ``device``, or None inside a capture that would have to create one (a
+    captured step's eager warm-up creates them; a capture without one keeps a single stream)."""
     lst = _SUBPIX_STREAMS.setdefault(device, [])
+    if len(lst) < n and torch.cuda.is_current_stream_capturing():
+        return None
     while len(lst) < n:
         lst.append(torch.cuda.Stream(device=device))
     return lst[:n]
@@ -342,9 +346,10 @@ def _subpixel_dgrad(dy, wd, dX, res, bnref, N, H, W, P, Q, Cg_dy, ldy_in, G, Ig,
     # on none: a partial fusion would leave part of the sums in the accumulator
     fuse = bnref if (bnref is not None and G == 1 and Cg_x == Ig and len(live) == len(parts)) else None
     conc = SUBPIXEL_CONC and dy.is_cuda and len(live) > 1 and not lib().deterministic()
+    sides = _subpix_streams(dy.device, len(live) - 1) if conc else None
+    conc = sides is not None
     if conc:
         cur = torch.cuda.current_stream(dy.device)
-        sides = _subpix_streams(dy.device, len(live) - 1)
         for st in sides:
             st.wait_stream(cur)
     ok = []
