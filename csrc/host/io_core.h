@@ -294,6 +294,22 @@ inline void resize_crop_bilinear(const uint8_t* src, int64_t H, int64_t W, int64
     const uint8_t* r0 = src + a * rs;
     const uint8_t* r1 = src + std::min<int64_t>(a + 1, H - 1) * rs;
     uint8_t* d = dst + i * cw * C;
+    if (C == 3) {
+      // RGB: channels unrolled, 32-bit sums (255 * 2^11 * 2^11 + 2^21 < 2^31: the same values as the
+      // 64-bit form below), four taps' pointers hoisted per output pixel
+      const int32_t wy1 = wy, wy0 = ONE - wy;
+      for (int64_t j = 0; j < cw; ++j) {
+        const int32_t w1 = wx[j], w0 = ONE - w1;
+        const uint8_t *a0 = r0 + x0[j], *a1 = r0 + x1[j], *b0 = r1 + x0[j], *b1 = r1 + x1[j];
+        uint8_t* o = d + j * 3;
+        for (int c = 0; c < 3; ++c) {
+          const int32_t top = a0[c] * w0 + a1[c] * w1, bot = b0[c] * w0 + b1[c] * w1;
+          const int32_t v = (top * wy0 + bot * wy1 + (1 << (2 * BITS - 1))) >> (2 * BITS);
+          o[c] = (uint8_t)(v > 255 ? 255 : v);
+        }
+      }
+      continue;
+    }
     for (int64_t j = 0; j < cw; ++j) {
       const int32_t w1 = wx[j], w0 = ONE - w1;
       for (int64_t c = 0; c < C; ++c) {
