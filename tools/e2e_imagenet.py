@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--images", type=int, default=6144)
     ap.add_argument("--val-images", type=int, default=512)
+    ap.add_argument("--unique", type=int, default=2048,
+                    help="distinct JPEGs generated; the rest of --images are hard links to them (same decode work)")
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--workers", type=int, default=16)
     ap.add_argument("--epochs", type=int, default=2)
@@ -36,9 +38,15 @@ def main():
         os.makedirs(tr)
         os.makedirs(va)
         t0 = time.perf_counter()
-        make_jpegs(tr, a.images, seed=0)  # writes <d>/synsets.txt
+        u = min(a.unique, a.images)
+        make_jpegs(tr, u, seed=0)  # writes <d>/synsets.txt
+        names = sorted(os.listdir(tr))
+        for i in range(u, a.images):  # nXXXXXXXX_<i>.JPEG: the synset prefix keeps the label
+            src = names[i % u]
+            os.link(os.path.join(tr, src), os.path.join(tr, f"{src.split('_')[0]}_{i}.JPEG"))
         make_jpegs(va, a.val_images, seed=1)
-        print(f"[e2e] generated {a.images} + {a.val_images} JPEGs in {time.perf_counter() - t0:.1f} s", flush=True)
+        print(f"[e2e] {a.images} train ({u} distinct) + {a.val_images} val JPEGs in {time.perf_counter() - t0:.1f} s",
+              flush=True)
         cmd = [sys.executable, os.path.join(ROOT, "ResNet", "pytorch", "train.py"), "-m", a.model, "--data-dir", d,
                "--epochs", str(a.epochs), "--batch-size", str(a.batch), "--workers", str(a.workers),
                "--val-steps", "2", "--profile", "timer", "--checkpoint-dir", os.path.join(d, "ckpt")]
