@@ -41,6 +41,7 @@ from .. import ops as F
 from ..ops.bn import STAT_ROWS, STAT_SHARDS
 from ..ops.common import workspace
 from ..ops.conv import ColsumBox, GradJoin, no_wgrad_side
+from .branch import BranchEdge as _BranchEdge
 
 
 import os
@@ -88,25 +89,6 @@ def _side_stream(device, depth):
     if st is None:
         st = _STREAMS[key] = torch.cuda.Stream(device=device)
     return st
-
-
-class _BranchEdge(torch.autograd.Function):
-    """Identity at a stream fork / join. Its backward runs on the branch's stream (autograd runs a
-    node's backward on its forward stream) and marks the gradient crossing the edge as used by
-    both streams: a gradient allocated on one stream and read on the other would otherwise go
-    back to its allocating stream's pool while the other stream may still read it."""
-
-    @staticmethod
-    def forward(ctx, t, other):
-        ctx.other = other
-        return t.view_as(t)
-
-    @staticmethod
-    def backward(ctx, g):
-        if g is not None:
-            g.record_stream(torch.cuda.current_stream(g.device))
-            g.record_stream(ctx.other)
-        return g, None
 
 
 def _bn(c):

@@ -345,3 +345,4 @@ def test_level_statistics_handoff_matches_separate_passes():
     cos = lambda a, b: torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()  # noqa: E731
     assert cos(dx0, dx1) > 0.999 and cos(g0, g1) > 0.999
     assert not any("_dv_block_stats" in mm.__dict__ for mm in list(m.modules()) + list(b.modules()))
+
