@@ -324,20 +324,36 @@ void dispatch_tile(const FwdParams& p, hipStream_t st) {
 // (256 channels) x 4 row lanes walking FR_ROWS rows; statistics meet in LDS, one coalesced atomic
 // row per block into shard blockIdx.y % SHARDS.
 constexpr int FR_ROWS = 64;  // rows per block on large grids; small ones shrink it (dv_conv_fwd)
+// BatchNorm-backward sums of a split-K dgrad's output (the conv epilogue's BNR, modes 1 / 2: the
+// split blocks only write fp32 slabs, so the pass that stores dX reduces it): x = the BN input at
+// dX's offsets (dense, ld = N), prm = [scale, shift, mean, invstd][N], acc = [SHARDS][2][N]
+struct FinBnr {
+  const u16* x;
+  const float* prm;
+  float* acc;
+  int mode, act;
+  float slope;
+  float* det;
+};
+
 __global__ __launch_bounds__(256) void splitk_finalize_kernel(const float* __restrict__ ypart, int ksplit, int M, int N,
                                                               const float* __restrict__ bias, int act, float slope,
                                                               const u16* __restrict__ res, float* __restrict__ stats,
-                                                              u16* __restrict__ y, int ldy, int fr, float* __restrict__ det) {
+                                                              u16* __restrict__ y, int ldy, int fr, float* __restrict__ det,
+                                                              FinBnr bnr) {
   __shared__ float red[2][4][256];
   const int lc = threadIdx.x & 63, lr = threadIdx.x >> 6;
   const int n = blockIdx.x * 256 + lc * 4;
   const bool nv = n < N;  // N % 4 == 0: whole column quads
   const int64_t slab = (int64_t)M * N;
-  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f}, bv[4], kq[4];
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f}, bv[4], kq[4], bsc[4], bsh[4], bmu[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     bv[r] = (bias && nv) ? bias[n + r] : 0.f;
     kq[r] = (stats && nv) ? stat_shift(stats, N)[n + r] : 0.f;
+    bsc[r] = (bnr.acc && nv) ? bnr.prm[n + r] : 0.f;
+    bsh[r] = (bnr.acc && nv) ? bnr.prm[N + n + r] : 0.f;
+    bmu[r] = (bnr.acc && nv) ? bnr.prm[2 * N + n + r] : 0.f;
   }
   const int m1 = min(M, (int)(blockIdx.y + 1) * fr);
   for (int m = blockIdx.y * fr + lr; nv && m < m1; m += 4) {
@@ -356,13 +372,27 @@ __global__ __launch_bounds__(256) void splitk_finalize_kernel(const float* __res
       else if (act == ACT_LEAKY) t = t > 0.f ? t : t * slope;
       t += rv[r];
       v[r] = t;
-      const float d = t - kq[r];
-      s1[r] += d; s2[r] = fmaf(d, d, s2[r]);
+      if (stats) {  // (the BN-backward sums below use the same accumulators)
+        const float d = t - kq[r];
+        s1[r] += d; s2[r] = fmaf(d, d, s2[r]);
+      }
     }
     uint2 pk; pk.x = pack2bf(v[0], v[1]); pk.y = pack2bf(v[2], v[3]);
     *reinterpret_cast<uint2*>(y + (int64_t)m * ldy + n) = pk;
+    if (bnr.acc) {  // of the stored bf16 gradient, as the unfused reduce pass would read it back
+      const uint2 xr = *reinterpret_cast<const uint2*>(bnr.x + (int64_t)m * N + n);
+      const float d[4] = {bf2f(pk.x & 0xffff), bf2f(pk.x >> 16), bf2f(pk.y & 0xffff), bf2f(pk.y >> 16)};
+      const float xv[4] = {bf2f(xr.x & 0xffff), bf2f(xr.x >> 16), bf2f(xr.y & 0xffff), bf2f(xr.y >> 16)};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float dz = d[r];
+        if (bnr.mode == 2 && !(xv[r] * bsc[r] + bsh[r] > 0.f)) dz = bnr.act == 2 ? d[r] * bnr.slope : 0.f;
+        s1[r] += dz;
+        s2[r] = fmaf(dz, xv[r] - bmu[r], s2[r]);
+      }
+    }
   }
-  if (!stats) return;
+  if (!stats && !bnr.acc) return;
 #pragma unroll
   for (int r = 0; r < 4; ++r) { red[0][lr][lc * 4 + r] = s1[r]; red[1][lr][lc * 4 + r] = s2[r]; }
   __syncthreads();
@@ -371,9 +401,15 @@ __global__ __launch_bounds__(256) void splitk_finalize_kernel(const float* __res
     float t1 = 0.f, t2 = 0.f;
 #pragma unroll
     for (int q = 0; q < 4; ++q) { t1 += red[0][q][threadIdx.x]; t2 += red[1][q][threadIdx.x]; }
-    float* sh = stat_row(stats, det, blockIdx.y, N);
-    atomicAdd(sh + c, t1);
-    atomicAdd(sh + N + c, t2);
+    if (bnr.acc) {  // sum dz*(x - mean) -> sum dz*xhat: one invstd per channel
+      float* sh = stat_row(bnr.acc, bnr.det, blockIdx.y, N);
+      atomicAdd(sh + c, t1);
+      atomicAdd(sh + N + c, t2 * bnr.prm[3 * N + c]);
+    } else {
+      float* sh = stat_row(stats, det, blockIdx.y, N);
+      atomicAdd(sh + c, t1);
+      atomicAdd(sh + N + c, t2);
+    }
   }
 }
 
@@ -414,15 +450,23 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
     return -1;
   const u16* fin_res = nullptr;
   float* fin_stats = nullptr;
+  FinBnr fin_bnr{};
   if (a.ksplit > 1 && a.ypart) {
     // split-K: single group, identity output map; bias / activation / residual / BN statistics
-    // are applied by the finalize pass (no BN-backward statistics, no masked residual)
-    const bool ok = a.G == 1 && !a.tgather && !a.bnmode && !a.resbits && !a.reflect && (a.Kout % 4) == 0 &&
+    // and the BN-backward sums of a dgrad (modes 1 / 2: no mask bits, no second BN) are applied
+    // by the finalize pass (no masked residual)
+    const bool bn_ok = !a.bnmode || ((a.bnmode == 1 || a.bnmode == 2) && !a.bnx2 && a.bnx && a.bnprm && a.bnacc &&
+                                     !a.res && !a.stats && a.ldy == a.Kout);
+    const bool ok = a.G == 1 && !a.tgather && bn_ok && !a.resbits && !a.reflect && (a.Kout % 4) == 0 &&
                     (a.ldy % 4) == 0 && a.OH == a.P && a.OW == a.Q && a.osh == 1 && a.osw == 1 && !a.oph && !a.opw;
     if (!ok) return -1;
     p.ksplit = a.ksplit; p.ypart = a.ypart;
     fin_res = p.res; fin_stats = p.stats;  // applied by the finalize pass, not the split blocks
     p.res = nullptr; p.stats = nullptr;
+    if (a.bnmode) {
+      fin_bnr = FinBnr{(const u16*)a.bnx, a.bnprm, a.bnacc, a.bnmode, a.bnact, a.bnslope, nullptr};
+      p.bnmode = 0;  // the split blocks store raw slabs
+    }
   }
   // statistics of a residual output (y = conv + bias + residual) are accumulated from the 16-B
   // vector stores of a single-group tensor (conv_fwd_core.h RST)
@@ -526,9 +570,12 @@ int dv_conv_fwd(const ConvFwdArgs& a, hipStream_t st) {
     fr = std::max(4, std::min(FR_ROWS, (fr + 3) / 4 * 4));
     const dim3 grid((unsigned)ncb, (unsigned)((p.M + fr - 1) / fr));
     const DetStats fdet(fin_stats ? grid.y : 0, p.N, st);
+    const DetStats bdet(fin_bnr.acc ? grid.y : 0, p.N, st);
+    fin_bnr.det = bdet.slab;
     splitk_finalize_kernel<<<grid, dim3(256), 0, st>>>(p.ypart, dv_g_last_ksplit, p.M, p.N, p.bias, p.act, p.slope,
-                                                       fin_res, fin_stats, p.y, p.ldy, fr, fdet.slab);
+                                                       fin_res, fin_stats, p.y, p.ldy, fr, fdet.slab, fin_bnr);
     fdet.fold(fin_stats);
+    if (fin_bnr.acc) bdet.fold(fin_bnr.acc);
   }
   return bn_status;
 }

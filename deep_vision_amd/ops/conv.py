@@ -159,6 +159,7 @@ def conv_ksplit(M, O, K, G=1):
 
 
 DGRAD_SPLIT = os.environ.get("DV_DGRAD_SPLIT", "1") != "0"
+FIN_BNR = os.environ.get("DV_FIN_BNR", "1") != "0"  # split-K dgrads: BN-backward sums in the finalize pass
 
 
 def dgrad_ksplit(M, O, K, G=1):
@@ -262,11 +263,12 @@ def _dgrad(dy, weight, x_shape, Cg_x, G, stride, padding, dilation, device, accu
         dX, res = alloc_cl((N, G * Cg_x, H, W), zero=((scatter and not zfill) or Cg_x != Ig), device=device), None
     if (sh, sw) == (1, 1):
         # an under-filled grid (small maps, long K: YOLOv3's 13x13 3x3 dgrads, 88 tiles of 128x128 on
-        # 256 CUs, K = 9216) splits K across blocks; the BatchNorm-backward sums then come from the
-        # BN's own (small) reduce pass instead of this epilogue
+        # 256 CUs, K = 9216) splits K across blocks; the BatchNorm-backward sums (modes 1 / 2, one
+        # BN) then come from the split-K finalize pass that stores dX (csrc/conv_fwd.hip FinBnr)
         ks = dgrad_ksplit(N * H * W, Ig, R * S * Cg_dy, G) if resmask is None else 1
         fuse = (bnref if (bnref is not None and G == 1 and Cg_x == Ig and (res is not None or accum is None)
-                          and ks == 1) else None)
+                          and (ks == 1 or (FIN_BNR and bnref.mode in (1, 2) and bnref.x2 is None and res is None)))
+                else None)
         if conv_fwd_raw(dy, wd, dX, None, None, N, P, Q, Cg_dy, ldy_in, G, Ig, H, W, R, S, (1, 1), (-ph, -pw),
                         (-dh, -dw), ldy=G * Cg_x, res=res, bnref=fuse, resmask=resmask, ksplit=ks):
             fuse.mark_fused(dX)

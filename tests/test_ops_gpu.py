@@ -894,7 +894,7 @@ def test_darknet_residual_post_activation_add():
 def test_dgrad_split_k_small_grid(C, O, H, bnfuse):
     """Stride-1 3x3 dgrads on under-filled grids split K across blocks (ops.conv.dgrad_ksplit:
     YOLOv3's 13x13 layers): against fp32 torch, with and without a BatchNorm in front (its
-    backward sums then come from its own reduce pass, not the dgrad epilogue)."""
+    backward sums then come from the split-K finalize pass that stores dX)."""
     from deep_vision_amd import nn, ops as F
     from deep_vision_amd.ops import conv as Cv
 
@@ -906,10 +906,15 @@ def test_dgrad_split_k_small_grid(C, O, H, bnfuse):
     dy = torch.randn(N, O, H, H, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     xi = x.clone().requires_grad_(True)
     if bnfuse:
+        from deep_vision_amd.ops.bn import COUNTERS
+
         bn = nn.BatchNorm2d(C).to(DEV)
         h = F.batch_norm_act(xi, bn, "relu")
         y = F.conv2d(h, conv.weight, None, 1, 1)
+        n0 = COUNTERS["bwd_reduce_fused"]
         y.backward(dy)
+        # the BN-backward sums come from the split-K finalize pass (csrc/conv_fwd.hip FinBnr)
+        assert COUNTERS["bwd_reduce_fused"] - n0 == (1 if Cv.FIN_BNR else 0)
         xr = x.float().requires_grad_(True)
         hr = torch.relu(torch.nn.functional.batch_norm(xr, None, None, bn.weight.float(), bn.bias.float(), True))
         yr = torch.nn.functional.conv2d(hr.to(torch.bfloat16).float(), conv.weight.to(torch.bfloat16).float(), None, 1, 1)
