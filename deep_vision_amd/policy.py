@@ -28,6 +28,10 @@ DV_WGRAD_SIDE_GRAPH        0 / 1 forces the inside-a-capture decision
 DV_KEEP_HW_QUEUES          1 leaves GPU_MAX_HW_QUEUES as the caller set it
 =========================  =====================================================================
 
+(Per-kernel A/B switches that do not change the process's stream / queue layout stay with their
+kernels in ops/conv.py: DV_SUBPIXEL_CONC -- a strided dgrad's parity parts on streams of their own,
+off in deterministic mode; DV_DGRAD_SPLIT; DV_FIN_BNR.)
+
 Reference: the reference launches every trainer one way (R/ResNet/pytorch/train.py:353-355
 DataParallel over all GPUs; R/YOLO/tensorflow/train.py:281-294 MirroredStrategy).
 """
