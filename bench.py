@@ -239,7 +239,10 @@ def main():
     if args.policy:
         rec = _policy.describe()
         rec["rank"] = int(__import__("os").environ.get("RANK", "0"))
-        print(json.dumps(rec), flush=True)
+        sys.stdout.flush()
+        # one write(2) per line: the ranks of a torchrun share the pipe, and a line written in pieces
+        # (text + newline) could interleave with another rank's
+        __import__("os").write(sys.stdout.fileno(), (json.dumps(rec) + "\n").encode())
         return
 
     import os

@@ -61,7 +61,10 @@ def _torchrun(nproc, *args):
     env["OMP_NUM_THREADS"] = "1"
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
-    recs = [json.loads(line) for line in out.stdout.splitlines() if line.startswith("{")]
+    recs, dec, txt, i = [], json.JSONDecoder(), out.stdout, 0
+    while (i := txt.find("{", i)) >= 0:  # objects, even if two ranks' lines ran together
+        obj, i = dec.raw_decode(txt, i)
+        recs.append(obj)
     assert sorted(r["rank"] for r in recs) == list(range(nproc)), out.stdout
     return recs
 
